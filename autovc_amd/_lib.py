@@ -1,0 +1,130 @@
+"""ctypes binding of libautovc_hip.so (the C-ABI declared in include/autovc_hip.h).
+
+This is the only place the product path touches native code.  There is no CPU or
+PyTorch fallback: if the library is missing or fails to load, every op raises.
+Tensors cross the boundary as raw device pointers (``tensor.data_ptr()``) plus
+int64 sizes, and every call is enqueued on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AUTOVC_HIP_LIB", os.path.join(_HERE, "libautovc_hip.so"))
+
+_lib = None
+_lock = threading.Lock()
+
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_f32 = ctypes.c_float
+c_ptr = ctypes.c_void_p
+
+# name -> argtypes (restype is always int status unless listed in _RESTYPES)
+_SIGS: dict[str, list] = {}
+_RESTYPES = {"autovc_last_error": ctypes.c_char_p,
+             "autovc_gemm_workspace_floats": c_i64, "autovc_bn_workspace_bytes": c_i64,
+             "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
+             "autovc_colsum_workspace_floats": c_i64}
+
+
+def sig(name: str, *argtypes):
+    _SIGS[name] = list(argtypes)
+
+
+sig("autovc_last_error")
+sig("autovc_abi_version")
+sig("autovc_device_sync")
+sig("autovc_stft_mel_f32", c_ptr, c_ptr, c_ptr, c_int, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_int, c_int, c_ptr, c_ptr)
+sig("autovc_gemm_workspace_floats", c_int, c_int, c_int)
+sig("autovc_gemm_f32", c_int, c_int, c_int,
+    c_ptr, c_i64, c_int, c_int, c_int, c_int,
+    c_ptr, c_i64, c_int, c_int, c_int, c_int,
+    c_ptr, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_ptr)
+sig("autovc_bn_workspace_bytes", c_int)
+sig("autovc_bn_stats_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_ptr,
+    c_ptr, c_ptr)
+sig("autovc_bn_act_fwd_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_int,
+    c_ptr, c_i64, c_ptr, c_i64, c_ptr)
+sig("autovc_bn_act_bwd_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr,
+    c_ptr, c_f32, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
+sig("autovc_lstm_fwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64,
+    c_ptr, c_ptr, c_int, c_ptr)
+sig("autovc_lstm_bwd_workspace_floats", c_int, c_int, c_int)
+sig("autovc_lstm_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_int, c_int, c_ptr, c_ptr)
+sig("autovc_blstm_fwd_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr)
+sig("autovc_blstm_bwd_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr)
+sig("autovc_frame_concat_f32", c_int, c_int, c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_ptr)
+sig("autovc_frame_concat_bwd_f32", c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_i64, c_ptr,
+    c_int, c_ptr)
+sig("autovc_code_gather_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr)
+sig("autovc_code_gather_bwd_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr)
+sig("autovc_loss_workspace_bytes")
+sig("autovc_loss_f32", c_int, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
+sig("autovc_loss_bwd_f32", c_int, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int, c_ptr)
+sig("autovc_adam_f32", c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32,
+    c_f32, c_ptr)
+sig("autovc_conv_pack_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr)
+sig("autovc_conv_unpack_grad_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr)
+sig("autovc_transpose_f32", c_int, c_int, c_ptr, c_ptr, c_ptr)
+sig("autovc_colsum_workspace_floats", c_int)
+sig("autovc_colsum_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes library; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise HipLibraryError(
+                f"libautovc_hip.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+        # torch first: its libamdhip64.so.7 is then the one the library binds to
+        import torch  # noqa: F401
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, c_int)
+        _lib = lib
+        return lib
+
+
+def exported_symbols() -> list[str]:
+    return sorted(_SIGS)
+
+
+def call(name: str, *args):
+    """Call an entry point and convert a non-zero status into an exception."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.autovc_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError(f"{name}: {msg}")
+        raise HipLibraryError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (None -> NULL)."""
+    return 0 if t is None else t.data_ptr()

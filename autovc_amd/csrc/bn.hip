@@ -1,0 +1,222 @@
+// BatchNorm1d (+ ReLU / tanh / identity) for NTC activations, train and eval mode.
+//
+// Reference: nn.BatchNorm1d(C) after every ConvNorm (model_vc_mel.py:57,100,140,151,160)
+// followed by F.relu (encoder/decoder, :69,:115) or torch.tanh (postnet :165) or nothing
+// (last postnet layer :167).  Train mode: batch statistics over (B, T) per channel,
+// biased variance for normalisation, unbiased for running_var, momentum 0.1, eps 1e-5,
+// num_batches_tracked += 1.
+//
+// Channel statistics are a column reduction of the (M = B*T, C) activation: a partial
+// kernel (grid = column tiles x row splits, coalesced 256 B row segments per wave,
+// double accumulators about a per-channel shift = row 0) and a finalize kernel that
+// sums the partials in a fixed order -> deterministic, no atomics.
+#include <algorithm>
+
+#include "common.h"
+#include "../../include/autovc_hip.h"
+
+namespace {
+
+constexpr int kRowSplits = 64;
+
+enum Act { kNone = 0, kRelu = 1, kTanh = 2 };
+
+__device__ __forceinline__ float act_fwd(float v, int act) {
+  return act == kRelu ? fmaxf(v, 0.f) : (act == kTanh ? tanhf(v) : v);
+}
+
+// derivative of the activation expressed through its OUTPUT z
+__device__ __forceinline__ float act_grad(float dz, float z, int act) {
+  return act == kRelu ? (z > 0.f ? dz : 0.f) : (act == kTanh ? dz * (1.f - z * z) : dz);
+}
+
+// ---- statistics: partial[rs][c] = (sum (x - x0), sum (x - x0)^2) ------------------
+__global__ __launch_bounds__(256) void stats_partial_kernel(int64_t M, int C, const float* __restrict__ y, int64_t ld,
+                                                           double* __restrict__ part) {
+  __shared__ double red[4][64][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int rs = blockIdx.y, RS = gridDim.y;
+  const int64_t r0 = M * rs / RS, r1 = M * (rs + 1) / RS;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    const double x0 = y[c];
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      const double d = (double)y[r * ld + c] - x0;
+      s1 += d;
+      s2 += d * d;
+    }
+  }
+  red[w][lane][0] = s1;
+  red[w][lane][1] = s2;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    double a = 0.0, b = 0.0;
+    for (int q = 0; q < 4; ++q) { a += red[q][lane][0]; b += red[q][lane][1]; }
+    part[((int64_t)rs * C + c) * 2 + 0] = a;
+    part[((int64_t)rs * C + c) * 2 + 1] = b;
+  }
+}
+
+__global__ void stats_finalize_kernel(int64_t M, int C, const float* __restrict__ y, const double* __restrict__ part,
+                                      int RS, float* __restrict__ mean, float* __restrict__ var,
+                                      float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
+                                      int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int rs = 0; rs < RS; ++rs) {
+    a += part[((int64_t)rs * C + c) * 2 + 0];
+    b += part[((int64_t)rs * C + c) * 2 + 1];
+  }
+  const double n = (double)M;
+  const double mu_s = a / n;
+  double v = b / n - mu_s * mu_s;
+  if (v < 0.0) v = 0.0;
+  const double mu = (double)y[c] + mu_s;
+  mean[c] = (float)mu;
+  var[c] = (float)v;
+  if (run_mean) run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mu);
+  if (run_var) run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * v * n / (n > 1.0 ? n - 1.0 : 1.0));
+}
+
+// ---- apply: z = act(y * alpha + beta') (+ residual), alpha = gamma/sqrt(var+eps) -------
+__global__ void apply_kernel(int64_t M, int C, const float* __restrict__ y, int64_t ldy,
+                             const float* __restrict__ mean, const float* __restrict__ var,
+                             const float* __restrict__ gamma, const float* __restrict__ beta, float eps, int act,
+                             const float* __restrict__ res, int64_t ldr, float* __restrict__ z, int64_t ldz) {
+  const int64_t total = M * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / C;
+    const int c = (int)(i % C);
+    const float invstd = 1.0f / sqrtf(var[c] + eps);
+    const float alpha = invstd * (gamma ? gamma[c] : 1.f);
+    const float b = (beta ? beta[c] : 0.f) - mean[c] * alpha;
+    float v = act_fwd(fmaf(y[m * ldy + c], alpha, b), act);
+    if (res) v += res[m * ldr + c];
+    z[m * ldz + c] = v;
+  }
+}
+
+// ---- backward reduce: partial sums of dy_act and dy_act * xhat ----------------------
+__global__ __launch_bounds__(256) void bwd_partial_kernel(int64_t M, int C, const float* __restrict__ dz, int64_t lddz,
+                                                         const float* __restrict__ z, int64_t ldz,
+                                                         const float* __restrict__ y, int64_t ldy,
+                                                         const float* __restrict__ mean, int act,
+                                                         double* __restrict__ part) {
+  __shared__ double red[4][64][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int rs = blockIdx.y, RS = gridDim.y;
+  const int64_t r0 = M * rs / RS, r1 = M * (rs + 1) / RS;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    const float mu = mean[c];
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      const float g = act_grad(dz[r * lddz + c], act == kNone ? 0.f : z[r * ldz + c], act);
+      s1 += (double)g;
+      s2 += (double)g * (double)(y[r * ldy + c] - mu);
+    }
+  }
+  red[w][lane][0] = s1;
+  red[w][lane][1] = s2;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    double a = 0.0, b = 0.0;
+    for (int q = 0; q < 4; ++q) { a += red[q][lane][0]; b += red[q][lane][1]; }
+    part[((int64_t)rs * C + c) * 2 + 0] = a;
+    part[((int64_t)rs * C + c) * 2 + 1] = b;
+  }
+}
+
+// sums -> dbeta = sum dy_act, dgamma = sum dy_act * xhat ; keeps the raw sums for apply
+__global__ void bwd_finalize_kernel(int C, const double* __restrict__ part, int RS, const float* __restrict__ var,
+                                    float eps, float* __restrict__ sums, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int rs = 0; rs < RS; ++rs) {
+    a += part[((int64_t)rs * C + c) * 2 + 0];
+    b += part[((int64_t)rs * C + c) * 2 + 1];
+  }
+  const float invstd = 1.0f / sqrtf(var[c] + eps);
+  const float sdy = (float)a, sdyx = (float)(b * (double)invstd);
+  sums[2 * c] = sdy;
+  sums[2 * c + 1] = sdyx;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + sdy : sdy;
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + sdyx : sdyx;
+}
+
+// dy = (dy_act - sdy/M - xhat * sdyx/M) * invstd * gamma
+__global__ void bwd_apply_kernel(int64_t M, int C, const float* __restrict__ dz, int64_t lddz,
+                                 const float* __restrict__ z, int64_t ldz, const float* __restrict__ y, int64_t ldy,
+                                 const float* __restrict__ mean, const float* __restrict__ var,
+                                 const float* __restrict__ gamma, float eps, int act, const float* __restrict__ sums,
+                                 float* __restrict__ dy, int64_t lddy) {
+  const int64_t total = M * C;
+  const float inv_m = 1.0f / (float)M;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / C;
+    const int c = (int)(i % C);
+    const float invstd = 1.0f / sqrtf(var[c] + eps);
+    const float g = act_grad(dz[m * lddz + c], act == kNone ? 0.f : z[m * ldz + c], act);
+    const float xhat = (y[m * ldy + c] - mean[c]) * invstd;
+    const float v = (g - sums[2 * c] * inv_m - xhat * sums[2 * c + 1] * inv_m) * invstd * (gamma ? gamma[c] : 1.f);
+    dy[m * lddy + c] = v;
+  }
+}
+
+int grid_for(int64_t total) { return (int)std::min<int64_t>((total + 255) / 256, 8192); }
+
+}  // namespace
+
+extern "C" int64_t autovc_bn_workspace_bytes(int C) {
+  return (int64_t)kRowSplits * C * 2 * sizeof(double) + (int64_t)2 * C * sizeof(float);
+}
+
+extern "C" int autovc_bn_stats_f32(int64_t M, int C, const float* y, int64_t ldy, float* mean, float* var,
+                                   float* running_mean, float* running_var, float momentum, int64_t* num_batches,
+                                   void* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && C > 0, "autovc_bn_stats_f32: bad dims");
+  AVC_CHECK_ARG(y && mean && var && workspace, "autovc_bn_stats_f32: null pointer");
+  double* part = reinterpret_cast<double*>(workspace);
+  const int RS = (int)std::min<int64_t>(kRowSplits, M);
+  hipLaunchKernelGGL(stats_partial_kernel, dim3((C + 63) / 64, RS), dim3(256), 0, stream, M, C, y, ldy, part);
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, M, C, y,
+                     (const double*)part, RS, mean, var, running_mean, running_var, momentum, num_batches);
+  AVC_CHECK_LAUNCH("autovc_bn_stats_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_act_fwd_f32(int64_t M, int C, const float* y, int64_t ldy, const float* mean,
+                                     const float* var, const float* gamma, const float* beta, float eps, int act,
+                                     const float* residual, int64_t ldr, float* z, int64_t ldz, hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && C > 0 && y && mean && var && z, "autovc_bn_act_fwd_f32: bad args");
+  AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_bn_act_fwd_f32: unknown activation %d", act);
+  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(M * C)), dim3(256), 0, stream, M, C, y, ldy, mean, var, gamma,
+                     beta, eps, act, residual, ldr, z, ldz);
+  AVC_CHECK_LAUNCH("autovc_bn_act_fwd_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t lddz, const float* z, int64_t ldz,
+                                     const float* y, int64_t ldy, const float* mean, const float* var,
+                                     const float* gamma, float eps, int act, float* dy, int64_t lddy,
+                                     float* dgamma, float* dbeta, int accumulate, void* workspace,
+                                     hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && C > 0 && dz && y && mean && var && dy && workspace, "autovc_bn_act_bwd_f32: bad args");
+  AVC_CHECK_ARG(act == kNone || z, "autovc_bn_act_bwd_f32: activation backward needs the output z");
+  double* part = reinterpret_cast<double*>(workspace);
+  float* sums = reinterpret_cast<float*>(part + (int64_t)kRowSplits * C * 2);
+  const int RS = (int)std::min<int64_t>(kRowSplits, M);
+  hipLaunchKernelGGL(bwd_partial_kernel, dim3((C + 63) / 64, RS), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y,
+                     ldy, mean, act, part);
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, (const double*)part, RS,
+                     var, eps, sums, dgamma, dbeta, accumulate);
+  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(M * C)), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y, ldy,
+                     mean, var, gamma, eps, act, (const float*)sums, dy, lddy);
+  AVC_CHECK_LAUNCH("autovc_bn_act_bwd_f32");
+  return avc::kOk;
+}

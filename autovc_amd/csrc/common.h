@@ -1,0 +1,55 @@
+// Shared helpers for the autovc_amd HIP library (gfx950 / MI355X only).
+//
+// Error model (DESIGN.md "Boundary"): every extern "C" entry point returns an
+// int status (0 = ok, <0 = error) and records a message retrievable through
+// autovc_last_error() (thread-local).  No C++ exception crosses the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdarg>
+
+namespace avc {
+
+void set_error(const char* fmt, ...);
+
+constexpr int kOk = 0;
+constexpr int kErrArg = -1;     // bad shape / pointer / alignment
+constexpr int kErrLaunch = -2;  // hip launch or runtime failure
+
+}  // namespace avc
+
+#define AVC_CHECK_ARG(cond, ...)                 \
+  do {                                           \
+    if (!(cond)) {                               \
+      avc::set_error(__VA_ARGS__);               \
+      return avc::kErrArg;                       \
+    }                                            \
+  } while (0)
+
+#define AVC_CHECK_LAUNCH(name)                                              \
+  do {                                                                      \
+    hipError_t e_ = hipGetLastError();                                      \
+    if (e_ != hipSuccess) {                                                 \
+      avc::set_error("%s: launch failed: %s", name, hipGetErrorString(e_)); \
+      return avc::kErrLaunch;                                               \
+    }                                                                       \
+  } while (0)
+
+#define AVC_HIP(call, name)                                                 \
+  do {                                                                      \
+    hipError_t e_ = (call);                                                 \
+    if (e_ != hipSuccess) {                                                 \
+      avc::set_error("%s: %s", name, hipGetErrorString(e_));                \
+      return avc::kErrLaunch;                                               \
+    }                                                                       \
+  } while (0)
+
+#define AVC_ALIGNED16(p) ((reinterpret_cast<uintptr_t>(p) & 15u) == 0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Accurate (ocml) expf/tanhf: the LSTM parity bar is 1e-4 rel vs torch CPU.
+__device__ __forceinline__ float avc_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }

@@ -1,0 +1,513 @@
+"""Autograd ops of the Generator step, each forward/backward a sequence of C-ABI calls
+into libautovc_hip.so (no torch compute on the hot path, no fallback).
+
+Activations are frame-major / channel-last "NTC" (B, T, C) contiguous fp32 CUDA tensors:
+the layout the reference's LSTMs and mel tensors already use (model_vc_mel.py:64,70,112,
+116) — the reference's (B, C, T) conv layout is never materialised, the convolutions
+read NTC through the GEMM's implicit im2col operand.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+ACT = {"none": 0, "relu": 1, "tanh": 2}
+KS = 5      # ConvNorm kernel_size (model_vc_mel.py:53,96,137,147,157)
+PAD = 2     # ConvNorm padding
+
+
+# ---------------------------------------------------------------- helpers
+def _s():
+    return _lib.stream_ptr()
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _check(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: autovc_amd ops run on the GPU only (got a {t.device} tensor)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+
+
+class _Workspace:
+    """Per-device scratch buffer reused by every op (one stream: ops never overlap)."""
+    _bufs: dict = {}
+
+    @classmethod
+    def get(cls, device, nbytes, slot="main"):
+        key = (device, slot)
+        buf = cls._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 1) + 256, dtype=torch.uint8, device=device)
+            cls._bufs[key] = buf
+        return buf
+
+
+def _ws(device, nbytes, slot="main"):
+    return _Workspace.get(device, nbytes, slot).data_ptr()
+
+
+def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_conv=None,
+         bias1=None, bias2=None, accumulate=False, splits=1, a_off=0, b_off=0, c_off=0):
+    """C[M,N] (+)= A(m,k) B(k,n) (+bias); offsets are in floats from the tensors' data."""
+    ac = a_conv or (0, 0, 0)
+    bc = b_conv or (0, 0, 0)
+    ws = 0
+    if splits > 1:
+        ws = _ws(C.device, 4 * _lib.load().autovc_gemm_workspace_floats(M, N, splits), "gemm")
+    _lib.call("autovc_gemm_f32", M, N, K,
+              A.data_ptr() + 4 * a_off, lda, a_trans, ac[0], ac[1], ac[2],
+              B.data_ptr() + 4 * b_off, ldb, b_trans, bc[0], bc[1], bc[2],
+              C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, _s())
+
+
+def _splits_for(M, N, K):
+    """Split-K factor so that a (M,N) output tiled 128x128 fills ~256 CUs."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    s = 1
+    while tiles * s < 256 and K // (s * 2) >= 256:
+        s *= 2
+    return s
+
+
+def colsum(X2d, out, out2=None, accumulate=False):
+    M, N = X2d.shape
+    ws = _ws(X2d.device, 4 * _lib.load().autovc_colsum_workspace_floats(N), "colsum")
+    _lib.call("autovc_colsum_f32", M, N, X2d.data_ptr(), X2d.stride(0), _p(out), _p(out2),
+              int(accumulate), ws, _s())
+
+
+# ---------------------------------------------------------------- Conv1d + BN + act
+def _ceil4(n):
+    return (n + 3) // 4 * 4
+
+
+def _pad_last(x, n):
+    if x.shape[-1] == n:
+        return x.contiguous()
+    return torch.nn.functional.pad(x, (0, n - x.shape[-1])).contiguous()
+
+
+def _padded_weight(W, Cop, Cip):
+    """(Co, Ci, K) -> zero-padded (Cop, Cip, K) (only for channel counts % 4 != 0, e.g.
+    the 513/769-channel STFT generator)."""
+    Co, Ci, K = W.shape
+    if (Co, Ci) == (Cop, Cip):
+        return W.contiguous()
+    Wp = W.new_zeros((Cop, Cip, K))
+    Wp[:Co, :Ci] = W
+    return Wp
+
+
+def _conv_fwd(x, Wp, bp, T):
+    """y (B,T,Cop) = conv1d_k5p2(x (B,T,Cip)) + b as one implicit-im2col GEMM."""
+    B, _, Cip = x.shape
+    Cop = Wp.shape[0]
+    Wf = torch.empty((Cop, KS * Cip), device=x.device, dtype=torch.float32)
+    _lib.call("autovc_conv_pack_f32", Cop, Cip, KS, Wp.data_ptr(), Wf.data_ptr(), 0, _s())
+    y = torch.empty((B, T, Cop), device=x.device, dtype=torch.float32)
+    gemm(B * T, Cop, KS * Cip, x, Cip, 0, Wf, KS * Cip, 0, y, Cop, a_conv=(T, Cip, -PAD), bias1=bp)
+    return y
+
+
+def _conv_bwd(dy, x, Wp, need_x, need_w, need_b):
+    """Backward of _conv_fwd given dy (B,T,Cop): (dx (B,T,Cip), dWp (Cop,Cip,K), db (Cop))."""
+    B, T, Cip = x.shape
+    Cop = Wp.shape[0]
+    M = B * T
+    dev = x.device
+    dx = dW = db = None
+    if need_b:
+        db = torch.empty(Cop, device=dev, dtype=torch.float32)
+        colsum(dy.view(M, Cop), db)
+    if need_w:
+        dWf = torch.empty((Cop, KS * Cip), device=dev, dtype=torch.float32)
+        gemm(Cop, KS * Cip, M, dy, Cop, 1, x, Cip, 1, dWf, KS * Cip, b_conv=(T, Cip, -PAD),
+             splits=_splits_for(Cop, KS * Cip, M))
+        dW = torch.empty((Cop, Cip, KS), device=dev, dtype=torch.float32)
+        _lib.call("autovc_conv_unpack_grad_f32", Cop, Cip, KS, dWf.data_ptr(), dW.data_ptr(), 0, _s())
+    if need_x:
+        Wd = torch.empty((KS * Cop, Cip), device=dev, dtype=torch.float32)
+        _lib.call("autovc_conv_pack_f32", Cop, Cip, KS, Wp.data_ptr(), 0, Wd.data_ptr(), _s())
+        dx = torch.empty((B, T, Cip), device=dev, dtype=torch.float32)
+        gemm(M, Cip, KS * Cop, dy, Cop, 0, Wd, Cip, 1, dx, Cip, a_conv=(T, Cop, -PAD))
+    return dx, dW, db
+
+
+class ConvBNActFn(torch.autograd.Function):
+    """ConvNorm (k=5, p=2) -> BatchNorm1d -> act [-> + residual], NTC in/out.
+
+    Forward: conv as one implicit-im2col MFMA GEMM (bias fused), BN statistics (train)
+    or running stats (eval), fused normalise + activation (+ residual) pass.
+    """
+
+    @staticmethod
+    def forward(ctx, x, W, b, gamma, beta, running_mean, running_var, nbt, training, act,
+                momentum, eps, residual):
+        _check(x, "conv_bn_act")
+        B, T, Ci = x.shape
+        Co = W.shape[0]
+        Cip, Cop = _ceil4(Ci), _ceil4(Co)
+        M = B * T
+        dev = x.device
+        xp = _pad_last(x, Cip)
+        Wp = _padded_weight(W, Cop, Cip)
+        bp = b if (b is None or Cop == Co) else _pad_last(b, Cop)
+        y = _conv_fwd(xp, Wp, bp, T)
+        if training:
+            mean = torch.empty(Co, device=dev, dtype=torch.float32)
+            var = torch.empty(Co, device=dev, dtype=torch.float32)
+            ws = _ws(dev, _lib.load().autovc_bn_workspace_bytes(Co), "bn")
+            _lib.call("autovc_bn_stats_f32", M, Co, y.data_ptr(), Cop, mean.data_ptr(), var.data_ptr(),
+                      _p(running_mean), _p(running_var), float(momentum), _p(nbt), ws, _s())
+        else:
+            mean, var = running_mean, running_var
+        z = torch.empty((B, T, Co), device=dev, dtype=torch.float32)
+        res = residual.contiguous() if residual is not None else None
+        _lib.call("autovc_bn_act_fwd_f32", M, Co, y.data_ptr(), Cop, mean.data_ptr(), var.data_ptr(),
+                  _p(gamma), _p(beta), float(eps), ACT[act], _p(res), Co, z.data_ptr(), Co, _s())
+        ctx.training = training
+        ctx.act, ctx.eps = act, eps
+        ctx.has_res = residual is not None
+        ctx.dims = (Ci, Co, Cip, Cop)
+        # the activation backward reads the forward output; the residual layer has act none
+        ctx.save_for_backward(xp, Wp, gamma, y, None if ctx.has_res else z, mean, var)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        xp, Wp, gamma, y, z, mean, var = ctx.saved_tensors
+        if not ctx.training:
+            raise NotImplementedError("autovc_amd: backward through eval-mode BatchNorm is not supported")
+        Ci, Co, Cip, Cop = ctx.dims
+        dz = dz.contiguous()
+        B, T, _ = xp.shape
+        M = B * T
+        dev = xp.device
+        dy = (torch.zeros if Cop != Co else torch.empty)((B, T, Cop), device=dev, dtype=torch.float32)
+        dgamma = torch.empty(Co, device=dev, dtype=torch.float32) if ctx.needs_input_grad[3] else None
+        dbeta = torch.empty(Co, device=dev, dtype=torch.float32) if ctx.needs_input_grad[4] else None
+        ws = _ws(dev, _lib.load().autovc_bn_workspace_bytes(Co), "bn")
+        _lib.call("autovc_bn_act_bwd_f32", M, Co, dz.data_ptr(), Co, _p(z), Co, y.data_ptr(), Cop,
+                  mean.data_ptr(), var.data_ptr(), _p(gamma), float(ctx.eps), ACT[ctx.act],
+                  dy.data_ptr(), Cop, _p(dgamma), _p(dbeta), 0, ws, _s())
+        dx, dW, db = _conv_bwd(dy, xp, Wp, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               ctx.needs_input_grad[2])
+        if dx is not None and Cip != Ci:
+            dx = dx[..., :Ci].contiguous()
+        if dW is not None and (Cop, Cip) != (Co, Ci):
+            dW = dW[:Co, :Ci].contiguous()
+        if db is not None and Cop != Co:
+            db = db[:Co].contiguous()
+        dres = dz if ctx.has_res else None
+        return dx, dW, db, dgamma, dbeta, None, None, None, None, None, None, None, dres
+
+
+def conv_bn_act(x, conv, bn, act, residual=None):
+    """x (B,T,Ci) -> act(bn(conv(x))) (+ residual); conv: nn.Conv1d, bn: nn.BatchNorm1d."""
+    training = bn.training
+    momentum = bn.momentum if bn.momentum is not None else 0.0
+    nbt = bn.num_batches_tracked if (training and bn.track_running_stats) else None
+    if not training and (bn.running_mean is None or bn.running_var is None):
+        raise RuntimeError("eval-mode BatchNorm without running stats is not supported")
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    return ConvBNActFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, rm, rv, nbt, training, act,
+                             momentum, bn.eps, residual)
+
+
+class ConvFn(torch.autograd.Function):
+    """Plain ConvNorm (k=5, p=2) on NTC activations (ConvNorm.forward API path)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        _check(x, "conv")
+        B, T, Ci = x.shape
+        Co = W.shape[0]
+        Cip, Cop = _ceil4(Ci), _ceil4(Co)
+        xp = _pad_last(x, Cip)
+        Wp = _padded_weight(W, Cop, Cip)
+        bp = b if (b is None or Cop == Co) else _pad_last(b, Cop)
+        y = _conv_fwd(xp, Wp, bp, T)
+        ctx.save_for_backward(xp, Wp)
+        ctx.dims = (Ci, Co, Cip, Cop)
+        ctx.has_b = b is not None
+        return y if Cop == Co else y[..., :Co].contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        xp, Wp = ctx.saved_tensors
+        Ci, Co, Cip, Cop = ctx.dims
+        dyp = _pad_last(dy, Cop)
+        dx, dW, db = _conv_bwd(dyp, xp, Wp, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               ctx.has_b and ctx.needs_input_grad[2])
+        if dx is not None and Cip != Ci:
+            dx = dx[..., :Ci].contiguous()
+        if dW is not None and (Cop, Cip) != (Co, Ci):
+            dW = dW[:Co, :Ci].contiguous()
+        if db is not None and Cop != Co:
+            db = db[:Co].contiguous()
+        return dx, dW, db
+
+
+def conv_only(x, W, b):
+    return ConvFn.apply(x, W, b)
+
+
+# ---------------------------------------------------------------- Linear
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b):
+        _check(x, "linear")
+        x = x.contiguous()
+        lead = x.shape[:-1]
+        K = x.shape[-1]
+        N = W.shape[0]
+        M = x.numel() // K
+        y = torch.empty((*lead, N), device=x.device, dtype=torch.float32)
+        gemm(M, N, K, x, K, 0, W, K, 0, y, N, bias1=b)
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy = dy.contiguous()
+        K = x.shape[-1]
+        N = W.shape[0]
+        M = x.numel() // K
+        dx = dW = db = None
+        if ctx.needs_input_grad[1]:
+            dW = torch.empty_like(W)
+            gemm(N, K, M, dy, N, 1, x, K, 1, dW, K, splits=_splits_for(N, K, M))
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.empty(N, device=dy.device, dtype=torch.float32)
+            colsum(dy.view(M, N), db)
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            gemm(M, K, N, dy, N, 0, W, K, 1, dx, K)
+        return dx, dW, db
+
+
+def linear(x, W, b):
+    return LinearFn.apply(x, W, b)
+
+
+# ---------------------------------------------------------------- LSTM layers
+class LSTMLayerFn(torch.autograd.Function):
+    """One unidirectional nn.LSTM layer with large H (decoder lstm1 / lstm2)."""
+
+    @staticmethod
+    def forward(ctx, x, W_ih, W_hh, b_ih, b_hh, save):
+        _check(x, "lstm")
+        x = x.contiguous()
+        B, T, I = x.shape
+        H = W_hh.shape[1]
+        dev = x.device
+        gx = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+        gemm(B * T, 4 * H, I, x, I, 0, W_ih, I, 0, gx, 4 * H, bias1=b_ih, bias2=b_hh)
+        h = torch.empty((B, T, H), device=dev, dtype=torch.float32)
+        c = torch.empty((B, T, H), device=dev, dtype=torch.float32)
+        gates = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
+        _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
+                  h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), 0, _s())
+        ctx.save_for_backward(x, W_ih, W_hh, h, c, gates)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, W_ih, W_hh, h, c, gates = ctx.saved_tensors
+        if gates is None:
+            raise RuntimeError("LSTM backward needs the forward run with gradients enabled")
+        dh = dh.contiguous()
+        B, T, I = x.shape
+        H = W_hh.shape[1]
+        dev = x.device
+        WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
+        _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
+        splits = 4 if (4 * H) % 64 == 0 else 1
+        ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
+        dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+        _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
+                  WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
+        M = B * T
+        dx = dWih = dWhh = dbih = dbhh = None
+        if ctx.needs_input_grad[1]:
+            dWih = torch.empty_like(W_ih)
+            gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, dWih, I, splits=_splits_for(4 * H, I, M))
+        if ctx.needs_input_grad[2]:
+            dWhh = torch.empty_like(W_hh)
+            gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, dWhh, H, b_conv=(T, H, -1),
+                 splits=_splits_for(4 * H, H, M))
+        if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+            dbih = torch.empty(4 * H, device=dev, dtype=torch.float32)
+            dbhh = torch.empty(4 * H, device=dev, dtype=torch.float32)
+            colsum(dG.view(M, 4 * H), dbih, dbhh)
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I)
+        return dx, dWih, dWhh, dbih, dbhh, None
+
+
+class BLSTMLayerFn(torch.autograd.Function):
+    """One bidirectional nn.LSTM layer with H=32 (encoder, model_vc_mel.py:61)."""
+
+    @staticmethod
+    def forward(ctx, x, Wih_f, Whh_f, bih_f, bhh_f, Wih_b, Whh_b, bih_b, bhh_b, save):
+        _check(x, "blstm")
+        x = x.contiguous()
+        B, T, I = x.shape
+        H = Whh_f.shape[1]
+        G = 4 * H
+        dev = x.device
+        gx = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32)
+        gemm(B * T, G, I, x, I, 0, Wih_f, I, 0, gx, 2 * G, bias1=bih_f, bias2=bhh_f)
+        gemm(B * T, G, I, x, I, 0, Wih_b, I, 0, gx, 2 * G, bias1=bih_b, bias2=bhh_b, c_off=G)
+        h = torch.empty((B, T, 2 * H), device=dev, dtype=torch.float32)
+        c = torch.empty((B, T, 2 * H), device=dev, dtype=torch.float32)
+        gates = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32) if save else None
+        _lib.call("autovc_blstm_fwd_f32", B, T, H, 2, gx.data_ptr(), Whh_f.data_ptr(), Whh_b.data_ptr(),
+                  h.data_ptr(), c.data_ptr(), _p(gates), _s())
+        ctx.save_for_backward(x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates = ctx.saved_tensors
+        if gates is None:
+            raise RuntimeError("BLSTM backward needs the forward run with gradients enabled")
+        dh = dh.contiguous()
+        B, T, I = x.shape
+        H = Whh_f.shape[1]
+        G = 4 * H
+        M = B * T
+        dev = x.device
+        dG = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32)
+        _lib.call("autovc_blstm_bwd_f32", B, T, H, 2, dh.data_ptr(), gates.data_ptr(), c.data_ptr(),
+                  Whh_f.data_ptr(), Whh_b.data_ptr(), dG.data_ptr(), _s())
+        grads = [None] * 10
+        for d, (iW, iH, iBi, iBh) in enumerate(((1, 2, 3, 4), (5, 6, 7, 8))):
+            Wih = (Wih_f, Wih_b)[d]
+            Whh = (Whh_f, Whh_b)[d]
+            if ctx.needs_input_grad[iW]:
+                g = torch.empty_like(Wih)
+                gemm(G, I, M, dG, 2 * G, 1, x, I, 1, g, I, a_off=d * G, splits=_splits_for(G, I, M))
+                grads[iW] = g
+            if ctx.needs_input_grad[iH]:
+                g = torch.empty_like(Whh)
+                # previous step in processing order: t-1 forward, t+1 backward direction
+                gemm(G, H, M, dG, 2 * G, 1, h, 2 * H, 1, g, H, a_off=d * G, b_off=d * H,
+                     b_conv=(T, H, -1 if d == 0 else 1), splits=_splits_for(G, H, M))
+                grads[iH] = g
+        if any(ctx.needs_input_grad[i] for i in (3, 4, 7, 8)):
+            db_ih = torch.empty(2 * G, device=dev, dtype=torch.float32)
+            db_hh = torch.empty(2 * G, device=dev, dtype=torch.float32)
+            colsum(dG.view(M, 2 * G), db_ih, db_hh)
+            grads[3], grads[4] = db_ih[:G], db_hh[:G]
+            grads[7], grads[8] = db_ih[G:], db_hh[G:]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            gemm(M, I, G, dG, 2 * G, 0, Wih_f, I, 1, dx, I)
+            gemm(M, I, G, dG, 2 * G, 0, Wih_b, I, 1, dx, I, a_off=G, accumulate=True)
+        grads[0] = dx
+        return tuple(grads)
+
+
+# ---------------------------------------------------------------- glue / bottleneck
+class FrameConcatFn(torch.autograd.Function):
+    """out[b, t] = [X[b, t // rep], E[b]]  (model_vc_mel.py:64-66 with rep=1; :186-192)."""
+
+    @staticmethod
+    def forward(ctx, X, E, T, rep):
+        X = X.contiguous()
+        E = E.contiguous()
+        B = E.shape[0]
+        C1 = X.shape[-1]
+        C2 = E.shape[-1]
+        out = torch.empty((B, T, C1 + C2), device=X.device, dtype=torch.float32)
+        _lib.call("autovc_frame_concat_f32", B, T, C1, C2, rep, X.data_ptr(), C1, E.data_ptr(),
+                  out.data_ptr(), _s())
+        ctx.dims = (B, T, C1, C2, rep)
+        ctx.xshape = X.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, T, C1, C2, rep = ctx.dims
+        dout = dout.contiguous()
+        dX = torch.empty(ctx.xshape, device=dout.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        dE = torch.empty((B, C2), device=dout.device, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        if dX is not None or dE is not None:
+            _lib.call("autovc_frame_concat_bwd_f32", B, T, C1, C2, rep, dout.data_ptr(), _p(dX), C1, _p(dE),
+                      0, _s())
+        return dX, dE, None, None
+
+
+class CodeGatherFn(torch.autograd.Function):
+    """codes = cat_k [h_fwd[:, k*freq + freq-1], h_bwd[:, k*freq]] (model_vc_mel.py:74-79)."""
+
+    @staticmethod
+    def forward(ctx, h, freq):
+        h = h.contiguous()
+        B, T, D2 = h.shape
+        if T % freq != 0:
+            # the reference indexes out_forward[:, i+freq-1] past the end -> IndexError (F11)
+            raise IndexError(f"index {T // freq * freq + freq - 1} is out of bounds for dimension 1 "
+                             f"with size {T} (T must be a multiple of freq={freq})")
+        codes = torch.empty((B, (T // freq) * D2), device=h.device, dtype=torch.float32)
+        _lib.call("autovc_code_gather_f32", B, T, D2 // 2, freq, h.data_ptr(), codes.data_ptr(), _s())
+        ctx.dims = (B, T, D2 // 2, freq)
+        return codes
+
+    @staticmethod
+    def backward(ctx, dcodes):
+        B, T, D, freq = ctx.dims
+        dh = torch.empty((B, T, 2 * D), device=dcodes.device, dtype=torch.float32)
+        _lib.call("autovc_code_gather_bwd_f32", B, T, D, freq, dcodes.contiguous().data_ptr(), dh.data_ptr(),
+                  _s())
+        return dh, None
+
+
+# ---------------------------------------------------------------- losses
+class _LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, kind):
+        _check(a, "loss")
+        a = a.contiguous()
+        b = b.contiguous()
+        if a.numel() != b.numel():
+            raise ValueError(f"loss: size mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+        out = torch.empty((), device=a.device, dtype=torch.float32)
+        ws = _ws(a.device, _lib.load().autovc_loss_workspace_bytes(), "loss")
+        _lib.call("autovc_loss_f32", kind, a.numel(), a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, _s())
+        ctx.kind = kind
+        ctx.save_for_backward(a, b)
+        ctx.shapes = (a.shape, b.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        ga = torch.empty_like(a) if ctx.needs_input_grad[0] else None
+        gb = torch.empty_like(b) if ctx.needs_input_grad[1] else None
+        if ga is not None or gb is not None:
+            _lib.call("autovc_loss_bwd_f32", ctx.kind, a.numel(), a.data_ptr(), b.data_ptr(), g.data_ptr(),
+                      _p(ga), _p(gb), 0, 0, _s())
+        return ga, gb, None
+
+
+def mse_loss(a, b):
+    """F.mse_loss(a, b) (mean) for equal-numel tensors (solver_encoder.py:230,233)."""
+    return _LossFn.apply(a, b, 0)
+
+
+def l1_loss(a, b):
+    """F.l1_loss(a, b) (mean) (solver_encoder.py:236)."""
+    return _LossFn.apply(a, b, 1)

@@ -1,0 +1,163 @@
+/*
+ * autovc_hip.h — C-ABI of libautovc_hip.so, the MI355X (gfx950) hot path of AutoVC.
+ *
+ * The reference (sebakeaaen/autovc) has no FFI layer: its hot path is Python calling
+ * numpy/ATen/cuDNN.  Each entry point below replaces the reference call named in its
+ * comment (file:line in the reference tree); the Python host modules in autovc_amd/
+ * keep the reference's Python API and call these through ctypes.
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer unless the comment says "host";
+ *   - the caller owns every buffer (the library never allocates caller memory);
+ *     scratch is passed in as an explicit workspace pointer;
+ *   - fp32 everywhere ("f32" suffix); activations are frame-major / channel-last:
+ *     a (B, T, C) tensor is contiguous with C fastest ("NTC");
+ *   - all work is enqueued on `stream` (hipStream_t); nothing synchronises;
+ *   - return 0 on success, < 0 on error; autovc_last_error() (thread-local) says why.
+ */
+#ifndef AUTOVC_HIP_H_
+#define AUTOVC_HIP_H_
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AUTOVC_HIP_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- core */
+const char* autovc_last_error(void);
+int autovc_abi_version(void);
+int autovc_device_sync(void);
+
+/* ---------------------------------------------------------------- front end
+ * Replaces make_spect.py:36-48 (Spect.pySTFT) + :51-52,79-86 (mel projection,
+ * 20*log10 - 16, clip((.+100)/100, 0, 1)).
+ *   wav        : concatenated utterances (after the host filtfilt + dither of
+ *                make_spect.py:74-76), float64 as the reference computes it
+ *   wav_off    : [n_utt+1] int64 sample offsets
+ *   frame_off  : [n_utt+1] int64 frame offsets, frames_u = L_u // 256 + 1
+ *   mel_*      : sparse mel basis (librosa Slaney 80x513): per mel m the first bin,
+ *                the bin count and the offset of its weights in mel_w
+ *   out        : (total_frames, n_mels) for AUTOVC_FE_SPMEL,
+ *                (total_frames, 513)    for AUTOVC_FE_STFT (frame-major)
+ */
+#define AUTOVC_FE_SPMEL 0
+#define AUTOVC_FE_STFT 1
+int autovc_stft_mel_f32(const double* wav, const int64_t* wav_off, const int64_t* frame_off,
+                        int n_utt, int64_t total_frames, const int* mel_lo, const int* mel_len,
+                        const int* mel_woff, const float* mel_w, int n_mels, int mode,
+                        float* out, hipStream_t stream);
+
+/* ---------------------------------------------------------------- GEMM (fp32 MFMA)
+ * Replaces the ATen/cuDNN GEMMs behind nn.Conv1d (implicit im2col, model_vc_mel.py:28-38),
+ * nn.LSTM input projections (model_vc_mel.py:61,90,104) and nn.Linear (:10,106), forward
+ * and backward.  C[M,N] (ldc) = sum_k A(m,k) B(k,n) (+ bias1[n] + bias2[n]) (+ C if
+ * accumulate).  a_trans=0: A[m*lda+k], 1: A[k*lda+m].  b_trans=0: B[n*ldb+k], 1: B[k*ldb+n].
+ * *_conv_T > 0 turns the operand into the im2col view of an NTC activation with T frames
+ * per sequence, C channels and first tap offset tap0 (-2 for k=5/pad=2; -1 = "previous
+ * frame").  splits > 1 = split-K with a workspace of autovc_gemm_workspace_floats floats.
+ */
+int64_t autovc_gemm_workspace_floats(int M, int N, int splits);
+int autovc_gemm_f32(int M, int N, int K,
+                    const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
+                    const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
+                    float* C, int64_t ldc, const float* bias1, const float* bias2,
+                    int accumulate, int splits, float* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------- BatchNorm1d + act
+ * Replaces nn.BatchNorm1d (train/eval) + F.relu / torch.tanh / identity after each
+ * ConvNorm (model_vc_mel.py:57,69,100,115,140,151,160,165,167).  y, z are (M=B*T, C)
+ * row-major with leading dims.  act: 0 none, 1 relu, 2 tanh.  stats writes the batch
+ * mean / biased var and (if given) updates running_mean / running_var (unbiased,
+ * momentum) and num_batches_tracked.  fwd: z = act(gamma (y-mean)/sqrt(var+eps) + beta)
+ * (+ residual).  bwd: dy from dz (z = the forward output), dgamma/dbeta (+)=.
+ * workspace: autovc_bn_workspace_bytes(C) bytes.
+ */
+#define AUTOVC_ACT_NONE 0
+#define AUTOVC_ACT_RELU 1
+#define AUTOVC_ACT_TANH 2
+int64_t autovc_bn_workspace_bytes(int C);
+int autovc_bn_stats_f32(int64_t M, int C, const float* y, int64_t ldy, float* mean, float* var,
+                        float* running_mean, float* running_var, float momentum,
+                        int64_t* num_batches, void* workspace, hipStream_t stream);
+int autovc_bn_act_fwd_f32(int64_t M, int C, const float* y, int64_t ldy, const float* mean,
+                          const float* var, const float* gamma, const float* beta, float eps,
+                          int act, const float* residual, int64_t ldr, float* z, int64_t ldz,
+                          hipStream_t stream);
+int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t lddz, const float* z,
+                          int64_t ldz, const float* y, int64_t ldy, const float* mean,
+                          const float* var, const float* gamma, float eps, int act, float* dy,
+                          int64_t lddy, float* dgamma, float* dbeta, int accumulate,
+                          void* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------- LSTM recurrences
+ * Replaces the cuDNN/mkldnn recurrence of nn.LSTM (model_vc_mel.py:61,90,104).
+ * gx = x W_ih^T + b_ih + b_hh precomputed (autovc_gemm_f32).  Large H (multiple of 16):
+ * one launch per step; h written at h[b*h_ldb + t*h_ldt + j]; c_all (B,T,H); gates
+ * (B,T,4H) post-activation [i|f|g|o] (null in inference).  Backward produces dG (B,T,4H)
+ * (pre-activation gate grads) from dh_out using W_hh^T (H,4H); workspace of
+ * autovc_lstm_bwd_workspace_floats floats.  Small H (=32, encoder BLSTM): whole sequence
+ * in one launch, ndir directions, gx (B,T,ndir*4H), h/c (B,T,ndir*H), W_hh (4H,H) per direction.
+ */
+int autovc_lstm_fwd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                        const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                        float* gates, int reverse, hipStream_t stream);
+int64_t autovc_lstm_bwd_workspace_floats(int B, int H, int splits);
+int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                        const float* gates, const float* c_all, const float* W_hh_T, float* dG,
+                        int reverse, int splits, float* workspace, hipStream_t stream);
+int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
+                         const float* W_hh_b, float* h, float* c_all, float* gates,
+                         hipStream_t stream);
+int autovc_blstm_bwd_f32(int B, int T, int H, int ndir, const float* dh_out, const float* gates,
+                         const float* c_all, const float* W_hh_f, const float* W_hh_b, float* dG,
+                         hipStream_t stream);
+
+/* ---------------------------------------------------------------- bottleneck / glue
+ * frame_concat: out[b,t] = [X[b, t/rep] (C1), E[b] (C2)]  — encoder input
+ *   (model_vc_mel.py:64-66, rep=1) and decoder input (code up-sample ++ c_trg, :186-192,
+ *   rep=freq).  code_gather: codes[b,k] = [h_fwd[b,k*freq+freq-1], h_bwd[b,k*freq]]
+ *   (model_vc_mel.py:74-79; exact copies; bwd = exact inverse scatter).
+ */
+int autovc_frame_concat_f32(int B, int T, int C1, int C2, int rep, const float* X, int64_t ldx,
+                            const float* E, float* out, hipStream_t stream);
+int autovc_frame_concat_bwd_f32(int B, int T, int C1, int C2, int rep, const float* dout,
+                                float* dX, int64_t ldx, float* dE, int accumulate,
+                                hipStream_t stream);
+int autovc_code_gather_f32(int B, int T, int D, int freq, const float* h, float* codes,
+                           hipStream_t stream);
+int autovc_code_gather_bwd_f32(int B, int T, int D, int freq, const float* dcodes, float* dh,
+                               hipStream_t stream);
+
+/* ---------------------------------------------------------------- losses / optimiser
+ * loss kind 0 = F.mse_loss, 1 = F.l1_loss (mean), solver_encoder.py:230,233,236; the
+ * scalar stays on the device.  adam: torch.optim.Adam step (solver_encoder.py:130,300)
+ * over one flat fp32 buffer of every parameter.
+ */
+int64_t autovc_loss_workspace_bytes(void);
+int autovc_loss_f32(int kind, int64_t n, const float* a, const float* b, float* out,
+                    void* workspace, hipStream_t stream);
+int autovc_loss_bwd_f32(int kind, int64_t n, const float* a, const float* b, const float* gout,
+                        float* ga, float* gb, int acc_a, int acc_b, hipStream_t stream);
+int autovc_adam_f32(int64_t n, float* p, const float* g, float* m, float* v, float lr,
+                    float beta1, float beta2, float eps, float weight_decay,
+                    float bias_correction1, float bias_correction2_sqrt, hipStream_t stream);
+
+/* ---------------------------------------------------------------- layout helpers */
+int autovc_conv_pack_f32(int Co, int Ci, int K, const float* W, float* Wf, float* Wd,
+                         hipStream_t stream);
+int autovc_conv_unpack_grad_f32(int Co, int Ci, int K, const float* dWf, float* dW,
+                                int accumulate, hipStream_t stream);
+int autovc_transpose_f32(int R, int C, const float* in, float* out, hipStream_t stream);
+int64_t autovc_colsum_workspace_floats(int N);
+int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, float* out2,
+                      int accumulate, float* workspace, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AUTOVC_HIP_H_ */

@@ -1,0 +1,275 @@
+"""GPU parity of the Generator path (libautovc_hip.so kernels) against the oracle and the
+reference goldens.  Tolerances as tests/test_oracle_generator.py."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import generator as og
+
+pytestmark = pytest.mark.gpu
+G = np.load(os.path.join(GOLDEN, "generator_golden.npz"))
+FWD_TOL = 1e-4
+
+
+def rel(a, b):
+    a = a.detach().cpu().double().numpy() if torch.is_tensor(a) else np.asarray(a, np.float64)
+    b = b.detach().cpu().double().numpy() if torch.is_tensor(b) else np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+def build(dev, prefix=""):
+    from autovc_amd.model_vc_mel import Generator
+    g = Generator(32, 256, 512, 32)
+    g.load_state_dict(og.make_weights())
+    return g.to(dev)
+
+
+# ------------------------------------------------------------------ GEMM unit tests
+@pytest.mark.parametrize("M,N,K,at,bt", [(256, 128, 64, 0, 0), (300, 200, 36, 0, 1), (100, 260, 520, 1, 0),
+                                         (64, 80, 1024, 1, 1), (8192, 512, 2560, 0, 0)])
+def test_gemm_layouts(cuda, M, N, K, at, bt):
+    from autovc_amd import functional as AF
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    Ad = (A.t() if at else A).contiguous().to(cuda)
+    Bd = (B if bt else B.t()).contiguous().to(cuda)
+    C = torch.empty(M, N, device=cuda)
+    AF.gemm(M, N, K, Ad, M if at else K, at, Bd, N if bt else K, bt, C, N, bias1=bias.to(cuda))
+    ref = A.double() @ B.double() + bias.double()
+    assert rel(C, ref) < 1e-5
+
+
+def test_gemm_splitk_accumulate(cuda):
+    from autovc_amd import functional as AF
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(4096, 96, generator=g)   # stored [K][M] (a_trans)
+    B = torch.randn(4096, 160, generator=g)  # stored [K][N] (b_trans)
+    C0 = torch.randn(96, 160, generator=g)
+    C = C0.clone().to(cuda)
+    AF.gemm(96, 160, 4096, A.to(cuda), 96, 1, B.to(cuda), 160, 1, C, 160, accumulate=True, splits=8)
+    assert rel(C, C0.double() + A.double().t() @ B.double()) < 1e-5
+
+
+def test_conv_implicit_im2col_fwd_bwd(cuda):
+    from autovc_amd import functional as AF
+    torch.manual_seed(0)
+    B, T, Ci, Co = 3, 40, 36, 52
+    x = torch.randn(B, T, Ci, requires_grad=True)
+    W = torch.randn(Co, Ci, 5, requires_grad=True)
+    b = torch.randn(Co, requires_grad=True)
+    y = torch.nn.functional.conv1d(x.transpose(1, 2), W, b, padding=2).transpose(1, 2)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xd, Wd, bd = (t.detach().to(cuda).requires_grad_() for t in (x, W, b))
+    yd = AF.conv_only(xd, Wd, bd)
+    yd.backward(gy.to(cuda))
+    assert rel(yd, y) < 1e-5
+    assert rel(xd.grad, x.grad) < 1e-5 and rel(Wd.grad, W.grad) < 1e-5 and rel(bd.grad, b.grad) < 1e-5
+
+
+def test_conv_padded_channels_513(cuda):
+    """Channel counts % 4 != 0 (the 513/769-bin STFT generator) go through zero padding."""
+    from autovc_amd import functional as AF
+    torch.manual_seed(1)
+    x = torch.randn(2, 32, 513, requires_grad=True)
+    W = torch.randn(7, 513, 5, requires_grad=True)
+    b = torch.randn(7, requires_grad=True)
+    y = torch.nn.functional.conv1d(x.transpose(1, 2), W, b, padding=2).transpose(1, 2)
+    y.sum().backward()
+    xd, Wd, bd = (t.detach().to(cuda).requires_grad_() for t in (x, W, b))
+    yd = AF.conv_only(xd, Wd, bd)
+    yd.sum().backward()
+    assert rel(yd, y) < 1e-5 and rel(xd.grad, x.grad) < 1e-5 and rel(Wd.grad, W.grad) < 1e-5
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh", "none"])
+def test_conv_bn_act_train_fwd_bwd(cuda, act):
+    from autovc_amd import functional as AF
+    torch.manual_seed(2)
+    conv = torch.nn.Conv1d(64, 96, 5, padding=2)
+    bn = torch.nn.BatchNorm1d(96)
+    x = torch.randn(4, 64, 48).transpose(1, 2).contiguous().requires_grad_()
+    f = {"relu": torch.relu, "tanh": torch.tanh, "none": lambda v: v}[act]
+    z = f(bn(conv(x.transpose(1, 2)))).transpose(1, 2)
+    gz = torch.randn_like(z)
+    z.backward(gz)
+    conv_d, bn_d = torch.nn.Conv1d(64, 96, 5, padding=2).to(cuda), torch.nn.BatchNorm1d(96).to(cuda)
+    conv_d.load_state_dict(conv.state_dict())
+    with torch.no_grad():
+        bn_d.running_mean.zero_()
+        bn_d.running_var.fill_(1)
+        bn_d.num_batches_tracked.zero_()
+    xd = x.detach().to(cuda).requires_grad_()
+    zd = AF.conv_bn_act(xd, conv_d, bn_d, act)
+    zd.backward(gz.to(cuda))
+    assert rel(zd, z) < FWD_TOL
+    assert rel(xd.grad, x.grad) < 1e-4
+    assert rel(conv_d.weight.grad, conv.weight.grad) < 1e-4
+    assert rel(bn_d.weight.grad, bn.weight.grad) < 1e-4 and rel(bn_d.bias.grad, bn.bias.grad) < 1e-4
+    assert rel(bn_d.running_mean, bn.running_mean) < 1e-5 and rel(bn_d.running_var, bn.running_var) < 1e-5
+    assert int(bn_d.num_batches_tracked) == 1
+
+
+# ------------------------------------------------------------------ LSTM unit tests
+@pytest.mark.parametrize("B,T,I,H", [(64, 16, 512, 1024), (3, 9, 320, 512), (17, 5, 64, 64)])
+def test_lstm_layer_fwd_bwd(cuda, B, T, I, H):
+    from autovc_amd import functional as AF
+    torch.manual_seed(3)
+    s = 1 / H ** 0.5
+    x = torch.randn(B, T, I, requires_grad=True)
+    ps = [(torch.rand(*sh) * 2 - 1).mul_(s).requires_grad_() for sh in ((4 * H, I), (4 * H, H), (4 * H,), (4 * H,))]
+    h = og.OracleGenerator._lstm_dir(x, *ps, reverse=False)
+    gh = torch.randn_like(h)
+    h.backward(gh)
+    xd = x.detach().to(cuda).requires_grad_()
+    pd = [p.detach().to(cuda).requires_grad_() for p in ps]
+    hd = AF.LSTMLayerFn.apply(xd, *pd, True)
+    hd.backward(gh.to(cuda))
+    assert rel(hd, h) < FWD_TOL
+    assert rel(xd.grad, x.grad) < 1e-4
+    for a, b in zip(pd, ps):
+        assert rel(a.grad, b.grad) < 1e-4
+
+
+@pytest.mark.parametrize("B,T,I", [(64, 128, 512), (5, 7, 64)])
+def test_blstm_layer_fwd_bwd(cuda, B, T, I):
+    from autovc_amd import functional as AF
+    torch.manual_seed(4)
+    H = 32
+    s = 1 / H ** 0.5
+    x = torch.randn(B, T, I, requires_grad=True)
+    shapes = ((4 * H, I), (4 * H, H), (4 * H,), (4 * H,))
+    pf = [(torch.rand(*sh) * 2 - 1).mul_(s).requires_grad_() for sh in shapes]
+    pb = [(torch.rand(*sh) * 2 - 1).mul_(s).requires_grad_() for sh in shapes]
+    h = torch.cat([og.OracleGenerator._lstm_dir(x, *pf, reverse=False),
+                   og.OracleGenerator._lstm_dir(x, *pb, reverse=True)], -1)
+    gh = torch.randn_like(h)
+    h.backward(gh)
+    xd = x.detach().to(cuda).requires_grad_()
+    pfd = [p.detach().to(cuda).requires_grad_() for p in pf]
+    pbd = [p.detach().to(cuda).requires_grad_() for p in pb]
+    hd = AF.BLSTMLayerFn.apply(xd, *pfd, *pbd, True)
+    hd.backward(gh.to(cuda))
+    assert rel(hd, h) < FWD_TOL
+    assert rel(xd.grad, x.grad) < 1e-4
+    for a, b in zip(pfd + pbd, pf + pb):
+        assert rel(a.grad, b.grad) < 1e-4
+
+
+def test_code_gather_bit_exact(cuda):
+    from autovc_amd import functional as AF
+    h = torch.randn(5, 128, 64)
+    codes = AF.CodeGatherFn.apply(h.to(cuda), 32).cpu()
+    ref = torch.cat([torch.cat((h[:, i + 31, :32], h[:, i, 32:]), -1) for i in range(0, 128, 32)], -1)
+    assert torch.equal(codes, ref)
+    hd = h.to(cuda).requires_grad_()
+    g = torch.randn(5, 256)
+    AF.CodeGatherFn.apply(hd, 32).backward(g.to(cuda))
+    hr = h.clone().requires_grad_()
+    torch.cat([torch.cat((hr[:, i + 31, :32], hr[:, i, 32:]), -1) for i in range(0, 128, 32)], -1).backward(g)
+    assert torch.equal(hd.grad.cpu(), hr.grad)
+
+
+def test_frame_concat_upsample_bit_exact(cuda):
+    from autovc_amd import functional as AF
+    codes = torch.randn(3, 4, 64)
+    e = torch.randn(3, 256)
+    out = AF.FrameConcatFn.apply(codes.to(cuda), e.to(cuda), 128, 32).cpu()
+    ref = torch.cat((codes.repeat_interleave(32, 1), e.unsqueeze(1).expand(-1, 128, -1)), -1)
+    assert torch.equal(out, ref)
+
+
+# ------------------------------------------------------------------ Generator
+def test_generator_train_forward_vs_reference_golden(cuda):
+    g = build(cuda)
+    g.train()
+    x = torch.from_numpy(G["x"]).to(cuda)
+    e = torch.from_numpy(G["emb"]).to(cuda)
+    with torch.no_grad():
+        x_id, x_psnt, code = g(x, e, e)
+        code_rec = g(x_psnt, e, None)
+    assert x_id.shape == (2, 1, 128, 80) and x_psnt.shape == (2, 1, 128, 80) and code.shape == (2, 256)
+    assert rel(x_id, G["train_x_identic"]) < FWD_TOL
+    assert rel(x_psnt, G["train_x_psnt"]) < FWD_TOL
+    assert rel(code, G["train_code_real"]) < FWD_TOL
+    assert rel(code_rec, G["train_code_reconst"]) < FWD_TOL
+
+
+def test_generator_eval_and_t160(cuda):
+    g = build(cuda)
+    g.eval()
+    e = torch.from_numpy(G["emb"]).to(cuda)
+    with torch.no_grad():
+        _, x_psnt, code = g(torch.from_numpy(G["x"]).to(cuda), e, e)
+    assert rel(x_psnt, G["eval_x_psnt"]) < FWD_TOL and rel(code, G["eval_code_real"]) < FWD_TOL
+    g2 = build(cuda)
+    with torch.no_grad():
+        _, x_psnt, code = g2(torch.from_numpy(G["x160"]).to(cuda), e, e)
+    assert code.shape == (2, 320)
+    assert rel(x_psnt, G["t160_x_psnt"]) < FWD_TOL and rel(code, G["t160_code_real"]) < FWD_TOL
+
+
+def test_generator_t_not_multiple_of_freq_raises(cuda):
+    g = build(cuda)
+    with pytest.raises(IndexError):
+        g(torch.rand(1, 130, 80, device=cuda), torch.rand(1, 256, device=cuda), None)
+
+
+def test_one_training_step_grads_vs_reference_golden(cuda):
+    from autovc_amd import functional as AF
+    g = build(cuda)
+    g.train()
+    x = torch.from_numpy(G["x"]).to(cuda)
+    e = torch.from_numpy(G["emb"]).to(cuda)
+    x_id, x_psnt, code = g(x, e, e)
+    l_id = AF.mse_loss(x.squeeze(), x_id.squeeze())
+    l_psnt = AF.mse_loss(x, x_psnt.squeeze())
+    l_cd = AF.l1_loss(code, g(x_psnt, e, None))
+    (l_id + l_psnt + l_cd).backward()
+    assert rel(torch.stack([l_id, l_psnt, l_cd]), G["train_losses"]) < FWD_TOL
+    params = dict(g.named_parameters())
+    for i, n in enumerate(G["param_names"]):
+        gn = params[n].grad.norm().item()
+        if n.endswith("0.conv.bias"):
+            assert abs(gn - G["grad_norm"][i]) < 1e-6, n
+        else:
+            assert abs(gn - G["grad_norm"][i]) <= 1e-2 * G["grad_norm"][i], (n, gn, G["grad_norm"][i])
+    bufs = dict(g.named_buffers())
+    got = np.concatenate([bufs[k].float().flatten().cpu().numpy() for k in G["step1_buffer_names"]])
+    assert rel(got, G["step1_buffers"]) < FWD_TOL  # encoder BN updated twice, decoder/postnet once
+
+
+def test_full_size_step_vs_oracle(cuda):
+    """B=64, T=128 (BASELINE config 2 shape): forward outputs and gradients vs the CPU oracle."""
+    from autovc_amd import functional as AF
+    gen = torch.Generator().manual_seed(1234)
+    x = torch.clamp(torch.randn(64, 128, 80, generator=gen) * 0.18 + 0.43, 0, 1)
+    e = torch.randn(64, 256, generator=gen)
+    e = e / e.norm(dim=1, keepdim=True) * 0.8
+    P = og.make_weights()
+    params = {k: v for k, v in P.items() if v.dtype == torch.float32 and "running_" not in k}
+    for v in params.values():
+        v.requires_grad_(True)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))  # GPU boxes show many host CPUs
+    g_loss, a, b, c = og.solver_losses(og.OracleGenerator(P), x, e)
+    g_loss.backward()
+    gd = build(cuda)
+    xd, ed = x.to(cuda), e.to(cuda)
+    x_id, x_psnt, code = gd(xd, ed, ed)
+    la = AF.mse_loss(xd, x_id.squeeze())
+    lb = AF.mse_loss(xd, x_psnt.squeeze())
+    lc = AF.l1_loss(code, gd(x_psnt, ed, None))
+    (la + lb + lc).backward()
+    assert rel(torch.stack([la, lb, lc]), torch.stack([a, b, c])) < FWD_TOL
+    for n, p in gd.named_parameters():
+        ref = params[n].grad
+        if n.endswith("0.conv.bias"):
+            assert p.grad.norm().item() < 1e-4 + ref.norm().item() * 10, n
+            continue
+        err = (p.grad.cpu().double() - ref.double()).norm() / ref.double().norm()
+        assert err < 1e-2, (n, float(err))

@@ -1,0 +1,136 @@
+"""Oracle pinning for the Generator: oracle/generator.py (CPU restatement) against the
+golden arrays produced by the reference's own model_vc_mel.Generator / model_vc_stft /
+solver_encoder.Solver.train (tests/golden/make_generator_golden.py).
+
+Tolerances: forward <= 1e-4 rel (max-abs / max); one-step gradient norms
+<= 1e-2 rel per tensor (the reference's own fp32 noise is ~1e-3, F8) except pre-BN conv
+biases whose true gradient is 0 (compared absolutely); Adam step 1 moves each parameter
+by ~lr*sign(grad), so parameters are compared at 2.01e-4 abs with near-all elements
+exact to 1e-6; loss trajectory: step 1 <= 1e-4 rel, steps 2-10 see check_trajectory."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import generator as og
+
+G = np.load(os.path.join(GOLDEN, "generator_golden.npz"))
+FWD_TOL = 1e-4
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+def test_key_order_matches_reference_state_dict():
+    assert [k for k, _ in og.generator_keys()] == list(G["keys"])
+    assert [k for k, _ in og.generator_keys(n_in=513, n_out=513, prefix="model.")] == list(G["stft_keys"])
+
+
+def test_deterministic_weights_are_reproducible():
+    a, b = og.make_weights(), og.make_weights()
+    assert all(torch.equal(a[k], b[k]) for k in a)
+
+
+def _inputs():
+    return torch.from_numpy(G["x"]), torch.from_numpy(G["emb"])
+
+
+def test_train_forward_and_losses():
+    P = og.make_weights()
+    x, e = _inputs()
+    gen = og.OracleGenerator(P, training=True)
+    with torch.no_grad():
+        _, l_id, l_psnt, l_cd = og.solver_losses(gen, x, e)
+    P2 = og.make_weights()
+    gen2 = og.OracleGenerator(P2, training=True)
+    with torch.no_grad():
+        x_id, x_psnt, code = gen2.forward(x, e, e)
+        code_rec = gen2.forward(x_psnt, e, None)
+    assert rel(x_id, G["train_x_identic"]) < FWD_TOL
+    assert rel(x_psnt, G["train_x_psnt"]) < FWD_TOL
+    assert rel(code, G["train_code_real"]) < FWD_TOL
+    assert rel(code_rec, G["train_code_reconst"]) < FWD_TOL
+    assert rel([l_id.item(), l_psnt.item(), l_cd.item()], G["train_losses"]) < FWD_TOL
+
+
+def test_one_step_grads_adam_and_running_stats():
+    P = og.make_weights()
+    x, e = _inputs()
+    hist, grads = og.train_steps(P, [(x, e)], n_steps=1)
+    names = list(G["param_names"])
+    for i, n in enumerate(names):
+        g = grads[n]
+        if n.endswith("0.conv.bias") and ("encoder" in n or "decoder" in n or "postnet" in n):
+            # pre-BN conv bias: true gradient is exactly 0; compare absolutely
+            assert abs(g.norm().item() - G["grad_norm"][i]) < 1e-6, n
+            continue
+        assert abs(g.norm().item() - G["grad_norm"][i]) <= 1e-2 * G["grad_norm"][i] + 1e-9, n
+    diffs = []
+    for i, n in enumerate(names):
+        v = P[n].flatten()[:64].numpy()
+        d = np.abs(v - G["step1_param_slice"][i][:len(v)])
+        assert d.max() < 2.01e-4, n
+        if not n.endswith("0.conv.bias"):
+            diffs.append(d)
+    assert np.mean(np.concatenate(diffs) > 1e-6) < 0.02
+    bufs = np.concatenate([P[k].float().flatten().numpy() for k in G["step1_buffer_names"]])
+    assert rel(bufs, G["step1_buffers"]) < FWD_TOL
+
+
+def test_eval_forward():
+    P = og.make_weights()
+    x, e = _inputs()
+    with torch.no_grad():
+        x_id, x_psnt, code = og.OracleGenerator(P, training=False).forward(x, e, e)
+    assert rel(x_psnt, G["eval_x_psnt"]) < FWD_TOL and rel(code, G["eval_code_real"]) < FWD_TOL
+
+
+def test_t160_code_width():
+    P = og.make_weights()
+    _, e = _inputs()
+    with torch.no_grad():
+        _, x_psnt, code = og.OracleGenerator(P).forward(torch.from_numpy(G["x160"]), e, e)
+    assert code.shape == (2, 320)
+    assert rel(x_psnt, G["t160_x_psnt"]) < FWD_TOL and rel(code, G["t160_code_real"]) < FWD_TOL
+
+
+def test_solver_trajectory_matches_reference_solver_train():
+    P = og.make_weights()
+    x, e = _inputs()
+    hist, _ = og.train_steps(P, [(x, e)], n_steps=10)
+    traj = np.array(hist)
+    assert rel(traj[0], G["solver_traj"][0]) < 1e-4
+    check_trajectory(traj, G["solver_traj"])
+
+
+def check_trajectory(traj, ref):
+    """Steps 2-10: reconstruction losses within 5 %, the content-code L1 loss within 15 %.
+    L_cd is an L1 of two nearly equal code sets; its sign-driven Adam updates amplify
+    rounding: an fp64 restatement of the same 10 steps differs from the reference's fp32
+    run by 7 % on L_cd at steps 5-10 (and < 0.3 % on the other two)."""
+    traj, ref = np.asarray(traj), np.asarray(ref)
+    assert np.all(np.abs(traj[:, :2] - ref[:, :2]) <= 0.05 * np.abs(ref[:, :2])), (traj, ref)
+    assert np.all(np.abs(traj[:, 2] - ref[:, 2]) <= 0.15 * np.abs(ref[:, 2])), (traj, ref)
+
+
+def test_stft_variant_513_bins():
+    P = og.make_weights(prefix="model.", n_in=513, n_out=513)
+    _, e = _inputs()
+    xs = torch.from_numpy(G["stft_x"])
+    gen = og.OracleGenerator(P, prefix="model.", training=True)
+    with torch.no_grad():
+        x_id, x_psnt, code = gen.forward(xs, e, e)
+    assert rel(x_psnt, G["stft_x_psnt"]) < FWD_TOL and rel(code, G["stft_code_real"]) < FWD_TOL
+    assert bool(G["stft_forward_raises"])  # the reference GeneratorSTFT.forward is broken (F10)
+
+
+def test_t_not_multiple_of_freq_raises():
+    P = og.make_weights()
+    x = torch.rand(1, 130, 80)
+    with pytest.raises(IndexError):
+        og.OracleGenerator(P).forward(x, torch.rand(1, 256), None)
