@@ -16,6 +16,8 @@
 //    dh_rec = dG_t W_hh through the pre-transposed W_hh^T.
 //  * small H (encoder BLSTM, H=32): the whole sequence in one launch, one workgroup per
 //    (direction, 8 batch rows), W_hh in LDS, one barrier per step (two in backward).
+#include <hip/hip_ext.h>
+
 #include "common.h"
 #include "../../include/autovc_hip.h"
 
@@ -334,5 +336,39 @@ extern "C" int autovc_blstm_bwd_f32(int B, int T, int H, int ndir, const float* 
   hipLaunchKernelGGL(blstm_bwd_kernel, dim3((B + SB - 1) / SB, ndir), dim3(kThreads), 0, stream, B, T, dh_out,
                      gates, c_all, W_hh_f, W_hh_b, dG, ndir);
   AVC_CHECK_LAUNCH("autovc_blstm_bwd_f32");
+  return avc::kOk;
+}
+
+// ------------------------------------------------------------------ measurement
+// Same launches as autovc_lstm_fwd_f32, each bracketed by hipExtLaunchKernelGGL's own
+// start/stop events (timestamps taken by the dispatch itself, so the inter-kernel gap is
+// excluded); synchronises and writes the mean per-launch kernel time in microseconds to
+// *avg_us (host).  Used by bench.py for the roofline of the recurrent kernel.
+extern "C" int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                                         const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                                         float* gates, hipStream_t stream, float* avg_us) {
+  AVC_CHECK_ARG(B > 0 && T > 1 && H > 0 && H % 16 == 0 && avg_us, "autovc_lstm_fwd_timed_f32: bad args");
+  AVC_CHECK_ARG(gx && W_hh && h && c_all, "autovc_lstm_fwd_timed_f32: null pointer");
+  StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, W_hh, h, h_ldb, h_ldt, c_all, gates};
+  hipEvent_t* ev = new hipEvent_t[2 * T];
+  for (int i = 0; i < 2 * T; ++i) AVC_HIP(hipEventCreate(&ev[i]), "autovc_lstm_fwd_timed_f32/event");
+  for (int s = 0; s < T; ++s) {
+    const int tp = s == 0 ? -1 : s - 1;
+    hipExtLaunchKernelGGL(lstm_fwd_step_kernel, dim3(H / U), dim3(kThreads), 0, stream, ev[2 * s], ev[2 * s + 1], 0,
+                          a, s, tp);
+  }
+  AVC_CHECK_LAUNCH("autovc_lstm_fwd_timed_f32");
+  AVC_HIP(hipStreamSynchronize(stream), "autovc_lstm_fwd_timed_f32/sync");
+  double tot = 0.0;
+  int n = 0;
+  for (int s = 1; s < T; ++s) {  // step 0 has no recurrent product: excluded from the mean
+    float ms = 0.f;
+    AVC_HIP(hipEventElapsedTime(&ms, ev[2 * s], ev[2 * s + 1]), "autovc_lstm_fwd_timed_f32/elapsed");
+    tot += ms;
+    ++n;
+  }
+  for (int i = 0; i < 2 * T; ++i) (void)hipEventDestroy(ev[i]);
+  delete[] ev;
+  *avg_us = (float)(tot / n * 1000.0);
   return avc::kOk;
 }

@@ -277,20 +277,24 @@ class LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
-        dy = dy.contiguous()
         K = x.shape[-1]
         N = W.shape[0]
         M = x.numel() // K
+        Np = _ceil4(N)  # 513-bin projection: pad the output axis for the float4 GEMM operands
+        dy = _pad_last(dy.reshape(M, N), Np)
+        Wp = W.contiguous() if Np == N else torch.cat([W, W.new_zeros(Np - N, K)], 0)
         dx = dW = db = None
         if ctx.needs_input_grad[1]:
-            dW = torch.empty_like(W)
-            gemm(N, K, M, dy, N, 1, x, K, 1, dW, K, splits=_splits_for(N, K, M))
+            dW = torch.empty((Np, K), device=W.device, dtype=torch.float32)
+            gemm(Np, K, M, dy, Np, 1, x, K, 1, dW, K, splits=_splits_for(Np, K, M))
+            dW = dW if Np == N else dW[:N].contiguous()
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = torch.empty(N, device=dy.device, dtype=torch.float32)
-            colsum(dy.view(M, N), db)
+            db = torch.empty(Np, device=dy.device, dtype=torch.float32)
+            colsum(dy, db)
+            db = db if Np == N else db[:N].contiguous()
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            gemm(M, K, N, dy, N, 0, W, K, 1, dx, K)
+            gemm(M, K, Np, dy, Np, 0, Wp, K, 1, dx, K)
         return dx, dW, db
 
 

@@ -105,6 +105,12 @@ int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t lddz, const
 int autovc_lstm_fwd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                         const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                         float* gates, int reverse, hipStream_t stream);
+/* autovc_lstm_fwd_f32 with every step launch timed by its own dispatch events;
+ * synchronises; *avg_us (HOST pointer) = mean kernel time of steps 1..T-1 (bench.py). */
+int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_ldb,
+                              int64_t gx_ldt, const float* W_hh, float* h, int64_t h_ldb,
+                              int64_t h_ldt, float* c_all, float* gates, hipStream_t stream,
+                              float* avg_us);
 int64_t autovc_lstm_bwd_workspace_floats(int B, int H, int splits);
 int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
                         const float* gates, const float* c_all, const float* W_hh_T, float* dG,

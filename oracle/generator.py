@@ -95,8 +95,12 @@ class OracleGenerator:
     """Functional Generator over a parameter map P (key -> tensor).  Tensors that need
     gradients are leaves the caller created with requires_grad."""
 
-    def __init__(self, P: dict, dim_neck=32, freq=32, prefix="", training=True):
+    def __init__(self, P: dict, dim_neck=32, freq=32, prefix="", training=True, fused_lstm=False):
+        """fused_lstm=True runs the LSTMs through torch's own fused CPU kernel (the op the
+        reference's nn.LSTM calls) instead of the explicit per-step restatement: same
+        semantics, reference-speed — used for the CPU-baseline timing."""
         self.P, self.dim_neck, self.freq, self.pre, self.training = P, dim_neck, freq, prefix, training
+        self.fused_lstm = fused_lstm
 
     def _g(self, k):
         return self.P[self.pre + k]
@@ -136,6 +140,14 @@ class OracleGenerator:
         return torch.stack(outs, dim=1)
 
     def _lstm(self, x, p, layers, bidir):
+        if self.fused_lstm:
+            ws = []
+            for l in range(layers):
+                for sfx in [""] + (["_reverse"] if bidir else []):
+                    ws += [self._g(f"{p}.{n}_l{l}{sfx}") for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+            H = ws[1].shape[1]
+            h0 = x.new_zeros(layers * (2 if bidir else 1), x.shape[0], H)
+            return torch._VF.lstm(x, (h0, h0), ws, True, layers, 0.0, self.training, bidir, True)[0]
         for l in range(layers):
             a = [self._g(f"{p}.{n}_l{l}") for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
             fw = self._lstm_dir(x, *a, reverse=False)

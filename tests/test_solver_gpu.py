@@ -1,0 +1,71 @@
+"""GPU Solver step (FusedAdam, device losses) vs the reference Solver.train goldens."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import generator as og
+
+pytestmark = pytest.mark.gpu
+G = np.load(os.path.join(GOLDEN, "generator_golden.npz"))
+
+
+def _solver():
+    import contextlib
+    import sys
+    import types
+    from autovc_amd.solver_encoder import Solver
+    cfg = types.SimpleNamespace(main_dir=".", lambda_cd=1.0, dim_neck=32, dim_emb=256, dim_pre=512, freq=32,
+                                lr=1e-4, batch_size=2, num_iters=10, ema=0.9999, run_name="t", model_type="spmel",
+                                log_step=1000)
+    with contextlib.redirect_stdout(sys.stderr):
+        s = Solver(None, cfg)
+    s.G.load_state_dict(og.make_weights())
+    return s
+
+
+def test_adam_step_matches_reference(cuda):
+    s = _solver()
+    x = torch.from_numpy(G["x"]).to(cuda)
+    e = torch.from_numpy(G["emb"]).to(cuda)
+    s.G.train()
+    s.train_step(x, e)
+    params = dict(s.G.named_parameters())
+    diffs = []
+    for i, n in enumerate(G["param_names"]):
+        v = params[n].detach().flatten()[:64].cpu().numpy()
+        d = np.abs(v - G["step1_param_slice"][i][:len(v)])
+        assert d.max() < 2.01e-4, n
+        if not n.endswith("0.conv.bias"):
+            diffs.append(d)
+    assert np.mean(np.concatenate(diffs) > 1e-6) < 0.02
+
+
+def test_ten_step_trajectory_matches_reference_solver(cuda):
+    from test_oracle_generator import check_trajectory
+    s = _solver()
+    x = torch.from_numpy(G["x"]).to(cuda)
+    e = torch.from_numpy(G["emb"]).to(cuda)
+    s.G.train()
+    traj = []
+    for _ in range(10):
+        _, a, b, c = s.train_step(x, e)
+        traj.append([a.item(), b.item(), c.item()])
+    traj = np.array(traj)
+    assert np.abs(traj[0] - G["solver_traj"][0]).max() / np.abs(G["solver_traj"][0]).max() < 1e-4
+    check_trajectory(traj, G["solver_traj"])
+
+
+def test_optimizer_state_dict_roundtrip(cuda):
+    s = _solver()
+    x = torch.from_numpy(G["x"]).to(cuda)
+    e = torch.from_numpy(G["emb"]).to(cuda)
+    s.train_step(x, e)
+    sd = s.g_optimizer.state_dict()
+    assert len(sd["state"]) == 74 and all(set(v) == {"step", "exp_avg", "exp_avg_sq"} for v in sd["state"].values())
+    s2 = _solver()
+    s2.g_optimizer.load_state_dict(sd)
+    for f1, f2 in zip(s.g_optimizer._flat, s2.g_optimizer._flat):
+        assert torch.equal(f1["m"], f2["m"]) and torch.equal(f1["v"], f2["v"]) and f1["step"] == f2["step"]
