@@ -17,7 +17,7 @@
 
 namespace {
 
-constexpr int kRowSplits = 64;
+constexpr int kRowSplits = 128;
 
 enum Act { kNone = 0, kRelu = 1, kTanh = 2 };
 
@@ -58,18 +58,36 @@ __global__ __launch_bounds__(256) void stats_partial_kernel(int64_t M, int C, co
   }
 }
 
-__global__ void stats_finalize_kernel(int64_t M, int C, const float* __restrict__ y, const double* __restrict__ part,
-                                      int RS, float* __restrict__ mean, float* __restrict__ var,
-                                      float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
-                                      int64_t* __restrict__ nbt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) *nbt += 1;
+// sum of partials [RS][C][2] for this block's 64 columns: 4 waves x RS/4 partials each
+__device__ __forceinline__ void sum_partials(const double* __restrict__ part, int RS, int C, int c, double& a,
+                                             double& b) {
+  __shared__ double red[4][64][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (int rs = w; rs < RS; rs += 4) {
+      s1 += part[((int64_t)rs * C + c) * 2 + 0];
+      s2 += part[((int64_t)rs * C + c) * 2 + 1];
+    }
+  red[w][lane][0] = s1;
+  red[w][lane][1] = s2;
+  __syncthreads();
+  a = red[0][lane][0] + red[1][lane][0] + red[2][lane][0] + red[3][lane][0];
+  b = red[0][lane][1] + red[1][lane][1] + red[2][lane][1] + red[3][lane][1];
+}
+
+// grid = ceil(C/64), block 256
+__global__ __launch_bounds__(256) void stats_finalize_kernel(int64_t M, int C, const float* __restrict__ y,
+                                                            const double* __restrict__ part, int RS,
+                                                            float* __restrict__ mean, float* __restrict__ var,
+                                                            float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                            float momentum, int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double a, b;
+  sum_partials(part, RS, C, c, a, b);
+  if (threadIdx.x >= 64) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int rs = 0; rs < RS; ++rs) {
-    a += part[((int64_t)rs * C + c) * 2 + 0];
-    b += part[((int64_t)rs * C + c) * 2 + 1];
-  }
   const double n = (double)M;
   const double mu_s = a / n;
   double v = b / n - mu_s * mu_s;
@@ -131,16 +149,14 @@ __global__ __launch_bounds__(256) void bwd_partial_kernel(int64_t M, int C, cons
 }
 
 // sums -> dbeta = sum dy_act, dgamma = sum dy_act * xhat ; keeps the raw sums for apply
-__global__ void bwd_finalize_kernel(int C, const double* __restrict__ part, int RS, const float* __restrict__ var,
-                                    float eps, float* __restrict__ sums, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int rs = 0; rs < RS; ++rs) {
-    a += part[((int64_t)rs * C + c) * 2 + 0];
-    b += part[((int64_t)rs * C + c) * 2 + 1];
-  }
+__global__ __launch_bounds__(256) void bwd_finalize_kernel(int C, const double* __restrict__ part, int RS,
+                                                          const float* __restrict__ var, float eps,
+                                                          float* __restrict__ sums, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double a, b;
+  sum_partials(part, RS, C, c, a, b);
+  if (threadIdx.x >= 64 || c >= C) return;
   const float invstd = 1.0f / sqrtf(var[c] + eps);
   const float sdy = (float)a, sdyx = (float)(b * (double)invstd);
   sums[2 * c] = sdy;
@@ -184,7 +200,7 @@ extern "C" int autovc_bn_stats_f32(int64_t M, int C, const float* y, int64_t ldy
   double* part = reinterpret_cast<double*>(workspace);
   const int RS = (int)std::min<int64_t>(kRowSplits, M);
   hipLaunchKernelGGL(stats_partial_kernel, dim3((C + 63) / 64, RS), dim3(256), 0, stream, M, C, y, ldy, part);
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, M, C, y,
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, M, C, y,
                      (const double*)part, RS, mean, var, running_mean, running_var, momentum, num_batches);
   AVC_CHECK_LAUNCH("autovc_bn_stats_f32");
   return avc::kOk;
@@ -213,7 +229,7 @@ extern "C" int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t 
   const int RS = (int)std::min<int64_t>(kRowSplits, M);
   hipLaunchKernelGGL(bwd_partial_kernel, dim3((C + 63) / 64, RS), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y,
                      ldy, mean, act, part);
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, (const double*)part, RS,
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, C, (const double*)part, RS,
                      var, eps, sums, dgamma, dbeta, accumulate);
   hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(M * C)), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y, ldy,
                      mean, var, gamma, eps, act, (const float*)sums, dy, lddy);

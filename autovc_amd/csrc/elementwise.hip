@@ -219,7 +219,7 @@ __global__ void transpose_kernel(int R, int C, const float* __restrict__ in, flo
 }
 
 // column sums: out[c] (+)= sum_r X[r*ld + c]  (two-stage, deterministic)
-constexpr int kColSplits = 64;
+constexpr int kColSplits = 128;
 
 __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t M, int N, const float* __restrict__ X,
                                                             int64_t ld, float* __restrict__ part) {
@@ -236,12 +236,19 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t M, int N, c
   if (w == 0 && c < N) part[(int64_t)rs * N + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
-__global__ void colsum_finalize_kernel(int N, int RS, const float* __restrict__ part, float* __restrict__ out,
-                                       float* __restrict__ out2, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(int N, int RS, const float* __restrict__ part,
+                                                              float* __restrict__ out, float* __restrict__ out2,
+                                                              int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int rs = 0; rs < RS; ++rs) s += part[(int64_t)rs * N + c];
+  if (c < N)
+    for (int rs = w; rs < RS; rs += 4) s += part[(int64_t)rs * N + c];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || c >= N) return;
+  s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
   out[c] = accumulate ? out[c] + s : s;
   if (out2) out2[c] = accumulate ? out2[c] + s : s;
 }
@@ -364,7 +371,7 @@ extern "C" int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, f
   AVC_CHECK_ARG(M > 0 && N > 0 && X && out && workspace, "autovc_colsum_f32: bad args");
   const int RS = (int)std::min<int64_t>(kColSplits, M);
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 63) / 64, RS), dim3(256), 0, stream, M, N, X, ld, workspace);
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, N, RS,
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, N, RS,
                      (const float*)workspace, out, out2, accumulate);
   AVC_CHECK_LAUNCH("autovc_colsum_f32");
   return avc::kOk;

@@ -18,13 +18,14 @@
 //   LSTM      dW_hh = dG^T h_{t-1}   : B = h shifted one frame (CK, C = H, tap0 = -1)
 // (Conv1d semantics: model_vc_mel.py:20-38,49-59,92-102,132-161.)
 //
-// Tiling: 128x128 block tile, BK = 16, 256 threads = 4 waves in 2x2, each wave 64x64 =
-// 2x2 MFMA 32x32 tiles (64 accumulators / lane).  LDS holds [row][BK+4] images of both
-// operands (row stride 80 B: conflict-free ds_read_b128 fragment reads); within a BK
-// stage lane half h takes k = 8h..8h+7 for its 8 MFMAs (the k order inside a stage is
-// a permutation applied to A and B alike, so the sum is unchanged).  Register-staged
-// double buffer, one barrier per stage.  Split-K writes fp32 slabs reduced in k order
-// by a second kernel (deterministic; no float atomics).
+// Tiling (templated, picked per shape): block tile BM x BN, k-stage BK, 4 waves each
+// owning (WM/32) x (WN/32) MFMA 32x32 tiles.  RK operands sit in LDS as [row][BK+4]
+// (row stride keeps the ds_read_b128 fragment reads conflict-free), CK operands as
+// [BK][rows+4] (staged by coalesced float4 rows, read with ds_read_b32).  Within a stage
+// lane half h takes k = h*BK/2 + p for MFMA p (the k order inside a stage is a
+// permutation applied to A and B alike, so the sum is unchanged).  Register-staged double
+// buffer, one barrier per stage; XCD-aware tile order.  Split-K writes fp32 slabs
+// reduced in k order by a second kernel (deterministic; no float atomics).
 #include <algorithm>
 
 #include "common.h"
@@ -32,94 +33,147 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 16, LDK = BK + 4;
-constexpr int kThreads = 256;
-
 struct Opnd {
   const float* p;
   int64_t ld;
   int conv_T, conv_C, tap0;  // conv_T == 0: plain matrix
 };
 
-// load 4 consecutive contiguous-index elements of an operand at (r..., k...) -> float4
-// RK: row r, k..k+3 contiguous.   CK: k-row kk, r..r+3 contiguous.
-template <bool RK>
-__device__ __forceinline__ f32x4 load4(const Opnd& o, int64_t r, int64_t k, int64_t R, int64_t K) {
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  const int64_t f = RK ? r : k;        // frame / row index of storage
-  const int64_t q = RK ? k : r;        // contiguous index
-  const bool in = RK ? (r < R && k < K) : (k < K && r < R);
-  if (!in) return v;
-  int64_t off = f * o.ld + q;
-  if (o.conv_T > 0) {
-    const int tap = (int)(q / o.conv_C);
-    const int64_t tt = f % o.conv_T + tap + o.tap0;
-    if (tt < 0 || tt >= o.conv_T) return v;
-    off += (int64_t)o.tap0 * o.ld;
+// One operand tile (ROWS x BK) of a stage: staging map, LDS image and fragment reads.
+//   RK: LDS [ROWS][BK+4], staged as float4 along k, fragments read with ds_read_b128.
+//   CK: LDS [BK][ROWS+4], staged as float4 along rows (coalesced), fragments ds_read_b32.
+// Per staging slot the loader keeps its source pointer and the conv-mask state (frame
+// position in the sequence, tap) and advances them by BK per stage: no 64-bit divisions
+// in the k loop.
+template <bool RK, int ROWS, int BK, int NT>
+struct OpTile {
+  static constexpr int LD = RK ? BK + 4 : ROWS + 4;
+  static constexpr int FLOATS = RK ? ROWS * LD : BK * LD;
+  static constexpr int F4 = ROWS * BK / 4;           // float4 per stage
+  static constexpr int PER = F4 / NT;
+  static_assert(PER * NT == F4, "staging map");
+  f32x4 v[PER];
+  const float* ptr[PER];
+  int kpos[PER];            // current k of the slot (RK: k index; CK: frame index f)
+  int tpos[PER];            // conv: frame position within its sequence (RK: fixed; CK: advancing)
+  int tap[PER];             // conv: RK: k / C (advancing); CK: q / C (fixed)
+  int kmod[PER];            // conv RK: k % C
+  bool rok[PER];            // row index inside the operand
+  __device__ __forceinline__ static void coords(int e, int& r, int& k) {
+    if (RK) { r = e / (BK / 4); k = 4 * (e % (BK / 4)); }
+    else    { k = e / (ROWS / 4); r = 4 * (e % (ROWS / 4)); }
   }
-  return *reinterpret_cast<const f32x4*>(o.p + off);
-}
-
-// Each thread stages 2 float4 per operand tile (128 rows x 16 k = 512 float4).
-template <bool RK>
-struct Stager {
-  f32x4 v[2];
-  __device__ __forceinline__ void load(const Opnd& o, int64_t r0, int64_t k0, int64_t R, int64_t K, int tid) {
+  __device__ __forceinline__ void init(const Opnd& o, int64_t r0, int64_t kbeg, int64_t R) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int i = 0; i < PER; ++i) {
+      int rr, kk;
+      coords(threadIdx.x + i * NT, rr, kk);
+      const int r = (int)(r0 + rr), k = (int)(kbeg + kk);
+      const int shift = o.conv_T > 0 ? o.tap0 : 0;   // tap0 only means something for a conv view
+      rok[i] = r < R;
+      kpos[i] = k;
       if (RK) {
-        const int row = (tid >> 2) + 64 * s, kq = tid & 3;
-        v[s] = load4<true>(o, r0 + row, k0 + 4 * kq, R, K);
+        ptr[i] = o.p + ((int64_t)r + shift) * o.ld + k;
+        if (o.conv_T > 0) { tpos[i] = r % o.conv_T; tap[i] = k / o.conv_C; kmod[i] = k % o.conv_C; }
       } else {
-        const int kr = tid & 15, rq = (tid >> 4) + 16 * s;
-        v[s] = load4<false>(o, r0 + 4 * rq, k0 + kr, R, K);
+        ptr[i] = o.p + ((int64_t)k + shift) * o.ld + r;
+        if (o.conv_T > 0) { tpos[i] = k % o.conv_T; tap[i] = r / o.conv_C; }
       }
     }
   }
-  __device__ __forceinline__ void store(float* lds, int tid) const {
+  __device__ __forceinline__ void load(const Opnd& o, int64_t K) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (RK) {
-        const int row = (tid >> 2) + 64 * s, kq = tid & 3;
-        *reinterpret_cast<f32x4*>(lds + row * LDK + 4 * kq) = v[s];
-      } else {
-        const int kr = tid & 15, rq = (tid >> 4) + 16 * s;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) lds[(4 * rq + j) * LDK + kr] = v[s][j];
+    for (int i = 0; i < PER; ++i) {
+      bool ok = rok[i] && kpos[i] < K;
+      if (o.conv_T > 0) {
+        const int tt = tpos[i] + tap[i] + o.tap0;
+        ok = ok && tt >= 0 && tt < o.conv_T;
       }
+      v[i] = ok ? *reinterpret_cast<const f32x4*>(ptr[i]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      // advance one stage
+      kpos[i] += BK;
+      if (RK) {
+        ptr[i] += BK;
+        if (o.conv_T > 0) {
+          kmod[i] += BK;
+          while (kmod[i] >= o.conv_C) { kmod[i] -= o.conv_C; ++tap[i]; }
+        }
+      } else {
+        ptr[i] += (int64_t)BK * o.ld;
+        if (o.conv_T > 0) {
+          tpos[i] += BK;
+          while (tpos[i] >= o.conv_T) tpos[i] -= o.conv_T;
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* lds) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int r, k;
+      coords(threadIdx.x + i * NT, r, k);
+      *reinterpret_cast<f32x4*>(lds + (RK ? r * LD + k : k * LD + r)) = v[i];
+    }
+  }
+  // fragment values of MFMA p (0..BK/2-1) for tile row `row`, lane half h: k = h*BK/2 + p
+  __device__ __forceinline__ void frag(const float* lds, int row, int h, float (&out)[BK / 2]) const {
+    if (RK) {
+#pragma unroll
+      for (int c = 0; c < BK / 8; ++c) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(lds + row * LD + h * (BK / 2) + 4 * c);
+        out[4 * c] = x[0]; out[4 * c + 1] = x[1]; out[4 * c + 2] = x[2]; out[4 * c + 3] = x[3];
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < BK / 2; ++p) out[p] = lds[(h * (BK / 2) + p) * LD + row];
     }
   }
 };
 
-template <bool A_RK, bool B_RK>
-__global__ __launch_bounds__(kThreads, 2) void gemm_kernel(
+// Block tile BM x BN, k-stage BK, waves of WM x WN (each (WM/32) x (WN/32) MFMA 32x32x2).
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
     int k_per_split, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float smem[2][2][BM * LDK];  // [buf][A/B]
+  constexpr int NWN = BN / WN;
+  constexpr int NT = 64 * (BM / WM) * NWN;
+  constexpr int TI = WM / 32, TJ = WN / 32;
+  using TA = OpTile<A_RK, BM, BK, NT>;
+  using TBt = OpTile<B_RK, BN, BK, NT>;
+  __shared__ __attribute__((aligned(16))) float smem[2][TA::FLOATS + TBt::FLOATS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  const int wr = wave / NWN, wc = wave % NWN;
+  // XCD-aware tile order (speed only): blocks b, b+8, ... share an XCD under round-robin
+  // dispatch; give each such group a contiguous run of tiles (x fastest) so tiles that
+  // share A rows sit on one L2.  Bijective for any grid size.
+  const int nx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int L = blockIdx.x + nx * blockIdx.y;
+  const int xcd = L % 8, slot = L / 8, qq = nwg / 8, rr = nwg % 8;
+  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
+  const int64_t m0 = (int64_t)(logical / nx) * BM, n0 = (int64_t)(logical % nx) * BN;
   const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
   const int64_t kend = min((int64_t)K, kbeg + k_per_split);
   const int nk = (int)((kend - kbeg + BK - 1) / BK);
 
-  f32x16 acc[2][2];
+  f32x16 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  Stager<A_RK> sa;
-  Stager<B_RK> sb;
+  TA sa;
+  TBt sb;
+  sa.init(A, m0, kbeg, M);
+  sb.init(B, n0, kbeg, N);
   if (nk > 0) {
-    sa.load(A, m0, kbeg, M, kend, tid);
-    sb.load(B, n0, kbeg, N, kend, tid);
-    sa.store(smem[0][0], tid);
-    sb.store(smem[0][1], tid);
+    sa.load(A, kend);
+    sb.load(B, kend);
+    sa.store(smem[0]);
+    sb.store(smem[0] + TA::FLOATS);
   }
   __syncthreads();
 
@@ -127,33 +181,26 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) {
-      sa.load(A, m0, kbeg + (int64_t)(kt + 1) * BK, M, kend, tid);
-      sb.load(B, n0, kbeg + (int64_t)(kt + 1) * BK, N, kend, tid);
+      sa.load(A, kend);
+      sb.load(B, kend);
     }
-    const float* As = smem[buf][0];
-    const float* Bs = smem[buf][1];
-    f32x4 af[2][2], bf[2][2];
+    const float* As = smem[buf];
+    const float* Bs = smem[buf] + TA::FLOATS;
+    float af[TI][BK / 2], bf[TJ][BK / 2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const float* pa = As + (wr * 64 + t * 32 + li) * LDK + 8 * h;
-      const float* pb = Bs + (wc * 64 + t * 32 + li) * LDK + 8 * h;
-      af[t][0] = *reinterpret_cast<const f32x4*>(pa);
-      af[t][1] = *reinterpret_cast<const f32x4*>(pa + 4);
-      bf[t][0] = *reinterpret_cast<const f32x4*>(pb);
-      bf[t][1] = *reinterpret_cast<const f32x4*>(pb + 4);
-    }
+    for (int i = 0; i < TI; ++i) sa.frag(As, wr * WM + i * 32 + li, h, af[i]);
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
+    for (int j = 0; j < TJ; ++j) sb.frag(Bs, wc * WN + j * 32 + li, h, bf[j]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int p = 0; p < BK / 2; ++p)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][p >> 2][p & 3], bf[j][p >> 2][p & 3],
-                                                            acc[i][j], 0, 0, 0);
-    }
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][p], bf[j][p], acc[i][j], 0, 0, 0);
     if (kt + 1 < nk) {
-      sa.store(smem[buf ^ 1][0], tid);
-      sb.store(smem[buf ^ 1][1], tid);
+      sa.store(smem[buf ^ 1]);
+      sb.store(smem[buf ^ 1] + TA::FLOATS);
     }
     __syncthreads();
   }
@@ -162,8 +209,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(
   float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
   const int64_t ld = slab ? N : ldc;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t n = n0 + wc * 64 + j * 32 + li;
+  for (int j = 0; j < TJ; ++j) {
+    const int64_t n = n0 + wc * WN + j * 32 + li;
     if (n >= N) continue;
     float bsum = 0.f;
     if (!slab) {
@@ -171,10 +218,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(
       if (bias2) bsum += bias2[n];
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < TI; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t m = m0 + wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (m < M) {
           float v = acc[i][j][r] + bsum;
           float* dst = out + m * ld + n;
@@ -205,6 +252,53 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
 
 bool aligned_ld(int64_t ld) { return (ld & 3) == 0; }
 
+// Tile configurations (id -> BM, BN, BK; waves of 64x64 unless noted)
+struct GemmShape { int id, bm, bn, bk; };
+constexpr GemmShape kCfg[] = {
+    {0, 128, 128, 16},   // 4 waves of 64x64
+    {1, 128, 64, 16},    // 4 waves of 64x32: twice the blocks for small grids
+    {2, 128, 128, 32},   // 4 waves of 64x64, half the barriers
+    {3, 64, 64, 16},     // 4 waves of 32x32: small outputs
+};
+
+#ifndef AVC_GEMM_FORCE_CFG
+#define AVC_GEMM_FORCE_CFG -1
+#endif
+int g_force_cfg = AVC_GEMM_FORCE_CFG;  // tools/gemm_bench.hip overrides this
+
+GemmShape pick_config(int M, int N, int K, int splits) {
+  if (g_force_cfg >= 0) return kCfg[g_force_cfg];
+  // tools/gemm_bench.hip sweep (round 1): 128x128/BK32 wins once the 128-tile grid fills
+  // the chip >= 2x over (117-119 TF at 8192x1024..4096); narrow or short outputs are faster on
+  // 64x64 tiles (4 blocks per CU: 85-105 TF where 128x128 gave 68-92).
+  const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
+  if (t128 >= 512) return kCfg[2];
+  return kCfg[3];
+}
+
+template <int BM, int BN, int BK, int WM, int WN>
+void launch_layouts(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
+                    float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), 0, st, M, N, K, \
+                                         oa, ob, C, ldc, b1, b2, acc, kps, slab)
+  if (!a_trans && !b_trans) AVC_L(true, true);
+  else if (!a_trans && b_trans) AVC_L(true, false);
+  else if (a_trans && !b_trans) AVC_L(false, true);
+  else AVC_L(false, false);
+#undef AVC_L
+}
+
+void launch_gemm(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
+                 float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
+  switch (id) {
+    case 0: launch_layouts<128, 128, 16, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 1: launch_layouts<128, 64, 16, 64, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 2: launch_layouts<128, 128, 32, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    default: launch_layouts<64, 64, 16, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t autovc_gemm_workspace_floats(int M, int N, int splits) {
@@ -229,23 +323,19 @@ extern "C" int autovc_gemm_f32(int M, int N, int K,
   AVC_CHECK_ARG(!b_conv_T || (b_conv_C % 4 == 0 && b_conv_C > 0),
                 "autovc_gemm_f32: B conv channels must be a positive multiple of 4");
   if (splits < 1) splits = 1;
+  const GemmShape cfg = pick_config(M, N, K, splits);
+  const int BKc = cfg.bk;
   int64_t kps = ((int64_t)K + splits - 1) / splits;
-  kps = ((kps + BK - 1) / BK) * BK;
+  kps = ((kps + BKc - 1) / BKc) * BKc;
   splits = (int)((K + kps - 1) / kps);
   if (splits < 1) splits = 1;
   AVC_CHECK_ARG(splits == 1 || workspace, "autovc_gemm_f32: split-K needs a workspace");
   Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0};
   Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0};
-  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, splits);
   float* slab = splits > 1 ? workspace : nullptr;
-#define AVC_GEMM_LAUNCH(AR, BR)                                                                   \
-  hipLaunchKernelGGL((gemm_kernel<AR, BR>), grid, dim3(kThreads), 0, stream, M, N, K, oa, ob, C, \
-                     ldc, bias1, bias2, accumulate, (int)kps, slab)
-  if (!a_trans && !b_trans) AVC_GEMM_LAUNCH(true, true);
-  else if (!a_trans && b_trans) AVC_GEMM_LAUNCH(true, false);
-  else if (a_trans && !b_trans) AVC_GEMM_LAUNCH(false, true);
-  else AVC_GEMM_LAUNCH(false, false);
-#undef AVC_GEMM_LAUNCH
+  const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, splits);
+  launch_gemm(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
+              slab);
   AVC_CHECK_LAUNCH("autovc_gemm_f32");
   if (splits > 1) {
     const int64_t total = (int64_t)M * N;

@@ -7,16 +7,20 @@
 //
 // Two regimes:
 //  * large H (decoder lstm1 H=512, lstm2 H=1024): one launch per time step on the
-//    caller's stream (a kernel boundary is cheaper than a grid barrier on MI355X,
-//    MI355X_MICROARCH.md price list "boundary" vs "barrier-xcd").  Workgroup = 4 hidden
-//    units x all 4 gates (16 W_hh rows) x every batch row; the 64x16xH product runs on
-//    v_mfma_f32_16x16x4_f32 with h and W read as float4 straight from L2/MALL, and the
-//    cell update is fused (no gates round trip through HBM).  Backward = per step a
-//    pointwise kernel (dG_t from dh, dc) and a split-K recurrent product
-//    dh_rec = dG_t W_hh through the pre-transposed W_hh^T.
+//    caller's stream (a kernel boundary, ~1.5 us, is cheaper than a grid barrier on
+//    MI355X: MI355X_MICROARCH.md price list "boundary" vs "barrier-xcd").  Each step is a
+//    small-M GEMM (64 batch x 4H gate rows x H) cut into 32x32 output tiles = 256
+//    workgroups for H=1024: a tile is 32 batch rows x (8 hidden units x 4 gates), so the
+//    cell update is fused into the epilogue.  Operands are register-staged into a
+//    double-buffered, XOR-swizzled LDS tile (see tile_gemm) and each wave's 16x16
+//    quadrant runs on v_mfma_f32_16x16x4_f32 (exact fp32).
+//    Backward = per step the same tile kernel computing split-K partials of
+//    dh_rec = dG_t W_hh (through the pre-transposed W_hh^T) + a pointwise kernel.
 //  * small H (encoder BLSTM, H=32): the whole sequence in one launch, one workgroup per
-//    (direction, 8 batch rows), W_hh in LDS, one barrier per step (two in backward).
+//    (direction, 8 batch rows), the thread's W_hh rows/columns held in registers.
 #include <hip/hip_ext.h>
+
+#include <algorithm>
 
 #include "common.h"
 #include "../../include/autovc_hip.h"
@@ -24,33 +28,124 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int U = 4;          // hidden units per workgroup (large-H kernels)
-constexpr int NCOL = 4 * U;   // 16 MFMA columns = 4 gates x U units
+constexpr int TB = 32;          // batch rows per tile
+constexpr int TN = 32;          // output columns per tile
+constexpr int UT = TN / 4;      // hidden units per forward tile (x 4 gates)
 
-__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+// Register-staged tile GEMM: the 32 x 32 output tile of a workgroup,
+//   C[r][n] = sum_k A_r[k] * B_n[k]   (A rows: batch, B rows: weight rows; K contiguous),
+// over chunks of KCH k.  Each thread prefetches its PER float4 of the next D chunks into
+// VGPRs (plain global_load_dwordx4: far cheaper to issue than LDS-DMA, which capped the
+// first version at ~25 GB/s per CU — tools/lstm_step_bench.hip), writes the current
+// chunk to one of two LDS buffers (XOR-swizzled 16-B slots: conflict-free ds_read_b128),
+// one barrier per chunk.  NW = 4 waves: one 16x16 quadrant each; NW = 8: quadrant x
+// k-half, the halves summed through LDS at the end.  v_mfma_f32_16x16x4_f32 throughout.
+template <int KCH, int NW, int D>
+struct Tile {
+  static constexpr int SLOTS = KCH / 4;             // float4 slots per row per chunk
+  static constexpr int NT = 64 * NW;
+  static constexpr int PER = TB * SLOTS / NT;       // float4 per thread per operand per chunk
+  static constexpr int CF = (TB + TN) * KCH;        // floats per LDS chunk buffer
+  static constexpr int SUB = KCH / 16 / (NW / 4);   // 16-k sub-blocks per wave per chunk
+  static constexpr int RED = 4 * 16 * 17;
+  static constexpr int LDS_FLOATS = 2 * CF + RED;
+  static_assert(PER * NT == TB * SLOTS && TB == TN, "staging map covers the tile exactly");
+};
 
-// acc(16 rows of X x 16 W rows) += X[16 x K] * Wr[16 x K]^T with f32 MFMA 16x16x4.
-// xrow: this lane's X row (already offset by 4*(lane>>4)), or null (row absent -> 0)
-// wrow: this lane's W row (already offset by 4*(lane>>4))
-__device__ __forceinline__ f32x4 mfma_rows(const float* xrow, const float* wrow, int K) {
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  int kc = 0;
-  for (; kc + 32 <= K; kc += 32) {
-    const f32x4 x0 = xrow ? ld4(xrow + kc) : z, w0 = ld4(wrow + kc);
-    const f32x4 x1 = xrow ? ld4(xrow + kc + 16) : z, w1 = ld4(wrow + kc + 16);
+// swizzled float4 position of slot sl in row r
+__device__ __forceinline__ int swz(int sl, int r) { return (sl & ~15) | ((sl & 15) ^ (r & 15)); }
+
+template <int KCH, int NW, int D, class AR, class BR>
+__device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, int K) {
+  using C = Tile<KCH, NW, D>;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* arow[C::PER];
+  const float* brow[C::PER];
+  int srow[C::PER], spos[C::PER];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[j], w0[j], a0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[j], w1[j], a1, 0, 0, 0);
+  for (int i = 0; i < C::PER; ++i) {
+    const int e = tid + i * C::NT;
+    const int r = e / C::SLOTS, sl = e % C::SLOTS;
+    srow[i] = r;
+    spos[i] = swz(sl, r);
+    arow[i] = arow_of(r) + 4 * sl;
+    brow[i] = brow_of(r) + 4 * sl;
   }
-  for (; kc < K; kc += 16) {
-    const f32x4 x0 = xrow ? ld4(xrow + kc) : z, w0 = ld4(wrow + kc);
+  const int nc = K / KCH;
+  f32x4 sa[D][C::PER], sb[D][C::PER];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[j], w0[j], a0, 0, 0, 0);
+  for (int d = 0; d < D; ++d)
+    if (d < nc)
+#pragma unroll
+      for (int i = 0; i < C::PER; ++i) {
+        sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + d * KCH);
+        sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + d * KCH);
+      }
+  const int q = w & 3, kh = w >> 2, g = lane >> 4;
+  const int ra = (q >> 1) * 16 + (lane & 15), rb = (q & 1) * 16 + (lane & 15);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nc; c0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int c = c0 + d;
+      if (c < nc) {
+        float* L = lds + (c & 1) * C::CF;
+#pragma unroll
+        for (int i = 0; i < C::PER; ++i) {
+          *reinterpret_cast<f32x4*>(L + srow[i] * KCH + 4 * spos[i]) = sa[d][i];
+          *reinterpret_cast<f32x4*>(L + (TB + srow[i]) * KCH + 4 * spos[i]) = sb[d][i];
+        }
+        __syncthreads();   // chunk c visible; buffer (c+1)&1 no longer read (last read at c-1)
+        if (c + D < nc)
+#pragma unroll
+          for (int i = 0; i < C::PER; ++i) {
+            sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + (c + D) * KCH);
+            sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + (c + D) * KCH);
+          }
+        f32x4 av[C::SUB], bv[C::SUB];
+#pragma unroll
+        for (int s = 0; s < C::SUB; ++s) {
+          const int sl = (kh * C::SUB + s) * 4 + g;
+          av[s] = *reinterpret_cast<const f32x4*>(L + ra * KCH + 4 * swz(sl, ra));
+          bv[s] = *reinterpret_cast<const f32x4*>(L + (TB + rb) * KCH + 4 * swz(sl, rb));
+        }
+        // MFMA local k index (lane>>4) <-> actual k = 16*sub + 4g + jj: same map for A and B
+#pragma unroll
+        for (int s = 0; s < C::SUB; ++s)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            if (s & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][jj], bv[s][jj], acc1, 0, 0, 0);
+            else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][jj], bv[s][jj], acc0, 0, 0, 0);
+          }
+      }
+    }
   }
-  return a0 + a1;
+  f32x4 acc = acc0 + acc1;
+  if (NW == 8) {
+    float* red = lds + 2 * C::CF;
+    if (kh == 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(q * 16 + 4 * g + r) * 17 + (lane & 15)] = acc[r];
+    __syncthreads();
+    if (kh == 0)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += red[(q * 16 + 4 * g + r) * 17 + (lane & 15)];
+  }
+  return acc;  // valid in waves 0..3 (quadrant q = wave)
 }
+
+// configuration used by the product kernels (chosen with tools/lstm_step_bench.hip)
+#ifndef AVC_LSTM_KCH
+#define AVC_LSTM_KCH 128
+#endif
+#ifndef AVC_LSTM_NW
+#define AVC_LSTM_NW 8
+#endif
+#ifndef AVC_LSTM_D
+#define AVC_LSTM_D 1
+#endif
+constexpr int KCH = AVC_LSTM_KCH, NWV = AVC_LSTM_NW, DPF = AVC_LSTM_D;
+using TileP = Tile<KCH, NWV, DPF>;
 
 struct StepArgs {
   int B, T, H;
@@ -61,49 +156,57 @@ struct StepArgs {
   float* gates;                              // (B, T, 4H) post-activation gates or null
 };
 
-// One forward time step of a large-H layer.  grid.x = H / U.
-__global__ __launch_bounds__(kThreads) void lstm_fwd_step_kernel(StepArgs a, int t, int tp) {
-  __shared__ float tile[4][16][NCOL + 1];
+// One forward time step of a large-H layer.  grid = (H / 8, ceil(B / 32)).
+// ABL != 0 only in the ablation build of tools/lstm_step_bench.hip (bit 0: every block
+// reads the same W_hh rows, bit 1: every lane reads the same h row) — never launched here.
+template <int ABL = 0, int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+__global__ __launch_bounds__(64 * NW_) void lstm_fwd_step_kernel(StepArgs a, int t, int tp) {
+  using C = Tile<KCH_, NW_, D_>;
+  __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j0 = blockIdx.x * U;
   const int H = a.H;
-  const int n = lane & 15;                         // MFMA column: gate n>>2, unit n&3
-  const int wr = (n >> 2) * H + j0 + (n & 3);      // W_hh row of that column
-  const int nbt = (a.B + 15) >> 4;
-  for (int bt0 = 0; bt0 < nbt; bt0 += 4) {
-    const int bt = bt0 + w;
-    const int b = bt * 16 + n;                     // A row (batch) of this lane
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (tp >= 0 && bt < nbt) {
-      const float* xrow = b < a.B ? a.h + (int64_t)b * a.h_ldb + (int64_t)tp * a.h_ldt + 4 * (lane >> 4) : nullptr;
-      acc = mfma_rows(xrow, a.W + (int64_t)wr * H + 4 * (lane >> 4), H);
-    }
-    // C/D map: col = lane&15, row = 4*(lane>>4) + r
+  const int j0 = blockIdx.x * UT, b0 = blockIdx.y * TB;
+  // epilogue operands (input-gate pre-activations, previous cell) prefetched before the
+  // recurrent product so their latency hides under it
+  const int bl = (threadIdx.x & 255) >> 3, u = threadIdx.x & 7;
+  const int b = b0 + bl, j = j0 + u;
+  const bool own = threadIdx.x < 256 && b < a.B;
+  float gxv[4] = {0.f, 0.f, 0.f, 0.f}, cp = 0.f;
+  if (own) {
+    const float* g = a.gx + (int64_t)b * a.gx_ldb + (int64_t)t * a.gx_ldt;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) tile[w][4 * (lane >> 4) + r][n] = acc[r];
-    __syncthreads();
-    {
-      const int bl = lane >> 2, u = lane & 3;
-      const int bb = bt * 16 + bl, j = j0 + u;
-      if (bt < nbt && bb < a.B) {
-        const float* g = a.gx + (int64_t)bb * a.gx_ldb + (int64_t)t * a.gx_ldt;
-        const float gi = tile[w][bl][0 * U + u] + g[0 * H + j];
-        const float gf = tile[w][bl][1 * U + u] + g[1 * H + j];
-        const float gg = tile[w][bl][2 * U + u] + g[2 * H + j];
-        const float go = tile[w][bl][3 * U + u] + g[3 * H + j];
-        const float i_ = avc_sigmoid(gi), f_ = avc_sigmoid(gf), g_ = tanhf(gg), o_ = avc_sigmoid(go);
-        const int64_t cb = (int64_t)bb * a.T * H;
-        const float cp = tp >= 0 ? a.c[cb + (int64_t)tp * H + j] : 0.f;
-        const float cn = f_ * cp + i_ * g_;
-        a.c[cb + (int64_t)t * H + j] = cn;
-        a.h[(int64_t)bb * a.h_ldb + (int64_t)t * a.h_ldt + j] = o_ * tanhf(cn);
-        if (a.gates) {
-          float* gs = a.gates + ((int64_t)bb * a.T + t) * 4 * H;
-          gs[0 * H + j] = i_; gs[1 * H + j] = f_; gs[2 * H + j] = g_; gs[3 * H + j] = o_;
-        }
-      }
-    }
-    __syncthreads();
+    for (int q = 0; q < 4; ++q) gxv[q] = g[q * H + j];
+    if (tp >= 0) cp = a.c[(int64_t)b * a.T * H + (int64_t)tp * H + j];
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (tp >= 0) {
+    auto arow_of = [&](int r) {
+      const int b = (ABL & 2) ? 0 : min(b0 + r, a.B - 1);  // rows past B: any valid row, result unused
+      return a.h + (int64_t)b * a.h_ldb + (int64_t)tp * a.h_ldt;
+    };
+    auto brow_of = [&](int r) {  // tile column r = gate*8 + unit
+      return a.W + (int64_t)((r >> 3) * H + ((ABL & 1) ? 0 : j0) + (r & 7)) * H;
+    };
+    acc = tile_gemm<KCH_, NW_, D_>(smem, arow_of, brow_of, H);
+  }
+  __syncthreads();
+  float* tile = smem;                                      // [32][33] after the chunk buffers are drained
+  if (w < 4) {
+    const int wi = w >> 1, wn = w & 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[(wi * 16 + 4 * (lane >> 4) + r) * (TN + 1) + wn * 16 + (lane & 15)] = acc[r];
+  }
+  __syncthreads();
+  if (!own) return;
+  const float* tr = tile + bl * (TN + 1);
+  const float i_ = avc_sigmoid(tr[0 * UT + u] + gxv[0]), f_ = avc_sigmoid(tr[1 * UT + u] + gxv[1]);
+  const float g_ = tanhf(tr[2 * UT + u] + gxv[2]), o_ = avc_sigmoid(tr[3 * UT + u] + gxv[3]);
+  const float cn = f_ * cp + i_ * g_;
+  a.c[(int64_t)b * a.T * H + (int64_t)t * H + j] = cn;
+  a.h[(int64_t)b * a.h_ldb + (int64_t)t * a.h_ldt + j] = o_ * tanhf(cn);
+  if (a.gates) {
+    float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H;
+    gs[0 * H + j] = i_; gs[1 * H + j] = f_; gs[2 * H + j] = g_; gs[3 * H + j] = o_;
   }
 }
 
@@ -127,15 +230,22 @@ __global__ void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp, int first) {
   if (idx >= BH) return;
   const int b = (int)(idx / a.H), j = (int)(idx % a.H);
   const int H = a.H;
-  float dh = a.dh_out ? a.dh_out[(int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j] : 0.f;
-  if (!first && a.P)
-    for (int s = 0; s < a.S; ++s) dh += a.P[(int64_t)s * BH + idx];
   const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H;
   const float i_ = gs[j], f_ = gs[H + j], g_ = gs[2 * H + j], o_ = gs[3 * H + j];
   const float cc = a.c[((int64_t)b * a.T + t) * H + j];
   const float cp = tp >= 0 ? a.c[((int64_t)b * a.T + tp) * H + j] : 0.f;
+  float dh = a.dh_out ? a.dh_out[(int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j] : 0.f;
+  float dcs = 0.f;
+  if (!first) {
+    dcs = a.dc_state[idx];
+    float p[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) p[s] = s < a.S ? a.P[(int64_t)s * BH + idx] : 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) dh += p[s];
+  }
   const float tc = tanhf(cc);
-  const float dc = (first ? 0.f : a.dc_state[idx]) + dh * o_ * (1.f - tc * tc);
+  const float dc = dcs + dh * o_ * (1.f - tc * tc);
   float* d = a.dG + ((int64_t)b * a.T + t) * 4 * H;
   d[j] = dc * g_ * i_ * (1.f - i_);
   d[H + j] = dc * cp * f_ * (1.f - f_);
@@ -145,59 +255,73 @@ __global__ void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp, int first) {
 }
 
 // Split-K recurrent product P[s][b][j] = sum_{r in split s} dG[b][t][r] W^T[j][r].
-// grid = (H/16, S); 4 waves cover batch tiles of 16.
-__global__ __launch_bounds__(kThreads) void lstm_bwd_rec_kernel(int B, int T, int H, const float* dG,
-                                                               int t, const float* WT, float* P, int S) {
+// grid = (H/32, ceil(B/32), S).
+template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+__global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, int H, const float* dG, int t,
+                                                               const float* WT, float* P) {
+  using C = Tile<KCH_, NW_, D_>;
+  __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j0 = blockIdx.x * 16, s = blockIdx.y;
+  const int j0 = blockIdx.x * TN, b0 = blockIdx.y * TB, s = blockIdx.z, S = gridDim.z;
   const int K4 = 4 * H, ks = K4 / S, kb = s * ks;
-  const int n = lane & 15;
-  const int nbt = (B + 15) >> 4;
-  for (int bt = w; bt < nbt; bt += 4) {
-    const int b = bt * 16 + n;
-    const float* xrow = b < B ? dG + ((int64_t)b * T + t) * K4 + kb + 4 * (lane >> 4) : nullptr;
-    const f32x4 acc = mfma_rows(xrow, WT + (int64_t)(j0 + n) * K4 + kb + 4 * (lane >> 4), ks);
+  auto arow_of = [&](int r) { return dG + ((int64_t)min(b0 + r, B - 1) * T + t) * K4 + kb; };
+  auto brow_of = [&](int r) { return WT + (int64_t)(j0 + r) * K4 + kb; };
+  const f32x4 acc = tile_gemm<KCH_, NW_, D_>(smem, arow_of, brow_of, ks);
+  if (w >= 4) return;
+  const int wi = w >> 1, wn = w & 1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int bb = bt * 16 + 4 * (lane >> 4) + r;
-      if (bb < B) P[((int64_t)s * B + bb) * H + j0 + n] = acc[r];
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int b = b0 + wi * 16 + 4 * (lane >> 4) + r;
+    if (b < B) P[((int64_t)s * B + b) * H + j0 + wn * 16 + (lane & 15)] = acc[r];
   }
 }
 
 // ------------------------------------------------------------------ small H (BLSTM)
 // Whole sequence, both directions in one launch.  grid = (ceil(B/8), ndir); block 256 =
 // 8 batch rows x 32 units.  gx: (B,T,ndir*4H) [dir-major blocks]; h out: (B,T,ndir*H).
+// Forward: thread (b, j) keeps W_hh rows {q*H + j} (4 x 32 floats) in registers.
 constexpr int SH = 32, SB = 8;
 
 __global__ __launch_bounds__(kThreads) void blstm_fwd_kernel(int B, int T, const float* gx, const float* Whh_f,
                                                             const float* Whh_b, float* hout, float* call,
                                                             float* gates, int ndir) {
-  __shared__ float Ws[4 * SH][SH + 1];
   __shared__ float hs[2][SB][SH];
   const int dir = blockIdx.y;
   const int bl = threadIdx.x / SH, j = threadIdx.x % SH;
   const int b = blockIdx.x * SB + bl;
   const float* W = dir ? Whh_b : Whh_f;
-  for (int e = threadIdx.x; e < 4 * SH * SH; e += kThreads) Ws[e / SH][e % SH] = W[e];
+  float wr[4][SH];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int k = 0; k < SH; k += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(W + (q * SH + j) * SH + k);
+      wr[q][k] = v[0]; wr[q][k + 1] = v[1]; wr[q][k + 2] = v[2]; wr[q][k + 3] = v[3];
+    }
   hs[0][bl][j] = 0.f;
   __syncthreads();
   const int G = ndir * 4 * SH, HO = ndir * SH;
   float c = 0.f;
   int cur = 0;
+  float gnext[4] = {0.f, 0.f, 0.f, 0.f};
+  if (b < B) {
+    const float* g = gx + ((int64_t)b * T + (dir ? T - 1 : 0)) * G + dir * 4 * SH;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gnext[q] = g[q * SH + j];
+  }
   for (int s = 0; s < T; ++s) {
     const int t = dir ? T - 1 - s : s;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (b < B) {
-      const float* g = gx + ((int64_t)b * T + t) * G + dir * 4 * SH;
+    float acc[4] = {gnext[0], gnext[1], gnext[2], gnext[3]};
+    if (b < B && s + 1 < T) {   // prefetch next step's input gates
+      const float* g = gx + ((int64_t)b * T + (dir ? t - 1 : t + 1)) * G + dir * 4 * SH;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = g[q * SH + j];
+      for (int q = 0; q < 4; ++q) gnext[q] = g[q * SH + j];
     }
-#pragma unroll 8
+#pragma unroll
     for (int k = 0; k < SH; ++k) {
       const float hv = hs[cur][bl][k];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = fmaf(hv, Ws[q * SH + j][k], acc[q]);
+      for (int q = 0; q < 4; ++q) acc[q] = fmaf(hv, wr[q][k], acc[q]);
     }
     const float i_ = avc_sigmoid(acc[0]), f_ = avc_sigmoid(acc[1]), g_ = tanhf(acc[2]), o_ = avc_sigmoid(acc[3]);
     c = f_ * c + i_ * g_;
@@ -217,34 +341,32 @@ __global__ __launch_bounds__(kThreads) void blstm_fwd_kernel(int B, int T, const
 }
 
 // Backward of blstm_fwd_kernel: per direction, walk the sequence in reverse processing
-// order.  dG: (B,T,ndir*4H).  dh_out: (B,T,ndir*H) or null.
+// order.  dG: (B,T,ndir*4H).  dh_out: (B,T,ndir*H) or null.  Thread (b, j) keeps W_hh
+// column j (4H floats) in registers for dh_rec[b][j] = sum_r dG[b][r] W[r][j].
 __global__ __launch_bounds__(kThreads) void blstm_bwd_kernel(int B, int T, const float* dh_out, const float* gates,
                                                             const float* call, const float* Whh_f,
                                                             const float* Whh_b, float* dG, int ndir) {
-  __shared__ float Ws[4 * SH][SH + 1];
-  __shared__ float dgs[SB][4 * SH + 1];
-  __shared__ float dhr[SB][SH];
+  __shared__ float dgs[SB][4 * SH];
   const int dir = blockIdx.y;
   const int bl = threadIdx.x / SH, j = threadIdx.x % SH;
   const int b = blockIdx.x * SB + bl;
   const float* W = dir ? Whh_b : Whh_f;
-  for (int e = threadIdx.x; e < 4 * SH * SH; e += kThreads) Ws[e / SH][e % SH] = W[e];
-  dhr[bl][j] = 0.f;
-  __syncthreads();
+  float wc[4 * SH];
+#pragma unroll
+  for (int r = 0; r < 4 * SH; ++r) wc[r] = W[r * SH + j];
   const int G = ndir * 4 * SH, HO = ndir * SH;
-  float dcs = 0.f;
+  float dcs = 0.f, dhr = 0.f;
   for (int s = T - 1; s >= 0; --s) {
     const int t = dir ? T - 1 - s : s;
     const int tp = dir ? t + 1 : t - 1;   // previous step in processing order
-    const bool has_prev = s > 0;
     float di = 0.f, df = 0.f, dg = 0.f, dO = 0.f;
     if (b < B) {
       const int64_t bt = (int64_t)b * T + t;
-      float dh = dhr[bl][j] + (dh_out ? dh_out[bt * HO + dir * SH + j] : 0.f);
+      const float dh = dhr + (dh_out ? dh_out[bt * HO + dir * SH + j] : 0.f);
       const float* gs = gates + bt * G + dir * 4 * SH;
       const float i_ = gs[j], f_ = gs[SH + j], g_ = gs[2 * SH + j], o_ = gs[3 * SH + j];
       const float cc = call[bt * HO + dir * SH + j];
-      const float cp = has_prev ? call[((int64_t)b * T + tp) * HO + dir * SH + j] : 0.f;
+      const float cp = s > 0 ? call[((int64_t)b * T + tp) * HO + dir * SH + j] : 0.f;
       const float tc = tanhf(cc);
       const float dc = dcs + dh * o_ * (1.f - tc * tc);
       di = dc * g_ * i_ * (1.f - i_);
@@ -257,13 +379,23 @@ __global__ __launch_bounds__(kThreads) void blstm_bwd_kernel(int B, int T, const
     }
     dgs[bl][j] = di; dgs[bl][SH + j] = df; dgs[bl][2 * SH + j] = dg; dgs[bl][3 * SH + j] = dO;
     __syncthreads();
-    // dh_rec[b][j] = sum_r dG[b][r] W[r][j]
     float acc = 0.f;
-#pragma unroll 8
-    for (int r = 0; r < 4 * SH; ++r) acc = fmaf(dgs[bl][r], Ws[r][j], acc);
-    dhr[bl][j] = acc;
+#pragma unroll
+    for (int r = 0; r < 4 * SH; ++r) acc = fmaf(dgs[bl][r], wc[r], acc);
+    dhr = acc;
     __syncthreads();
   }
+}
+
+bool lstm_shape_ok(int B, int H) { return B > 0 && H > 0 && H % 64 == 0; }
+
+// k-chunk of the tile GEMM: the tuned KCH when it divides K, else 64
+template <int ABL = 0>
+void launch_fwd_step(dim3 grid, hipStream_t st, const StepArgs& a, int t, int tp) {
+  if (a.H % KCH == 0)
+    hipLaunchKernelGGL((lstm_fwd_step_kernel<ABL, KCH, NWV, DPF>), grid, dim3(64 * NWV), 0, st, a, t, tp);
+  else
+    hipLaunchKernelGGL((lstm_fwd_step_kernel<ABL, 64, NWV, DPF>), grid, dim3(64 * NWV), 0, st, a, t, tp);
 }
 
 }  // namespace
@@ -272,16 +404,16 @@ __global__ __launch_bounds__(kThreads) void blstm_bwd_kernel(int B, int T, const
 extern "C" int autovc_lstm_fwd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                                    const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                                    float* gates, int reverse, hipStream_t stream) {
-  AVC_CHECK_ARG(B > 0 && T > 0 && H > 0, "autovc_lstm_fwd_f32: bad dims B=%d T=%d H=%d", B, T, H);
-  AVC_CHECK_ARG(H % 16 == 0, "autovc_lstm_fwd_f32: H must be a multiple of 16 (got %d)", H);
+  AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H), "autovc_lstm_fwd_f32: bad dims B=%d T=%d H=%d (H must be a multiple of 64)", B, T, H);
   AVC_CHECK_ARG(gx && W_hh && h && c_all, "autovc_lstm_fwd_f32: null pointer");
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh) && AVC_ALIGNED16(h) && (h_ldb % 4 == 0) && (h_ldt % 4 == 0),
                 "autovc_lstm_fwd_f32: W_hh / h must be 16-byte aligned with strides %% 4 == 0");
   StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, W_hh, h, h_ldb, h_ldt, c_all, gates};
+  const dim3 grid(H / UT, (B + TB - 1) / TB);
   for (int s = 0; s < T; ++s) {
     const int t = reverse ? T - 1 - s : s;
     const int tp = s == 0 ? -1 : (reverse ? t + 1 : t - 1);
-    hipLaunchKernelGGL(lstm_fwd_step_kernel, dim3(H / U), dim3(kThreads), 0, stream, a, t, tp);
+    launch_fwd_step(grid, stream, a, t, tp);
   }
   AVC_CHECK_LAUNCH("autovc_lstm_fwd_f32");
   return avc::kOk;
@@ -294,8 +426,9 @@ extern "C" int64_t autovc_lstm_bwd_workspace_floats(int B, int H, int splits) {
 extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
                                    const float* gates, const float* c_all, const float* W_hh_T, float* dG,
                                    int reverse, int splits, float* workspace, hipStream_t stream) {
-  AVC_CHECK_ARG(B > 0 && T > 0 && H > 0 && H % 16 == 0, "autovc_lstm_bwd_f32: bad dims");
-  AVC_CHECK_ARG(splits >= 1 && (4 * H) % (16 * splits) == 0, "autovc_lstm_bwd_f32: 4H must split into multiples of 16");
+  AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H), "autovc_lstm_bwd_f32: bad dims");
+  AVC_CHECK_ARG(splits >= 1 && splits <= 8 && (4 * H) % (64 * splits) == 0,
+                "autovc_lstm_bwd_f32: 4H must split into multiples of 64 (splits <= 8)");
   AVC_CHECK_ARG(gates && c_all && W_hh_T && dG && workspace, "autovc_lstm_bwd_f32: null pointer");
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_T) && AVC_ALIGNED16(dG), "autovc_lstm_bwd_f32: W_hh_T/dG alignment");
   float* P = workspace;
@@ -303,14 +436,19 @@ extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int
   BwdArgs a{B, T, H, dh_out, d_ldb, d_ldt, gates, c_all, dG, dcs, P, splits};
   const int64_t BH = (int64_t)B * H;
   const int pw_blocks = (int)((BH + 255) / 256);
+  const dim3 rgrid(H / TN, (B + TB - 1) / TB, splits);
   for (int s = T - 1; s >= 0; --s) {
     const int t = reverse ? T - 1 - s : s;
     const int tp = s == 0 ? -1 : (reverse ? t + 1 : t - 1);
     const int first = s == T - 1;
     hipLaunchKernelGGL(lstm_bwd_pointwise_kernel, dim3(pw_blocks), dim3(256), 0, stream, a, t, tp, first);
-    if (s > 0)
-      hipLaunchKernelGGL(lstm_bwd_rec_kernel, dim3(H / 16, splits), dim3(kThreads), 0, stream, B, T, H,
-                         (const float*)dG, t, W_hh_T, P, splits);
+    if (s == 0) continue;
+    if ((4 * H / splits) % KCH == 0)
+      hipLaunchKernelGGL((lstm_bwd_rec_kernel<KCH, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
+                         (const float*)dG, t, W_hh_T, P);
+    else
+      hipLaunchKernelGGL((lstm_bwd_rec_kernel<64, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
+                         (const float*)dG, t, W_hh_T, P);
   }
   AVC_CHECK_LAUNCH("autovc_lstm_bwd_f32");
   return avc::kOk;
@@ -321,6 +459,7 @@ extern "C" int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* 
   AVC_CHECK_ARG(H == SH, "autovc_blstm_fwd_f32: small-H kernel is built for H=%d (got %d)", SH, H);
   AVC_CHECK_ARG(B > 0 && T > 0 && (ndir == 1 || ndir == 2), "autovc_blstm_fwd_f32: bad dims");
   AVC_CHECK_ARG(gx && W_hh_f && h && c_all && (ndir == 1 || W_hh_b), "autovc_blstm_fwd_f32: null pointer");
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_f) && (ndir == 1 || AVC_ALIGNED16(W_hh_b)), "autovc_blstm_fwd_f32: W alignment");
   hipLaunchKernelGGL(blstm_fwd_kernel, dim3((B + SB - 1) / SB, ndir), dim3(kThreads), 0, stream, B, T, gx,
                      W_hh_f, W_hh_b, h, c_all, gates, ndir);
   AVC_CHECK_LAUNCH("autovc_blstm_fwd_f32");
@@ -347,15 +486,20 @@ extern "C" int autovc_blstm_bwd_f32(int B, int T, int H, int ndir, const float* 
 extern "C" int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                                          const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                                          float* gates, hipStream_t stream, float* avg_us) {
-  AVC_CHECK_ARG(B > 0 && T > 1 && H > 0 && H % 16 == 0 && avg_us, "autovc_lstm_fwd_timed_f32: bad args");
+  AVC_CHECK_ARG(T > 1 && lstm_shape_ok(B, H) && avg_us, "autovc_lstm_fwd_timed_f32: bad args");
   AVC_CHECK_ARG(gx && W_hh && h && c_all, "autovc_lstm_fwd_timed_f32: null pointer");
   StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, W_hh, h, h_ldb, h_ldt, c_all, gates};
+  const dim3 grid(H / UT, (B + TB - 1) / TB);
   hipEvent_t* ev = new hipEvent_t[2 * T];
   for (int i = 0; i < 2 * T; ++i) AVC_HIP(hipEventCreate(&ev[i]), "autovc_lstm_fwd_timed_f32/event");
   for (int s = 0; s < T; ++s) {
     const int tp = s == 0 ? -1 : s - 1;
-    hipExtLaunchKernelGGL(lstm_fwd_step_kernel, dim3(H / U), dim3(kThreads), 0, stream, ev[2 * s], ev[2 * s + 1], 0,
-                          a, s, tp);
+    if (H % KCH == 0)
+      hipExtLaunchKernelGGL((lstm_fwd_step_kernel<0, KCH, NWV, DPF>), grid, dim3(64 * NWV), 0, stream, ev[2 * s],
+                            ev[2 * s + 1], 0, a, s, tp);
+    else
+      hipExtLaunchKernelGGL((lstm_fwd_step_kernel<0, 64, NWV, DPF>), grid, dim3(64 * NWV), 0, stream, ev[2 * s],
+                            ev[2 * s + 1], 0, a, s, tp);
   }
   AVC_CHECK_LAUNCH("autovc_lstm_fwd_timed_f32");
   AVC_HIP(hipStreamSynchronize(stream), "autovc_lstm_fwd_timed_f32/sync");

@@ -1,0 +1,66 @@
+"""Utterance crops for Generator training — reference data_loader.py:11-102, same contract.
+
+`get_loader(root_dir, batch_size, len_crop, model_type, num_workers)` returns a torch
+DataLoader over speakers: each item is a random utterance of that speaker (never index 0/1,
+which hold the speaker id and embedding, data_loader.py:68), randomly cropped to len_crop
+frames or zero-padded at the end (:70-78), plus the speaker embedding.  `train.pkl` is the
+user's metadata file in the reference layout [spk, emb, 'spk/file.npy', ...].
+
+Differences: spectrograms are loaded in-process (no multiprocessing.Manager),
+items stay on the host (the Solver moves each batch to the GPU with one non-blocking copy
+instead of a per-item .to(device), :69), and an optional rank/world pair shards speakers
+for data-parallel training.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+
+import numpy as np
+import torch
+from torch.utils import data
+
+
+class Utterances(data.Dataset):
+    def __init__(self, data_dir, len_crop, model_type):
+        self.root_dir = os.path.join(data_dir, model_type)
+        self.len_crop = len_crop
+        with open(os.path.join(self.root_dir, "train.pkl"), "rb") as f:
+            meta = pickle.load(f)  # user-provided metadata, as the reference does
+        self.train_dataset = []
+        for sbmt in meta:
+            uttrs = [sbmt[0], np.asarray(sbmt[1], dtype=np.float32)]
+            for rel in sbmt[2:]:
+                uttrs.append(np.load(os.path.join(self.root_dir, rel)).astype(np.float32, copy=False))
+            self.train_dataset.append(uttrs)
+        self.num_tokens = len(self.train_dataset)
+
+    def __getitem__(self, index):
+        list_uttrs = self.train_dataset[index]
+        emb_org = torch.from_numpy(list_uttrs[1])
+        a = np.random.randint(2, len(list_uttrs))
+        tmp = list_uttrs[a]
+        if tmp.shape[0] < self.len_crop:
+            uttr = np.pad(tmp, ((0, self.len_crop - tmp.shape[0]), (0, 0)), "constant")
+        elif tmp.shape[0] > self.len_crop:
+            left = np.random.randint(tmp.shape[0] - self.len_crop)
+            uttr = tmp[left:left + self.len_crop, :]
+        else:
+            uttr = tmp
+        return torch.from_numpy(np.ascontiguousarray(uttr, dtype=np.float32)), emb_org
+
+    def __len__(self):
+        return self.num_tokens
+
+
+def get_loader(root_dir, batch_size=16, len_crop=128, model_type="spmel", num_workers=0, rank=None, world=None):
+    """data_loader.py:90-102 (shuffle, drop_last, seeded workers); rank/world optionally
+    shard the speakers across data-parallel ranks."""
+    dataset = Utterances(root_dir, len_crop, model_type)
+    sampler = None
+    if world is not None and world > 1:
+        sampler = data.distributed.DistributedSampler(dataset, num_replicas=world, rank=rank, shuffle=True,
+                                                      drop_last=True)
+    worker_init_fn = lambda x: np.random.seed((torch.initial_seed()) % (2 ** 32))  # noqa: E731
+    return data.DataLoader(dataset=dataset, batch_size=batch_size, shuffle=sampler is None, sampler=sampler,
+                           num_workers=num_workers, drop_last=True, worker_init_fn=worker_init_fn)

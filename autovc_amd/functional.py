@@ -66,11 +66,13 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
 
 
 def _splits_for(M, N, K):
-    """Split-K factor so that a (M,N) output tiled 128x128 fills ~256 CUs."""
-    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    """Split-K factor for the long-K weight-gradient GEMMs: >= 1024 blocks of 64x64 output
+    tiles (4 per CU) while each split keeps >= 1024 k (tools/gemm_bench.hip sweep: conv dW
+    512x2560x8192 42.7 TF unsplit -> 81.6 TF at 4 splits)."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
     s = 1
-    while tiles * s < 256 and K // (s * 2) >= 256:
-        s *= 2
+    while tiles * s < 1024 and K // (s + 1) >= 1024 and s < 8:
+        s += 1
     return s
 
 
@@ -79,6 +81,21 @@ def colsum(X2d, out, out2=None, accumulate=False):
     ws = _ws(X2d.device, 4 * _lib.load().autovc_colsum_workspace_floats(N), "colsum")
     _lib.call("autovc_colsum_f32", M, N, X2d.data_ptr(), X2d.stride(0), _p(out), _p(out2),
               int(accumulate), ws, _s())
+
+
+class _GradOut:
+    """Destination of one parameter gradient.  Parameters managed by FusedAdam carry
+    `_avc_flat` and a .grad view into the optimizer's flat gradient buffer: backward then
+    accumulates straight into it (kernel-side accumulate) and hands autograd None, instead
+    of returning a fresh tensor that AccumulateGrad adds in a separate pass."""
+
+    def __init__(self, param, shape, device):
+        g = param.grad if (param is not None and getattr(param, "_avc_flat", False)) else None
+        self.acc = g is not None and tuple(g.shape) == tuple(shape) and g.is_contiguous()
+        self.buf = g if self.acc else torch.empty(shape, device=device, dtype=torch.float32)
+
+    def result(self):
+        return None if self.acc else self.buf
 
 
 # ---------------------------------------------------------------- Conv1d + BN + act
@@ -114,22 +131,27 @@ def _conv_fwd(x, Wp, bp, T):
     return y
 
 
-def _conv_bwd(dy, x, Wp, need_x, need_w, need_b):
-    """Backward of _conv_fwd given dy (B,T,Cop): (dx (B,T,Cip), dWp (Cop,Cip,K), db (Cop))."""
+def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None):
+    """Backward of _conv_fwd given dy (B,T,Cop): (dx (B,T,Cip), dW, db).  W / b are the
+    parameters: when their gradients live in a flat buffer (and no channel padding is in
+    play) dW / db are accumulated there and returned as None."""
     B, T, Cip = x.shape
     Cop = Wp.shape[0]
     M = B * T
     dev = x.device
     dx = dW = db = None
+    padded = W is None or tuple(W.shape) != tuple(Wp.shape)
     if need_b:
-        db = torch.empty(Cop, device=dev, dtype=torch.float32)
-        colsum(dy.view(M, Cop), db)
+        go = _GradOut(None if padded else b, (Cop,), dev)
+        colsum(dy.view(M, Cop), go.buf, accumulate=go.acc)
+        db = go.result()
     if need_w:
         dWf = torch.empty((Cop, KS * Cip), device=dev, dtype=torch.float32)
         gemm(Cop, KS * Cip, M, dy, Cop, 1, x, Cip, 1, dWf, KS * Cip, b_conv=(T, Cip, -PAD),
              splits=_splits_for(Cop, KS * Cip, M))
-        dW = torch.empty((Cop, Cip, KS), device=dev, dtype=torch.float32)
-        _lib.call("autovc_conv_unpack_grad_f32", Cop, Cip, KS, dWf.data_ptr(), dW.data_ptr(), 0, _s())
+        go = _GradOut(None if padded else W, (Cop, Cip, KS), dev)
+        _lib.call("autovc_conv_unpack_grad_f32", Cop, Cip, KS, dWf.data_ptr(), go.buf.data_ptr(), int(go.acc), _s())
+        dW = go.result()
     if need_x:
         Wd = torch.empty((KS * Cop, Cip), device=dev, dtype=torch.float32)
         _lib.call("autovc_conv_pack_f32", Cop, Cip, KS, Wp.data_ptr(), 0, Wd.data_ptr(), _s())
@@ -174,6 +196,7 @@ class ConvBNActFn(torch.autograd.Function):
         ctx.act, ctx.eps = act, eps
         ctx.has_res = residual is not None
         ctx.dims = (Ci, Co, Cip, Cop)
+        ctx.params = (W, b, gamma, beta)
         # the activation backward reads the forward output; the residual layer has act none
         ctx.save_for_backward(xp, Wp, gamma, y, None if ctx.has_res else z, mean, var)
         return z
@@ -188,15 +211,23 @@ class ConvBNActFn(torch.autograd.Function):
         B, T, _ = xp.shape
         M = B * T
         dev = xp.device
+        W_param, b_param, g_param, be_param = ctx.params
         dy = (torch.zeros if Cop != Co else torch.empty)((B, T, Cop), device=dev, dtype=torch.float32)
-        dgamma = torch.empty(Co, device=dev, dtype=torch.float32) if ctx.needs_input_grad[3] else None
-        dbeta = torch.empty(Co, device=dev, dtype=torch.float32) if ctx.needs_input_grad[4] else None
+        need_g, need_b = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+        gg = _GradOut(g_param, (Co,), dev) if need_g else None
+        gb = _GradOut(be_param, (Co,), dev) if need_b else None
+        acc = bool(gg is not None and gb is not None and gg.acc and gb.acc)
+        if not acc:  # both-or-neither: one accumulate flag for the pair
+            gg = _GradOut(None, (Co,), dev) if need_g else None
+            gb = _GradOut(None, (Co,), dev) if need_b else None
         ws = _ws(dev, _lib.load().autovc_bn_workspace_bytes(Co), "bn")
         _lib.call("autovc_bn_act_bwd_f32", M, Co, dz.data_ptr(), Co, _p(z), Co, y.data_ptr(), Cop,
                   mean.data_ptr(), var.data_ptr(), _p(gamma), float(ctx.eps), ACT[ctx.act],
-                  dy.data_ptr(), Cop, _p(dgamma), _p(dbeta), 0, ws, _s())
+                  dy.data_ptr(), Cop, _p(gg.buf if gg else None), _p(gb.buf if gb else None), int(acc), ws, _s())
+        dgamma = gg.result() if gg else None
+        dbeta = gb.result() if gb else None
         dx, dW, db = _conv_bwd(dy, xp, Wp, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               ctx.needs_input_grad[2])
+                               ctx.needs_input_grad[2], W_param, b_param)
         if dx is not None and Cip != Ci:
             dx = dx[..., :Ci].contiguous()
         if dW is not None and (Cop, Cip) != (Co, Ci):
@@ -236,6 +267,7 @@ class ConvFn(torch.autograd.Function):
         ctx.save_for_backward(xp, Wp)
         ctx.dims = (Ci, Co, Cip, Cop)
         ctx.has_b = b is not None
+        ctx.params = (W, b)
         return y if Cop == Co else y[..., :Co].contiguous()
 
     @staticmethod
@@ -244,7 +276,7 @@ class ConvFn(torch.autograd.Function):
         Ci, Co, Cip, Cop = ctx.dims
         dyp = _pad_last(dy, Cop)
         dx, dW, db = _conv_bwd(dyp, xp, Wp, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               ctx.has_b and ctx.needs_input_grad[2])
+                               ctx.has_b and ctx.needs_input_grad[2], *ctx.params)
         if dx is not None and Cip != Ci:
             dx = dx[..., :Ci].contiguous()
         if dW is not None and (Cop, Cip) != (Co, Ci):
@@ -272,26 +304,31 @@ class LinearFn(torch.autograd.Function):
         gemm(M, N, K, x, K, 0, W, K, 0, y, N, bias1=b)
         ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
+        ctx.params = (W, b)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
+        W_param, b_param = ctx.params
         K = x.shape[-1]
         N = W.shape[0]
         M = x.numel() // K
+        dev = x.device
         Np = _ceil4(N)  # 513-bin projection: pad the output axis for the float4 GEMM operands
         dy = _pad_last(dy.reshape(M, N), Np)
         Wp = W.contiguous() if Np == N else torch.cat([W, W.new_zeros(Np - N, K)], 0)
         dx = dW = db = None
         if ctx.needs_input_grad[1]:
-            dW = torch.empty((Np, K), device=W.device, dtype=torch.float32)
-            gemm(Np, K, M, dy, Np, 1, x, K, 1, dW, K, splits=_splits_for(Np, K, M))
-            dW = dW if Np == N else dW[:N].contiguous()
+            go = _GradOut(W_param if Np == N else None, (Np, K), dev)
+            gemm(Np, K, M, dy, Np, 1, x, K, 1, go.buf, K, splits=_splits_for(Np, K, M), accumulate=go.acc)
+            dW = go.result()
+            dW = dW if (dW is None or Np == N) else dW[:N].contiguous()
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = torch.empty(Np, device=dy.device, dtype=torch.float32)
-            colsum(dy, db)
-            db = db if Np == N else db[:N].contiguous()
+            go = _GradOut(b_param if Np == N else None, (Np,), dev)
+            colsum(dy, go.buf, accumulate=go.acc)
+            db = go.result()
+            db = db if (db is None or Np == N) else db[:N].contiguous()
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             gemm(M, K, Np, dy, Np, 0, Wp, K, 1, dx, K)
@@ -321,11 +358,13 @@ class LSTMLayerFn(torch.autograd.Function):
         _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
                   h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), 0, _s())
         ctx.save_for_backward(x, W_ih, W_hh, h, c, gates)
+        ctx.params = (W_ih, W_hh, b_ih, b_hh)
         return h
 
     @staticmethod
     def backward(ctx, dh):
         x, W_ih, W_hh, h, c, gates = ctx.saved_tensors
+        p_ih, p_hh, p_bih, p_bhh = ctx.params
         if gates is None:
             raise RuntimeError("LSTM backward needs the forward run with gradients enabled")
         dh = dh.contiguous()
@@ -334,7 +373,7 @@ class LSTMLayerFn(torch.autograd.Function):
         dev = x.device
         WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
         _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
-        splits = 4 if (4 * H) % 64 == 0 else 1
+        splits = 4 if (4 * H) % 256 == 0 else 1
         ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
         dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
@@ -342,16 +381,20 @@ class LSTMLayerFn(torch.autograd.Function):
         M = B * T
         dx = dWih = dWhh = dbih = dbhh = None
         if ctx.needs_input_grad[1]:
-            dWih = torch.empty_like(W_ih)
-            gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, dWih, I, splits=_splits_for(4 * H, I, M))
+            go = _GradOut(p_ih, W_ih.shape, dev)
+            gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I, splits=_splits_for(4 * H, I, M), accumulate=go.acc)
+            dWih = go.result()
         if ctx.needs_input_grad[2]:
-            dWhh = torch.empty_like(W_hh)
-            gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, dWhh, H, b_conv=(T, H, -1),
-                 splits=_splits_for(4 * H, H, M))
+            go = _GradOut(p_hh, W_hh.shape, dev)
+            gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
+                 splits=_splits_for(4 * H, H, M), accumulate=go.acc)
+            dWhh = go.result()
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
-            dbih = torch.empty(4 * H, device=dev, dtype=torch.float32)
-            dbhh = torch.empty(4 * H, device=dev, dtype=torch.float32)
-            colsum(dG.view(M, 4 * H), dbih, dbhh)
+            gi, gh = _GradOut(p_bih, (4 * H,), dev), _GradOut(p_bhh, (4 * H,), dev)
+            if gi.acc != gh.acc:
+                gi, gh = _GradOut(None, (4 * H,), dev), _GradOut(None, (4 * H,), dev)
+            colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc)
+            dbih, dbhh = gi.result(), gh.result()
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I)
@@ -378,6 +421,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         _lib.call("autovc_blstm_fwd_f32", B, T, H, 2, gx.data_ptr(), Whh_f.data_ptr(), Whh_b.data_ptr(),
                   h.data_ptr(), c.data_ptr(), _p(gates), _s())
         ctx.save_for_backward(x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates)
+        ctx.params = ((Wih_f, Whh_f, bih_f, bhh_f), (Wih_b, Whh_b, bih_b, bhh_b))
         return h
 
     @staticmethod
@@ -395,25 +439,26 @@ class BLSTMLayerFn(torch.autograd.Function):
         _lib.call("autovc_blstm_bwd_f32", B, T, H, 2, dh.data_ptr(), gates.data_ptr(), c.data_ptr(),
                   Whh_f.data_ptr(), Whh_b.data_ptr(), dG.data_ptr(), _s())
         grads = [None] * 10
+        dG2 = dG.view(M, 2 * G)
         for d, (iW, iH, iBi, iBh) in enumerate(((1, 2, 3, 4), (5, 6, 7, 8))):
-            Wih = (Wih_f, Wih_b)[d]
-            Whh = (Whh_f, Whh_b)[d]
+            pW, pH, pBi, pBh = ctx.params[d]
             if ctx.needs_input_grad[iW]:
-                g = torch.empty_like(Wih)
-                gemm(G, I, M, dG, 2 * G, 1, x, I, 1, g, I, a_off=d * G, splits=_splits_for(G, I, M))
-                grads[iW] = g
+                go = _GradOut(pW, pW.shape, dev)
+                gemm(G, I, M, dG, 2 * G, 1, x, I, 1, go.buf, I, a_off=d * G, splits=_splits_for(G, I, M),
+                     accumulate=go.acc)
+                grads[iW] = go.result()
             if ctx.needs_input_grad[iH]:
-                g = torch.empty_like(Whh)
+                go = _GradOut(pH, pH.shape, dev)
                 # previous step in processing order: t-1 forward, t+1 backward direction
-                gemm(G, H, M, dG, 2 * G, 1, h, 2 * H, 1, g, H, a_off=d * G, b_off=d * H,
-                     b_conv=(T, H, -1 if d == 0 else 1), splits=_splits_for(G, H, M))
-                grads[iH] = g
-        if any(ctx.needs_input_grad[i] for i in (3, 4, 7, 8)):
-            db_ih = torch.empty(2 * G, device=dev, dtype=torch.float32)
-            db_hh = torch.empty(2 * G, device=dev, dtype=torch.float32)
-            colsum(dG.view(M, 2 * G), db_ih, db_hh)
-            grads[3], grads[4] = db_ih[:G], db_hh[:G]
-            grads[7], grads[8] = db_ih[G:], db_hh[G:]
+                gemm(G, H, M, dG, 2 * G, 1, h, 2 * H, 1, go.buf, H, a_off=d * G, b_off=d * H,
+                     b_conv=(T, H, -1 if d == 0 else 1), splits=_splits_for(G, H, M), accumulate=go.acc)
+                grads[iH] = go.result()
+            if ctx.needs_input_grad[iBi] or ctx.needs_input_grad[iBh]:
+                gi, gh = _GradOut(pBi, (G,), dev), _GradOut(pBh, (G,), dev)
+                if gi.acc != gh.acc:
+                    gi, gh = _GradOut(None, (G,), dev), _GradOut(None, (G,), dev)
+                colsum(dG2[:, d * G:(d + 1) * G], gi.buf, gh.buf, accumulate=gi.acc)
+                grads[iBi], grads[iBh] = gi.result(), gh.result()
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)

@@ -1,0 +1,84 @@
+"""Spect — reference make_spect.py:13-94 with the STFT / mel / log / clip on the GPU.
+
+Same constructor (config with speaker_embed, model_type, main_dir), same directory
+walk (<main_dir>/wav48_silence_trimmed/<spk>/*, files containing 'mic1' skipped), same
+per-speaker RandomState(int(spk[1:])) dither stream consumed in sorted file order, same
+outputs (spmel: (T, 80) float32; stft: (513, T) float32, the reference's on-disk layout).
+Host: wav decode (16-bit PCM at 16 kHz; librosa.load's int16/32768), Butterworth filtfilt
+and dither (make_spect.py:72-76).  GPU: one fused STFT+mel launch per speaker
+(autovc_amd.dsp.stft_mel -> autovc_stft_mel_f32).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from . import dsp
+
+
+def load_wav(path, sr=16000):
+    from scipy.io import wavfile
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", wavfile.WavFileWarning)
+        fs, data = wavfile.read(path)
+    if fs != sr:
+        raise ValueError(f"{path}: sample rate {fs} (resampling to {sr} is not implemented)")
+    if data.ndim > 1:
+        data = data.mean(axis=1)
+    if data.dtype == np.int16:
+        return data.astype(np.float32) / 32768.0
+    if data.dtype == np.int32:
+        return (data / 2147483648.0).astype(np.float32)
+    return data.astype(np.float32)
+
+
+class Spect(object):
+    def __init__(self, config):
+        self.speaker_embed = getattr(config, "speaker_embed", True)
+        self.model_type = config.model_type
+        self.targetDir = config.main_dir
+        self.cutoff = dsp.CUTOFF
+        self.fs = dsp.FS
+        self.order = dsp.ORDER
+        self.fft_length = dsp.FFT_LENGTH
+        self.hop_length = dsp.HOP_LENGTH
+        self.n_fft = dsp.FFT_LENGTH
+        self.n_mels = 128  # unused by the reference too (it builds an 80-mel basis)
+        self.device = getattr(config, "device", "cuda")
+
+    def butter_highpass(self):
+        return dsp.butter_highpass()
+
+    def speaker(self, wav_paths, speaker):
+        """All kept files of one speaker -> {name: array} (reference layouts)."""
+        prng = np.random.RandomState(int(speaker[1:]))
+        names, wavs = [], []
+        for p in sorted(wav_paths):
+            fname = os.path.basename(p)
+            if "mic1" in fname:
+                continue
+            wavs.append(dsp.preprocess(load_wav(p, self.fs), prng))
+            names.append(fname[:fname.rfind(".")])
+        if self.model_type not in ("spmel", "stft"):
+            raise NotImplementedError(f"model_type {self.model_type!r}: only 'spmel' and 'stft' are on the GPU path")
+        outs = dsp.stft_mel(wavs, self.model_type, device=self.device)
+        res = {}
+        for n, o in zip(names, outs):
+            a = o.cpu().numpy()
+            res[n] = a if self.model_type == "spmel" else np.ascontiguousarray(a.T)
+        return res
+
+    def spect(self):
+        rootDir = os.path.join(self.targetDir, "wav48_silence_trimmed")
+        saveDir = os.path.join(self.targetDir, self.model_type)
+        dirName, subdirList, _ = next(os.walk(rootDir))
+        print("Found directory: %s" % dirName)
+        for subdir in sorted(subdirList):
+            print(subdir)
+            os.makedirs(os.path.join(saveDir, subdir), exist_ok=True)
+            _, _, fileList = next(os.walk(os.path.join(dirName, subdir)))
+            out = self.speaker([os.path.join(dirName, subdir, f) for f in fileList], subdir)
+            for name, S in out.items():
+                np.save(os.path.join(saveDir, subdir, name), S.astype(np.float32), allow_pickle=False)

@@ -56,6 +56,7 @@ class FusedAdam(torch.optim.Optimizer):
             flat_p[o:o + n].copy_(p.detach().reshape(-1))
             p.data = flat_p[o:o + n].view_as(p)
             p.grad = flat_g[o:o + n].view_as(p)
+            p._avc_flat = True  # autovc_amd.functional accumulates this gradient in place
         return dict(p=flat_p, g=flat_g, m=flat_m, v=flat_v, offs=offs, step=0, params=list(params))
 
     # -- flat buffers (used by autovc_amd.ddp)

@@ -1,0 +1,67 @@
+// Tile-configuration sweep for autovc_gemm_f32 on the Generator-step shapes (not part of
+// the product).  hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_bench.hip -o tools/gemm_bench
+#include "../autovc_amd/csrc/gemm.hip"
+#include "../autovc_amd/csrc/capi.cpp"
+
+#include <cstdio>
+#include <cstdlib>
+
+struct Case { const char* name; int M, N, K, at, bt, aconv, bconv, C, splits; };
+
+int main() {
+  const int T = 128;
+  Case cases[] = {
+      {"conv fwd 512->512", 8192, 512, 2560, 0, 0, 1, 0, 512, 1},
+      {"conv fwd 336->512", 8192, 512, 1680, 0, 0, 1, 0, 336, 1},
+      {"conv dX 512<-512", 8192, 512, 2560, 0, 1, 1, 0, 512, 1},
+      {"conv dW s1", 512, 2560, 8192, 1, 1, 0, 1, 512, 1},
+      {"conv dW s2", 512, 2560, 8192, 1, 1, 0, 1, 512, 2},
+      {"conv dW s3", 512, 2560, 8192, 1, 1, 0, 1, 512, 3},
+      {"conv dW s4", 512, 2560, 8192, 1, 1, 0, 1, 512, 4},
+      {"lstm2 proj K512", 8192, 4096, 512, 0, 0, 0, 0, 0, 1},
+      {"lstm2 proj K1024", 8192, 4096, 1024, 0, 0, 0, 0, 0, 1},
+      {"lstm1 proj K320", 8192, 2048, 320, 0, 0, 0, 0, 0, 1},
+      {"lstm2 dW_ih/hh s1", 4096, 1024, 8192, 1, 1, 0, 0, 0, 1},
+      {"lstm2 dW_ih l0 s1", 4096, 512, 8192, 1, 1, 0, 0, 0, 1},
+      {"lstm2 dW_ih l0 s2", 4096, 512, 8192, 1, 1, 0, 0, 0, 2},
+      {"lstm2 dx l1", 8192, 1024, 4096, 0, 1, 0, 0, 0, 1},
+      {"lstm2 dx l0", 8192, 512, 4096, 0, 1, 0, 0, 0, 1},
+  };
+  float *A, *B, *Cm, *ws;
+  const size_t big = (size_t)8192 * 4096;
+  (void)hipMalloc(&A, big * 4);
+  (void)hipMalloc(&B, big * 4);
+  (void)hipMalloc(&Cm, big * 4);
+  (void)hipMalloc(&ws, 4 * big * 4);
+  (void)hipMemset(A, 0, big * 4);
+  (void)hipMemset(B, 0, big * 4);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (const Case& c : cases) {
+    printf("%-20s M=%5d N=%5d K=%5d s=%d :", c.name, c.M, c.N, c.K, c.splits);
+    for (int cfg = 0; cfg < 4; ++cfg) {
+      g_force_cfg = cfg;
+      const int lda = c.at ? c.M : (c.aconv ? c.C : c.K);
+      const int ldb = c.bt ? (c.bconv ? c.C : c.N) : c.K;
+      auto run = [&]() {
+        return autovc_gemm_f32(c.M, c.N, c.K, A, lda, c.at, c.aconv ? T : 0, c.C, -2, B, ldb, c.bt,
+                               c.bconv ? T : 0, c.C, -2, Cm, c.N, nullptr, nullptr, 0, c.splits, ws, 0);
+      };
+      if (run() != 0) { printf(" cfg%d ERR(%s)", cfg, autovc_last_error()); continue; }
+      (void)hipDeviceSynchronize();
+      (void)hipEventRecord(e0, 0);
+      for (int i = 0; i < 10; ++i) run();
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      const double us = ms * 100.0;
+      printf("  cfg%d %7.1fus %6.1fTF", cfg, us, 2.0 * c.M * c.N * c.K / (us * 1e-6) / 1e12);
+      const hipError_t err = hipGetLastError();
+      if (err != hipSuccess) { printf("\nHIP error %s\n", hipGetErrorString(err)); return 1; }
+    }
+    printf("\n");
+  }
+  return 0;
+}

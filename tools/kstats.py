@@ -1,0 +1,14 @@
+"""Summarise a rocprofv3 kernel_stats.csv: per-kernel total/avg and per-step share."""
+import csv
+import sys
+
+path = sys.argv[1]
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
+rows = list(csv.DictReader(open(path)))
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+for r in rows[: int(sys.argv[3]) if len(sys.argv) > 3 else 22]:
+    name = r["Name"].replace("(anonymous namespace)::", "")
+    name = name[: name.find("(")] if "(" in name else name
+    print(f"{float(r['TotalDurationNs'])/1e6/steps:8.3f} ms/step {float(r['Percentage']):6.2f}% "
+          f"n/step={int(r['Calls'])/steps:7.1f} avg={float(r['AverageNs'])/1e3:8.2f}us  {name[:90]}")
+print(f"total {tot/1e6/steps:.3f} ms/step")
