@@ -27,7 +27,8 @@ _SIGS: dict[str, list] = {}
 _RESTYPES = {"autovc_last_error": ctypes.c_char_p,
              "autovc_gemm_workspace_floats": c_i64, "autovc_bn_workspace_bytes": c_i64,
              "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
-             "autovc_colsum_workspace_floats": c_i64}
+             "autovc_colsum_workspace_floats": c_i64, "autovc_wavenet_packed_floats": c_i64,
+             "autovc_wavenet_workspace_bytes": c_i64}
 
 
 def sig(name: str, *argtypes):
@@ -77,6 +78,13 @@ sig("autovc_conv_unpack_grad_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_p
 sig("autovc_transpose_f32", c_int, c_int, c_ptr, c_ptr, c_ptr)
 sig("autovc_colsum_workspace_floats", c_int)
 sig("autovc_colsum_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
+sig("autovc_wavenet_packed_floats", c_int, c_int, c_int, c_int, c_int, c_int)
+sig("autovc_wavenet_workspace_bytes", c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int)
+sig("autovc_wavenet_upsample_f32", c_int, c_int, c_int, c_int, ctypes.POINTER(c_int), c_ptr, c_ptr, c_ptr,
+    c_ptr, c_ptr)
+sig("autovc_wavenet_generate_f32", c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+    c_int, c_int, c_ptr, c_ptr, c_int, ctypes.c_uint64, c_int, c_f32, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
+    c_int, c_ptr)
 
 
 class HipLibraryError(RuntimeError):

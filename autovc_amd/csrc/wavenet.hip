@@ -1,0 +1,626 @@
+// WaveNet vocoder inference (r9y9 wavenet_vocoder 0.1.1 incremental_forward, driven by
+// synthesis.py:44-73) for gfx950.
+//
+// Per output sample the network is a chain of 24 residual layers; every layer needs the
+// whole previous layer's output, so one sample step is a sequence of grid-wide
+// dependencies.  The step is laid out as 2 kernels per layer + 1 head kernel:
+//
+//   gate(l)  : z = W_conv(l) [x_l(t-2d); x_l(t-d); x_l(t)] + pre(l, t)   (512 x 1536)
+//              g = tanh(z[:256]) * sigmoid(z[256:])                       -> gbuf (B x 256)
+//              gate(0) first samples the previous output (MoL head tail + Philox draw)
+//              and builds x_0 = first_conv(input) on the fly.
+//   resid(l) : x_{l+1}(t) = (W_out g + b_out + x_l(t)) * sqrt(.5)       -> ring(l+1)
+//              skips      = (skips + W_skip g + b_skip) * sqrt(.5)        (legacy)
+//   head     : h1 = relu(W1 relu(skips) + b1)
+//
+// pre(l, t) = W_cond(l) c_up(t) + b_cond(l) + b_conv(l) for every layer and sample comes
+// from ONE MFMA GEMM per time chunk (autovc_gemm_f32) — the conditioning 1x1 convs are
+// sample-independent, so they leave the sequential chain.
+//
+// Layer inputs live in per-layer rings of RING (power of two >= 2*d_max + 1) frames: the
+// dilated taps read ring slots (t - j*d) & (RING-1); slots before t = 0 are zero, as the
+// reference's zero-initialised conv input buffers.
+//
+// Every kernel reads the current step t from a device counter slot and forwards it to the
+// next slot, so a captured hipGraph of S steps replays for any t (graph mode).
+#include "common.h"
+#include "../../include/autovc_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+namespace {
+
+constexpr float kSqrtHalf = 0.70710677f;  // float(math.sqrt(0.5))
+constexpr int kBT = 8;                    // utterances per batch tile
+constexpr int kMaxNO = 32;                // MoL head width limit (3 x up to 10 mixtures)
+constexpr int kCtrSlots = 128;
+constexpr int kGateWaves = 6;             // waves per gate workgroup (K = 3 x 512 = 6 chunks of 256)
+
+struct WnArgs {
+  int B, T, R, G, S, NO, K, RING, n_layers, lps, Tch, legacy;
+  const float* packed;
+  const float* pre;
+  float* ring;
+  float* yin;
+  float* skip;
+  float* h1;
+  float* gbuf;
+  int* ctr;
+  const float* teacher;
+  int teacher_len;
+  float* y_out;
+  float* mol_out;
+  uint32_t seed_lo, seed_hi;
+  int utt_base;
+  float log_scale_min;
+};
+
+// ---- packed weight layout (floats): see autovc_wavenet_packed_floats
+__host__ __device__ inline int64_t layer_floats(const WnArgs& a) {
+  const int H = a.G / 2;
+  return (int64_t)a.G * a.K * a.R + (int64_t)(a.R + a.S) * H + (a.R + a.S);
+}
+__host__ __device__ inline const float* layer_base(const WnArgs& a, int l) {
+  return a.packed + 2 * (int64_t)a.R + l * layer_floats(a);
+}
+__host__ __device__ inline const float* head_base(const WnArgs& a) { return layer_base(a, a.n_layers); }
+
+// ---- Philox4x32-10 uniforms (oracle/wavenet.py philox_uniforms)
+__device__ inline void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ inline float uniform_from_word(uint32_t w) {
+#pragma clang fp contract(off)
+  const double v = ((double)(w >> 9) + 0.5) * 1.1920928955078125e-07;  // 2^-23
+  return (float)(1e-5 + (1.0 - 2e-5) * v);
+}
+
+// sample_from_discretized_mix_logistic (wavenet_vocoder/mixture.py) with Philox uniforms.
+__device__ float mol_sample(const float* y, int nr, int64_t t, int utt, const WnArgs& a) {
+  float u[12];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    uint32_t c[4] = {(uint32_t)t, (uint32_t)utt, (uint32_t)j, 0u};
+    philox(c, a.seed_lo, a.seed_hi);
+    u[4 * j] = uniform_from_word(c[0]);
+    u[4 * j + 1] = uniform_from_word(c[1]);
+    u[4 * j + 2] = uniform_from_word(c[2]);
+    u[4 * j + 3] = uniform_from_word(c[3]);
+  }
+  int best = 0;
+  float bv = -INFINITY;
+  for (int j = 0; j < nr; ++j) {
+    const float uj = j < 10 ? u[j] : 0.5f;  // nr <= 10 is checked on the host
+    const float v = y[j] - logf(-logf(uj));
+    if (v > bv) { bv = v; best = j; }
+  }
+  const float mean = y[nr + best];
+  const float ls = fmaxf(y[2 * nr + best], a.log_scale_min);
+  const float ul = u[10];
+  const float x = mean + expf(ls) * (logf(ul) - logf(1.0f - ul));
+  return fminf(fmaxf(x, -1.0f), 1.0f);
+}
+
+// Butterfly reduction of NV per-lane partial sums over the 64 lanes of a wave: NV-1
+// shuffles for the halving rounds instead of 6*NV.  On return lane L with
+// (L & (64/NV - 1)) == 0 holds the full sum of value L / (64/NV).
+template <int NV>
+__device__ inline float wave_reduce_multi(float (&v)[NV], int lane) {
+  float cur[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) cur[j] = v[j];
+  int n = NV;
+  int m = 32;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    if (n > 1) {
+      const int half = n / 2;
+      const bool up = (lane & m) != 0;
+#pragma unroll
+      for (int j = 0; j < NV / 2; ++j) {
+        if (j < half) {
+          const float keep = up ? cur[j + half] : cur[j];
+          const float send = up ? cur[j] : cur[j + half];
+          cur[j] = keep + __shfl_xor(send, m);
+        }
+      }
+      n = half;
+    } else {
+      cur[0] += __shfl_xor(cur[0], m);
+    }
+    m >>= 1;
+  }
+  return cur[0];
+}
+
+__device__ inline float dot4(f32x4 w, f32x4 x, float acc) {
+  acc += w[0] * x[0];
+  acc += w[1] * x[1];
+  acc += w[2] * x[2];
+  acc += w[3] * x[3];
+  return acc;
+}
+
+__device__ inline f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+__device__ inline int read_step(const WnArgs& a, int slot, int next_delta) {
+  const int t = a.ctr[slot];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[slot + 1 == 2 * a.n_layers + 1 ? 0 : slot + 1] = t + next_delta;
+  return t;
+}
+
+// All step kernels are latency-bound (a few MB per launch spread over 256 CUs), so each
+// wave issues every load it needs before the first use: batch rows beyond the tile are
+// clamped to a valid row (their sums are computed and dropped) instead of branching, and
+// the K dimension of the gate GEMV is split across the waves of a workgroup.
+
+// MoL parameters of step tp = tp1 - 1 (from h1) for the batch tile, then the input of
+// step tp1.  Runs on the whole workgroup (NW waves).  Writes s_in[b].
+template <int NW>
+__device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_mol, float* s_in) {
+  constexpr int MAXR = (kMaxNO + NW - 1) / NW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* hb = head_base(a);
+  const float* W2 = hb + (int64_t)a.S * a.S + a.S;
+  const float* b2 = W2 + (int64_t)a.NO * a.S;
+  const int tp = tp1 - 1;
+  if (tp >= 0) {
+    float acc[MAXR][kBT];
+#pragma unroll
+    for (int q = 0; q < MAXR; ++q)
+#pragma unroll
+      for (int b = 0; b < kBT; ++b) acc[q][b] = 0.f;
+    for (int k = lane * 4; k < a.S; k += 256) {
+      f32x4 h[kBT];
+#pragma unroll
+      for (int b = 0; b < kBT; ++b) h[b] = ld4(a.h1 + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + k);
+      f32x4 w[MAXR];
+#pragma unroll
+      for (int q = 0; q < MAXR; ++q) {
+        const int r = wave + q * NW;
+        w[q] = ld4(W2 + (int64_t)(r < a.NO ? r : 0) * a.S + k);
+      }
+#pragma unroll
+      for (int q = 0; q < MAXR; ++q)
+#pragma unroll
+        for (int b = 0; b < kBT; ++b) acc[q][b] = dot4(w[q], h[b], acc[q][b]);
+    }
+#pragma unroll
+    for (int q = 0; q < MAXR; ++q) {
+      const int r = wave + q * NW;
+      if (r < a.NO) {  // wave-uniform
+        const float v = wave_reduce_multi<kBT>(acc[q], lane);
+        if ((lane & 7) == 0) s_mol[(lane >> 3) * kMaxNO + r] = v + b2[r];
+      }
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nb) {
+    const int b = threadIdx.x;
+    const int gb = b0 + b;
+    float in_v = 0.f;
+    float smp = 0.f;
+    if (tp >= 0) smp = mol_sample(s_mol + b * kMaxNO, a.NO / 3, tp, a.utt_base + gb, a);
+    if (a.teacher != nullptr && tp1 < a.teacher_len) in_v = a.teacher[(int64_t)gb * a.teacher_len + tp1];
+    else if (tp >= 0) in_v = smp;
+    if (s_in) s_in[b] = in_v;
+    if (blockIdx.x == 0) {
+      if (tp1 < a.T) a.yin[(int64_t)gb * a.T + tp1] = in_v;
+      if (tp >= 0) {
+        a.y_out[(int64_t)gb * a.T + tp] = smp;
+        if (a.mol_out)
+          for (int j = 0; j < a.NO; ++j) a.mol_out[((int64_t)gb * a.T + tp) * a.NO + j] = s_mol[b * kMaxNO + j];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// gate(l): one workgroup per gate pair (o, o + G/2) and batch tile; its NW waves split the
+// K = taps*R inputs in 256-float chunks (a chunk never straddles a tap: R % 256 == 0).
+template <int NW, bool L0>
+__global__ __launch_bounds__(64 * NW) void wn_gate_kernel(WnArgs a, int layer, int slot) {
+  __shared__ float s_mol[L0 ? kBT * kMaxNO : 1];
+  __shared__ float s_in[kBT];
+  __shared__ float s_red[NW][2 * kBT];
+  const int t = read_step(a, slot, 0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b0 = blockIdx.y * kBT;
+  const int nb = min(kBT, a.B - b0);
+  if (L0) sample_stage<NW>(a, t, b0, nb, s_mol, s_in);
+  const int H = a.G / 2;
+  const int o = blockIdx.x;
+  const int KR = a.K * a.R;
+  const float* WA = layer_base(a, layer);
+  const float* wa = WA + (int64_t)o * KR;
+  const float* wb = WA + (int64_t)(o + H) * KR;
+  const int d = 1 << (layer % a.lps);
+  float acc[2 * kBT];
+#pragma unroll
+  for (int j = 0; j < 2 * kBT; ++j) acc[j] = 0.f;
+  for (int c = wave; c * 256 < KR; c += NW) {
+    const int kc = c * 256;
+    const int tap = kc / a.R;
+    const int tau = t - (a.K - 1 - tap) * d;
+    if (tau < 0) continue;  // wave-uniform: zero history before the first sample
+    const int k = kc + lane * 4;
+    const int i = k - tap * a.R;
+    const f32x4 va = ld4(wa + k), vb = ld4(wb + k);
+    f32x4 x[kBT];
+    if (L0) {
+      const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
+      float in_v[kBT];
+#pragma unroll
+      for (int b = 0; b < kBT; ++b)
+        in_v[b] = tau == t ? s_in[b] : a.yin[(int64_t)(b0 + (b < nb ? b : 0)) * a.T + tau];
+#pragma unroll
+      for (int b = 0; b < kBT; ++b) {
+        x[b][0] = in_v[b] * fw[0] + fb[0];
+        x[b][1] = in_v[b] * fw[1] + fb[1];
+        x[b][2] = in_v[b] * fw[2] + fb[2];
+        x[b][3] = in_v[b] * fw[3] + fb[3];
+      }
+    } else {
+      const float* xr = a.ring + (((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B + b0) * a.R + i;
+#pragma unroll
+      for (int b = 0; b < kBT; ++b) x[b] = ld4(xr + (int64_t)(b < nb ? b : 0) * a.R);
+    }
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) {
+      acc[b] = dot4(va, x[b], acc[b]);
+      acc[kBT + b] = dot4(vb, x[b], acc[kBT + b]);
+    }
+  }
+  const float s = wave_reduce_multi<2 * kBT>(acc, lane);
+  if ((lane & 3) == 0) s_red[wave][lane >> 2] = s;
+  __syncthreads();
+  if ((int)threadIdx.x < nb) {
+    const int b = threadIdx.x;
+    float za = 0.f, zb = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) { za += s_red[w][b]; zb += s_red[w][kBT + b]; }
+    const int gb = b0 + b;
+    const float* pre = a.pre + ((int64_t)(t % a.Tch) * a.B + gb) * ((int64_t)a.n_layers * a.G) + (int64_t)layer * a.G;
+    za += pre[o];
+    zb += pre[o + H];
+    a.gbuf[(int64_t)gb * H + o] = tanhf(za) * avc_sigmoid(zb);
+  }
+}
+
+// resid(l): one wave per output row of [W_out; W_skip] (the last layer only needs skip).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void wn_resid_kernel(WnArgs a, int layer, int slot) {
+  const int t = read_step(a, slot, 0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b0 = blockIdx.y * kBT;
+  const int nb = min(kBT, a.B - b0);
+  const int H = a.G / 2;
+  const bool last = layer == a.n_layers - 1;
+  const int row = blockIdx.x * NW + wave + (last ? a.R : 0);
+  if (row >= a.R + a.S) return;
+  const float* base = layer_base(a, layer) + (int64_t)a.G * a.K * a.R;
+  const float* w = base + (int64_t)row * H;
+  const float* bias = base + (int64_t)(a.R + a.S) * H;
+  const int slot_t = t & (a.RING - 1);
+  // residual operand, fetched ahead of the reduction
+  float res = 0.f;
+  const int bl = (lane >> 3) < nb ? (lane >> 3) : 0;
+  const int gbl = b0 + bl;
+  if (row < a.R) {
+    res = layer == 0 ? a.yin[(int64_t)gbl * a.T + t] * a.packed[row] + a.packed[a.R + row]
+                     : a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gbl) * a.R + row];
+  }
+  float acc[kBT];
+#pragma unroll
+  for (int b = 0; b < kBT; ++b) acc[b] = 0.f;
+  for (int k = lane * 4; k < H; k += 256) {
+    const f32x4 wv = ld4(w + k);
+    f32x4 g[kBT];
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) g[b] = ld4(a.gbuf + (int64_t)(b0 + (b < nb ? b : 0)) * H + k);
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) acc[b] = dot4(wv, g[b], acc[b]);
+  }
+  const float s = wave_reduce_multi<kBT>(acc, lane);
+  if ((lane & 7) != 0) return;
+  const int b = lane >> 3;
+  if (b >= nb) return;
+  const int gb = b0 + b;
+  const float v = s + bias[row];
+  if (row < a.R) {
+    a.ring[(((int64_t)(layer + 1) * a.RING + slot_t) * a.B + gb) * a.R + row] = (v + res) * kSqrtHalf;
+  } else {
+    float* sp = a.skip + (int64_t)gb * a.S + (row - a.R);
+    if (layer == 0) *sp = v;
+    else *sp = a.legacy ? (*sp + v) * kSqrtHalf : (*sp + v);
+  }
+}
+
+// head: h1 = relu(W1 relu(skips) + b1); advances the step counter.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot) {
+  read_step(a, slot, 1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b0 = blockIdx.y * kBT;
+  const int nb = min(kBT, a.B - b0);
+  const int row = blockIdx.x * NW + wave;
+  if (row >= a.S) return;
+  const float* W1 = head_base(a);
+  const float* b1 = W1 + (int64_t)a.S * a.S;
+  float acc[kBT];
+#pragma unroll
+  for (int b = 0; b < kBT; ++b) acc[b] = 0.f;
+  for (int k = lane * 4; k < a.S; k += 256) {
+    const f32x4 wv = ld4(W1 + (int64_t)row * a.S + k);
+    f32x4 x[kBT];
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) x[b] = ld4(a.skip + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + k);
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) {
+      x[b][0] = fmaxf(x[b][0], 0.f); x[b][1] = fmaxf(x[b][1], 0.f);
+      x[b][2] = fmaxf(x[b][2], 0.f); x[b][3] = fmaxf(x[b][3], 0.f);
+      acc[b] = dot4(wv, x[b], acc[b]);
+    }
+  }
+  const float s = wave_reduce_multi<kBT>(acc, lane);
+  if ((lane & 7) != 0) return;
+  const int b = lane >> 3;
+  if (b >= nb) return;
+  a.h1[(int64_t)(b0 + b) * a.S + row] = fmaxf(s + b1[row], 0.f);
+}
+
+// Sample the last output (step T-1) after the final head.
+__global__ __launch_bounds__(256) void wn_final_sample_kernel(WnArgs a, int tp1) {
+  __shared__ float s_mol[kBT * kMaxNO];
+  const int b0 = blockIdx.y * kBT;
+  sample_stage<4>(a, tp1, b0, min(kBT, a.B - b0), s_mol, nullptr);
+}
+
+__global__ void wn_set_ctr_kernel(int* ctr, int t) { ctr[0] = t; }
+
+// ---- upsample network: 4 x [ConvTranspose2d(1,1,(3,s),stride (1,s),pad (1,0)) + ReLU]
+// One workgroup per (utterance, conditioning frame): time never mixes across frames
+// (kernel == stride), so every stage of a frame stays in LDS; the last stage writes the
+// time-major (T, B, C) conditioning the GEMM consumes.
+constexpr int kUpMaxStages = 8;
+struct UpArgs {
+  int B, Tc, C, n, P;
+  int s[kUpMaxStages];
+  int woff[kUpMaxStages];
+};
+
+__global__ __launch_bounds__(256) void wn_upsample_kernel(UpArgs u, const float* __restrict__ c,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out) {
+  extern __shared__ float lds[];
+  const int frame = blockIdx.x, b = blockIdx.y;
+  const int prev_max = u.P / u.s[u.n - 1];
+  float* buf0 = lds;
+  float* buf1 = lds + u.C * prev_max;
+  for (int f = threadIdx.x; f < u.C; f += blockDim.x) buf0[f] = c[((int64_t)b * u.C + f) * u.Tc + frame];
+  __syncthreads();
+  int n_in = 1;
+  float* in = buf0;
+  float* nxt = buf1;
+  for (int st = 0; st < u.n; ++st) {
+    const int s = u.s[st];
+    const float* ws = w + u.woff[st];  // [3][s]
+    const float bs = bias[st];
+    const int n_out = n_in * s;
+    const bool last = st == u.n - 1;
+    for (int e = threadIdx.x; e < u.C * n_out; e += blockDim.x) {
+      const int f = e % u.C, q = e / u.C;   // q: position within the frame
+      const int p = q / s, j = q - p * s;
+      float acc = bs;
+      // out[f] = sum_k w[k][j] in[f + 1 - k]
+      if (f + 1 < u.C) acc += ws[j] * in[p * u.C + f + 1];
+      acc += ws[s + j] * in[p * u.C + f];
+      if (f >= 1) acc += ws[2 * s + j] * in[p * u.C + f - 1];
+      acc = fmaxf(acc, 0.f);
+      if (last) out[(((int64_t)frame * u.P + q) * u.B + b) * u.C + f] = acc;
+      else nxt[q * u.C + f] = acc;
+    }
+    __syncthreads();
+    float* tmp = in; in = nxt; nxt = tmp;
+    n_in = n_out;
+  }
+}
+
+// ---- graph cache: a captured S-step graph depends only on WnArgs and S.
+struct GraphKey {
+  WnArgs a;
+  int steps;
+  int device;
+  bool operator<(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) < 0; }
+};
+std::mutex g_mu;
+std::map<GraphKey, hipGraphExec_t> g_graphs;
+std::vector<GraphKey> g_order;
+hipStream_t g_capture_stream[64] = {};
+
+int enqueue_step(const WnArgs& a, hipStream_t s) {
+  const int H = a.G / 2;
+  const dim3 bt(1, (a.B + kBT - 1) / kBT);
+  for (int l = 0; l < a.n_layers; ++l) {
+    if (l == 0) {
+      hipLaunchKernelGGL((wn_gate_kernel<kGateWaves, true>), dim3(H, bt.y), dim3(64 * kGateWaves), 0, s, a, 0, 0);
+    } else {
+      hipLaunchKernelGGL((wn_gate_kernel<kGateWaves, false>), dim3(H, bt.y), dim3(64 * kGateWaves), 0, s, a, l, 2 * l);
+    }
+    const int rows = (l == a.n_layers - 1) ? a.S : a.R + a.S;
+    hipLaunchKernelGGL((wn_resid_kernel<4>), dim3((rows + 3) / 4, bt.y), dim3(256), 0, s, a, l, 2 * l + 1);
+  }
+  hipLaunchKernelGGL((wn_head_kernel<4>), dim3((a.S + 3) / 4, bt.y), dim3(256), 0, s, a, 2 * a.n_layers);
+  AVC_CHECK_LAUNCH("autovc_wavenet_generate_f32");
+  return avc::kOk;
+}
+
+int get_graph(const WnArgs& a, int steps, hipGraphExec_t* out) {
+  int dev = 0;
+  AVC_HIP(hipGetDevice(&dev), "hipGetDevice");
+  GraphKey key;
+  memset(&key, 0, sizeof(key));
+  key.a = a;
+  key.steps = steps;
+  key.device = dev;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_graphs.find(key);
+  if (it != g_graphs.end()) { *out = it->second; return avc::kOk; }
+  if (dev < 0 || dev >= 64) { avc::set_error("wavenet: device index %d", dev); return avc::kErrArg; }
+  if (!g_capture_stream[dev]) AVC_HIP(hipStreamCreateWithFlags(&g_capture_stream[dev], hipStreamNonBlocking), "hipStreamCreate");
+  hipStream_t cs = g_capture_stream[dev];
+  AVC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+  int rc = avc::kOk;
+  for (int i = 0; i < steps && rc == avc::kOk; ++i) rc = enqueue_step(a, cs);
+  hipGraph_t graph = nullptr;
+  const hipError_t e = hipStreamEndCapture(cs, &graph);
+  if (rc != avc::kOk) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+  AVC_HIP(e, "hipStreamEndCapture");
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  AVC_HIP(ei, "hipGraphInstantiate");
+  if (g_order.size() >= 8) {  // bounded cache: drop the oldest graph
+    auto old = g_graphs.find(g_order.front());
+    if (old != g_graphs.end()) { (void)hipGraphExecDestroy(old->second); g_graphs.erase(old); }
+    g_order.erase(g_order.begin());
+  }
+  g_graphs[key] = exec;
+  g_order.push_back(key);
+  *out = exec;
+  return avc::kOk;
+}
+
+int64_t ring_frames(int n_layers, int lps, int K) {
+  const int64_t dmax = (int64_t)1 << (std::min(n_layers, lps) - 1);
+  const int64_t need = (K - 1) * dmax + 1;
+  int64_t r = 1;
+  while (r < need) r <<= 1;
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t autovc_wavenet_packed_floats(int n_layers, int taps, int R, int G, int S, int n_out) {
+  if (n_layers <= 0 || taps <= 0 || R <= 0 || G <= 0 || S <= 0 || n_out <= 0) return -1;
+  const int64_t H = G / 2;
+  const int64_t per = (int64_t)G * taps * R + (int64_t)(R + S) * H + (R + S);
+  return 2 * (int64_t)R + n_layers * per + (int64_t)S * S + S + (int64_t)n_out * S + n_out;
+}
+
+int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_per_stack, int taps, int R, int G,
+                                       int S) {
+  if (B <= 0 || T <= 0 || n_layers <= 0 || layers_per_stack <= 0 || taps <= 0) return -1;
+  const int64_t ring = (int64_t)(n_layers + 1) * ring_frames(n_layers, layers_per_stack, taps) * B * R;
+  const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + (int64_t)B * (G / 2);
+  return floats * 4 + kCtrSlots * 4 + 256;
+}
+
+int autovc_wavenet_upsample_f32(int B, int Tc, int C, int n_stages, const int* scales, const float* c,
+                                const float* w, const float* bias, float* out, hipStream_t stream) {
+  AVC_CHECK_ARG(B > 0 && Tc > 0 && C > 0 && n_stages > 0 && n_stages <= kUpMaxStages,
+                "autovc_wavenet_upsample_f32: bad dims B=%d Tc=%d C=%d n=%d", B, Tc, C, n_stages);
+  AVC_CHECK_ARG(scales && c && w && bias && out, "autovc_wavenet_upsample_f32: null pointer");
+  UpArgs u;
+  memset(&u, 0, sizeof(u));
+  u.B = B; u.Tc = Tc; u.C = C; u.n = n_stages; u.P = 1;
+  int off = 0;
+  for (int i = 0; i < n_stages; ++i) {
+    AVC_CHECK_ARG(scales[i] > 0, "autovc_wavenet_upsample_f32: scale %d", scales[i]);
+    u.s[i] = scales[i];
+    u.woff[i] = off;
+    off += 3 * scales[i];
+    u.P *= scales[i];
+  }
+  const int64_t lds = (int64_t)C * (u.P / u.s[n_stages - 1]) * 2 * 4;
+  AVC_CHECK_ARG(lds <= 160 * 1024, "autovc_wavenet_upsample_f32: C * prod(scales[:-1]) too large for LDS");
+  hipLaunchKernelGGL(wn_upsample_kernel, dim3(Tc, B), dim3(256), (size_t)lds, stream, u, c, w, bias, out);
+  AVC_CHECK_LAUNCH("autovc_wavenet_upsample_f32");
+  return avc::kOk;
+}
+
+int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int layers_per_stack, int taps, int R,
+                                int G, int S, int n_out, int legacy, const float* packed, const float* pre, int Tch,
+                                uint64_t seed, int utt_base, float log_scale_min, const float* teacher,
+                                int teacher_len, float* y_out, float* mol_out, void* workspace, int graph_steps,
+                                hipStream_t stream) {
+  static const char* fn = "autovc_wavenet_generate_f32";
+  AVC_CHECK_ARG(B > 0 && T > 0 && 0 <= t0 && t0 < t1 && t1 <= T, "%s: bad range B=%d T=%d t=[%d,%d)", fn, B, T, t0, t1);
+  AVC_CHECK_ARG(Tch > 0 && t1 - t0 <= Tch, "%s: chunk [%d,%d) longer than the conditioning chunk %d", fn, t0, t1, Tch);
+  AVC_CHECK_ARG(n_layers >= 1 && 2 * n_layers + 1 < kCtrSlots && layers_per_stack >= 1 && layers_per_stack <= 16 &&
+                    taps >= 1,
+                "%s: bad layer structure layers=%d per_stack=%d taps=%d", fn, n_layers, layers_per_stack, taps);
+  AVC_CHECK_ARG(R > 0 && R % 256 == 0 && G > 0 && G % 512 == 0 && S > 0 && S % 256 == 0,
+                "%s: channel counts must be multiples of 256 (R=%d, G/2=%d, S=%d)", fn, R, G / 2, S);
+  AVC_CHECK_ARG(n_out % 3 == 0 && n_out / 3 >= 1 && n_out / 3 <= 10 && n_out <= kMaxNO,
+                "%s: out_channels %d is not 3 x (1..10) logistic mixtures", fn, n_out);
+  AVC_CHECK_ARG(packed && pre && y_out && workspace, "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(packed) && AVC_ALIGNED16(workspace), "%s: packed/workspace must be 16-byte aligned", fn);
+  AVC_CHECK_ARG(teacher == nullptr || (teacher_len >= 0 && teacher_len <= T), "%s: teacher_len %d", fn, teacher_len);
+  AVC_CHECK_ARG(graph_steps >= 0 && graph_steps <= 4096, "%s: graph_steps %d", fn, graph_steps);
+
+  auto round64 = [](int64_t n) { return (n + 63) / 64 * 64; };
+  const int RING = (int)ring_frames(n_layers, layers_per_stack, taps);
+  float* ws = static_cast<float*>(workspace);
+  WnArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = B; a.T = T; a.R = R; a.G = G; a.S = S; a.NO = n_out; a.K = taps; a.RING = RING;
+  a.n_layers = n_layers; a.lps = layers_per_stack; a.Tch = Tch; a.legacy = legacy ? 1 : 0;
+  a.packed = packed; a.pre = pre;
+  a.ring = ws;                 ws += round64((int64_t)(n_layers + 1) * RING * B * R);
+  a.yin = ws;                  ws += round64((int64_t)B * T);
+  a.skip = ws;                 ws += round64((int64_t)B * S);
+  a.h1 = ws;                   ws += round64((int64_t)B * S);
+  a.gbuf = ws;                 ws += round64((int64_t)B * (G / 2));
+  a.ctr = reinterpret_cast<int*>(ws);
+  a.teacher = teacher; a.teacher_len = teacher ? teacher_len : 0;
+  a.y_out = y_out; a.mol_out = mol_out;
+  a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32);
+  a.utt_base = utt_base; a.log_scale_min = log_scale_min;
+  const int64_t used = reinterpret_cast<char*>(a.ctr + kCtrSlots) - static_cast<char*>(workspace);
+  AVC_CHECK_ARG(used <= autovc_wavenet_workspace_bytes(B, T, n_layers, layers_per_stack, taps, R, G, S),
+                "%s: workspace layout overflow", fn);
+
+  if (t0 == 0) AVC_HIP(hipMemsetAsync(workspace, 0, (size_t)used, stream), "hipMemsetAsync");
+  hipLaunchKernelGGL(wn_set_ctr_kernel, dim3(1), dim3(1), 0, stream, a.ctr, t0);
+  AVC_CHECK_LAUNCH(fn);
+  int t = t0;
+  if (graph_steps > 0 && t1 - t0 >= graph_steps) {
+    hipGraphExec_t exec = nullptr;
+    const int rc = get_graph(a, graph_steps, &exec);
+    if (rc != avc::kOk) return rc;
+    for (; t + graph_steps <= t1; t += graph_steps) AVC_HIP(hipGraphLaunch(exec, stream), "hipGraphLaunch");
+  }
+  for (; t < t1; ++t) {
+    const int rc = enqueue_step(a, stream);
+    if (rc != avc::kOk) return rc;
+  }
+  if (t1 == T) {
+    hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);
+    AVC_CHECK_LAUNCH(fn);
+  }
+  return avc::kOk;
+}
+
+}  // extern "C"

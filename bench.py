@@ -82,6 +82,72 @@ def lstm_roofline(solver, B, T, dev):
             "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(us, 3)}
 
 
+def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=True):
+    """BASELINE config 4 / SURVEY §8d C4: r9y9 WaveNet (24 layers, 512 residual channels),
+    8 utterances x 128 conditioning frames (32,768 samples = 2.048 s each) synthesised in one
+    batch.  Timed: the whole job (upsample, per-chunk conditioning GEMM, every sample step
+    incl. sampling).  Roofline: weight streaming — every sample step reads the packed
+    per-step weights once (98.6 MB fp32)."""
+    from autovc_amd import _lib, synthesis
+    from autovc_amd.hparams import hparams
+    torch.manual_seed(4322)
+    model = synthesis.build_model()
+    model.make_generation_fast_()
+    model = model.to(dev).eval()
+    g = torch.Generator().manual_seed(4321)
+    c = torch.clamp(torch.randn(n_utt, 80, Tc, generator=g) * 0.18 + 0.43, 0, 1).to(dev)
+    T = Tc * hparams.hop_size
+    model.generate(c[:, :, : max(1, warmup_steps // hparams.hop_size)], seed=1, log_scale_min=hparams.log_scale_min)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    y = model.generate(c, seed=2, log_scale_min=hparams.log_scale_min)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert y.shape == (n_utt, T) and bool(torch.isfinite(y).all())
+    packed = _lib.load().autovc_wavenet_packed_floats(model.layers, model.kernel_size, model.residual_channels,
+                                                       model.gate_channels, model.skip_out_channels,
+                                                       model.out_channels)
+    step_bytes = 4 * packed
+    achieved = step_bytes * T / dt / 1e9
+    out = {"workload": f"r9y9 WaveNet incremental synthesis, {n_utt} utterances x {T} samples (16 kHz), fp32",
+           "samples_per_s": round(n_utt * T / dt, 1), "rtf_aggregate": round(n_utt * T / dt / 16000.0, 3),
+           "rtf_per_stream": round(T / 16000.0 / dt, 3), "wall_s": round(dt, 3),
+           "us_per_sample_step": round(dt / T * 1e6, 2),
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_per_step": step_bytes,
+                        "note": "weight-streaming convention: packed per-step weights once per sample step"}}
+    if cpu:
+        out["cpu_baseline"] = wavenet_cpu_baseline(n_utt, seconds_cpu)
+        out["vs_cpu_baseline"] = round(out["samples_per_s"] / out["cpu_baseline"]["value"], 1)
+    return out
+
+
+def wavenet_cpu_baseline(n_utt, seconds):
+    """oracle/wavenet.py (fp32 torch CPU ops, the reference's own per-step structure) on a
+    bounded number of sample steps of the same batch."""
+    from oracle import wavenet as ow
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    hp = ow.HPARAMS
+    o = ow.OracleWaveNet(ow.make_weights(hp), hp, dtype=torch.float32)
+    g = torch.Generator().manual_seed(4321)
+    c = torch.clamp(torch.randn(n_utt, 80, 1, generator=g) * 0.18 + 0.43, 0, 1)
+    cu = o.upsample(c)
+    steps = 16
+    while True:
+        u = ow.philox_uniforms(3, list(range(n_utt)), 0, steps)
+        t0 = time.perf_counter()
+        o.incremental(cu[:, :, :steps], steps, uniforms=u)
+        dt = time.perf_counter() - t0
+        if dt > seconds / 4 or steps >= 1024:
+            break
+        steps *= 2
+    return {"value": round(n_utt * steps / dt, 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} incremental steps x {n_utt} utterances of oracle/wavenet.py (fp32, torch "
+                      f"{torch.__version__} CPU, {threads} threads), {dt:.2f} s"}
+
+
 def cpu_baseline(B, T, seconds=15.0):
     """The oracle's CPU restatement of the same training step (fused torch CPU LSTM, conv1d,
     batch_norm, Adam — the reference's own CPU ops), timed on this host."""
@@ -122,6 +188,7 @@ def main():
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-wavenet", action="store_true")
     args = ap.parse_args()
 
     from autovc_amd import ddp
@@ -162,6 +229,11 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(B, T)
+    wn = None
+    if not args.no_wavenet:
+        # config 4 per GPU (vocoder batches shard with no collective): every rank synthesises
+        # its own 8 utterances; rank 0 reports the per-GPU rate
+        wn = wavenet_bench(dev, cpu=(not args.no_cpu_baseline and rank == 0 and world == 1))
 
     if rank == 0:
         value = world * B * T * args.steps / dt
@@ -175,6 +247,7 @@ def main():
                        "dim_neck": 32, "dim_emb": 256, "dim_pre": 512, "freq": 32},
             "final_loss": round(last_loss, 6),
             "roofline": roof, "cpu_baseline": cpu,
+            "wavenet": wn,
         }
         if cpu:
             line["vs_cpu_baseline"] = round(value / cpu["value"], 2)

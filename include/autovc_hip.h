@@ -162,6 +162,47 @@ int64_t autovc_colsum_workspace_floats(int N);
 int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, float* out2,
                       int accumulate, float* workspace, hipStream_t stream);
 
+/* ---------------------------------------------------------------- WaveNet vocoder
+ * Replaces wavenet_vocoder 0.1.1 WaveNet.incremental_forward as called by
+ * synthesis.py:67-69 (third-party, absent from the reference tree; restated in
+ * oracle/wavenet.py, parity unpinned).
+ *
+ * upsample: the upsample_conv stack (n_stages x [ConvTranspose2d(1,1,(3,s),stride (1,s),
+ *   pad (1,0)) + ReLU], hparams.py:110-114).  c (B, C, Tc) as wavegen builds it
+ *   (synthesis.py:57), w = per-stage (3, s) kernels concatenated, bias[n_stages];
+ *   out (Tc*prod(s), B, C) time-major.
+ *
+ * generate: runs sample steps t0 <= t < t1 of the incremental loop for B utterances.
+ *   packed   weights after make_generation_fast_ (weight norm folded), floats:
+ *              first_conv w[R], b[R];
+ *              per layer: conv (G, taps*R) linearised (o, tap, i) [tap 0 = oldest],
+ *                         [conv1x1_out (R, G/2); conv1x1_skip (S, G/2)], their biases [R+S];
+ *              last_conv_layers.1 W (S, S), b[S]; last_conv_layers.3 W (n_out, S), b[n_out]
+ *            (autovc_wavenet_packed_floats gives the size)
+ *   pre      (Tch, B, n_layers*G): conditioning 1x1 + both biases of every layer; row
+ *            (t % Tch) must hold step t (one autovc_gemm_f32 over the upsampled c per chunk)
+ *   seed, utt_base: Philox4x32-10 key and the global index of utterance 0 (the draw of
+ *            sample t of utterance u depends only on (seed, u, t))
+ *   teacher  optional (B, teacher_len): the input at step t < teacher_len (test_inputs)
+ *   y_out    (B, T) samples; mol_out optional (B, T, n_out) head outputs
+ *   workspace autovc_wavenet_workspace_bytes; zeroed by the call with t0 == 0 and carried
+ *            to the following chunks
+ *   graph_steps > 0 replays a captured hipGraph of that many steps (cached per argument
+ *            set); 0 launches the kernels directly.
+ */
+int64_t autovc_wavenet_packed_floats(int n_layers, int taps, int R, int G, int S, int n_out);
+int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_per_stack, int taps,
+                                       int R, int G, int S);
+int autovc_wavenet_upsample_f32(int B, int Tc, int C, int n_stages, const int* scales /* host */,
+                                const float* c, const float* w, const float* bias, float* out,
+                                hipStream_t stream);
+int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int layers_per_stack,
+                                int taps, int R, int G, int S, int n_out, int legacy,
+                                const float* packed, const float* pre, int Tch, uint64_t seed,
+                                int utt_base, float log_scale_min, const float* teacher,
+                                int teacher_len, float* y_out, float* mol_out, void* workspace,
+                                int graph_steps, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,133 @@
+"""WaveNet vocoder on the MI355X (libautovc_hip.so) against the CPU restatement
+oracle/wavenet.py (parity UNPINNED upstream: see tests/test_oracle_wavenet.py).
+
+Bars (WaveNet row):
+  (1) teacher-forced per-step MoL parameters: <= 1e-4 relative (max-abs / max);
+  (2) deterministic sampling with the shared Philox uniforms: every sample within 1e-4;
+  (3) output length 256 * Tc, samples in [-1, 1].
+Plus properties of the HIP path itself: hipGraph replay == direct launches (bit-exact),
+batch / shard / chunk invariance, and the reference's error behaviour."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import wavenet as ow
+
+pytestmark = pytest.mark.gpu
+
+LSM = ow.HPARAMS["log_scale_min"]
+
+
+def _model(hp, cuda, seed=4322):
+    from autovc_amd.wavenet import WaveNet
+    m = WaveNet(out_channels=hp["out_channels"], layers=hp["layers"], stacks=hp["stacks"],
+                residual_channels=hp["residual_channels"], gate_channels=hp["gate_channels"],
+                skip_out_channels=hp["skip_out_channels"], kernel_size=hp["kernel_size"],
+                cin_channels=hp["cin_channels"], upsample_conditional_features=True,
+                upsample_scales=list(hp["upsample_scales"]), scalar_input=True, legacy=True)
+    m.make_generation_fast_()
+    W = ow.make_weights(hp, seed)
+    m.load_state_dict(W)
+    return m.to(cuda).eval(), W
+
+
+def _cond(B, Tc, seed=4321):
+    rs = np.random.RandomState(seed)
+    return torch.from_numpy(np.clip(rs.normal(0.43, 0.18, (B, 80, Tc)), 0, 1).astype(np.float32))
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def test_upsample_matches_oracle(cuda):
+    hp = ow.small_hparams()
+    m, W = _model(hp, cuda)
+    c = _cond(3, 5)
+    got = m.upsample(c.to(cuda)).permute(1, 2, 0)          # (T, B, C) -> (B, C, T)
+    want = ow.OracleWaveNet(W, hp).upsample(c)
+    assert got.shape == want.shape == (3, 80, 5 * 256)
+    assert rel(got, want) < 1e-6
+
+
+@pytest.mark.parametrize("B,layers,stacks", [(3, 24, 4), (9, 6, 2)])
+def test_teacher_forced_mol_and_samples(cuda, B, layers, stacks):
+    hp = ow.small_hparams(layers=layers, stacks=stacks)
+    m, W = _model(hp, cuda)
+    c = _cond(B, 2)
+    T = 512
+    rs = np.random.RandomState(11)
+    teacher = torch.from_numpy(rs.uniform(-0.9, 0.9, (B, T)).astype(np.float32))
+    seed = 1234567
+    y, mol = m.generate(c.to(cuda), T=T, seed=seed, teacher=teacher.to(cuda), return_mol=True, log_scale_min=LSM)
+    o = ow.OracleWaveNet(W, hp)
+    u = ow.philox_uniforms(seed, list(range(B)), 0, T)
+    y_ref, mol_ref = o.incremental(o.upsample(c), T, uniforms=u, teacher=teacher.double(), return_mol=True)
+    assert rel(mol, mol_ref) < 1e-4
+    assert (y.double().cpu() - y_ref).abs().max().item() < 1e-4
+
+
+def test_free_running_matches_oracle(cuda):
+    hp = ow.HPARAMS
+    m, W = _model(hp, cuda)
+    c = _cond(2, 2, seed=7)
+    seed = 2024
+    y = m.generate(c.to(cuda), seed=seed, log_scale_min=LSM)
+    o = ow.OracleWaveNet(W, hp)
+    u = ow.philox_uniforms(seed, [0, 1], 0, 512)
+    y_ref = o.incremental(o.upsample(c), 512, uniforms=u)
+    assert y.shape == (2, 512)
+    assert (y.double().cpu() - y_ref).abs().max().item() < 1e-4
+
+
+def test_graph_replay_is_bit_exact(cuda):
+    hp = ow.small_hparams()
+    m, _ = _model(hp, cuda)
+    c = _cond(4, 2).to(cuda)
+    a = m.generate(c, seed=5, log_scale_min=LSM, graph_steps=0)
+    b = m.generate(c, seed=5, log_scale_min=LSM, graph_steps=32)
+    d = m.generate(c, seed=5, log_scale_min=LSM, graph_steps=7)      # graph + direct remainder
+    assert torch.equal(a, b) and torch.equal(a, d)
+
+
+def test_batch_shard_and_chunk_invariance(cuda):
+    hp = ow.small_hparams()
+    m, _ = _model(hp, cuda)
+    c = _cond(3, 2).to(cuda)
+    full = m.generate(c, seed=77, log_scale_min=LSM)
+    alone = m.generate(c[2:3], seed=77, utt_base=2, log_scale_min=LSM)
+    chunked = m.generate(c, seed=77, log_scale_min=LSM, chunk=96)
+    assert (full[2:3] - alone).abs().max().item() < 1e-5
+    assert (full - chunked).abs().max().item() < 1e-5
+
+
+def test_wavegen_api(cuda):
+    from autovc_amd import synthesis
+    torch.manual_seed(0)
+    model = synthesis.build_model().to(cuda)      # r9y9 init, weight norm still attached
+    torch.manual_seed(0)
+    mel = np.clip(np.random.RandomState(3).normal(0.43, 0.18, (3, 80)), 0, 1).astype(np.float32)
+    y = synthesis.wavegen(model, c=mel)
+    assert y.shape == (3 * 256,) and y.dtype == np.float32
+    assert np.isfinite(y).all() and np.abs(y).max() <= 1.0
+    mels = [mel, mel[:2]]
+    ys = synthesis.wavegen_batch(model, mels, seed=9)
+    assert [len(v) for v in ys] == [768, 512]
+    solo = synthesis.wavegen_batch(model, [mel[:2]], seed=9, utt_offset=1)[0]
+    assert np.abs(solo - ys[1]).max() < 1e-5
+
+
+def test_error_behaviour(cuda):
+    hp = ow.small_hparams()
+    m, _ = _model(hp, cuda)
+    c = _cond(1, 1).to(cuda)
+    with pytest.raises(ValueError):
+        m.generate(c, T=100)
+    m.train()
+    with pytest.raises(RuntimeError, match="eval"):
+        m.generate(c)
+    m.eval()
+    with pytest.raises(RuntimeError, match="cuda"):
+        m.generate(c.cpu())
