@@ -121,33 +121,35 @@ __device__ float mol_sample(const float* y, int nr, int64_t t, int utt, const Wn
 
 // Butterfly reduction of NV per-lane partial sums over the 64 lanes of a wave: NV-1
 // shuffles for the halving rounds instead of 6*NV.  On return lane L with
-// (L & (64/NV - 1)) == 0 holds the full sum of value L / (64/NV).
+// (L & (64/NV - 1)) == 0 holds the full sum of value L / (64/NV).  Every array index is a
+// compile-time constant (template recursion): a runtime index would make the compiler
+// demote the array to LDS, which costs ~15 us per launch.
+template <int N, int M>
+__device__ inline void butterfly(float* cur, int lane) {
+  if constexpr (M >= 1) {
+    if constexpr (N > 1) {
+      const bool up = (lane & M) != 0;
+#pragma unroll
+      for (int j = 0; j < N / 2; ++j) {
+        const float keep = up ? cur[j + N / 2] : cur[j];
+        const float send = up ? cur[j] : cur[j + N / 2];
+        cur[j] = keep + __shfl_xor(send, M);
+      }
+      butterfly<N / 2, M / 2>(cur, lane);
+    } else {
+      cur[0] += __shfl_xor(cur[0], M);
+      butterfly<1, M / 2>(cur, lane);
+    }
+  }
+}
+
 template <int NV>
 __device__ inline float wave_reduce_multi(float (&v)[NV], int lane) {
+  static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "power-of-two value count");
   float cur[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) cur[j] = v[j];
-  int n = NV;
-  int m = 32;
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    if (n > 1) {
-      const int half = n / 2;
-      const bool up = (lane & m) != 0;
-#pragma unroll
-      for (int j = 0; j < NV / 2; ++j) {
-        if (j < half) {
-          const float keep = up ? cur[j + half] : cur[j];
-          const float send = up ? cur[j] : cur[j + half];
-          cur[j] = keep + __shfl_xor(send, m);
-        }
-      }
-      n = half;
-    } else {
-      cur[0] += __shfl_xor(cur[0], m);
-    }
-    m >>= 1;
-  }
+  butterfly<NV, 32>(cur, lane);
   return cur[0];
 }
 
