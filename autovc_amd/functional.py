@@ -68,11 +68,15 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
 def _splits_for(M, N, K):
     """Split-K factor for the long-K weight-gradient GEMMs: >= 1024 blocks of 64x64 output
     tiles (4 per CU) while each split keeps >= 1024 k (tools/gemm_bench.hip sweep: conv dW
-    512x2560x8192 42.7 TF unsplit -> 81.6 TF at 4 splits)."""
+    512x2560x8192 42.7 TF unsplit -> 81.6 TF at 4 splits).  Tiny outputs (the BLSTM weight
+    gradients, 128 x 32..512 over K = B*T = 8192: 2-16 tiles) split deep instead — up to 64
+    ways with >= 256 k each — so the serial k loop stops dominating (42 us -> a few us)."""
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     s = 1
     while tiles * s < 1024 and K // (s + 1) >= 1024 and s < 8:
         s += 1
+    if tiles < 64:
+        s = max(s, min(64, K // 256, max(1, 1024 // tiles)))
     return s
 
 

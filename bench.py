@@ -132,8 +132,8 @@ def wavenet_cpu_baseline(n_utt, seconds):
     hp = ow.HPARAMS
     o = ow.OracleWaveNet(ow.make_weights(hp), hp, dtype=torch.float32)
     g = torch.Generator().manual_seed(4321)
-    c = torch.clamp(torch.randn(n_utt, 80, 1, generator=g) * 0.18 + 0.43, 0, 1)
-    cu = o.upsample(c)
+    c = torch.clamp(torch.randn(n_utt, 80, 4, generator=g) * 0.18 + 0.43, 0, 1)
+    cu = o.upsample(c)          # 1024 samples: enough for the largest sample below
     steps = 16
     while True:
         u = ow.philox_uniforms(3, list(range(n_utt)), 0, steps)
