@@ -72,15 +72,20 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
     brow[i] = brow_of(r) + 4 * sl;
   }
   const int nc = K / KCH;
+  // Loads run D chunks ahead.  They are issued unconditionally (past the last chunk the
+  // address is clamped to the last chunk, an L2 hit) so the k loop is straight-line code
+  // and hipcc can wait with vmcnt(4 (D-1)) for the oldest chunk only: a conditional load
+  // makes it wait vmcnt(0) at the join, which silently degrades D > 1 to D = 1.
   f32x4 sa[D][C::PER], sb[D][C::PER];
 #pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (d < nc)
+  for (int d = 0; d < D; ++d) {
+    const int cl = min(d, nc - 1);
 #pragma unroll
-      for (int i = 0; i < C::PER; ++i) {
-        sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + d * KCH);
-        sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + d * KCH);
-      }
+    for (int i = 0; i < C::PER; ++i) {
+      sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + cl * KCH);
+      sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + cl * KCH);
+    }
+  }
   const int q = w & 3, kh = w >> 2, g = lane >> 4;
   const int ra = (q >> 1) * 16 + (lane & 15), rb = (q & 1) * 16 + (lane & 15);
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -88,20 +93,20 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const int c = c0 + d;
+      float* L = lds + (c & 1) * C::CF;
+#pragma unroll
+      for (int i = 0; i < C::PER; ++i) {
+        *reinterpret_cast<f32x4*>(L + srow[i] * KCH + 4 * spos[i]) = sa[d][i];
+        *reinterpret_cast<f32x4*>(L + (TB + srow[i]) * KCH + 4 * spos[i]) = sb[d][i];
+      }
+      __syncthreads();   // chunk c visible; buffer (c+1)&1 no longer read (last read at c-1)
+      const int cn = min(c + D, nc - 1);
+#pragma unroll
+      for (int i = 0; i < C::PER; ++i) {
+        sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + cn * KCH);
+        sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + cn * KCH);
+      }
       if (c < nc) {
-        float* L = lds + (c & 1) * C::CF;
-#pragma unroll
-        for (int i = 0; i < C::PER; ++i) {
-          *reinterpret_cast<f32x4*>(L + srow[i] * KCH + 4 * spos[i]) = sa[d][i];
-          *reinterpret_cast<f32x4*>(L + (TB + srow[i]) * KCH + 4 * spos[i]) = sb[d][i];
-        }
-        __syncthreads();   // chunk c visible; buffer (c+1)&1 no longer read (last read at c-1)
-        if (c + D < nc)
-#pragma unroll
-          for (int i = 0; i < C::PER; ++i) {
-            sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + (c + D) * KCH);
-            sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + (c + D) * KCH);
-          }
         f32x4 av[C::SUB], bv[C::SUB];
 #pragma unroll
         for (int s = 0; s < C::SUB; ++s) {
@@ -136,13 +141,13 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
 
 // configuration used by the product kernels (chosen with tools/lstm_step_bench.hip)
 #ifndef AVC_LSTM_KCH
-#define AVC_LSTM_KCH 128
+#define AVC_LSTM_KCH 64
 #endif
 #ifndef AVC_LSTM_NW
 #define AVC_LSTM_NW 8
 #endif
 #ifndef AVC_LSTM_D
-#define AVC_LSTM_D 1
+#define AVC_LSTM_D 2
 #endif
 constexpr int KCH = AVC_LSTM_KCH, NWV = AVC_LSTM_NW, DPF = AVC_LSTM_D;
 using TileP = Tile<KCH, NWV, DPF>;
@@ -224,53 +229,60 @@ struct BwdArgs {
   float* P; int S;                             // (S,B,H) partials or null
 };
 
-// operands of one (b, j) element of the pointwise pass, loaded ahead of use
-struct PointIn {
-  float i_, f_, g_, o_, cc, cp, dh, dcs;
-};
-
-__device__ __forceinline__ PointIn point_load(const BwdArgs& a, int b, int j, int t, int tp, int first) {
-  const int64_t idx = (int64_t)b * a.H + j;
-  const int H = a.H;
-  const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H;
-  PointIn v;
-  v.i_ = gs[j]; v.f_ = gs[H + j]; v.g_ = gs[2 * H + j]; v.o_ = gs[3 * H + j];
-  v.cc = a.c[((int64_t)b * a.T + t) * H + j];
-  v.cp = tp >= 0 ? a.c[((int64_t)b * a.T + tp) * H + j] : 0.f;
-  v.dh = a.dh_out ? a.dh_out[(int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j] : 0.f;
-  v.dcs = first ? 0.f : a.dc_state[idx];
-  return v;
-}
-
-// dh += sum_s P[s] (fixed order), then the cell backward; writes dG[t] and dc_state.
-__device__ __forceinline__ void point_finish(const BwdArgs& a, PointIn v, int b, int j, int t, int first) {
-  const int64_t idx = (int64_t)b * a.H + j;
-  const int64_t BH = (int64_t)a.B * a.H;
-  const int H = a.H;
-  float dh = v.dh;
-  if (!first) {
-    float p[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) p[s] = s < a.S ? a.P[(int64_t)s * BH + idx] : 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) dh += p[s];
-  }
-  const float tc = tanhf(v.cc);
-  const float dc = v.dcs + dh * v.o_ * (1.f - tc * tc);
-  float* d = a.dG + ((int64_t)b * a.T + t) * 4 * H;
-  d[j] = dc * v.g_ * v.i_ * (1.f - v.i_);
-  d[H + j] = dc * v.cp * v.f_ * (1.f - v.f_);
-  d[2 * H + j] = dc * v.i_ * (1.f - v.g_ * v.g_);
-  d[3 * H + j] = dh * tc * v.o_ * (1.f - v.o_);
-  a.dc_state[idx] = dc * v.f_;
-}
-
-// Pointwise pass of the first backward step (no recurrent partials yet): thread per (b, j).
-__global__ void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp, int first) {
+// Pointwise pass of one backward step: thread per (b, j).  Every operand is loaded
+// unconditionally before first use (optional operands are template switches, the previous
+// cell is read at a clamped step and masked): a load behind a runtime condition makes
+// hipcc wait vmcnt(0) per load, serialising a dozen HBM round trips.
+template <int S, bool FIRST, bool HAS_DH>
+__global__ __launch_bounds__(256) void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)a.B * a.H) return;
-  const int b = (int)(idx / a.H), j = (int)(idx % a.H);
-  point_finish(a, point_load(a, b, j, t, tp, first), b, j, t, first);
+  const int64_t BH = (int64_t)a.B * a.H;
+  if (idx >= BH) return;
+  const int H = a.H;
+  const int b = (int)(idx / H), j = (int)(idx % H);
+  const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H;
+  const float i_ = gs[j], f_ = gs[H + j], g_ = gs[2 * H + j], o_ = gs[3 * H + j];
+  const float cc = a.c[((int64_t)b * a.T + t) * H + j];
+  const float cpr = a.c[((int64_t)b * a.T + (tp >= 0 ? tp : t)) * H + j];
+  float dh = 0.f, dcs = 0.f;
+  if (HAS_DH) dh = a.dh_out[(int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j];
+  float p[S];
+  if (!FIRST) {
+    dcs = a.dc_state[idx];
+#pragma unroll
+    for (int s = 0; s < S; ++s) p[s] = a.P[(int64_t)s * BH + idx];
+#pragma unroll
+    for (int s = 0; s < S; ++s) dh += p[s];
+  }
+  const float cp = tp >= 0 ? cpr : 0.f;
+  const float tc = tanhf(cc);
+  const float dc = dcs + dh * o_ * (1.f - tc * tc);
+  float* d = a.dG + ((int64_t)b * a.T + t) * 4 * H;
+  d[j] = dc * g_ * i_ * (1.f - i_);
+  d[H + j] = dc * cp * f_ * (1.f - f_);
+  d[2 * H + j] = dc * i_ * (1.f - g_ * g_);
+  d[3 * H + j] = dh * tc * o_ * (1.f - o_);
+  a.dc_state[idx] = dc * f_;
+}
+
+template <int S>
+void launch_pointwise(int blocks, hipStream_t st, const BwdArgs& a, int t, int tp, bool first) {
+  if (first) {
+    if (a.dh_out) hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, true, true>), dim3(blocks), dim3(256), 0, st, a, t, tp);
+    else hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, true, false>), dim3(blocks), dim3(256), 0, st, a, t, tp);
+  } else {
+    if (a.dh_out) hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, false, true>), dim3(blocks), dim3(256), 0, st, a, t, tp);
+    else hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, false, false>), dim3(blocks), dim3(256), 0, st, a, t, tp);
+  }
+}
+
+void launch_pointwise_any(int blocks, hipStream_t st, const BwdArgs& a, int t, int tp, bool first) {
+  switch (a.S) {
+    case 1: launch_pointwise<1>(blocks, st, a, t, tp, first); break;
+    case 2: launch_pointwise<2>(blocks, st, a, t, tp, first); break;
+    case 4: launch_pointwise<4>(blocks, st, a, t, tp, first); break;
+    default: launch_pointwise<8>(blocks, st, a, t, tp, first); break;
+  }
 }
 
 // Split-K recurrent product P[s][b][j] = sum_{r in split s} dG[b][t][r] W^T[j][r]
@@ -450,8 +462,8 @@ extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int
                                    const float* gates, const float* c_all, const float* W_hh_T, float* dG,
                                    int reverse, int splits, float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H), "autovc_lstm_bwd_f32: bad dims");
-  AVC_CHECK_ARG(splits >= 1 && splits <= 8 && (4 * H) % (64 * splits) == 0,
-                "autovc_lstm_bwd_f32: 4H must split into multiples of 64 (splits <= 8)");
+  AVC_CHECK_ARG((splits == 1 || splits == 2 || splits == 4 || splits == 8) && (4 * H) % (64 * splits) == 0,
+                "autovc_lstm_bwd_f32: splits must be 1, 2, 4 or 8 and 4H must split into multiples of 64");
   AVC_CHECK_ARG(gates && c_all && W_hh_T && dG && workspace, "autovc_lstm_bwd_f32: null pointer");
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_T) && AVC_ALIGNED16(dG), "autovc_lstm_bwd_f32: W_hh_T/dG alignment");
   float* P = workspace;
@@ -464,7 +476,7 @@ extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int
     const int t = reverse ? T - 1 - s : s;
     const int tp = s == 0 ? -1 : (reverse ? t + 1 : t - 1);
     const int first = s == T - 1;
-    hipLaunchKernelGGL(lstm_bwd_pointwise_kernel, dim3(pw_blocks), dim3(256), 0, stream, a, t, tp, first);
+    launch_pointwise_any(pw_blocks, stream, a, t, tp, first);
     if (s == 0) continue;
     if ((4 * H / splits) % KCH == 0)
       hipLaunchKernelGGL((lstm_bwd_rec_kernel<KCH, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,

@@ -77,16 +77,16 @@ int main() {
     const dim3 grid(H / UT, (B + TB - 1) / TB);
     printf("H=%d empty %.2f us\n", H, timeit([&](int s, hipEvent_t e0, hipEvent_t e1) {
       hipExtLaunchKernelGGL(empty_kernel, grid, dim3(256), 0, 0, e0, e1, 0, a, s, s - 1); }, T, 3));
-    printf("H=%d fwd k64w4d2 %.2f | k64w4d1 %.2f | k128w4d2 %.2f | k128w4d1 %.2f | k64w8d2 %.2f | k128w8d2 %.2f | k128w8d1 %.2f | k256w8d1 %.2f\n", H,
-           fwd<0, 64, 4, 2>(a, T), fwd<0, 64, 4, 1>(a, T), fwd<0, 128, 4, 2>(a, T), fwd<0, 128, 4, 1>(a, T),
-           fwd<0, 64, 8, 2>(a, T), fwd<0, 128, 8, 2>(a, T), fwd<0, 128, 8, 1>(a, T), fwd<0, 256, 8, 1>(a, T));
+    printf("H=%d fwd k64w8d1 %.2f | k64w8d2 %.2f | k64w8d3 %.2f | k64w8d4 %.2f | k128w8d1 %.2f | k128w8d2 %.2f | k128w8d3 %.2f | k128w4d2 %.2f\n", H,
+           fwd<0, 64, 8, 1>(a, T), fwd<0, 64, 8, 2>(a, T), fwd<0, 64, 8, 3>(a, T), fwd<0, 64, 8, 4>(a, T),
+           fwd<0, 128, 8, 1>(a, T), fwd<0, 128, 8, 2>(a, T), fwd<0, 128, 8, 3>(a, T), fwd<0, 128, 4, 2>(a, T));
     printf("H=%d fwd default ablations: full %.2f | W-shared %.2f | h-shared %.2f | both %.2f\n", H,
            fwd<0, KCH, NWV, DPF>(a, T), fwd<1, KCH, NWV, DPF>(a, T), fwd<2, KCH, NWV, DPF>(a, T), fwd<3, KCH, NWV, DPF>(a, T));
     for (int S : {4, 2}) {
       if ((4 * H / S) % 256) continue;
-      printf("H=%d rec S=%d k64w4d2 %.2f | k128w4d2 %.2f | k64w8d2 %.2f | k128w8d2 %.2f | k128w8d1 %.2f\n", H, S,
-             rec<64, 4, 2>(B, T, H, g, W, P, S), rec<128, 4, 2>(B, T, H, g, W, P, S), rec<64, 8, 2>(B, T, H, g, W, P, S),
-             rec<128, 8, 2>(B, T, H, g, W, P, S), rec<128, 8, 1>(B, T, H, g, W, P, S));
+      printf("H=%d rec S=%d k64w8d1 %.2f | k64w8d2 %.2f | k64w8d3 %.2f | k128w8d1 %.2f | k128w8d2 %.2f | k128w8d3 %.2f\n", H, S,
+             rec<64, 8, 1>(B, T, H, g, W, P, S), rec<64, 8, 2>(B, T, H, g, W, P, S), rec<64, 8, 3>(B, T, H, g, W, P, S),
+             rec<128, 8, 1>(B, T, H, g, W, P, S), rec<128, 8, 2>(B, T, H, g, W, P, S), rec<128, 8, 3>(B, T, H, g, W, P, S));
     }
     (void)hipFree(gx); (void)hipFree(W); (void)hipFree(h); (void)hipFree(c); (void)hipFree(g); (void)hipFree(P);
   }
