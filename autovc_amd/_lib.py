@@ -76,6 +76,7 @@ sig("autovc_adam_f32", c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_f32, c_f32, c
 sig("autovc_conv_pack_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_conv_unpack_grad_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr)
 sig("autovc_transpose_f32", c_int, c_int, c_ptr, c_ptr, c_ptr)
+sig("autovc_l2norm_rows_f32", c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr)
 sig("autovc_colsum_workspace_floats", c_int)
 sig("autovc_colsum_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_wavenet_packed_floats", c_int, c_int, c_int, c_int, c_int, c_int)

@@ -203,6 +203,25 @@ __global__ void conv_unpack_grad_kernel(int Co, int Ci, int K, const float* __re
 }
 
 // out[c][r] = in[r][c], 32x32 LDS tiles
+// out[m] = x[m] / ||x[m]||_2 (model_bl.py:17-19): one 256-thread workgroup per row, the
+// squares summed in fixed order (per-thread strided partials, then an LDS tree).
+__global__ __launch_bounds__(256) void l2norm_rows_kernel(int N, const float* __restrict__ x, int64_t ldx,
+                                                          float* __restrict__ out, int64_t ldo) {
+  __shared__ float part[256];
+  const float* row = x + (int64_t)blockIdx.x * ldx;
+  float s = 0.f;
+  for (int n = threadIdx.x; n < N; n += 256) s += row[n] * row[n];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float norm = sqrtf(part[0]);
+  float* o = out + (int64_t)blockIdx.x * ldo;
+  for (int n = threadIdx.x; n < N; n += 256) o[n] = row[n] / norm;
+}
+
 __global__ void transpose_kernel(int R, int C, const float* __restrict__ in, float* __restrict__ out) {
   __shared__ float tile[32][33];
   const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
@@ -361,6 +380,14 @@ extern "C" int autovc_transpose_f32(int R, int C, const float* in, float* out, h
   AVC_CHECK_ARG(R > 0 && C > 0 && in && out && in != out, "autovc_transpose_f32: bad args");
   hipLaunchKernelGGL(transpose_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, stream, R, C, in, out);
   AVC_CHECK_LAUNCH("autovc_transpose_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_l2norm_rows_f32(int M, int N, const float* x, int64_t ldx, float* out, int64_t ldo,
+                                     hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && N > 0 && x && out && ldx >= N && ldo >= N, "autovc_l2norm_rows_f32: bad args");
+  hipLaunchKernelGGL(l2norm_rows_kernel, dim3(M), dim3(256), 0, stream, N, x, ldx, out, ldo);
+  AVC_CHECK_LAUNCH("autovc_l2norm_rows_f32");
   return avc::kOk;
 }
 

@@ -158,6 +158,9 @@ int autovc_conv_pack_f32(int Co, int Ci, int K, const float* W, float* Wf, float
 int autovc_conv_unpack_grad_f32(int Co, int Ci, int K, const float* dWf, float* dW,
                                 int accumulate, hipStream_t stream);
 int autovc_transpose_f32(int R, int C, const float* in, float* out, hipStream_t stream);
+/* row-wise L2 normalisation: the D-VECTOR speaker encoder's embeds / ||embeds|| (model_bl.py:17-19) */
+int autovc_l2norm_rows_f32(int M, int N, const float* x, int64_t ldx, float* out, int64_t ldo,
+                           hipStream_t stream);
 int64_t autovc_colsum_workspace_floats(int N);
 int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, float* out2,
                       int accumulate, float* workspace, hipStream_t stream);

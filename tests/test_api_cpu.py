@@ -76,10 +76,12 @@ def test_data_loader_crop_pad_and_batches(tmp_path):
         assert u.shape == (128, 80)
 
 
-def test_metadata_is_explicitly_out_of_scope():
+def test_metadata_refuses_cpu():
     import types
     from autovc_amd.make_metadata import Metadata
-    with pytest.raises(NotImplementedError):
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="MI355X"):
         Metadata(types.SimpleNamespace(main_dir=".", model_type="spmel")).metadata()
 
 

@@ -273,3 +273,41 @@ def test_full_size_step_vs_oracle(cuda):
             continue
         err = (p.grad.cpu().double() - ref.double()).norm() / ref.double().norm()
         assert err < 1e-2, (n, float(err))
+
+
+# ------------------------------------------------------------------ 513-bin variant, conversion caller
+def test_generator_stft_513_vs_reference_golden(cuda):
+    """model_vc_stft.GeneratorSTFT (513-bin, `model.` keys): the working arithmetic of the
+    reference (G.model(x, e, e), Appendix A-1) against its golden, through .forward."""
+    from autovc_amd.model_vc_stft import GeneratorSTFT
+    g = GeneratorSTFT(32, 256, 512, 32)
+    g.load_state_dict(og.make_weights(prefix="model.", n_in=513, n_out=513))
+    g = g.to(cuda).train()
+    x = torch.from_numpy(G["stft_x"]).to(cuda)
+    e = torch.from_numpy(G["emb"]).to(cuda)
+    with torch.no_grad():
+        x_id, x_psnt, code = g(x, e, e)
+    assert x_psnt.shape == G["stft_x_psnt"].shape and code.shape == G["stft_code_real"].shape
+    assert rel(x_id, G["stft_x_identic"]) < FWD_TOL
+    assert rel(x_psnt, G["stft_x_psnt"]) < FWD_TOL
+    assert rel(code, G["stft_code_real"]) < FWD_TOL
+
+
+def test_conversion_caller_flow(cuda):
+    """conversion.py:40-44,90-102 as a caller would run it: pad to a multiple of 32, B=1
+    eval forward with (emb_org, emb_trg), un-pad; the output is the oracle's."""
+    g = build(cuda).eval()
+    x = G["x160"][0, :150]                                  # (150, 80): not a multiple of 32
+    len_pad = 32 - x.shape[0] % 32
+    uttr = np.pad(x, ((0, len_pad), (0, 0)), "constant")
+    e_org = torch.from_numpy(G["emb"][0:1]).to(cuda)
+    e_trg = torch.from_numpy(G["emb"][1:2]).to(cuda)
+    with torch.no_grad():
+        _, x_psnt, _ = g(torch.from_numpy(uttr[None]).to(cuda), e_org, e_trg)
+    out = x_psnt[0, 0, :-len_pad, :].cpu()
+    ref_gen = og.OracleGenerator(og.make_weights(), training=False)
+    with torch.no_grad():
+        _, ref_psnt, _ = ref_gen.forward(torch.from_numpy(uttr[None]), torch.from_numpy(G["emb"][0:1]),
+                                         torch.from_numpy(G["emb"][1:2]))
+    assert out.shape == (150, 80)
+    assert rel(out, ref_psnt[0, 0, :-len_pad, :]) < FWD_TOL
