@@ -3,15 +3,24 @@
 //
 // Per output sample the network is a chain of 24 residual layers; every layer needs the
 // whole previous layer's output, so one sample step is a sequence of grid-wide
-// dependencies.  The step is laid out as 2 kernels per layer + 1 head kernel:
+// dependencies, each paid as a kernel boundary (the cheapest grid-wide sync on MI355X,
+// MI355X_MICROARCH.md price list).  The step is ONE kernel per layer + a skip tail + head:
 //
-//   gate(l)  : z = W_conv(l) [x_l(t-2d); x_l(t-d); x_l(t)] + pre(l, t)   (512 x 1536)
-//              g = tanh(z[:256]) * sigmoid(z[256:])                       -> gbuf (B x 256)
-//              gate(0) first samples the previous output (MoL head tail + Philox draw)
+//   layer(l) : g_l = tanh(z[:256]) * sigmoid(z[256:]),  z = the dilated conv of layer l:
+//                z = W_0 x_l(t-2d) + W_1 x_l(t-d) + W_2 x_l(t) + pre(l, t)
+//              with the current tap folded back one layer (exact in real arithmetic):
+//                x_l(t) = sqrt(.5) (W_out(l-1) g_(l-1) + b_out(l-1) + x_(l-1)(t))
+//                W_2 x_l(t) = [sqrt(.5) W_2 W_out(l-1)] g_(l-1) + [sqrt(.5) W_2] x_(l-1)(t)
+//                             + sqrt(.5) W_2 b_out(l-1)  (the last term folded into pre)
+//              so the layer's GEMV reads [x_l(t-2d); x_l(t-d); g_(l-1); x_(l-1)(t)] (1792
+//              inputs) and needs nothing produced in this launch.  The same kernel does
+//              layer l-1's residual work: its slice of x_l(t) (written to ring l for the
+//              later taps) and of the skip accumulation.
+//              layer(0) first samples the previous output (MoL head tail + Philox draw)
 //              and builds x_0 = first_conv(input) on the fly.
-//   resid(l) : x_{l+1}(t) = (W_out g + b_out + x_l(t)) * sqrt(.5)       -> ring(l+1)
-//              skips      = (skips + W_skip g + b_skip) * sqrt(.5)        (legacy)
+//   tail     : the last layer's skip rows
 //   head     : h1 = relu(W1 relu(skips) + b1)
+// 26 launches per sample step instead of 49 for the two-kernel-per-layer form.
 //
 // pre(l, t) = W_cond(l) c_up(t) + b_cond(l) + b_conv(l) for every layer and sample comes
 // from ONE MFMA GEMM per time chunk (autovc_gemm_f32) — the conditioning 1x1 convs are
@@ -39,10 +48,11 @@ constexpr float kSqrtHalf = 0.70710677f;  // float(math.sqrt(0.5))
 constexpr int kBT = 8;                    // utterances per batch tile
 constexpr int kMaxNO = 32;                // MoL head width limit (3 x up to 10 mixtures)
 constexpr int kCtrSlots = 128;
-constexpr int kGateWaves = 6;             // waves per gate workgroup (K = 3 x 512 = 6 chunks of 256)
+constexpr int kMaxResid = 4;              // residual rows per layer workgroup: R/H + S/H
+constexpr int kGateWaves = 7;             // waves per layer workgroup on the GEMV (1792 = 7 chunks of 256)
 
 struct WnArgs {
-  int B, T, R, G, S, NO, K, RING, n_layers, lps, Tch, legacy;
+  int B, T, R, G, S, NO, K, RING, n_layers, lps, Tch, legacy, n_kern;
   const float* packed;
   const float* pre;
   float* ring;
@@ -61,9 +71,16 @@ struct WnArgs {
 };
 
 // ---- packed weight layout (floats): see autovc_wavenet_packed_floats
+// per layer: gate block G x KX, KX = K*R + H: [W_0 .. W_(K-2) (tap-major) | sqrt(.5) W_(K-1) W_out(l-1)
+// (H) | sqrt(.5) W_(K-1) (R)] (layer 0: [W_0 .. W_(K-2) | 0 | W_(K-1)]); then the layer's
+// [W_out (R x H); W_skip (S x H)] and their biases (R + S).
+__host__ __device__ inline int gate_width(const WnArgs& a) { return a.K * a.R + a.G / 2; }
 __host__ __device__ inline int64_t layer_floats(const WnArgs& a) {
   const int H = a.G / 2;
-  return (int64_t)a.G * a.K * a.R + (int64_t)(a.R + a.S) * H + (a.R + a.S);
+  return (int64_t)a.G * gate_width(a) + (int64_t)(a.R + a.S) * H + (a.R + a.S);
+}
+__host__ __device__ inline float* gbuf_of(const WnArgs& a, int l) {
+  return a.gbuf + (int64_t)(l & 1) * a.B * (a.G / 2);
 }
 __host__ __device__ inline const float* layer_base(const WnArgs& a, int l) {
   return a.packed + 2 * (int64_t)a.R + l * layer_floats(a);
@@ -163,9 +180,12 @@ __device__ inline float dot4(f32x4 w, f32x4 x, float acc) {
 
 __device__ inline f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-__device__ inline int read_step(const WnArgs& a, int slot, int next_delta) {
+// step index: a kernel argument for direct launches (targ >= 0), else (graph replay) the
+// counter slot the previous kernel wrote
+__device__ inline int read_step(const WnArgs& a, int slot, int next_delta, int targ) {
+  if (targ >= 0) return targ;
   const int t = a.ctr[slot];
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[slot + 1 == 2 * a.n_layers + 1 ? 0 : slot + 1] = t + next_delta;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[slot + 1 == a.n_kern ? 0 : slot + 1] = t + next_delta;
   return t;
 }
 
@@ -236,63 +256,162 @@ __device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_
   __syncthreads();
 }
 
-// gate(l): one workgroup per gate pair (o, o + G/2) and batch tile; its NW waves split the
-// K = taps*R inputs in 256-float chunks (a chunk never straddles a tap: R % 256 == 0).
+// x_(l-1)(t) chunk for the current-tap fold: from the ring, or (l-1 == 0) first_conv(input)
+__device__ __forceinline__ void load_xprev(const WnArgs& a, int lprev, int t, int b0, int nb, int i,
+                                           const float* s_in, f32x4 (&x)[kBT]) {
+  if (lprev == 0) {
+    const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) {
+      const float in_v = s_in ? s_in[b] : a.yin[(int64_t)(b0 + (b < nb ? b : 0)) * a.T + t];
+      x[b][0] = in_v * fw[0] + fb[0];
+      x[b][1] = in_v * fw[1] + fb[1];
+      x[b][2] = in_v * fw[2] + fb[2];
+      x[b][3] = in_v * fw[3] + fb[3];
+    }
+  } else {
+    const float* xr = a.ring + (((int64_t)lprev * a.RING + (t & (a.RING - 1))) * a.B + b0) * a.R + i;
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) x[b] = ld4(xr + (int64_t)(b < nb ? b : 0) * a.R);
+  }
+}
+
+// layer(l): one workgroup per gate pair (o, o + G/2) and batch tile.  Waves 0..NW-1 split the
+// GEMV's KX inputs in 256-float chunks (no chunk straddles a segment: R, H % 256 == 0);
+// for l >= 1 wave NW does layer l-1's residual rows (R/H of x_l(t) and S/H skip rows per
+// workgroup).
 template <int NW, bool L0>
-__global__ __launch_bounds__(64 * NW) void wn_gate_kernel(WnArgs a, int layer, int slot) {
+__global__ __launch_bounds__(64 * (NW + 1)) void wn_layer_kernel(WnArgs a, int layer, int slot, int targ) {
   __shared__ float s_mol[L0 ? kBT * kMaxNO : 1];
   __shared__ float s_in[kBT];
   __shared__ float s_red[NW][2 * kBT];
-  const int t = read_step(a, slot, 0);
+  const int t = read_step(a, slot, 0, targ);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
-  if (L0) sample_stage<NW>(a, t, b0, nb, s_mol, s_in);
   const int H = a.G / 2;
   const int o = blockIdx.x;
-  const int KR = a.K * a.R;
-  const float* WA = layer_base(a, layer);
-  const float* wa = WA + (int64_t)o * KR;
-  const float* wb = WA + (int64_t)(o + H) * KR;
+  // the conditioning pre-activations (HBM, written by the chunk GEMM) are fetched first so
+  // their latency hides under the GEMV instead of trailing it
+  float pre_a = 0.f, pre_b = 0.f;
+  if ((int)threadIdx.x < nb) {
+    const float* pre = a.pre + ((int64_t)(t % a.Tch) * a.B + b0 + threadIdx.x) * ((int64_t)a.n_layers * a.G) +
+                       (int64_t)layer * a.G;
+    pre_a = pre[o];
+    pre_b = pre[o + H];
+  }
+  if (L0) sample_stage<NW + 1>(a, t, b0, nb, s_mol, s_in);
+  const int KX = gate_width(a);
+  const int KT = (a.K - 1) * a.R;              // end of the ring taps
+  const float* base = layer_base(a, layer);
   const int d = 1 << (layer % a.lps);
-  float acc[2 * kBT];
+  if (wave < NW) {
+    const float* wa = base + (int64_t)o * KX;
+    const float* wb = base + (int64_t)(o + H) * KX;
+    const float* gprev = L0 ? nullptr : gbuf_of(a, layer - 1);
+    float acc[2 * kBT];
 #pragma unroll
-  for (int j = 0; j < 2 * kBT; ++j) acc[j] = 0.f;
-  for (int c = wave; c * 256 < KR; c += NW) {
-    const int kc = c * 256;
-    const int tap = kc / a.R;
-    const int tau = t - (a.K - 1 - tap) * d;
-    if (tau < 0) continue;  // wave-uniform: zero history before the first sample
-    const int k = kc + lane * 4;
-    const int i = k - tap * a.R;
-    const f32x4 va = ld4(wa + k), vb = ld4(wb + k);
-    f32x4 x[kBT];
-    if (L0) {
-      const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
-      float in_v[kBT];
+    for (int j = 0; j < 2 * kBT; ++j) acc[j] = 0.f;
+    for (int c = wave; c * 256 < KX; c += NW) {
+      const int kc = c * 256;
+      const int k = kc + lane * 4;
+      const f32x4 va = ld4(wa + k), vb = ld4(wb + k);   // weights do not depend on the step: issue first
+      f32x4 x[kBT];
+      if (kc < KT) {                           // ring taps 0..K-2 of x_l
+        const int tap = kc / a.R;
+        const int tau = t - (a.K - 1 - tap) * d;
+        if (tau < 0) continue;                 // wave-uniform: zero history before the first sample
+        const int i = k - tap * a.R;
+        if (L0) {
+          const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
 #pragma unroll
-      for (int b = 0; b < kBT; ++b)
-        in_v[b] = tau == t ? s_in[b] : a.yin[(int64_t)(b0 + (b < nb ? b : 0)) * a.T + tau];
+          for (int b = 0; b < kBT; ++b) {
+            const float in_v = a.yin[(int64_t)(b0 + (b < nb ? b : 0)) * a.T + tau];
+            x[b][0] = in_v * fw[0] + fb[0];
+            x[b][1] = in_v * fw[1] + fb[1];
+            x[b][2] = in_v * fw[2] + fb[2];
+            x[b][3] = in_v * fw[3] + fb[3];
+          }
+        } else {
+          const float* xr = a.ring + (((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B + b0) * a.R + i;
+#pragma unroll
+          for (int b = 0; b < kBT; ++b) x[b] = ld4(xr + (int64_t)(b < nb ? b : 0) * a.R);
+        }
+      } else if (kc < KT + H) {                // g_(l-1) (layer 0: zero weights, skipped)
+        if (L0) continue;
+        const int j = k - KT;
+#pragma unroll
+        for (int b = 0; b < kBT; ++b) x[b] = ld4(gprev + (int64_t)(b0 + (b < nb ? b : 0)) * H + j);
+      } else {                                 // current tap: x_(l-1)(t) (layer 0: x_0(t))
+        const int i = k - KT - H;
+        load_xprev(a, L0 ? 0 : layer - 1, t, b0, nb, i, L0 ? s_in : nullptr, x);
+      }
 #pragma unroll
       for (int b = 0; b < kBT; ++b) {
-        x[b][0] = in_v[b] * fw[0] + fb[0];
-        x[b][1] = in_v[b] * fw[1] + fb[1];
-        x[b][2] = in_v[b] * fw[2] + fb[2];
-        x[b][3] = in_v[b] * fw[3] + fb[3];
+        acc[b] = dot4(va, x[b], acc[b]);
+        acc[kBT + b] = dot4(vb, x[b], acc[kBT + b]);
       }
-    } else {
-      const float* xr = a.ring + (((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B + b0) * a.R + i;
-#pragma unroll
-      for (int b = 0; b < kBT; ++b) x[b] = ld4(xr + (int64_t)(b < nb ? b : 0) * a.R);
     }
+    const float s = wave_reduce_multi<2 * kBT>(acc, lane);
+    if ((lane & 3) == 0) s_red[wave][lane >> 2] = s;
+  } else if (!L0) {
+    // layer l-1's residual rows: x_l(t) rows [o*R/H, (o+1)*R/H) and skip rows [o*S/H, ...).
+    // All loads of the wave (g once, every row's weights and residual) are issued before the
+    // first reduction: this wave is on the launch's critical path.
+    const int lp = layer - 1;
+    const float* pbase = layer_base(a, lp) + (int64_t)a.G * KX;
+    const float* bias = pbase + (int64_t)(a.R + a.S) * H;
+    const float* gprev = gbuf_of(a, lp);
+    const int rx = a.R / H, nr = rx + a.S / H;   // <= kMaxResid (host check)
+    const int slot_t = t & (a.RING - 1);
+    const int bl = (lane >> 3) < nb ? (lane >> 3) : 0;
+    const int gbl = b0 + bl;
+    int rows[kMaxResid];
+    float res[kMaxResid], bsv[kMaxResid];
 #pragma unroll
-    for (int b = 0; b < kBT; ++b) {
-      acc[b] = dot4(va, x[b], acc[b]);
-      acc[kBT + b] = dot4(vb, x[b], acc[kBT + b]);
+    for (int q = 0; q < kMaxResid; ++q) {
+      const int qq = q < nr ? q : 0;
+      rows[q] = qq < rx ? o * rx + qq : a.R + o * (nr - rx) + (qq - rx);
+      bsv[q] = bias[rows[q]];
+      res[q] = 0.f;
+      if (rows[q] < a.R)
+        res[q] = lp == 0 ? a.yin[(int64_t)gbl * a.T + t] * a.packed[rows[q]] + a.packed[a.R + rows[q]]
+                         : a.ring[(((int64_t)lp * a.RING + slot_t) * a.B + gbl) * a.R + rows[q]];
+    }
+    float acc[kMaxResid][kBT];
+#pragma unroll
+    for (int q = 0; q < kMaxResid; ++q)
+#pragma unroll
+      for (int b = 0; b < kBT; ++b) acc[q][b] = 0.f;
+    for (int k = lane * 4; k < H; k += 256) {
+      f32x4 g[kBT], wv[kMaxResid];
+#pragma unroll
+      for (int b = 0; b < kBT; ++b) g[b] = ld4(gprev + (int64_t)(b0 + (b < nb ? b : 0)) * H + k);
+#pragma unroll
+      for (int q = 0; q < kMaxResid; ++q) wv[q] = ld4(pbase + (int64_t)rows[q] * H + k);
+#pragma unroll
+      for (int q = 0; q < kMaxResid; ++q)
+#pragma unroll
+        for (int b = 0; b < kBT; ++b) acc[q][b] = dot4(wv[q], g[b], acc[q][b]);
+    }
+    const int b = lane >> 3;
+#pragma unroll
+    for (int q = 0; q < kMaxResid; ++q) {
+      const float v0 = wave_reduce_multi<kBT>(acc[q], lane);
+      if (q < nr && (lane & 7) == 0 && b < nb) {
+        const int gb = b0 + b;
+        const int row = rows[q];
+        const float v = v0 + bsv[q];
+        if (row < a.R) {
+          a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gb) * a.R + row] = (v + res[q]) * kSqrtHalf;
+        } else {
+          float* sp = a.skip + (int64_t)gb * a.S + (row - a.R);
+          if (lp == 0) *sp = v;
+          else *sp = a.legacy ? (*sp + v) * kSqrtHalf : (*sp + v);
+        }
+      }
     }
   }
-  const float s = wave_reduce_multi<2 * kBT>(acc, lane);
-  if ((lane & 3) == 0) s_red[wave][lane >> 2] = s;
   __syncthreads();
   if ((int)threadIdx.x < nb) {
     const int b = threadIdx.x;
@@ -300,44 +419,36 @@ __global__ __launch_bounds__(64 * NW) void wn_gate_kernel(WnArgs a, int layer, i
 #pragma unroll
     for (int w = 0; w < NW; ++w) { za += s_red[w][b]; zb += s_red[w][kBT + b]; }
     const int gb = b0 + b;
-    const float* pre = a.pre + ((int64_t)(t % a.Tch) * a.B + gb) * ((int64_t)a.n_layers * a.G) + (int64_t)layer * a.G;
-    za += pre[o];
-    zb += pre[o + H];
-    a.gbuf[(int64_t)gb * H + o] = tanhf(za) * avc_sigmoid(zb);
+    za += pre_a;
+    zb += pre_b;
+    gbuf_of(a, layer)[(int64_t)gb * H + o] = tanhf(za) * avc_sigmoid(zb);
   }
 }
 
-// resid(l): one wave per output row of [W_out; W_skip] (the last layer only needs skip).
+// tail: the last layer's skip rows, one wave per row.
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void wn_resid_kernel(WnArgs a, int layer, int slot) {
-  const int t = read_step(a, slot, 0);
+__global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, int targ) {
+  const int t = read_step(a, slot, 0, targ);
+  (void)t;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
   const int H = a.G / 2;
-  const bool last = layer == a.n_layers - 1;
-  const int row = blockIdx.x * NW + wave + (last ? a.R : 0);
-  if (row >= a.R + a.S) return;
-  const float* base = layer_base(a, layer) + (int64_t)a.G * a.K * a.R;
-  const float* w = base + (int64_t)row * H;
-  const float* bias = base + (int64_t)(a.R + a.S) * H;
-  const int slot_t = t & (a.RING - 1);
-  // residual operand, fetched ahead of the reduction
-  float res = 0.f;
-  const int bl = (lane >> 3) < nb ? (lane >> 3) : 0;
-  const int gbl = b0 + bl;
-  if (row < a.R) {
-    res = layer == 0 ? a.yin[(int64_t)gbl * a.T + t] * a.packed[row] + a.packed[a.R + row]
-                     : a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gbl) * a.R + row];
-  }
+  const int lp = a.n_layers - 1;
+  const int srow = blockIdx.x * NW + wave;
+  if (srow >= a.S) return;
+  const int row = a.R + srow;
+  const float* pbase = layer_base(a, lp) + (int64_t)a.G * gate_width(a);
+  const float* bias = pbase + (int64_t)(a.R + a.S) * H;
+  const float* gprev = gbuf_of(a, lp);
   float acc[kBT];
 #pragma unroll
   for (int b = 0; b < kBT; ++b) acc[b] = 0.f;
   for (int k = lane * 4; k < H; k += 256) {
-    const f32x4 wv = ld4(w + k);
+    const f32x4 wv = ld4(pbase + (int64_t)row * H + k);
     f32x4 g[kBT];
 #pragma unroll
-    for (int b = 0; b < kBT; ++b) g[b] = ld4(a.gbuf + (int64_t)(b0 + (b < nb ? b : 0)) * H + k);
+    for (int b = 0; b < kBT; ++b) g[b] = ld4(gprev + (int64_t)(b0 + (b < nb ? b : 0)) * H + k);
 #pragma unroll
     for (int b = 0; b < kBT; ++b) acc[b] = dot4(wv, g[b], acc[b]);
   }
@@ -345,21 +456,16 @@ __global__ __launch_bounds__(64 * NW) void wn_resid_kernel(WnArgs a, int layer, 
   if ((lane & 7) != 0) return;
   const int b = lane >> 3;
   if (b >= nb) return;
-  const int gb = b0 + b;
+  float* sp = a.skip + (int64_t)(b0 + b) * a.S + srow;
   const float v = s + bias[row];
-  if (row < a.R) {
-    a.ring[(((int64_t)(layer + 1) * a.RING + slot_t) * a.B + gb) * a.R + row] = (v + res) * kSqrtHalf;
-  } else {
-    float* sp = a.skip + (int64_t)gb * a.S + (row - a.R);
-    if (layer == 0) *sp = v;
-    else *sp = a.legacy ? (*sp + v) * kSqrtHalf : (*sp + v);
-  }
+  if (lp == 0) *sp = v;
+  else *sp = a.legacy ? (*sp + v) * kSqrtHalf : (*sp + v);
 }
 
 // head: h1 = relu(W1 relu(skips) + b1); advances the step counter.
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot) {
-  read_step(a, slot, 1);
+__global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, int targ) {
+  read_step(a, slot, 1, targ);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
@@ -459,19 +565,16 @@ std::map<GraphKey, hipGraphExec_t> g_graphs;
 std::vector<GraphKey> g_order;
 hipStream_t g_capture_stream[64] = {};
 
-int enqueue_step(const WnArgs& a, hipStream_t s) {
+int enqueue_step(const WnArgs& a, hipStream_t s, int targ) {
   const int H = a.G / 2;
-  const dim3 bt(1, (a.B + kBT - 1) / kBT);
+  const int nbt = (a.B + kBT - 1) / kBT;
+  constexpr int NT = 64 * (kGateWaves + 1);
   for (int l = 0; l < a.n_layers; ++l) {
-    if (l == 0) {
-      hipLaunchKernelGGL((wn_gate_kernel<kGateWaves, true>), dim3(H, bt.y), dim3(64 * kGateWaves), 0, s, a, 0, 0);
-    } else {
-      hipLaunchKernelGGL((wn_gate_kernel<kGateWaves, false>), dim3(H, bt.y), dim3(64 * kGateWaves), 0, s, a, l, 2 * l);
-    }
-    const int rows = (l == a.n_layers - 1) ? a.S : a.R + a.S;
-    hipLaunchKernelGGL((wn_resid_kernel<4>), dim3((rows + 3) / 4, bt.y), dim3(256), 0, s, a, l, 2 * l + 1);
+    if (l == 0) hipLaunchKernelGGL((wn_layer_kernel<kGateWaves, true>), dim3(H, nbt), dim3(NT), 0, s, a, 0, 0, targ);
+    else hipLaunchKernelGGL((wn_layer_kernel<kGateWaves, false>), dim3(H, nbt), dim3(NT), 0, s, a, l, l, targ);
   }
-  hipLaunchKernelGGL((wn_head_kernel<4>), dim3((a.S + 3) / 4, bt.y), dim3(256), 0, s, a, 2 * a.n_layers);
+  hipLaunchKernelGGL((wn_tail_kernel<4>), dim3((a.S + 3) / 4, nbt), dim3(256), 0, s, a, a.n_layers, targ);
+  hipLaunchKernelGGL((wn_head_kernel<4>), dim3((a.S + 3) / 4, nbt), dim3(256), 0, s, a, a.n_layers + 1, targ);
   AVC_CHECK_LAUNCH("autovc_wavenet_generate_f32");
   return avc::kOk;
 }
@@ -492,7 +595,7 @@ int get_graph(const WnArgs& a, int steps, hipGraphExec_t* out) {
   hipStream_t cs = g_capture_stream[dev];
   AVC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
   int rc = avc::kOk;
-  for (int i = 0; i < steps && rc == avc::kOk; ++i) rc = enqueue_step(a, cs);
+  for (int i = 0; i < steps && rc == avc::kOk; ++i) rc = enqueue_step(a, cs, -1);
   hipGraph_t graph = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &graph);
   if (rc != avc::kOk) { if (graph) (void)hipGraphDestroy(graph); return rc; }
@@ -527,7 +630,7 @@ extern "C" {
 int64_t autovc_wavenet_packed_floats(int n_layers, int taps, int R, int G, int S, int n_out) {
   if (n_layers <= 0 || taps <= 0 || R <= 0 || G <= 0 || S <= 0 || n_out <= 0) return -1;
   const int64_t H = G / 2;
-  const int64_t per = (int64_t)G * taps * R + (int64_t)(R + S) * H + (R + S);
+  const int64_t per = (int64_t)G * (taps * R + H) + (int64_t)(R + S) * H + (R + S);
   return 2 * (int64_t)R + n_layers * per + (int64_t)S * S + S + (int64_t)n_out * S + n_out;
 }
 
@@ -535,7 +638,7 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
                                        int S) {
   if (B <= 0 || T <= 0 || n_layers <= 0 || layers_per_stack <= 0 || taps <= 0) return -1;
   const int64_t ring = (int64_t)(n_layers + 1) * ring_frames(n_layers, layers_per_stack, taps) * B * R;
-  const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + (int64_t)B * (G / 2);
+  const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + 2 * (int64_t)B * (G / 2) + 5 * 64;
   return floats * 4 + kCtrSlots * 4 + 256;
 }
 
@@ -570,11 +673,13 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   static const char* fn = "autovc_wavenet_generate_f32";
   AVC_CHECK_ARG(B > 0 && T > 0 && 0 <= t0 && t0 < t1 && t1 <= T, "%s: bad range B=%d T=%d t=[%d,%d)", fn, B, T, t0, t1);
   AVC_CHECK_ARG(Tch > 0 && t1 - t0 <= Tch, "%s: chunk [%d,%d) longer than the conditioning chunk %d", fn, t0, t1, Tch);
-  AVC_CHECK_ARG(n_layers >= 1 && 2 * n_layers + 1 < kCtrSlots && layers_per_stack >= 1 && layers_per_stack <= 16 &&
+  AVC_CHECK_ARG(n_layers >= 1 && n_layers + 2 < kCtrSlots && layers_per_stack >= 1 && layers_per_stack <= 16 &&
                     taps >= 1,
                 "%s: bad layer structure layers=%d per_stack=%d taps=%d", fn, n_layers, layers_per_stack, taps);
-  AVC_CHECK_ARG(R > 0 && R % 256 == 0 && G > 0 && G % 512 == 0 && S > 0 && S % 256 == 0,
-                "%s: channel counts must be multiples of 256 (R=%d, G/2=%d, S=%d)", fn, R, G / 2, S);
+  AVC_CHECK_ARG(R > 0 && R % 256 == 0 && G > 0 && G % 512 == 0 && S > 0 && S % 256 == 0 &&
+                    R % (G / 2) == 0 && S % (G / 2) == 0 && (R + S) / (G / 2) <= kMaxResid && taps >= 2,
+                "%s: need R, G/2, S multiples of 256 with G/2 dividing R and S, taps >= 2 (R=%d, G/2=%d, S=%d)", fn,
+                R, G / 2, S);
   AVC_CHECK_ARG(n_out % 3 == 0 && n_out / 3 >= 1 && n_out / 3 <= 10 && n_out <= kMaxNO,
                 "%s: out_channels %d is not 3 x (1..10) logistic mixtures", fn, n_out);
   AVC_CHECK_ARG(packed && pre && y_out && workspace, "%s: null pointer", fn);
@@ -589,12 +694,13 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   memset(&a, 0, sizeof(a));
   a.B = B; a.T = T; a.R = R; a.G = G; a.S = S; a.NO = n_out; a.K = taps; a.RING = RING;
   a.n_layers = n_layers; a.lps = layers_per_stack; a.Tch = Tch; a.legacy = legacy ? 1 : 0;
+  a.n_kern = n_layers + 2;
   a.packed = packed; a.pre = pre;
   a.ring = ws;                 ws += round64((int64_t)(n_layers + 1) * RING * B * R);
   a.yin = ws;                  ws += round64((int64_t)B * T);
   a.skip = ws;                 ws += round64((int64_t)B * S);
   a.h1 = ws;                   ws += round64((int64_t)B * S);
-  a.gbuf = ws;                 ws += round64((int64_t)B * (G / 2));
+  a.gbuf = ws;                 ws += round64(2 * (int64_t)B * (G / 2));
   a.ctr = reinterpret_cast<int*>(ws);
   a.teacher = teacher; a.teacher_len = teacher ? teacher_len : 0;
   a.y_out = y_out; a.mol_out = mol_out;
@@ -615,7 +721,7 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
     for (; t + graph_steps <= t1; t += graph_steps) AVC_HIP(hipGraphLaunch(exec, stream), "hipGraphLaunch");
   }
   for (; t < t1; ++t) {
-    const int rc = enqueue_step(a, stream);
+    const int rc = enqueue_step(a, stream, t);
     if (rc != avc::kOk) return rc;
   }
   if (t1 == T) {

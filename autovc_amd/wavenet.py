@@ -11,8 +11,10 @@ incremental_forward runs entirely in libautovc_hip.so:
   upsample   autovc_wavenet_upsample_f32 (conditioning frames -> samples, time-major)
   pre        autovc_gemm_f32: every layer's conditioning 1x1 conv + both biases for a
              chunk of samples in one MFMA GEMM (sample-independent work off the chain)
-  generate   autovc_wavenet_generate_f32: the sample loop (2 kernels per layer + head,
-             sampling fused into the first layer's kernel), replayed as a hipGraph
+  generate   autovc_wavenet_generate_f32: the sample loop (one kernel per layer — each
+             layer's current conv tap folded back onto the previous layer's gate output —
+             + skip tail + head, sampling fused into the first layer's kernel), replayed as a
+             hipGraph
 Sampling draws its uniforms from a counter-based Philox stream keyed by (seed, utterance,
 sample), so batched, sharded and chunked runs produce the same waveform per utterance.
 The seed comes from torch's default generator (torch.manual_seed reproduces a run).
@@ -180,34 +182,59 @@ class WaveNet(nn.Module):
 
     # ---------------------------------------------------------------- HIP generation
     def _packed(self, dev):
-        R, G, S = self.residual_channels, self.gate_channels, self.skip_out_channels
-        parts = [_effective_weight(self.first_conv).reshape(R), self.first_conv.bias.reshape(R)]
+        """Weights in the layout of autovc_wavenet_packed_floats (include/autovc_hip.h).  Layer
+        l >= 1 carries its current conv tap folded back one layer (see csrc/wavenet.hip):
+        [W_0 .. W_(K-2) | sqrt(.5) W_(K-1) W_out(l-1) | sqrt(.5) W_(K-1)], the products on the
+        GEMM, and sqrt(.5) W_(K-1) b_out(l-1) joins the layer's conditioning bias."""
+        R, G, S, K = self.residual_channels, self.gate_channels, self.skip_out_channels, self.kernel_size
+        H = G // 2
+        sq = math.sqrt(0.5)
+        f32 = dict(device=dev, dtype=torch.float32)
+
+        def w2(m):
+            return _effective_weight(m).detach().to(**f32)
+
+        parts = [w2(self.first_conv).reshape(R), self.first_conv.bias.detach().to(**f32).reshape(R)]
         wc, bconv, bcond = [], [], []
-        for layer in self.conv_layers:
-            w = _effective_weight(layer.conv)                             # (G, R, K)
-            parts.append(w.transpose(1, 2).reshape(-1))                   # (G, K*R), tap 0 oldest
-            parts.append(_effective_weight(layer.conv1x1_out).reshape(-1))
-            parts.append(_effective_weight(layer.conv1x1_skip).reshape(-1))
-            parts.append(layer.conv1x1_out.bias.reshape(-1))
-            parts.append(layer.conv1x1_skip.bias.reshape(-1))
-            wc.append(_effective_weight(layer.conv1x1c).reshape(G, self.cin_channels))
-            bconv.append(layer.conv.bias.reshape(-1))
-            bcond.append(layer.conv1x1c.bias.reshape(-1))
+        prev_w = prev_b = None
+        for l, layer in enumerate(self.conv_layers):
+            W = w2(layer.conv)                                            # (G, R, K)
+            taps = W[:, :, : K - 1].permute(0, 2, 1).reshape(G, (K - 1) * R)
+            cur = W[:, :, K - 1].contiguous()                             # (G, R)
+            bc = layer.conv.bias.detach().to(**f32).reshape(G).clone()
+            if l == 0:
+                mblk = torch.zeros(G, H, **f32)
+                curblk = cur
+            else:
+                mblk = torch.empty(G, H, **f32)
+                Fh.gemm(G, H, R, cur, R, 0, prev_w, H, 1, mblk, H)         # W_(K-1) W_out(l-1)
+                mblk.mul_(sq)
+                curblk = cur * sq
+                cb = torch.empty(1, G, **f32)
+                Fh.gemm(1, G, R, prev_b.reshape(1, R), R, 0, cur, R, 0, cb, G)
+                bc = bc + sq * cb.reshape(G)
+            wout = w2(layer.conv1x1_out).reshape(R, H)
+            wskip = w2(layer.conv1x1_skip).reshape(S, H)
+            bout = layer.conv1x1_out.bias.detach().to(**f32).reshape(R)
+            parts += [torch.cat([taps, mblk, curblk], dim=1), wout, wskip, bout,
+                      layer.conv1x1_skip.bias.detach().to(**f32).reshape(S)]
+            prev_w, prev_b = wout.contiguous(), bout
+            wc.append(w2(layer.conv1x1c).reshape(G, self.cin_channels))
+            bconv.append(bc)
+            bcond.append(layer.conv1x1c.bias.detach().to(**f32).reshape(G))
         l1, l3 = self.last_conv_layers[1], self.last_conv_layers[3]
-        parts += [_effective_weight(l1).reshape(-1), l1.bias.reshape(-1),
-                  _effective_weight(l3).reshape(-1), l3.bias.reshape(-1)]
-        packed = torch.cat([p.detach().to(dev, torch.float32).reshape(-1) for p in parts]).contiguous()
+        parts += [w2(l1).reshape(-1), l1.bias.detach().to(**f32).reshape(-1),
+                  w2(l3).reshape(-1), l3.bias.detach().to(**f32).reshape(-1)]
+        packed = torch.cat([p.reshape(-1) for p in parts]).contiguous()
         n = _lib.load().autovc_wavenet_packed_floats(self.layers, self.kernel_size, R, G, S, self.out_channels)
         if packed.numel() != n:
             raise RuntimeError(f"WaveNet packing: {packed.numel()} floats, library expects {n}")
-        out = dict(packed=packed,
-                   wc=torch.cat(wc).detach().to(dev, torch.float32).contiguous(),
-                   bconv=torch.cat(bconv).detach().to(dev, torch.float32).contiguous(),
-                   bcond=torch.cat(bcond).detach().to(dev, torch.float32).contiguous())
+        out = dict(packed=packed, wc=torch.cat(wc).contiguous(), bconv=torch.cat(bconv).contiguous(),
+                   bcond=torch.cat(bcond).contiguous())
         if self.upsample_conv is not None:
             convs = [m for m in self.upsample_conv if isinstance(m, nn.ConvTranspose2d)]
-            out["up_w"] = torch.cat([_effective_weight(m).detach().reshape(-1) for m in convs]).to(dev, torch.float32)
-            out["up_b"] = torch.cat([m.bias.detach().reshape(-1) for m in convs]).to(dev, torch.float32)
+            out["up_w"] = torch.cat([_effective_weight(m).detach().reshape(-1) for m in convs]).to(**f32)
+            out["up_b"] = torch.cat([m.bias.detach().reshape(-1) for m in convs]).to(**f32)
         return out
 
     def upsample(self, c, P=None):

@@ -178,11 +178,15 @@ int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, 
  * generate: runs sample steps t0 <= t < t1 of the incremental loop for B utterances.
  *   packed   weights after make_generation_fast_ (weight norm folded), floats:
  *              first_conv w[R], b[R];
- *              per layer: conv (G, taps*R) linearised (o, tap, i) [tap 0 = oldest],
+ *              per layer l: gate block (G, taps*R + G/2) = [W_0 .. W_(taps-2) linearised
+ *                         (o, tap, i) | sqrt(.5) W_(taps-1) W_out(l-1) (G/2) | sqrt(.5) W_(taps-1) (R)]
+ *                         (layer 0: [W_0 .. W_(taps-2) | 0 | W_(taps-1)]) — the current tap folded
+ *                         back one layer so each layer is one launch;
  *                         [conv1x1_out (R, G/2); conv1x1_skip (S, G/2)], their biases [R+S];
  *              last_conv_layers.1 W (S, S), b[S]; last_conv_layers.3 W (n_out, S), b[n_out]
- *            (autovc_wavenet_packed_floats gives the size)
- *   pre      (Tch, B, n_layers*G): conditioning 1x1 + both biases of every layer; row
+ *            (autovc_wavenet_packed_floats gives the size; autovc_amd/wavenet.py builds it)
+ *   pre      (Tch, B, n_layers*G): conditioning 1x1 + both biases of every layer (+ the folded
+ *            sqrt(.5) W_(taps-1) b_out(l-1) for l >= 1); row
  *            (t % Tch) must hold step t (one autovc_gemm_f32 over the upsampled c per chunk)
  *   seed, utt_base: Philox4x32-10 key and the global index of utterance 0 (the draw of
  *            sample t of utterance u depends only on (seed, u, t))
