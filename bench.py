@@ -148,6 +148,115 @@ def wavenet_cpu_baseline(n_utt, seconds):
                       f"{torch.__version__} CPU, {threads} threads), {dt:.2f} s"}
 
 
+def synthetic_wavs(n, base_index, seed=5000):
+    """per utterance a seeded sum of 3 sinusoids (100-4000 Hz, amplitude
+    <= 0.3 each) + N(0, 0.01), clipped to +-0.99; 2-4 s long, cut so that the frame count
+    (L//256 + 1) is a multiple of 32 (no conversion padding)."""
+    import numpy as np
+    out = []
+    for i in range(n):
+        rs = np.random.RandomState(seed + base_index + i)
+        frames = 32 * rs.randint(4, 8)                     # 128..224 frames = 2.0..3.6 s
+        L = (frames - 1) * 256 + int(rs.randint(0, 256))
+        t = np.arange(L) / 16000.0
+        w = sum(rs.uniform(0.05, 0.3) * np.sin(2 * np.pi * rs.uniform(100, 4000) * t + rs.uniform(0, 6.3))
+                for _ in range(3))
+        w = w + rs.normal(0, 0.01, L)
+        out.append(np.clip(w, -0.99, 0.99))
+    return out
+
+
+def frontend_roofline(dev, n_utt=256):
+    """The fused STFT+mel kernel on a large batch (n_utt synthetic utterances, spmel and
+    513-bin stft modes), one launch each, timed with events on the launch stream.
+    Algorithmic bytes per frame: 256 new float64 samples in (the reference's filtfilt/dither
+    output is float64, make_spect.py:74-76) + the float32 row out (80 or 513 values)."""
+    from autovc_amd import _lib, dsp
+    import numpy as np
+    wavs = synthetic_wavs(n_utt, 100000)
+    lens = [len(w) for w in wavs]
+    fr_each = [dsp.n_frames(n) for n in lens]
+    fr = int(sum(fr_each))
+    wav = torch.from_numpy(np.concatenate(wavs).astype(np.float64)).to(dev)
+    woff = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int64, device=dev)
+    foff = torch.tensor(np.concatenate([[0], np.cumsum(fr_each)]), dtype=torch.int64, device=dev)
+    lo, ln, off, w = dsp._DeviceMel.get(dev, 80)
+    res = {}
+    for mode, width in (("spmel", 80), ("stft", 513)):
+        out = torch.empty((fr, width), dtype=torch.float32, device=dev)
+        args = (_lib.ptr(wav), _lib.ptr(woff), _lib.ptr(foff), n_utt, fr,
+                *((_lib.ptr(lo), _lib.ptr(ln), _lib.ptr(off), _lib.ptr(w), 80, 0) if mode == "spmel"
+                  else (0, 0, 0, 0, 0, 1)), _lib.ptr(out), _lib.stream_ptr(dev))
+        _lib.call("autovc_stft_mel_f32", *args)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):   # one launch per sample, events on the launch stream
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _lib.call("autovc_stft_mel_f32", *args)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e-3)
+        dt = sorted(ts)[2]
+        bpf = 256 * 8 + width * 4
+        res[mode] = {"frames": fr, "kernel_ms": round(dt * 1e3, 3), "frames_per_s": round(fr / dt, 1),
+                     "bytes_per_frame": bpf, "achieved": round(fr * bpf / dt / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(fr * bpf / dt / 1e9 / HBM_PEAK_GBS, 4)}
+    return res
+
+
+def e2e_bench(dev, rank, world, per_rank=8):
+    """BASELINE config 5 / SURVEY §8d C5: 64 synthetic utterances sharded 8 per GPU; host
+    filtfilt + dither -> GPU 513-bin STFT -> GeneratorSTFT conversion (eval) -> projection
+    to 80 mels (conversion.py:102) -> batched WaveNet synthesis.  Random-init weights (the
+    reference checkpoints are absent).  Timed per stage with the device synchronised."""
+    import numpy as np
+    from autovc_amd import pipeline, synthesis
+    from autovc_amd.model_vc_stft import GeneratorSTFT
+    torch.manual_seed(77)
+    G = GeneratorSTFT(32, 256, 512, 32).to(dev).eval()
+    voc = synthesis.build_model()
+    voc.make_generation_fast_()
+    voc = voc.to(dev).eval()
+    base = rank * per_rank
+    wavs = synthetic_wavs(per_rank, base)
+    g = torch.Generator().manual_seed(6000 + base)
+    e = torch.randn(2 * per_rank, 256, generator=g)
+    e = (e / e.norm(dim=1, keepdim=True) * 0.8).to(dev)
+    e_org, e_trg = e[:per_rank], e[per_rank:]
+    # warm-up on a short utterance pair (kernels loaded, graphs captured)
+    w0 = [wavs[0][: 127 * 256 + 10]]
+    m0 = pipeline.convert(G, pipeline.spectrograms(w0, "stft", device=dev, seeds=[base]), e_org[:1], e_trg[:1])
+    synthesis.wavegen_batch(voc, [m0[0][:4].cpu().numpy()], seed=1, utt_offset=base)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    specs = pipeline.spectrograms(wavs, "stft", device=dev, seeds=[base + i for i in range(per_rank)])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    mels = pipeline.convert(G, specs, e_org, e_trg)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    waves = synthesis.wavegen_batch(voc, [m.cpu().numpy() for m in mels], seed=3, utt_offset=base)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    stages = torch.tensor([t1 - t0, t2 - t1, t3 - t2, t3 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.all_reduce(stages, op=torch.distributed.ReduceOp.MAX)
+    s = [float(v) for v in stages.cpu()]
+    audio_s = sum(len(w) for w in waves) / 16000.0
+    assert all(len(w) == m.shape[0] * 256 and np.isfinite(w).all() for w, m in zip(waves, mels))
+    n_total = per_rank * world
+    return {"workload": f"C5: {n_total} synthetic utterances ({per_rank} per GPU, 2.0-3.6 s), host filtfilt+dither "
+                        "-> HIP 513-bin STFT -> GeneratorSTFT conversion -> mel projection -> WaveNet",
+            "utterances_per_s": round(n_total / s[3], 3), "rtf_node": round(audio_s * world / s[3], 3),
+            "rank0_audio_s": round(audio_s, 2),
+            "stage_s_max_over_ranks": {"spectrograms": round(s[0], 4), "convert": round(s[1], 4),
+                                       "vocode": round(s[2], 3), "total": round(s[3], 3)}}
+
+
 def cpu_baseline(B, T, seconds=15.0):
     """The oracle's CPU restatement of the same training step (fused torch CPU LSTM, conv1d,
     batch_norm, Adam — the reference's own CPU ops), timed on this host."""
@@ -189,6 +298,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-wavenet", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
 
     from autovc_amd import ddp
@@ -234,6 +344,11 @@ def main():
         # config 4 per GPU (vocoder batches shard with no collective): every rank synthesises
         # its own 8 utterances; rank 0 reports the per-GPU rate
         wn = wavenet_bench(dev, cpu=(not args.no_cpu_baseline and rank == 0 and world == 1))
+    e2e = fe = None
+    if not args.no_e2e:
+        e2e = e2e_bench(dev, rank, world)
+        if rank == 0:
+            fe = frontend_roofline(dev)
 
     if rank == 0:
         value = world * B * T * args.steps / dt
@@ -248,6 +363,7 @@ def main():
             "final_loss": round(last_loss, 6),
             "roofline": roof, "cpu_baseline": cpu,
             "wavenet": wn,
+            "e2e": e2e, "frontend": fe,
         }
         if cpu:
             line["vs_cpu_baseline"] = round(value / cpu["value"], 2)
