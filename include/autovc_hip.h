@@ -40,7 +40,10 @@ int autovc_device_sync(void);
  *   wav_off    : [n_utt+1] int64 sample offsets
  *   frame_off  : [n_utt+1] int64 frame offsets, frames_u = L_u // 256 + 1
  *   mel_*      : sparse mel basis (librosa Slaney 80x513): per mel m the first bin,
- *                the bin count and the offset of its weights in mel_w
+ *                the bin count and the offset of its weights in mel_w; n_mels <= 128
+ *                (the basis is staged in LDS per workgroup)
+ *   The transform runs in float64 (an fp32 FFT misses the 1e-4 bound on quiet stft
+ *   bins of loud frames); magnitudes, mel sums and the dB map in fp32.
  *   out        : (total_frames, n_mels) for AUTOVC_FE_SPMEL,
  *                (total_frames, 513)    for AUTOVC_FE_STFT (frame-major)
  */
