@@ -42,9 +42,18 @@ struct Opnd {
 // One operand tile (ROWS x BK) of a stage: staging map, LDS image and fragment reads.
 //   RK: LDS [ROWS][BK+4], staged as float4 along k, fragments read with ds_read_b128.
 //   CK: LDS [BK][ROWS+4], staged as float4 along rows (coalesced), fragments ds_read_b32.
-// Per staging slot the loader keeps its source pointer and the conv-mask state (frame
-// position in the sequence, tap) and advances them by BK per stage: no 64-bit divisions
-// in the k loop.
+// Loads are buffer loads (32-bit byte offsets from the operand base, descriptor range
+// 2 GiB): every masked element (row past the operand, k past K, conv tap outside its
+// sequence) gets an out-of-range offset and reads as zero in hardware, so the k loop has
+// no branches and a handful of VALU per float4.  The staging map gives every slot of a
+// thread the same k (RK) or the same row (CK), so the k/tap bookkeeping of RK operands
+// and the row/tap state of CK operands are per thread, not per slot.
+constexpr uint32_t kOOB = 0x80000000u;   // >= the descriptor's num_records: reads return 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)kOOB, 0x00020000);
+}
+
 template <bool RK, int ROWS, int BK, int NT>
 struct OpTile {
   static constexpr int LD = RK ? BK + 4 : ROWS + 4;
@@ -52,57 +61,81 @@ struct OpTile {
   static constexpr int F4 = ROWS * BK / 4;           // float4 per stage
   static constexpr int PER = F4 / NT;
   static_assert(PER * NT == F4, "staging map");
+  static_assert(RK ? NT % (BK / 4) == 0 : NT % (ROWS / 4) == 0, "slots of a thread share k (RK) / row (CK)");
   f32x4 v[PER];
-  const float* ptr[PER];
-  int kpos[PER];            // current k of the slot (RK: k index; CK: frame index f)
-  int tpos[PER];            // conv: frame position within its sequence (RK: fixed; CK: advancing)
-  int tap[PER];             // conv: RK: k / C (advancing); CK: q / C (fixed)
-  int kmod[PER];            // conv RK: k % C
-  bool rok[PER];            // row index inside the operand
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t off[PER];        // byte offset of the slot's next float4 (valid when unmasked)
+  bool rok[PER];            // RK: row inside the operand
+  int tpos[PER];            // conv: frame position in its sequence (RK: fixed; CK: advancing)
+  int kpos[PER];            // CK: frame index of the slot
+  int kk;                   // RK: k of the thread's slots
+  int tap, kmod;            // conv: RK: k / C, k % C (advancing); CK: q / C (fixed)
+  int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
+  bool rowok;               // CK: the thread's row inside the operand
   __device__ __forceinline__ static void coords(int e, int& r, int& k) {
     if (RK) { r = e / (BK / 4); k = 4 * (e % (BK / 4)); }
     else    { k = e / (ROWS / 4); r = 4 * (e % (ROWS / 4)); }
   }
   __device__ __forceinline__ void init(const Opnd& o, int64_t r0, int64_t kbeg, int64_t R) {
+    rsrc = make_rsrc(o.p);
+    const int shift = o.conv_T > 0 ? o.tap0 : 0;   // tap0 only means something for a conv view
+    if (o.conv_T > 0) {
+      step_q = RK ? BK / o.conv_C : 0;
+      step_r = RK ? BK % o.conv_C : BK % o.conv_T;
+    }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      int rr, kk;
-      coords(threadIdx.x + i * NT, rr, kk);
-      const int r = (int)(r0 + rr), k = (int)(kbeg + kk);
-      const int shift = o.conv_T > 0 ? o.tap0 : 0;   // tap0 only means something for a conv view
-      rok[i] = r < R;
-      kpos[i] = k;
+      int rr, kq;
+      coords(threadIdx.x + i * NT, rr, kq);
+      const int64_t r = r0 + rr, k = kbeg + kq;
       if (RK) {
-        ptr[i] = o.p + ((int64_t)r + shift) * o.ld + k;
-        if (o.conv_T > 0) { tpos[i] = r % o.conv_T; tap[i] = k / o.conv_C; kmod[i] = k % o.conv_C; }
+        rok[i] = r < R;
+        off[i] = (uint32_t)((((r + shift) * o.ld) + k) * 4);
+        if (o.conv_T > 0) tpos[i] = (int)(r % o.conv_T);
+        if (i == 0) {
+          kk = (int)k;
+          if (o.conv_T > 0) { tap = (int)(k / o.conv_C); kmod = (int)(k % o.conv_C); }
+        }
       } else {
-        ptr[i] = o.p + ((int64_t)k + shift) * o.ld + r;
-        if (o.conv_T > 0) { tpos[i] = k % o.conv_T; tap[i] = r / o.conv_C; }
+        kpos[i] = (int)k;
+        off[i] = (uint32_t)((((k + shift) * o.ld) + r) * 4);
+        if (o.conv_T > 0) tpos[i] = (int)(k % o.conv_T);
+        if (i == 0) {
+          rowok = r < R;
+          if (o.conv_T > 0) tap = (int)(r / o.conv_C);
+        }
       }
     }
   }
   __device__ __forceinline__ void load(const Opnd& o, int64_t K) {
+    if (RK) {
+      const bool kin = kk < K;
+      const int tt0 = tap + o.tap0;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      bool ok = rok[i] && kpos[i] < K;
-      if (o.conv_T > 0) {
-        const int tt = tpos[i] + tap[i] + o.tap0;
-        ok = ok && tt >= 0 && tt < o.conv_T;
+      for (int i = 0; i < PER; ++i) {
+        bool ok = rok[i] && kin;
+        if (o.conv_T > 0) ok = ok && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T;
+        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
+        off[i] += BK * 4;
       }
-      v[i] = ok ? *reinterpret_cast<const f32x4*>(ptr[i]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      // advance one stage
-      kpos[i] += BK;
-      if (RK) {
-        ptr[i] += BK;
-        if (o.conv_T > 0) {
-          kmod[i] += BK;
-          while (kmod[i] >= o.conv_C) { kmod[i] -= o.conv_C; ++tap[i]; }
-        }
-      } else {
-        ptr[i] += (int64_t)BK * o.ld;
-        if (o.conv_T > 0) {
-          tpos[i] += BK;
-          while (tpos[i] >= o.conv_T) tpos[i] -= o.conv_T;
+      kk += BK;
+      if (o.conv_T > 0) {   // k += BK as (tap, kmod) with the uniform BK / C, BK % C
+        tap += step_q;
+        kmod += step_r;
+        if (kmod >= o.conv_C) { kmod -= o.conv_C; ++tap; }
+      }
+    } else {
+      const int tt0 = tap + o.tap0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        bool ok = rowok && kpos[i] < K;
+        if (o.conv_T > 0) ok = ok && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T;
+        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
+        off[i] += (uint32_t)(BK * o.ld * 4);
+        kpos[i] += BK;
+        if (o.conv_T > 0) {   // (frame + BK) % T with the uniform BK % T
+          tpos[i] += step_r;
+          if (tpos[i] >= o.conv_T) tpos[i] -= o.conv_T;
         }
       }
     }
@@ -114,6 +147,14 @@ struct OpTile {
       coords(threadIdx.x + i * NT, r, k);
       *reinterpret_cast<f32x4*>(lds + (RK ? r * LD + k : k * LD + r)) = v[i];
     }
+  }
+  // fragment values of MFMAs p = 4g .. 4g+3 (k = h*BK/2 + p) for tile row `row`
+  __device__ __forceinline__ f32x4 frag4(const float* lds, int row, int h, int g) const {
+    if (RK) return *reinterpret_cast<const f32x4*>(lds + row * LD + h * (BK / 2) + 4 * g);
+    f32x4 v;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) v[jj] = lds[(h * (BK / 2) + 4 * g + jj) * LD + row];
+    return v;
   }
   // fragment values of MFMA p (0..BK/2-1) for tile row `row`, lane half h: k = h*BK/2 + p
   __device__ __forceinline__ void frag(const float* lds, int row, int h, float (&out)[BK / 2]) const {
@@ -131,7 +172,7 @@ struct OpTile {
 };
 
 // Block tile BM x BN, k-stage BK, waves of WM x WN (each (WM/32) x (WN/32) MFMA 32x32x2).
-template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK>
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool PIPE = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
@@ -186,18 +227,46 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
     }
     const float* As = smem[buf];
     const float* Bs = smem[buf] + TA::FLOATS;
-    float af[TI][BK / 2], bf[TJ][BK / 2];
+    if (PIPE) {
+      // fragments in groups of 4 k-steps, the next group's LDS reads issued ahead of the
+      // current group's MFMAs (one wave per SIMD at 1 block/CU: the reads must hide
+      // behind this wave's own matrix work)
+      constexpr int G = BK / 8;
+      f32x4 fa[2][TI], fb[2][TJ];
 #pragma unroll
-    for (int i = 0; i < TI; ++i) sa.frag(As, wr * WM + i * 32 + li, h, af[i]);
+      for (int i = 0; i < TI; ++i) fa[0][i] = sa.frag4(As, wr * WM + i * 32 + li, h, 0);
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) sb.frag(Bs, wc * WN + j * 32 + li, h, bf[j]);
+      for (int j = 0; j < TJ; ++j) fb[0][j] = sb.frag4(Bs, wc * WN + j * 32 + li, h, 0);
 #pragma unroll
-    for (int p = 0; p < BK / 2; ++p)
+      for (int g = 0; g < G; ++g) {
+        if (g + 1 < G) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+          for (int i = 0; i < TI; ++i) fa[(g + 1) & 1][i] = sa.frag4(As, wr * WM + i * 32 + li, h, g + 1);
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][p], bf[j][p], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TJ; ++j) fb[(g + 1) & 1][j] = sb.frag4(Bs, wc * WN + j * 32 + li, h, g + 1);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[g & 1][i][jj], fb[g & 1][j][jj], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      float af[TI][BK / 2], bf[TJ][BK / 2];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) sa.frag(As, wr * WM + i * 32 + li, h, af[i]);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) sb.frag(Bs, wc * WN + j * 32 + li, h, bf[j]);
+#pragma unroll
+      for (int p = 0; p < BK / 2; ++p)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][p], bf[j][p], acc[i][j], 0, 0, 0);
+    }
     if (kt + 1 < nk) {
       sa.store(smem[buf ^ 1]);
       sb.store(smem[buf ^ 1] + TA::FLOATS);
@@ -259,6 +328,11 @@ constexpr GemmShape kCfg[] = {
     {1, 128, 64, 16},    // 4 waves of 64x32: twice the blocks for small grids
     {2, 128, 128, 32},   // 4 waves of 64x64, half the barriers
     {3, 64, 64, 16},     // 4 waves of 32x32: small outputs
+    {4, 128, 128, 32},   // cfg 2 with the fragment reads pipelined behind the MFMAs
+    {5, 64, 64, 16},     // cfg 3 pipelined
+    {6, 128, 64, 32},    // 4 waves of 64x32, BK 32, pipelined
+    {7, 128, 128, 64},   // BK 64, pipelined (139 KB LDS, 1 block/CU)
+    {8, 64, 64, 32},     // BK 32, pipelined
 };
 
 #ifndef AVC_GEMM_FORCE_CFG
@@ -268,19 +342,21 @@ int g_force_cfg = AVC_GEMM_FORCE_CFG;  // tools/gemm_bench.hip overrides this
 
 GemmShape pick_config(int M, int N, int K, int splits) {
   if (g_force_cfg >= 0) return kCfg[g_force_cfg];
-  // tools/gemm_bench.hip sweep (round 1): 128x128/BK32 wins once the 128-tile grid fills
-  // the chip >= 2x over (117-119 TF at 8192x1024..4096); narrow or short outputs are faster on
-  // 64x64 tiles (4 blocks per CU: 85-105 TF where 128x128 gave 68-92).
+  // tools/gemm_bench.hip sweep (round 1, buffer-load staging, random operands):
+  // 128x128/BK32 once the 128-tile grid fills the chip >= 2x over (115-124 TF at
+  // 8192x1024..4096); narrower unsplit outputs on 64x64/BK32 with pipelined fragment
+  // reads (conv fwd/dX 105-109 TF); split-K weight gradients on 64x64/BK16 (92-99 TF).
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
   if (t128 >= 512) return kCfg[2];
-  return kCfg[3];
+  if (splits > 1) return kCfg[3];
+  return kCfg[8];
 }
 
-template <int BM, int BN, int BK, int WM, int WN>
+template <int BM, int BN, int BK, int WM, int WN, bool PIPE = false>
 void launch_layouts(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                     float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), 0, st, M, N, K, \
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE>), grid, dim3(NT), 0, st, M, N, K, \
                                          oa, ob, C, ldc, b1, b2, acc, kps, slab)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
@@ -295,6 +371,11 @@ void launch_gemm(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, in
     case 0: launch_layouts<128, 128, 16, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     case 1: launch_layouts<128, 64, 16, 64, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     case 2: launch_layouts<128, 128, 32, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 4: launch_layouts<128, 128, 32, 64, 64, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 5: launch_layouts<64, 64, 16, 32, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 6: launch_layouts<128, 64, 32, 64, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 7: launch_layouts<128, 128, 64, 64, 64, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 8: launch_layouts<64, 64, 32, 32, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     default: launch_layouts<64, 64, 16, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
   }
 }
@@ -322,6 +403,11 @@ extern "C" int autovc_gemm_f32(int M, int N, int K,
                 "autovc_gemm_f32: A conv channels must be a positive multiple of 4");
   AVC_CHECK_ARG(!b_conv_T || (b_conv_C % 4 == 0 && b_conv_C > 0),
                 "autovc_gemm_f32: B conv channels must be a positive multiple of 4");
+  // buffer-load byte offsets are 32-bit (descriptor range 2 GiB)
+  const int64_t a_ext = a_trans ? (int64_t)K * lda : (int64_t)M * lda;
+  const int64_t b_ext = b_trans ? (int64_t)K * ldb : (int64_t)N * ldb;
+  AVC_CHECK_ARG(4 * (a_ext + 2 * lda) < (int64_t)kOOB && 4 * (b_ext + 2 * ldb) < (int64_t)kOOB,
+                "autovc_gemm_f32: operand extents must stay below 2 GiB");
   if (splits < 1) splits = 1;
   const GemmShape cfg = pick_config(M, N, K, splits);
   const int BKc = cfg.bk;

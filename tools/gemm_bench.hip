@@ -8,7 +8,8 @@
 
 struct Case { const char* name; int M, N, K, at, bt, aconv, bconv, C, splits; };
 
-int main() {
+int main(int argc, char** argv) {
+  const int only_case = argc > 2 ? atoi(argv[1]) : -1, only_cfg = argc > 2 ? atoi(argv[2]) : -1;
   const int T = 128;
   Case cases[] = {
       {"conv fwd 512->512", 8192, 512, 2560, 0, 0, 1, 0, 512, 1},
@@ -33,14 +34,24 @@ int main() {
   (void)hipMalloc(&B, big * 4);
   (void)hipMalloc(&Cm, big * 4);
   (void)hipMalloc(&ws, 4 * big * 4);
-  (void)hipMemset(A, 0, big * 4);
-  (void)hipMemset(B, 0, big * 4);
+  {  // random operands (MFMA clocks differ on zeros)
+    float* h = (float*)malloc(big * 4);
+    for (size_t i = 0; i < big; ++i) h[i] = (float)((i * 2654435761u) % 1000) * 1e-3f - 0.5f;
+    (void)hipMemcpy(A, h, big * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(B, h, big * 4, hipMemcpyHostToDevice);
+    free(h);
+  }
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
+  int ci = -1;
   for (const Case& c : cases) {
+    ++ci;
+    if (only_case >= 0 && ci != only_case) continue;
     printf("%-20s M=%5d N=%5d K=%5d s=%d :", c.name, c.M, c.N, c.K, c.splits);
-    for (int cfg = 0; cfg < 4; ++cfg) {
+    for (int cfg = 2; cfg < 9; ++cfg) {
+      if (cfg == 5 || cfg == 6) continue;
+      if (only_cfg >= 0 && cfg != only_cfg) continue;
       g_force_cfg = cfg;
       const int lda = c.at ? c.M : (c.aconv ? c.C : c.K);
       const int ldb = c.bt ? (c.bconv ? c.C : c.N) : c.K;

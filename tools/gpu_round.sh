@@ -10,7 +10,7 @@ run_tests() {
   if [ -n "$PYTEST_K" ]; then timeout -k 10 ${T_TESTS:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$PYTEST_K" > gpurun_out/tests.log 2>&1
   else timeout -k 10 ${T_TESTS:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/tests.log 2>&1; fi; }
 run_bench() { timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; }
-run_prof()  { timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-wavenet > gpurun_out/prof.log 2>&1; }
+run_prof()  { timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-wavenet --no-e2e > gpurun_out/prof.log 2>&1; }
 case "$STEP" in
   tests) run_tests ;;
   bench) run_bench ;;
