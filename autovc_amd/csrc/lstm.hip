@@ -55,12 +55,18 @@ struct Tile {
 // swizzled float4 position of slot sl in row r
 __device__ __forceinline__ int swz(int sl, int r) { return (sl & ~15) | ((sl & 15) ^ (r & 15)); }
 
-template <int KCH, int NW, int D, class AR, class BR>
-__device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, int K) {
+// Two K segments: k < K1 reads the rows of (arow_of, brow_of), the next K2 those of
+// (arow2_of, brow2_of) — the stacked-layer step concatenates [input ; recurrent] this way
+// (K2 = 0: one segment).
+template <int KCH, int NW, int D, class AR, class BR, class AR2, class BR2>
+__device__ __forceinline__ f32x4 tile_gemm2(float* lds, AR arow_of, BR brow_of, int K1, AR2 arow2_of, BR2 brow2_of,
+                                            int K2) {
   using C = Tile<KCH, NW, D>;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* arow[C::PER];
   const float* brow[C::PER];
+  const float* arow2[C::PER];
+  const float* brow2[C::PER];
   int srow[C::PER], spos[C::PER];
 #pragma unroll
   for (int i = 0; i < C::PER; ++i) {
@@ -68,10 +74,15 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
     const int r = e / C::SLOTS, sl = e % C::SLOTS;
     srow[i] = r;
     spos[i] = swz(sl, r);
-    arow[i] = arow_of(r) + 4 * sl;
-    brow[i] = brow_of(r) + 4 * sl;
+    arow[i] = (K1 ? arow_of(r) : arow2_of(r)) + 4 * sl;
+    brow[i] = (K1 ? brow_of(r) : brow2_of(r)) + 4 * sl;
+    arow2[i] = (K2 ? arow2_of(r) : arow[i] - 4 * sl) + 4 * sl;
+    brow2[i] = (K2 ? brow2_of(r) : brow[i] - 4 * sl) + 4 * sl;
   }
-  const int nc = K / KCH;
+  const int nc1 = K1 / KCH, nc = (K1 + K2) / KCH;
+  auto at = [&](const float* const* p1, const float* const* p2, int i, int cl) {
+    return cl < nc1 ? p1[i] + cl * KCH : p2[i] + (cl - nc1) * KCH;
+  };
   // Loads run D chunks ahead.  They are issued unconditionally (past the last chunk the
   // address is clamped to the last chunk, an L2 hit) so the k loop is straight-line code
   // and hipcc can wait with vmcnt(4 (D-1)) for the oldest chunk only: a conditional load
@@ -82,8 +93,8 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
     const int cl = min(d, nc - 1);
 #pragma unroll
     for (int i = 0; i < C::PER; ++i) {
-      sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + cl * KCH);
-      sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + cl * KCH);
+      sa[d][i] = *reinterpret_cast<const f32x4*>(at(arow, arow2, i, cl));
+      sb[d][i] = *reinterpret_cast<const f32x4*>(at(brow, brow2, i, cl));
     }
   }
   const int q = w & 3, kh = w >> 2, g = lane >> 4;
@@ -103,8 +114,8 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
       const int cn = min(c + D, nc - 1);
 #pragma unroll
       for (int i = 0; i < C::PER; ++i) {
-        sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + cn * KCH);
-        sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + cn * KCH);
+        sa[d][i] = *reinterpret_cast<const f32x4*>(at(arow, arow2, i, cn));
+        sb[d][i] = *reinterpret_cast<const f32x4*>(at(brow, brow2, i, cn));
       }
       if (c < nc) {
         f32x4 av[C::SUB], bv[C::SUB];
@@ -139,6 +150,11 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
   return acc;  // valid in waves 0..3 (quadrant q = wave)
 }
 
+template <int KCH, int NW, int D, class AR, class BR>
+__device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, int K) {
+  return tile_gemm2<KCH, NW, D>(lds, arow_of, brow_of, K, arow_of, brow_of, 0);
+}
+
 // configuration used by the product kernels (chosen with tools/lstm_step_bench.hip)
 #ifndef AVC_LSTM_KCH
 #define AVC_LSTM_KCH 64
@@ -159,13 +175,19 @@ struct StepArgs {
   float* h; int64_t h_ldb, h_ldt;            // h out/in: h[b*h_ldb + t*h_ldt + j]
   float* c;                                  // (B, T, H) cell states
   float* gates;                              // (B, T, 4H) post-activation gates or null
+  const float* gx2;                          // second bias added to gx (same strides) or null
 };
 
-// One forward time step of a large-H layer.  grid = (H / 8, ceil(B / 32)).
+// One forward time step of a large-H layer, block (blockIdx.x, blockIdx.y) of grid
+// (H / 8, ceil(B / 32)).  Gate pre-activations = gx_t + [xin_t ; h_{t-1}] [W_in ; W]^T:
+// K_in = 0 for a layer whose input projection gx was precomputed by one GEMM over all
+// frames; K_in = I for the upper layer of a stacked pair, whose input is the lower layer's
+// h_t of this same launch wavefront (gx then holds only b_ih + b_hh, strides 0).
 // ABL != 0 only in the ablation build of tools/lstm_step_bench.hip (bit 0: every block
 // reads the same W_hh rows, bit 1: every lane reads the same h row) — never launched here.
-template <int ABL = 0, int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
-__global__ __launch_bounds__(64 * NW_) void lstm_fwd_step_kernel(StepArgs a, int t, int tp) {
+template <int ABL, int KCH_, int NW_, int D_>
+__device__ __forceinline__ void fwd_step_body(const StepArgs& a, int t, int tp, const float* xin, int64_t x_ldb,
+                                              int64_t x_ldt, const float* W_in, int K_in) {
   using C = Tile<KCH_, NW_, D_>;
   __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -181,37 +203,71 @@ __global__ __launch_bounds__(64 * NW_) void lstm_fwd_step_kernel(StepArgs a, int
     const float* g = a.gx + (int64_t)b * a.gx_ldb + (int64_t)t * a.gx_ldt;
 #pragma unroll
     for (int q = 0; q < 4; ++q) gxv[q] = g[q * H + j];
+    if (a.gx2) {
+      const float* g2 = a.gx2 + (int64_t)b * a.gx_ldb + (int64_t)t * a.gx_ldt;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gxv[q] += g2[q * H + j];
+    }
     if (tp >= 0) cp = a.c[(int64_t)b * a.T * H + (int64_t)tp * H + j];
   }
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (tp >= 0) {
-    auto arow_of = [&](int r) {
-      const int b = (ABL & 2) ? 0 : min(b0 + r, a.B - 1);  // rows past B: any valid row, result unused
-      return a.h + (int64_t)b * a.h_ldb + (int64_t)tp * a.h_ldt;
-    };
-    auto brow_of = [&](int r) {  // tile column r = gate*8 + unit
-      return a.W + (int64_t)((r >> 3) * H + ((ABL & 1) ? 0 : j0) + (r & 7)) * H;
-    };
-    acc = tile_gemm<KCH_, NW_, D_>(smem, arow_of, brow_of, H);
-  }
-  __syncthreads();
-  float* tile = smem;                                      // [32][33] after the chunk buffers are drained
-  if (w < 4) {
-    const int wi = w >> 1, wn = w & 1;
+  const int K_rec = tp >= 0 ? H : 0;
+  auto arow_of = [&](int r) {
+    const int b = (ABL & 2) ? 0 : min(b0 + r, a.B - 1);  // rows past B: any valid row, result unused
+    return a.h + (int64_t)b * a.h_ldb + (int64_t)max(tp, 0) * a.h_ldt;
+  };
+  auto brow_of = [&](int r) {  // tile column r = gate*8 + unit
+    return a.W + (int64_t)((r >> 3) * H + ((ABL & 1) ? 0 : j0) + (r & 7)) * H;
+  };
+  auto xrow_of = [&](int r) { return xin + (int64_t)min(b0 + r, a.B - 1) * x_ldb + (int64_t)t * x_ldt; };
+  auto wrow_of = [&](int r) { return W_in + (int64_t)((r >> 3) * H + j0 + (r & 7)) * K_in; };
+  float pre[4];
+  {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (K_in + K_rec > 0) acc = tile_gemm2<KCH_, NW_, D_>(smem, xrow_of, wrow_of, K_in, arow_of, brow_of, K_rec);
+    __syncthreads();
+    float* tile = smem;                                      // [32][33] after the chunk buffers are drained
+    if (w < 4) {
+      const int wi = w >> 1, wn = w & 1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) tile[(wi * 16 + 4 * (lane >> 4) + r) * (TN + 1) + wn * 16 + (lane & 15)] = acc[r];
+      for (int r = 0; r < 4; ++r) tile[(wi * 16 + 4 * (lane >> 4) + r) * (TN + 1) + wn * 16 + (lane & 15)] = acc[r];
+    }
+    __syncthreads();
+    if (!own) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pre[q] = tile[bl * (TN + 1) + q * UT + u];
   }
-  __syncthreads();
-  if (!own) return;
-  const float* tr = tile + bl * (TN + 1);
-  const float i_ = avc_sigmoid(tr[0 * UT + u] + gxv[0]), f_ = avc_sigmoid(tr[1 * UT + u] + gxv[1]);
-  const float g_ = tanhf(tr[2 * UT + u] + gxv[2]), o_ = avc_sigmoid(tr[3 * UT + u] + gxv[3]);
+  const float i_ = avc_sigmoid(pre[0] + gxv[0]), f_ = avc_sigmoid(pre[1] + gxv[1]);
+  const float g_ = tanhf(pre[2] + gxv[2]), o_ = avc_sigmoid(pre[3] + gxv[3]);
   const float cn = f_ * cp + i_ * g_;
   a.c[(int64_t)b * a.T * H + (int64_t)t * H + j] = cn;
   a.h[(int64_t)b * a.h_ldb + (int64_t)t * a.h_ldt + j] = o_ * tanhf(cn);
   if (a.gates) {
     float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H;
     gs[0 * H + j] = i_; gs[1 * H + j] = f_; gs[2 * H + j] = g_; gs[3 * H + j] = o_;
+  }
+}
+
+template <int ABL = 0, int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+__global__ __launch_bounds__(64 * NW_) void lstm_fwd_step_kernel(StepArgs a, int t, int tp) {
+  fwd_step_body<ABL, KCH_, NW_, D_>(a, t, tp, nullptr, 0, 0, nullptr, 0);
+}
+
+// Two stacked layers (nn.LSTM num_layers=2, decoder lstm2) as one launch per wavefront
+// step: blockIdx.z = 0 runs layer 0 at step t, z = 1 runs layer 1 at step t - 1 on the
+// layer-0 output h0_{t-1} written by the previous launch.  T + 1 launches instead of 2T,
+// both layers' blocks co-resident on every CU (2 blocks/CU), and no separate input
+// projection GEMM for layer 1 (it is the first K segment of its step).
+struct Stack2Args {
+  StepArgs l0, l1;
+  const float* W_ih1;   // (4H, H)
+};
+
+template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+__global__ __launch_bounds__(64 * NW_) void lstm2_fwd_step_kernel(Stack2Args a, int t) {
+  if (blockIdx.z == 0) {
+    if (t < a.l0.T) fwd_step_body<0, KCH_, NW_, D_>(a.l0, t, t - 1, nullptr, 0, 0, nullptr, 0);
+  } else if (t >= 1) {
+    fwd_step_body<0, KCH_, NW_, D_>(a.l1, t - 1, t - 2, a.l0.h, a.l0.h_ldb, a.l0.h_ldt, a.W_ih1, a.l1.H);
   }
 }
 
@@ -301,13 +357,15 @@ __global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, in
   const int K4 = 4 * H, ks = K4 / S, kb = s * ks;
   auto arow_of = [&](int r) { return dG + ((int64_t)min(b0 + r, B - 1) * T + t) * K4 + kb; };
   auto brow_of = [&](int r) { return WT + (int64_t)(j0 + r) * K4 + kb; };
-  const f32x4 acc = tile_gemm<KCH_, NW_, D_>(smem, arow_of, brow_of, ks);
-  if (w >= 4) return;
-  const int wi = w >> 1, wn = w & 1;
+  {
+    const f32x4 acc = tile_gemm<KCH_, NW_, D_>(smem, arow_of, brow_of, ks);
+    if (w >= 4) return;
+    const int wi = w >> 1, wn = w & 1;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int b = b0 + wi * 16 + 4 * (lane >> 4) + r;
-    if (b < B) P[((int64_t)s * B + b) * H + j0 + wn * 16 + (lane & 15)] = acc[r];
+    for (int r = 0; r < 4; ++r) {
+      const int b = b0 + wi * 16 + 4 * (lane >> 4) + r;
+      if (b < B) P[((int64_t)s * B + b) * H + j0 + wn * 16 + (lane & 15)] = acc[r];
+    }
   }
 }
 
@@ -443,7 +501,7 @@ extern "C" int autovc_lstm_fwd_f32(int B, int T, int H, const float* gx, int64_t
   AVC_CHECK_ARG(gx && W_hh && h && c_all, "autovc_lstm_fwd_f32: null pointer");
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh) && AVC_ALIGNED16(h) && (h_ldb % 4 == 0) && (h_ldt % 4 == 0),
                 "autovc_lstm_fwd_f32: W_hh / h must be 16-byte aligned with strides %% 4 == 0");
-  StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, W_hh, h, h_ldb, h_ldt, c_all, gates};
+  StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, W_hh, h, h_ldb, h_ldt, c_all, gates, nullptr};
   const dim3 grid(H / UT, (B + TB - 1) / TB);
   for (int s = 0; s < T; ++s) {
     const int t = reverse ? T - 1 - s : s;
@@ -451,6 +509,25 @@ extern "C" int autovc_lstm_fwd_f32(int B, int T, int H, const float* gx, int64_t
     launch_fwd_step(grid, stream, a, t, tp);
   }
   AVC_CHECK_LAUNCH("autovc_lstm_fwd_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm2_fwd_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                                    const float* W_hh0, const float* b_ih1, const float* b_hh1,
+                                    const float* W_ih1, const float* W_hh1, float* h0, float* c0, float* gates0,
+                                    float* h1, float* c1, float* gates1, hipStream_t stream) {
+  AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H) && H % KCH == 0,
+                "autovc_lstm2_fwd_f32: bad dims B=%d T=%d H=%d (H must be a multiple of %d)", B, T, H, KCH);
+  AVC_CHECK_ARG(gx0 && W_hh0 && b_ih1 && b_hh1 && W_ih1 && W_hh1 && h0 && c0 && h1 && c1,
+                "autovc_lstm2_fwd_f32: null pointer");
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh0) && AVC_ALIGNED16(W_ih1) && AVC_ALIGNED16(W_hh1) && AVC_ALIGNED16(h0) &&
+                AVC_ALIGNED16(h1), "autovc_lstm2_fwd_f32: weights / h must be 16-byte aligned");
+  Stack2Args a{StepArgs{B, T, H, gx0, gx_ldb, gx_ldt, W_hh0, h0, (int64_t)T * H, H, c0, gates0, nullptr},
+               StepArgs{B, T, H, b_ih1, 0, 0, W_hh1, h1, (int64_t)T * H, H, c1, gates1, b_hh1}, W_ih1};
+  const dim3 grid(H / UT, (B + TB - 1) / TB, 2);
+  for (int t = 0; t <= T; ++t)
+    hipLaunchKernelGGL((lstm2_fwd_step_kernel<KCH, NWV, DPF>), grid, dim3(64 * NWV), 0, stream, a, t);
+  AVC_CHECK_LAUNCH("autovc_lstm2_fwd_f32");
   return avc::kOk;
 }
 
@@ -523,7 +600,7 @@ extern "C" int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, i
                                          float* gates, hipStream_t stream, float* avg_us) {
   AVC_CHECK_ARG(T > 1 && lstm_shape_ok(B, H) && avg_us, "autovc_lstm_fwd_timed_f32: bad args");
   AVC_CHECK_ARG(gx && W_hh && h && c_all, "autovc_lstm_fwd_timed_f32: null pointer");
-  StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, W_hh, h, h_ldb, h_ldt, c_all, gates};
+  StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, W_hh, h, h_ldb, h_ldt, c_all, gates, nullptr};
   const dim3 grid(H / UT, (B + TB - 1) / TB);
   hipEvent_t* ev = new hipEvent_t[2 * T];
   for (int i = 0; i < 2 * T; ++i) AVC_HIP(hipEventCreate(&ev[i]), "autovc_lstm_fwd_timed_f32/event");

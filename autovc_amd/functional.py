@@ -368,41 +368,88 @@ class LSTMLayerFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh):
         x, W_ih, W_hh, h, c, gates = ctx.saved_tensors
-        p_ih, p_hh, p_bih, p_bhh = ctx.params
-        if gates is None:
-            raise RuntimeError("LSTM backward needs the forward run with gradients enabled")
-        dh = dh.contiguous()
+        return _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, ctx.params, ctx.needs_input_grad[:5]) + (None,)
+
+
+def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
+    """BPTT of one large-H layer: recurrence (C-ABI), weight/bias gradients straight into
+    the flat gradient buffer where the optimizer owns one, dx.  Returns (dx, dW_ih, dW_hh,
+    db_ih, db_hh) for autograd (None where accumulated in place or not needed)."""
+    p_ih, p_hh, p_bih, p_bhh = params
+    if gates is None:
+        raise RuntimeError("LSTM backward needs the forward run with gradients enabled")
+    dh = dh.contiguous()
+    B, T, I = x.shape
+    H = W_hh.shape[1]
+    dev = x.device
+    WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
+    _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
+    splits = 4 if (4 * H) % 256 == 0 else 1
+    ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
+    dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+    _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
+              WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
+    M = B * T
+    dx = dWih = dWhh = dbih = dbhh = None
+    if needs[1]:
+        go = _GradOut(p_ih, W_ih.shape, dev)
+        gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I, splits=_splits_for(4 * H, I, M), accumulate=go.acc)
+        dWih = go.result()
+    if needs[2]:
+        go = _GradOut(p_hh, W_hh.shape, dev)
+        gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
+             splits=_splits_for(4 * H, H, M), accumulate=go.acc)
+        dWhh = go.result()
+    if needs[3] or needs[4]:
+        gi, gh = _GradOut(p_bih, (4 * H,), dev), _GradOut(p_bhh, (4 * H,), dev)
+        if gi.acc != gh.acc:
+            gi, gh = _GradOut(None, (4 * H,), dev), _GradOut(None, (4 * H,), dev)
+        colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc)
+        dbih, dbhh = gi.result(), gh.result()
+    if needs[0]:
+        dx = torch.empty_like(x)
+        gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I)
+    return dx, dWih, dWhh, dbih, dbhh
+
+
+class LSTM2StackFn(torch.autograd.Function):
+    """Two stacked unidirectional large-H layers (decoder lstm2 = nn.LSTM(512, 1024, 2),
+    model_vc_mel.py:104,118).  Forward: one GEMM for the layer-0 input projection, then
+    autovc_lstm2_fwd_f32 runs both recurrences as a one-step-lagged wavefront (T + 1
+    launches; layer 1's input projection is the first K segment of its step).  Backward:
+    layer 1 then layer 0, as two LSTMLayerFn backwards."""
+
+    @staticmethod
+    def forward(ctx, x, W_ih0, W_hh0, b_ih0, b_hh0, W_ih1, W_hh1, b_ih1, b_hh1, save):
+        _check(x, "lstm")
+        x = x.contiguous()
         B, T, I = x.shape
-        H = W_hh.shape[1]
+        H = W_hh0.shape[1]
         dev = x.device
-        WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
-        _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
-        splits = 4 if (4 * H) % 256 == 0 else 1
-        ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
-        dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-        _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
-                  WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
-        M = B * T
-        dx = dWih = dWhh = dbih = dbhh = None
-        if ctx.needs_input_grad[1]:
-            go = _GradOut(p_ih, W_ih.shape, dev)
-            gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I, splits=_splits_for(4 * H, I, M), accumulate=go.acc)
-            dWih = go.result()
-        if ctx.needs_input_grad[2]:
-            go = _GradOut(p_hh, W_hh.shape, dev)
-            gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
-                 splits=_splits_for(4 * H, H, M), accumulate=go.acc)
-            dWhh = go.result()
-        if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
-            gi, gh = _GradOut(p_bih, (4 * H,), dev), _GradOut(p_bhh, (4 * H,), dev)
-            if gi.acc != gh.acc:
-                gi, gh = _GradOut(None, (4 * H,), dev), _GradOut(None, (4 * H,), dev)
-            colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc)
-            dbih, dbhh = gi.result(), gh.result()
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I)
-        return dx, dWih, dWhh, dbih, dbhh, None
+        gx0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+        gemm(B * T, 4 * H, I, x, I, 0, W_ih0, I, 0, gx0, 4 * H, bias1=b_ih0, bias2=b_hh0)
+        h0, c0, h1, c1 = (torch.empty((B, T, H), device=dev, dtype=torch.float32) for _ in range(4))
+        g0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
+        g1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
+        _lib.call("autovc_lstm2_fwd_f32", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W_hh0.data_ptr(),
+                  b_ih1.data_ptr(), b_hh1.data_ptr(), W_ih1.data_ptr(), W_hh1.data_ptr(), h0.data_ptr(),
+                  c0.data_ptr(), _p(g0), h1.data_ptr(), c1.data_ptr(), _p(g1), _s())
+        ctx.save_for_backward(x, W_ih0, W_hh0, h0, c0, g0, W_ih1, W_hh1, h1, c1, g1)
+        ctx.params = ((W_ih0, W_hh0, b_ih0, b_hh0), (W_ih1, W_hh1, b_ih1, b_hh1))
+        return h1
+
+    @staticmethod
+    def backward(ctx, dh1):
+        x, W_ih0, W_hh0, h0, c0, g0, W_ih1, W_hh1, h1, c1, g1 = ctx.saved_tensors
+        n = ctx.needs_input_grad
+        need0 = (n[0],) + tuple(n[1:5])
+        need1 = (any(need0),) + tuple(n[5:9])
+        dh0, *grads1 = _lstm_layer_backward(dh1, h0, W_ih1, W_hh1, h1, c1, g1, ctx.params[1], need1)
+        if dh0 is None:
+            grads0 = [None] * 5
+        else:
+            grads0 = _lstm_layer_backward(dh0, x, W_ih0, W_hh0, h0, c0, g0, ctx.params[0], need0)
+        return (grads0[0], *grads0[1:], *grads1, None)
 
 
 class BLSTMLayerFn(torch.autograd.Function):

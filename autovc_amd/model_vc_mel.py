@@ -92,6 +92,12 @@ class LSTM(nn.Module):
         if hx is not None:
             raise NotImplementedError("initial states are zero in AutoVC")
         save = torch.is_grad_enabled()
+        if (not self.bidirectional and self.num_layers == 2 and self.hidden_size % 64 == 0
+                and self.hidden_size >= 256):
+            # stacked pair as one wavefront (decoder lstm2, model_vc_mel.py:104)
+            return AF.LSTM2StackFn.apply(x, self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0, self.bias_hh_l0,
+                                         self.weight_ih_l1, self.weight_hh_l1, self.bias_ih_l1, self.bias_hh_l1,
+                                         save), None
         out = x
         for layer in range(self.num_layers):
             g = lambda n, s="": getattr(self, f"{n}_l{layer}{s}")  # noqa: E731

@@ -108,6 +108,16 @@ int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t lddz, const
 int autovc_lstm_fwd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                         const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                         float* gates, int reverse, hipStream_t stream);
+/* Two stacked large-H layers (nn.LSTM(I, H, num_layers=2), decoder lstm2,
+ * model_vc_mel.py:104,118) as a wavefront: launch t runs layer 0 step t and layer 1 step
+ * t-1 (T+1 launches).  gx0 = x W_ih0^T + b_ih0 + b_hh0 precomputed (strides as above);
+ * layer 1's input projection h0_t W_ih1^T runs inside its step (first K segment);
+ * h0/h1, c0/c1 (B,T,H) contiguous; gates0/gates1 (B,T,4H) or null.  Same arithmetic as
+ * two autovc_lstm_fwd_f32 calls with the layer-1 projection GEMM in between. */
+int autovc_lstm2_fwd_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                         const float* W_hh0, const float* b_ih1, const float* b_hh1, const float* W_ih1,
+                         const float* W_hh1, float* h0, float* c0, float* gates0, float* h1, float* c1,
+                         float* gates1, hipStream_t stream);
 /* autovc_lstm_fwd_f32 with every step launch timed by its own dispatch events;
  * synchronises; *avg_us (HOST pointer) = mean kernel time of steps 1..T-1 (bench.py). */
 int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_ldb,
