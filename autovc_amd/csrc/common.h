@@ -53,3 +53,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Accurate (ocml) expf/tanhf: the LSTM parity bar is 1e-4 rel vs torch CPU.
 __device__ __forceinline__ float avc_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// x + x[lane ^ M] inside each quad of lanes (M = 1 or 2): DPP quad_perm, VALU only
+template <int M>
+__device__ __forceinline__ float avc_quad_xor_add(float x) {
+  static_assert(M == 1 || M == 2, "quad lanes");
+  constexpr int ctrl = M == 1 ? 0xB1 : 0x4E;   // quad_perm [1,0,3,2] / [2,3,0,1]
+  return x + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), ctrl, 0xF, 0xF, false));
+}

@@ -17,7 +17,8 @@
 //    Backward = per step the same tile kernel computing split-K partials of
 //    dh_rec = dG_t W_hh (through the pre-transposed W_hh^T) + a pointwise kernel.
 //  * small H (encoder BLSTM, H=32): the whole sequence in one launch, one workgroup per
-//    (direction, 8 batch rows), the thread's W_hh rows/columns held in registers.
+//    (direction, 2 batch rows), a quad of lanes per (row, unit) splitting the 32-deep dot
+//    products, W_hh slices held in registers, per-step operands prefetched 8 steps ahead.
 #include <hip/hip_ext.h>
 
 #include <algorithm>
@@ -370,113 +371,162 @@ __global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, in
 }
 
 // ------------------------------------------------------------------ small H (BLSTM)
-// Whole sequence, both directions in one launch.  grid = (ceil(B/8), ndir); block 256 =
-// 8 batch rows x 32 units.  gx: (B,T,ndir*4H) [dir-major blocks]; h out: (B,T,ndir*H).
-// Forward: thread (b, j) keeps W_hh rows {q*H + j} (4 x 32 floats) in registers.
-constexpr int SH = 32, SB = 8;
+// Whole sequence, both directions in one launch.  grid = (ceil(B/2), ndir); block 256 =
+// 2 batch rows x 32 units x 4 k-quarters.  gx: (B,T,ndir*4H) [dir-major blocks]; h out:
+// (B,T,ndir*H).
+constexpr int SH = 32;
+
+// Latency layout: a step of the H = 32 recurrence is a 32-deep dot product per gate, so
+// each (batch row, unit) gets a quad of lanes that split k (or, backward, the 4 gate
+// blocks) four ways and combine with two DPP quad adds; a workgroup holds SB2 = 2 batch
+// rows (256 threads, one wave per SIMD), so per-step VALU work per SIMD is a quarter of
+// a thread-per-(b, j) layout, and B / 2 x ndir workgroups spread over as many CUs.
+// Per-step operands (input-gate pre-activations; in backward the saved gates, cells and
+// dh from above) are prefetched PD steps ahead into a register ring: the recurrence is a
+// fraction of a microsecond per step, a load issued in its own step a full HBM round trip.
+// The loop runs over T rounded up to PD with clamped addresses, so every load is
+// unconditional and hipcc counts its waits precisely; steps past T store nothing.
+constexpr int PD = 8, SB2 = 2, KQ = SH / 4;
 
 __global__ __launch_bounds__(kThreads) void blstm_fwd_kernel(int B, int T, const float* gx, const float* Whh_f,
                                                             const float* Whh_b, float* hout, float* call,
                                                             float* gates, int ndir) {
-  __shared__ float hs[2][SB][SH];
+  __shared__ __attribute__((aligned(16))) float hs[2][SB2][SH];
   const int dir = blockIdx.y;
-  const int bl = threadIdx.x / SH, j = threadIdx.x % SH;
-  const int b = blockIdx.x * SB + bl;
+  const int ks = threadIdx.x & 3, j = (threadIdx.x >> 2) & 31, bl = threadIdx.x >> 7;
+  const int b = blockIdx.x * SB2 + bl;
+  const int bc = min(b, B - 1);          // rows past B load a valid row, store nothing
   const float* W = dir ? Whh_b : Whh_f;
-  float wr[4][SH];
+  float wr[4][KQ];                       // W_hh[q*SH + j][ks*KQ + kk]
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int k = 0; k < SH; k += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(W + (q * SH + j) * SH + k);
+    for (int k = 0; k < KQ; k += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(W + (q * SH + j) * SH + ks * KQ + k);
       wr[q][k] = v[0]; wr[q][k + 1] = v[1]; wr[q][k + 2] = v[2]; wr[q][k + 3] = v[3];
     }
-  hs[0][bl][j] = 0.f;
+  if (threadIdx.x < SB2 * SH) hs[0][threadIdx.x / SH][threadIdx.x % SH] = 0.f;
   __syncthreads();
   const int G = ndir * 4 * SH, HO = ndir * SH;
+  // lane ks brings gate ks's input pre-activation; the quad sum adds it exactly once
+  auto gsrc = [&](int s) {
+    const int tt = min(s, T - 1);
+    return gx + ((int64_t)bc * T + (dir ? T - 1 - tt : tt)) * G + dir * 4 * SH + ks * SH + j;
+  };
+  float gq[PD];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) gq[d] = *gsrc(d);
   float c = 0.f;
   int cur = 0;
-  float gnext[4] = {0.f, 0.f, 0.f, 0.f};
-  if (b < B) {
-    const float* g = gx + ((int64_t)b * T + (dir ? T - 1 : 0)) * G + dir * 4 * SH;
+  const bool own = b < B;
+  for (int s0 = 0; s0 < T; s0 += PD) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) gnext[q] = g[q * SH + j];
-  }
-  for (int s = 0; s < T; ++s) {
-    const int t = dir ? T - 1 - s : s;
-    float acc[4] = {gnext[0], gnext[1], gnext[2], gnext[3]};
-    if (b < B && s + 1 < T) {   // prefetch next step's input gates
-      const float* g = gx + ((int64_t)b * T + (dir ? t - 1 : t + 1)) * G + dir * 4 * SH;
+    for (int d = 0; d < PD; ++d) {
+      const int s = s0 + d;
+      const int t = dir ? T - 1 - s : s;
+      float acc[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gnext[q] = g[q * SH + j];
-    }
+      for (int q = 0; q < 4; ++q) acc[q] = q == ks ? gq[d] : 0.f;
+      gq[d] = *gsrc(s + PD);
+      const float* hr = &hs[cur][bl][ks * KQ];
+      const f32x4 h0 = *reinterpret_cast<const f32x4*>(hr), h1 = *reinterpret_cast<const f32x4*>(hr + 4);
 #pragma unroll
-    for (int k = 0; k < SH; ++k) {
-      const float hv = hs[cur][bl][k];
+      for (int k = 0; k < KQ; ++k) {
+        const float hv = k < 4 ? h0[k] : h1[k - 4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = fmaf(hv, wr[q][k], acc[q]);
-    }
-    const float i_ = avc_sigmoid(acc[0]), f_ = avc_sigmoid(acc[1]), g_ = tanhf(acc[2]), o_ = avc_sigmoid(acc[3]);
-    c = f_ * c + i_ * g_;
-    const float h = o_ * tanhf(c);
-    hs[cur ^ 1][bl][j] = h;
-    if (b < B) {
-      hout[((int64_t)b * T + t) * HO + dir * SH + j] = h;
-      if (call) call[((int64_t)b * T + t) * HO + dir * SH + j] = c;
-      if (gates) {
-        float* gs = gates + ((int64_t)b * T + t) * G + dir * 4 * SH;
-        gs[j] = i_; gs[SH + j] = f_; gs[2 * SH + j] = g_; gs[3 * SH + j] = o_;
+        for (int q = 0; q < 4; ++q) acc[q] = fmaf(hv, wr[q][k], acc[q]);
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = avc_quad_xor_add<2>(avc_quad_xor_add<1>(acc[q]));
+      const float i_ = avc_sigmoid(acc[0]), f_ = avc_sigmoid(acc[1]), g_ = tanhf(acc[2]), o_ = avc_sigmoid(acc[3]);
+      c = f_ * c + i_ * g_;
+      const float h = o_ * tanhf(c);
+      if (ks == 0) hs[cur ^ 1][bl][j] = h;
+      if (own && s < T) {
+        const int64_t o = ((int64_t)b * T + t) * HO + dir * SH + j;
+        if (ks == 0) hout[o] = h;
+        if (call && ks == 1) call[o] = c;
+        if (gates) gates[((int64_t)b * T + t) * G + dir * 4 * SH + ks * SH + j] =
+            ks == 0 ? i_ : ks == 1 ? f_ : ks == 2 ? g_ : o_;
+      }
+      cur ^= 1;
+      __syncthreads();
     }
-    cur ^= 1;
-    __syncthreads();
   }
 }
 
 // Backward of blstm_fwd_kernel: per direction, walk the sequence in reverse processing
-// order.  dG: (B,T,ndir*4H).  dh_out: (B,T,ndir*H) or null.  Thread (b, j) keeps W_hh
-// column j (4H floats) in registers for dh_rec[b][j] = sum_r dG[b][r] W[r][j].
+// order.  dG: (B,T,ndir*4H).  dh_out: (B,T,ndir*H) or null (HAS_DH).  The quad of
+// (b, j) computes the pointwise step redundantly, lane ks stores gate ks of dG, and the
+// recurrent dh_rec[b][j] = sum_r dG[b][r] W[r][j] splits r by gate block (lane ks: rows
+// ks*SH .. +SH, W_hh column j of that block in registers), summed by two DPP quad adds.
+// dG_t goes through a double-buffered LDS row: one barrier per step.
+template <bool HAS_DH>
 __global__ __launch_bounds__(kThreads) void blstm_bwd_kernel(int B, int T, const float* dh_out, const float* gates,
                                                             const float* call, const float* Whh_f,
                                                             const float* Whh_b, float* dG, int ndir) {
-  __shared__ float dgs[SB][4 * SH];
+  __shared__ __attribute__((aligned(16))) float dgs[2][SB2][4 * SH];
   const int dir = blockIdx.y;
-  const int bl = threadIdx.x / SH, j = threadIdx.x % SH;
-  const int b = blockIdx.x * SB + bl;
+  const int ks = threadIdx.x & 3, j = (threadIdx.x >> 2) & 31, bl = threadIdx.x >> 7;
+  const int b = blockIdx.x * SB2 + bl;
+  const int bc = min(b, B - 1);
   const float* W = dir ? Whh_b : Whh_f;
-  float wc[4 * SH];
+  float wc[SH];                          // W_hh[ks*SH + i][j]
 #pragma unroll
-  for (int r = 0; r < 4 * SH; ++r) wc[r] = W[r * SH + j];
+  for (int i = 0; i < SH; ++i) wc[i] = W[(ks * SH + i) * SH + j];
   const int G = ndir * 4 * SH, HO = ndir * SH;
-  float dcs = 0.f, dhr = 0.f;
-  for (int s = T - 1; s >= 0; --s) {
-    const int t = dir ? T - 1 - s : s;
-    const int tp = dir ? t + 1 : t - 1;   // previous step in processing order
-    float di = 0.f, df = 0.f, dg = 0.f, dO = 0.f;
-    if (b < B) {
-      const int64_t bt = (int64_t)b * T + t;
-      const float dh = dhr + (dh_out ? dh_out[bt * HO + dir * SH + j] : 0.f);
-      const float* gs = gates + bt * G + dir * 4 * SH;
-      const float i_ = gs[j], f_ = gs[SH + j], g_ = gs[2 * SH + j], o_ = gs[3 * SH + j];
-      const float cc = call[bt * HO + dir * SH + j];
-      const float cp = s > 0 ? call[((int64_t)b * T + tp) * HO + dir * SH + j] : 0.f;
-      const float tc = tanhf(cc);
-      const float dc = dcs + dh * o_ * (1.f - tc * tc);
-      di = dc * g_ * i_ * (1.f - i_);
-      df = dc * cp * f_ * (1.f - f_);
-      dg = dc * i_ * (1.f - g_ * g_);
-      dO = dh * tc * o_ * (1.f - o_);
-      dcs = dc * f_;
-      float* d = dG + bt * G + dir * 4 * SH;
-      d[j] = di; d[SH + j] = df; d[2 * SH + j] = dg; d[3 * SH + j] = dO;
-    }
-    dgs[bl][j] = di; dgs[bl][SH + j] = df; dgs[bl][2 * SH + j] = dg; dgs[bl][3 * SH + j] = dO;
-    __syncthreads();
-    float acc = 0.f;
+  // backward walk step s (0 = the forward's last step) -> time index
+  auto tim = [&](int s) { const int ss = min(s, T - 1); return dir ? ss : T - 1 - ss; };
+  struct Ops { float g[4], cc, cp, dh; };
+  auto fetch = [&](Ops& o, int s) {
+    const int t = tim(s);
+    const int64_t bt = (int64_t)bc * T + t;
+    const float* gs = gates + bt * G + dir * 4 * SH + j;
 #pragma unroll
-    for (int r = 0; r < 4 * SH; ++r) acc = fmaf(dgs[bl][r], wc[r], acc);
-    dhr = acc;
-    __syncthreads();
+    for (int q = 0; q < 4; ++q) o.g[q] = gs[q * SH];
+    o.cc = call[bt * HO + dir * SH + j];
+    const int tp = dir ? min(t + 1, T - 1) : max(t - 1, 0);   // previous step in forward order
+    o.cp = call[((int64_t)bc * T + tp) * HO + dir * SH + j];
+    o.dh = HAS_DH ? dh_out[bt * HO + dir * SH + j] : 0.f;
+  };
+  Ops ring[PD];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) fetch(ring[d], d);
+  float dcs = 0.f, dhr = 0.f;
+  const bool own = b < B;
+  int cur = 0;
+  for (int s0 = 0; s0 < T; s0 += PD) {
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+      const int s = s0 + d;
+      const Ops o = ring[d];
+      fetch(ring[d], s + PD);
+      const int t = tim(s);
+      const float i_ = o.g[0], f_ = o.g[1], g_ = o.g[2], o_ = o.g[3];
+      const float dh = dhr + o.dh;
+      const float cp = s == T - 1 ? 0.f : o.cp;   // the forward's first step: c_prev = 0
+      const float tc = tanhf(o.cc);
+      const float dc = dcs + dh * o_ * (1.f - tc * tc);
+      const float di = dc * g_ * i_ * (1.f - i_);
+      const float df = dc * cp * f_ * (1.f - f_);
+      const float dg = dc * i_ * (1.f - g_ * g_);
+      const float dO = dh * tc * o_ * (1.f - o_);
+      dcs = dc * f_;
+      const float mine = ks == 0 ? di : ks == 1 ? df : ks == 2 ? dg : dO;
+      if (own && s < T) dG[((int64_t)b * T + t) * G + dir * 4 * SH + ks * SH + j] = mine;
+      dgs[cur][bl][ks * SH + j] = own ? mine : 0.f;
+      __syncthreads();
+      const float* dr = &dgs[cur][bl][ks * SH];
+      float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < SH; i += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(dr + i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part[e] = fmaf(v[e], wc[i + e], part[e]);
+      }
+      dhr = avc_quad_xor_add<2>(avc_quad_xor_add<1>((part[0] + part[1]) + (part[2] + part[3])));
+      cur ^= 1;
+    }
   }
 }
 
@@ -572,7 +622,7 @@ extern "C" int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* 
   AVC_CHECK_ARG(B > 0 && T > 0 && (ndir == 1 || ndir == 2), "autovc_blstm_fwd_f32: bad dims");
   AVC_CHECK_ARG(gx && W_hh_f && h && c_all && (ndir == 1 || W_hh_b), "autovc_blstm_fwd_f32: null pointer");
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_f) && (ndir == 1 || AVC_ALIGNED16(W_hh_b)), "autovc_blstm_fwd_f32: W alignment");
-  hipLaunchKernelGGL(blstm_fwd_kernel, dim3((B + SB - 1) / SB, ndir), dim3(kThreads), 0, stream, B, T, gx,
+  hipLaunchKernelGGL(blstm_fwd_kernel, dim3((B + SB2 - 1) / SB2, ndir), dim3(kThreads), 0, stream, B, T, gx,
                      W_hh_f, W_hh_b, h, c_all, gates, ndir);
   AVC_CHECK_LAUNCH("autovc_blstm_fwd_f32");
   return avc::kOk;
@@ -584,8 +634,12 @@ extern "C" int autovc_blstm_bwd_f32(int B, int T, int H, int ndir, const float* 
   AVC_CHECK_ARG(H == SH, "autovc_blstm_bwd_f32: small-H kernel is built for H=%d (got %d)", SH, H);
   AVC_CHECK_ARG(B > 0 && T > 0 && (ndir == 1 || ndir == 2), "autovc_blstm_bwd_f32: bad dims");
   AVC_CHECK_ARG(gates && c_all && W_hh_f && dG && (ndir == 1 || W_hh_b), "autovc_blstm_bwd_f32: null pointer");
-  hipLaunchKernelGGL(blstm_bwd_kernel, dim3((B + SB - 1) / SB, ndir), dim3(kThreads), 0, stream, B, T, dh_out,
-                     gates, c_all, W_hh_f, W_hh_b, dG, ndir);
+  if (dh_out)
+    hipLaunchKernelGGL(blstm_bwd_kernel<true>, dim3((B + SB2 - 1) / SB2, ndir), dim3(kThreads), 0, stream, B, T,
+                       dh_out, gates, c_all, W_hh_f, W_hh_b, dG, ndir);
+  else
+    hipLaunchKernelGGL(blstm_bwd_kernel<false>, dim3((B + SB2 - 1) / SB2, ndir), dim3(kThreads), 0, stream, B, T,
+                       dh_out, gates, c_all, W_hh_f, W_hh_b, dG, ndir);
   AVC_CHECK_LAUNCH("autovc_blstm_bwd_f32");
   return avc::kOk;
 }

@@ -136,7 +136,30 @@ def test_lstm_layer_fwd_bwd(cuda, B, T, I, H):
         assert rel(a.grad, b.grad) < 1e-4
 
 
-@pytest.mark.parametrize("B,T,I", [(64, 128, 512), (5, 7, 64)])
+@pytest.mark.parametrize("B,T,I,H", [(64, 16, 512, 1024), (3, 9, 320, 512)])
+def test_lstm2_stack_fwd_bwd(cuda, B, T, I, H):
+    """Two stacked layers as one wavefront (autovc_lstm2_fwd_f32) vs two oracle layers."""
+    from autovc_amd import functional as AF
+    torch.manual_seed(5)
+    s = 1 / H ** 0.5
+    x = torch.randn(B, T, I, requires_grad=True)
+    shapes = [(4 * H, I), (4 * H, H), (4 * H,), (4 * H,), (4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]
+    ps = [(torch.rand(*sh) * 2 - 1).mul_(s).requires_grad_() for sh in shapes]
+    h0 = og.OracleGenerator._lstm_dir(x, *ps[:4], reverse=False)
+    h1 = og.OracleGenerator._lstm_dir(h0, *ps[4:], reverse=False)
+    gh = torch.randn_like(h1)
+    h1.backward(gh)
+    xd = x.detach().to(cuda).requires_grad_()
+    pd = [p.detach().to(cuda).requires_grad_() for p in ps]
+    hd = AF.LSTM2StackFn.apply(xd, *pd, True)
+    hd.backward(gh.to(cuda))
+    assert rel(hd, h1) < FWD_TOL
+    assert rel(xd.grad, x.grad) < 1e-4
+    for a, b in zip(pd, ps):
+        assert rel(a.grad, b.grad) < 1e-4
+
+
+@pytest.mark.parametrize("B,T,I", [(64, 128, 512), (5, 7, 64), (9, 21, 64)])
 def test_blstm_layer_fwd_bwd(cuda, B, T, I):
     from autovc_amd import functional as AF
     torch.manual_seed(4)
