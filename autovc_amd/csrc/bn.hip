@@ -41,6 +41,7 @@ __global__ __launch_bounds__(256) void stats_partial_kernel(int64_t M, int C, co
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const double x0 = y[c];
+#pragma unroll 4
     for (int64_t r = r0 + w; r < r1; r += 4) {
       const double d = (double)y[r * ld + c] - x0;
       s1 += d;
@@ -65,6 +66,7 @@ __device__ __forceinline__ void sum_partials(const double* __restrict__ part, in
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double s1 = 0.0, s2 = 0.0;
   if (c < C)
+#pragma unroll 8
     for (int rs = w; rs < RS; rs += 4) {
       s1 += part[((int64_t)rs * C + c) * 2 + 0];
       s2 += part[((int64_t)rs * C + c) * 2 + 1];
@@ -100,17 +102,21 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(int64_t M, int C, c
 }
 
 // ---- apply: z = act(y * alpha + beta') (+ residual), alpha = gamma/sqrt(var+eps) -------
-__global__ void apply_kernel(int64_t M, int C, const float* __restrict__ y, int64_t ldy,
-                             const float* __restrict__ mean, const float* __restrict__ var,
-                             const float* __restrict__ gamma, const float* __restrict__ beta, float eps, int act,
-                             const float* __restrict__ res, int64_t ldr, float* __restrict__ z, int64_t ldz) {
-  const int64_t total = M * C;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / C;
-    const int c = (int)(i % C);
-    const float invstd = 1.0f / sqrtf(var[c] + eps);
-    const float alpha = invstd * (gamma ? gamma[c] : 1.f);
-    const float b = (beta ? beta[c] : 0.f) - mean[c] * alpha;
+// 2-D launch: blockIdx.x * 64 + lane = channel, (blockIdx.y, wave) stride the rows, so the
+// per-channel coefficients are computed once per thread and no 64-bit divide is needed.
+__global__ __launch_bounds__(256) void apply_kernel(int64_t M, int C, const float* __restrict__ y, int64_t ldy,
+                                                   const float* __restrict__ mean, const float* __restrict__ var,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   float eps, int act, const float* __restrict__ res, int64_t ldr,
+                                                   float* __restrict__ z, int64_t ldz) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (c >= C) return;
+  const float invstd = 1.0f / sqrtf(var[c] + eps);
+  const float alpha = invstd * (gamma ? gamma[c] : 1.f);
+  const float b = (beta ? beta[c] : 0.f) - mean[c] * alpha;
+  const int64_t rstep = (int64_t)gridDim.y * 4;
+#pragma unroll 4
+  for (int64_t m = (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6); m < M; m += rstep) {
     float v = act_fwd(fmaf(y[m * ldy + c], alpha, b), act);
     if (res) v += res[m * ldr + c];
     z[m * ldz + c] = v;
@@ -131,6 +137,7 @@ __global__ __launch_bounds__(256) void bwd_partial_kernel(int64_t M, int C, cons
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const float mu = mean[c];
+#pragma unroll 4
     for (int64_t r = r0 + w; r < r1; r += 4) {
       const float g = act_grad(dz[r * lddz + c], act == kNone ? 0.f : z[r * ldz + c], act);
       s1 += (double)g;
@@ -165,26 +172,34 @@ __global__ __launch_bounds__(256) void bwd_finalize_kernel(int C, const double* 
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + sdyx : sdyx;
 }
 
-// dy = (dy_act - sdy/M - xhat * sdyx/M) * invstd * gamma
-__global__ void bwd_apply_kernel(int64_t M, int C, const float* __restrict__ dz, int64_t lddz,
-                                 const float* __restrict__ z, int64_t ldz, const float* __restrict__ y, int64_t ldy,
-                                 const float* __restrict__ mean, const float* __restrict__ var,
-                                 const float* __restrict__ gamma, float eps, int act, const float* __restrict__ sums,
-                                 float* __restrict__ dy, int64_t lddy) {
-  const int64_t total = M * C;
+// dy = (dy_act - sdy/M - xhat * sdyx/M) * invstd * gamma   (2-D launch as apply_kernel)
+__global__ __launch_bounds__(256) void bwd_apply_kernel(int64_t M, int C, const float* __restrict__ dz, int64_t lddz,
+                                                       const float* __restrict__ z, int64_t ldz,
+                                                       const float* __restrict__ y, int64_t ldy,
+                                                       const float* __restrict__ mean, const float* __restrict__ var,
+                                                       const float* __restrict__ gamma, float eps, int act,
+                                                       const float* __restrict__ sums, float* __restrict__ dy,
+                                                       int64_t lddy) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (c >= C) return;
   const float inv_m = 1.0f / (float)M;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / C;
-    const int c = (int)(i % C);
-    const float invstd = 1.0f / sqrtf(var[c] + eps);
+  const float invstd = 1.0f / sqrtf(var[c] + eps);
+  const float mu = mean[c], s0 = sums[2 * c] * inv_m, s1 = sums[2 * c + 1] * inv_m;
+  const float gsc = invstd * (gamma ? gamma[c] : 1.f);
+  const int64_t rstep = (int64_t)gridDim.y * 4;
+#pragma unroll 4
+  for (int64_t m = (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6); m < M; m += rstep) {
     const float g = act_grad(dz[m * lddz + c], act == kNone ? 0.f : z[m * ldz + c], act);
-    const float xhat = (y[m * ldy + c] - mean[c]) * invstd;
-    const float v = (g - sums[2 * c] * inv_m - xhat * sums[2 * c + 1] * inv_m) * invstd * (gamma ? gamma[c] : 1.f);
-    dy[m * lddy + c] = v;
+    const float xhat = (y[m * ldy + c] - mu) * invstd;
+    dy[m * lddy + c] = (g - s0 - xhat * s1) * gsc;
   }
 }
 
-int grid_for(int64_t total) { return (int)std::min<int64_t>((total + 255) / 256, 8192); }
+// 2-D grid of the apply kernels: 64-channel column tiles x row groups (~8 rows per thread)
+dim3 grid2d(int64_t M, int C) {
+  const int64_t ry = std::max<int64_t>(1, std::min<int64_t>((M + 31) / 32, 4096));
+  return dim3((C + 63) / 64, (unsigned)ry);
+}
 
 }  // namespace
 
@@ -211,7 +226,7 @@ extern "C" int autovc_bn_act_fwd_f32(int64_t M, int C, const float* y, int64_t l
                                      const float* residual, int64_t ldr, float* z, int64_t ldz, hipStream_t stream) {
   AVC_CHECK_ARG(M > 0 && C > 0 && y && mean && var && z, "autovc_bn_act_fwd_f32: bad args");
   AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_bn_act_fwd_f32: unknown activation %d", act);
-  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(M * C)), dim3(256), 0, stream, M, C, y, ldy, mean, var, gamma,
+  hipLaunchKernelGGL(apply_kernel, grid2d(M, C), dim3(256), 0, stream, M, C, y, ldy, mean, var, gamma,
                      beta, eps, act, residual, ldr, z, ldz);
   AVC_CHECK_LAUNCH("autovc_bn_act_fwd_f32");
   return avc::kOk;
@@ -231,7 +246,7 @@ extern "C" int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t 
                      ldy, mean, act, part);
   hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, C, (const double*)part, RS,
                      var, eps, sums, dgamma, dbeta, accumulate);
-  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(M * C)), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y, ldy,
+  hipLaunchKernelGGL(bwd_apply_kernel, grid2d(M, C), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y, ldy,
                      mean, var, gamma, eps, act, (const float*)sums, dy, lddy);
   AVC_CHECK_LAUNCH("autovc_bn_act_bwd_f32");
   return avc::kOk;

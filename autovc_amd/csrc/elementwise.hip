@@ -121,6 +121,7 @@ __global__ __launch_bounds__(256) void loss_partial_kernel(int kind, int64_t n, 
 __global__ void loss_finalize_kernel(int64_t n, const double* __restrict__ part, int nb, float* __restrict__ out) {
   if (threadIdx.x != 0) return;
   double s = 0.0;
+#pragma unroll 16
   for (int i = 0; i < nb; ++i) s += part[i];
   *out = (float)(s / (double)n);
 }
@@ -249,6 +250,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t M, int N, c
   const int64_t r0 = M * rs / RS, r1 = M * (rs + 1) / RS;
   float s = 0.f;
   if (c < N)
+#pragma unroll 4
     for (int64_t r = r0 + w; r < r1; r += 4) s += X[r * ld + c];
   red[w][lane] = s;
   __syncthreads();
@@ -263,6 +265,7 @@ __global__ __launch_bounds__(256) void colsum_finalize_kernel(int N, int RS, con
   const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (c < N)
+#pragma unroll 8
     for (int rs = w; rs < RS; rs += 4) s += part[(int64_t)rs * N + c];
   red[w][lane] = s;
   __syncthreads();

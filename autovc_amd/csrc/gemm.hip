@@ -302,17 +302,23 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
   }
 }
 
-__global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const float* __restrict__ slab,
-                                     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias1,
-                                     const float* __restrict__ bias2, int accumulate) {
+// 2-D: blockIdx.x * 256 + thread = column, blockIdx.y strides rows (no 64-bit divide);
+// slabs summed in split order (deterministic)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(int64_t M, int64_t N, int splits,
+                                                           const float* __restrict__ slab, float* __restrict__ C,
+                                                           int64_t ldc, const float* __restrict__ bias1,
+                                                           const float* __restrict__ bias2, int accumulate) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
   const int64_t total = M * N;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / N, n = i % N;
+  float bsum = 0.f;
+  if (bias1) bsum += bias1[n];
+  if (bias2) bsum += bias2[n];
+  for (int64_t m = blockIdx.y; m < M; m += gridDim.y) {
+    const int64_t i = m * N + n;
     float v = 0.f;
     for (int s = 0; s < splits; ++s) v += slab[s * total + i];
-    if (bias1) v += bias1[n];
-    if (bias2) v += bias2[n];
+    v += bsum;
     float* dst = C + m * ldc + n;
     if (accumulate) v += *dst;
     *dst = v;
@@ -424,9 +430,9 @@ extern "C" int autovc_gemm_f32(int M, int N, int K,
               slab);
   AVC_CHECK_LAUNCH("autovc_gemm_f32");
   if (splits > 1) {
-    const int64_t total = (int64_t)M * N;
-    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, (int64_t)M, (int64_t)N,
+    const int gx = (N + 255) / 256;
+    const int gy = (int)std::max<int64_t>(1, std::min<int64_t>(M, 4096 / gx + 1));
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, gy), dim3(256), 0, stream, (int64_t)M, (int64_t)N,
                        splits, slab, C, ldc, bias1, bias2, accumulate);
     AVC_CHECK_LAUNCH("autovc_gemm_f32/splitk_reduce");
   }
