@@ -50,6 +50,9 @@ constexpr int kErrLaunch = -2;  // hip launch or runtime failure
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // Accurate (ocml) expf/tanhf: the LSTM parity bar is 1e-4 rel vs torch CPU.
 __device__ __forceinline__ float avc_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }

@@ -54,7 +54,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)kOOB, 0x00020000);
 }
 
-template <bool RK, int ROWS, int BK, int NT>
+template <bool RK, int ROWS, int BK, int NT, bool PAIRK = false>
 struct OpTile {
   static constexpr int LD = RK ? BK + 4 : ROWS + 4;
   static constexpr int FLOATS = RK ? ROWS * LD : BK * LD;
@@ -72,8 +72,18 @@ struct OpTile {
   int tap, kmod;            // conv: RK: k / C, k % C (advancing); CK: q / C (fixed)
   int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
   bool rowok;               // CK: the thread's row inside the operand
-  __device__ __forceinline__ static void coords(int e, int& r, int& k) {
+  // slot i of this thread -> (row r, k).  PAIRK (CK operands of the bf16 kernel): the
+  // thread's slots come in pairs at k, k + 1 of the same 4 rows, so they pack into bf16x2.
+  static_assert(!PAIRK || RK || (PER % 2 == 0 && BK % (2 * (NT / (ROWS / 4))) == 0), "k pairs");
+  __device__ __forceinline__ static void coords(int i, int& r, int& k) {
+    const int e = threadIdx.x + i * NT;
     if (RK) { r = e / (BK / 4); k = 4 * (e % (BK / 4)); }
+    else if (PAIRK) {
+      constexpr int C4 = ROWS / 4, KP = 2 * (NT / C4);
+      const int t = threadIdx.x;
+      k = (i >> 1) * KP + 2 * (t / C4) + (i & 1);
+      r = 4 * (t % C4);
+    }
     else    { k = e / (ROWS / 4); r = 4 * (e % (ROWS / 4)); }
   }
   __device__ __forceinline__ void init(const Opnd& o, int64_t r0, int64_t kbeg, int64_t R) {
@@ -86,7 +96,7 @@ struct OpTile {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int rr, kq;
-      coords(threadIdx.x + i * NT, rr, kq);
+      coords(i, rr, kq);
       const int64_t r = r0 + rr, k = kbeg + kq;
       if (RK) {
         rok[i] = r < R;
@@ -144,8 +154,34 @@ struct OpTile {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
-      coords(threadIdx.x + i * NT, r, k);
+      coords(i, r, k);
       *reinterpret_cast<f32x4*>(lds + (RK ? r * LD + k : k * LD + r)) = v[i];
+    }
+  }
+  // bf16 image [row][LDB] (k contiguous) for the bf16 MFMA: RK slots as one 8-byte write,
+  // CK slot pairs (k, k + 1) as four packed bf16x2 words
+  template <int LDB>
+  __device__ __forceinline__ void store_bf16(__bf16* lds) const {
+    if (RK) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        int r, k;
+        coords(i, r, k);
+        const bf16x4 b = {(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
+        *reinterpret_cast<bf16x4*>(lds + r * LDB + k) = b;
+      }
+    } else {
+      static_assert(PAIRK, "CK bf16 staging needs k pairs");
+#pragma unroll
+      for (int i = 0; i < PER; i += 2) {
+        int r, k;
+        coords(i, r, k);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const bf16x2 b = {(__bf16)v[i][jj], (__bf16)v[i + 1][jj]};
+          *reinterpret_cast<bf16x2*>(lds + (r + jj) * LDB + k) = b;
+        }
+      }
     }
   }
   // fragment values of MFMAs p = 4g .. 4g+3 (k = h*BK/2 + p) for tile row `row`
@@ -302,6 +338,114 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
   }
 }
 
+// bf16-MFMA GEMM ("bf16 compute, fp32 master": BASELINE config 3).  Same operand modes,
+// masking, split-K and epilogue as gemm_kernel; the fp32 operands are rounded to bf16
+// (RNE, v_cvt_pk_bf16_f32) when a stage is written to LDS as [row][BK + 8] bf16, and
+// v_mfma_f32_32x32x16_bf16 accumulates in fp32 (lane (r = l & 31, h = l >> 5) reads the 8
+// contiguous k = 16 ks + 8h .. +8 of its row with one ds_read_b128, the operand map of
+// the instruction, for A and B alike).
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
+    int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
+    const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
+    int k_per_split, float* __restrict__ slab) {
+  constexpr int NWN = BN / WN;
+  constexpr int NT = 64 * (BM / WM) * NWN;
+  constexpr int TI = WM / 32, TJ = WN / 32;
+  constexpr int LDB = BK + 8;
+  using TA = OpTile<A_RK, BM, BK, NT, true>;
+  using TBt = OpTile<B_RK, BN, BK, NT, true>;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2][(BM + BN) * LDB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / NWN, wc = wave % NWN;
+  const int nx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int L = blockIdx.x + nx * blockIdx.y;
+  const int xcd = L % 8, slot = L / 8, qq = nwg / 8, rr = nwg % 8;
+  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
+  const int64_t m0 = (int64_t)(logical / nx) * BM, n0 = (int64_t)(logical % nx) * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = min((int64_t)K, kbeg + k_per_split);
+  const int nk = (int)((kend - kbeg + BK - 1) / BK);
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  TA sa;
+  TBt sb;
+  sa.init(A, m0, kbeg, M);
+  sb.init(B, n0, kbeg, N);
+  if (nk > 0) {
+    sa.load(A, kend);
+    sb.load(B, kend);
+    sa.template store_bf16<LDB>(smem[0]);
+    sb.template store_bf16<LDB>(smem[0] + BM * LDB);
+  }
+  __syncthreads();
+
+  const int h = lane >> 5, li = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      sa.load(A, kend);
+      sb.load(B, kend);
+    }
+    const __bf16* As = smem[buf];
+    const __bf16* Bs = smem[buf] + BM * LDB;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[TI], fb[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(As + (wr * WM + i * 32 + li) * LDB + ks * 16 + 8 * h);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (wc * WN + j * 32 + li) * LDB + ks * 16 + 8 * h);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      sa.template store_bf16<LDB>(smem[buf ^ 1]);
+      sb.template store_bf16<LDB>(smem[buf ^ 1] + BM * LDB);
+    }
+    __syncthreads();
+  }
+
+  float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
+  const int64_t ld = slab ? N : ldc;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int64_t n = n0 + wc * WN + j * 32 + li;
+    if (n >= N) continue;
+    float bsum = 0.f;
+    if (!slab) {
+      if (bias1) bsum += bias1[n];
+      if (bias2) bsum += bias2[n];
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) {
+          float v = acc[i][j][r] + bsum;
+          float* dst = out + m * ld + n;
+          if (!slab && accumulate) v += *dst;
+          *dst = v;
+        }
+      }
+    }
+  }
+}
+
 // 2-D: blockIdx.x * 256 + thread = column, blockIdx.y strides rows (no 64-bit divide);
 // slabs summed in split order (deterministic)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(int64_t M, int64_t N, int splits,
@@ -386,36 +530,68 @@ void launch_gemm(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, in
   }
 }
 
+// bf16 tiles: 128x128 (4 waves of 64x64) once that grid fills the chip, else 64x64
+constexpr GemmShape kCfgBf16[] = {{0, 128, 128, 32}, {1, 64, 64, 32}};
+
+GemmShape pick_config_bf16(int M, int N, int splits) {
+  const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
+  return t128 >= 256 ? kCfgBf16[0] : kCfgBf16[1];
+}
+
+template <int BM, int BN, int BK, int WM, int WN>
+void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
+                         float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), 0, st, M, N, \
+                                         K, oa, ob, C, ldc, b1, b2, acc, kps, slab)
+  if (!a_trans && !b_trans) AVC_L(true, true);
+  else if (!a_trans && b_trans) AVC_L(true, false);
+  else if (a_trans && !b_trans) AVC_L(false, true);
+  else AVC_L(false, false);
+#undef AVC_L
+}
+
+void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa,
+                      Opnd ob, float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps,
+                      float* slab) {
+  if (id == 0)
+    launch_layouts_bf16<128, 128, 32, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
+                                              slab);
+  else
+    launch_layouts_bf16<64, 64, 32, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
+                                            slab);
+}
+
 }  // namespace
 
 extern "C" int64_t autovc_gemm_workspace_floats(int M, int N, int splits) {
   return splits > 1 ? (int64_t)splits * M * N : 0;
 }
 
-extern "C" int autovc_gemm_f32(int M, int N, int K,
+static int gemm_impl(bool bf16, int M, int N, int K,
                                const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
                                const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                float* C, int64_t ldc, const float* bias1, const float* bias2,
                                int accumulate, int splits, float* workspace, hipStream_t stream) {
-  AVC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "autovc_gemm_f32: negative dims");
+  AVC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "autovc_gemm: negative dims");
   if (M == 0 || N == 0) return avc::kOk;
-  AVC_CHECK_ARG(A && B && C, "autovc_gemm_f32: null operand");
-  AVC_CHECK_ARG(AVC_ALIGNED16(A) && AVC_ALIGNED16(B), "autovc_gemm_f32: A/B must be 16-byte aligned");
-  AVC_CHECK_ARG(aligned_ld(lda) && aligned_ld(ldb), "autovc_gemm_f32: lda/ldb must be multiples of 4");
+  AVC_CHECK_ARG(A && B && C, "autovc_gemm: null operand");
+  AVC_CHECK_ARG(AVC_ALIGNED16(A) && AVC_ALIGNED16(B), "autovc_gemm: A/B must be 16-byte aligned");
+  AVC_CHECK_ARG(aligned_ld(lda) && aligned_ld(ldb), "autovc_gemm: lda/ldb must be multiples of 4");
   // the contiguous extent of each operand must be a multiple of 4 (float4 staging)
-  AVC_CHECK_ARG(a_trans ? (M % 4 == 0) : (K % 4 == 0), "autovc_gemm_f32: A contiguous dim %% 4 != 0");
-  AVC_CHECK_ARG(b_trans ? (N % 4 == 0) : (K % 4 == 0), "autovc_gemm_f32: B contiguous dim %% 4 != 0");
+  AVC_CHECK_ARG(a_trans ? (M % 4 == 0) : (K % 4 == 0), "autovc_gemm: A contiguous dim %% 4 != 0");
+  AVC_CHECK_ARG(b_trans ? (N % 4 == 0) : (K % 4 == 0), "autovc_gemm: B contiguous dim %% 4 != 0");
   AVC_CHECK_ARG(!a_conv_T || (a_conv_C % 4 == 0 && a_conv_C > 0),
-                "autovc_gemm_f32: A conv channels must be a positive multiple of 4");
+                "autovc_gemm: A conv channels must be a positive multiple of 4");
   AVC_CHECK_ARG(!b_conv_T || (b_conv_C % 4 == 0 && b_conv_C > 0),
-                "autovc_gemm_f32: B conv channels must be a positive multiple of 4");
+                "autovc_gemm: B conv channels must be a positive multiple of 4");
   // buffer-load byte offsets are 32-bit (descriptor range 2 GiB)
   const int64_t a_ext = a_trans ? (int64_t)K * lda : (int64_t)M * lda;
   const int64_t b_ext = b_trans ? (int64_t)K * ldb : (int64_t)N * ldb;
   AVC_CHECK_ARG(4 * (a_ext + 2 * lda) < (int64_t)kOOB && 4 * (b_ext + 2 * ldb) < (int64_t)kOOB,
-                "autovc_gemm_f32: operand extents must stay below 2 GiB");
+                "autovc_gemm: operand extents must stay below 2 GiB");
   if (splits < 1) splits = 1;
-  const GemmShape cfg = pick_config(M, N, K, splits);
+  const GemmShape cfg = bf16 ? pick_config_bf16(M, N, splits) : pick_config(M, N, K, splits);
   const int BKc = cfg.bk;
   int64_t kps = ((int64_t)K + splits - 1) / splits;
   kps = ((kps + BKc - 1) / BKc) * BKc;
@@ -426,15 +602,37 @@ extern "C" int autovc_gemm_f32(int M, int N, int K,
   Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0};
   float* slab = splits > 1 ? workspace : nullptr;
   const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, splits);
-  launch_gemm(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
-              slab);
-  AVC_CHECK_LAUNCH("autovc_gemm_f32");
+  if (bf16)
+    launch_gemm_bf16(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate,
+                     (int)kps, slab);
+  else
+    launch_gemm(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
+                slab);
+  AVC_CHECK_LAUNCH("autovc_gemm");
   if (splits > 1) {
     const int gx = (N + 255) / 256;
     const int gy = (int)std::max<int64_t>(1, std::min<int64_t>(M, 4096 / gx + 1));
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, gy), dim3(256), 0, stream, (int64_t)M, (int64_t)N,
                        splits, slab, C, ldc, bias1, bias2, accumulate);
-    AVC_CHECK_LAUNCH("autovc_gemm_f32/splitk_reduce");
+    AVC_CHECK_LAUNCH("autovc_gemm/splitk_reduce");
   }
   return avc::kOk;
+}
+
+extern "C" int autovc_gemm_f32(int M, int N, int K,
+                               const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
+                               const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
+                               float* C, int64_t ldc, const float* bias1, const float* bias2,
+                               int accumulate, int splits, float* workspace, hipStream_t stream) {
+  return gemm_impl(false, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T, b_conv_C,
+                   b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
+}
+
+extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
+                                    const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
+                                    const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
+                                    float* C, int64_t ldc, const float* bias1, const float* bias2,
+                                    int accumulate, int splits, float* workspace, hipStream_t stream) {
+  return gemm_impl(true, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T, b_conv_C,
+                   b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
 }

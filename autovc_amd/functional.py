@@ -8,6 +8,8 @@ read NTC through the GEMM's implicit im2col operand.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from . import _lib
@@ -51,15 +53,40 @@ def _ws(device, nbytes, slot="main"):
     return _Workspace.get(device, nbytes, slot).data_ptr()
 
 
+_PRECISION = ["fp32"]
+
+
+@contextlib.contextmanager
+def precision(mode):
+    """Matmul precision inside the block: "fp32" (BASELINE config 2, exact fp32 MFMA) or
+    "bf16" (config 3: bf16-rounded operands, fp32 accumulation and fp32 everything else —
+    master weights, optimizer, BatchNorm, losses, recurrent cell math).  Wrap forward AND
+    backward (autograd runs the backward kernels after the forward block has exited)."""
+    if mode not in ("fp32", "bf16"):
+        raise ValueError(f"precision must be 'fp32' or 'bf16', got {mode!r}")
+    prev = _PRECISION[0]
+    _PRECISION[0] = mode
+    try:
+        yield
+    finally:
+        _PRECISION[0] = prev
+
+
+def current_precision():
+    return _PRECISION[0]
+
+
 def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_conv=None,
          bias1=None, bias2=None, accumulate=False, splits=1, a_off=0, b_off=0, c_off=0):
-    """C[M,N] (+)= A(m,k) B(k,n) (+bias); offsets are in floats from the tensors' data."""
+    """C[M,N] (+)= A(m,k) B(k,n) (+bias); offsets are in floats from the tensors' data.
+    bf16 MFMA under precision("bf16"), exact fp32 MFMA otherwise."""
     ac = a_conv or (0, 0, 0)
     bc = b_conv or (0, 0, 0)
     ws = 0
     if splits > 1:
         ws = _ws(C.device, 4 * _lib.load().autovc_gemm_workspace_floats(M, N, splits), "gemm")
-    _lib.call("autovc_gemm_f32", M, N, K,
+    fn = "autovc_gemm_bf16_f32" if _PRECISION[0] == "bf16" else "autovc_gemm_f32"
+    _lib.call(fn, M, N, K,
               A.data_ptr() + 4 * a_off, lda, a_trans, ac[0], ac[1], ac[2],
               B.data_ptr() + 4 * b_off, ldb, b_trans, bc[0], bc[1], bc[2],
               C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, _s())

@@ -80,6 +80,9 @@ class Solver(object):
         self.model_type = config.model_type
         self.speaker_embed = getattr(config, "speaker_embed", True)
         self.log_step = config.log_step
+        # matmul precision of the step: "fp32" (BASELINE config 2) or "bf16" (config 3:
+        # bf16 MFMA operands, fp32 master weights / Adam / BN / losses); not in the reference
+        self.precision = getattr(config, "precision", "fp32")
 
         self.path = "chkpnt_" + self.model_type + "_" + self.run_name + ".ckpt"
         self.file_exists = os.path.exists(self.path)
@@ -141,9 +144,10 @@ class Solver(object):
     def train_step(self, x_real, emb_org):
         """Losses, zero_grad, backward, Adam (solver_encoder.py:226-300).  Returns device
         scalars (g_loss, loss_id, loss_id_psnt, loss_cd); nothing synchronises."""
-        g_loss, l_id, l_psnt, l_cd, x_psnt = self.compute_losses(x_real, emb_org)
-        self.reset_grad()
-        g_loss.backward()
+        with AF.precision(self.precision):
+            g_loss, l_id, l_psnt, l_cd, x_psnt = self.compute_losses(x_real, emb_org)
+            self.reset_grad()
+            g_loss.backward()
         self._after_backward()
         self.g_optimizer.step()
         self._last_psnt = x_psnt

@@ -299,6 +299,7 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-wavenet", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-bf16", action="store_true")
     args = ap.parse_args()
 
     from autovc_amd import ddp
@@ -333,6 +334,36 @@ def main():
         dt = float(t.item())
     last_loss = float(losses[0].item())
 
+    def timed_steps(n):
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t_0 = time.perf_counter()
+        for _ in range(n):
+            out = solver.train_step(x, e)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        d = time.perf_counter() - t_0
+        if world > 1:
+            tt = torch.tensor([d], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            d = float(tt.item())
+        return d, out
+
+    bf = None
+    if not args.no_bf16:
+        # BASELINE config 3 numerics (bf16 matmul operands, fp32 master/optimizer/BN/loss),
+        # same solver and batch, after the fp32 measurement
+        solver.precision = "bf16"
+        timed_steps(max(2, args.warmup // 2))
+        dtb, lb = timed_steps(args.steps)
+        solver.precision = "fp32"
+        bf = {"value": round(world * B * T * args.steps / dtb, 1), "unit": "mel-frames/s",
+              "ms_per_step": round(dtb / args.steps * 1000, 3), "dtype": "bf16 MFMA operands, fp32 accumulate",
+              "final_loss": round(float(lb[0].item()), 6),
+              "note": "BASELINE config 3 precision; the headline value above is config 2 (fp32)"}
+
     roof = None
     if not args.no_roofline and rank == 0:
         roof = lstm_roofline(solver, B, T, dev)
@@ -361,7 +392,7 @@ def main():
                        "global_batch": B * world, "seq_len": T, "n_mels": 80, "parallelism": f"dp{world}",
                        "dim_neck": 32, "dim_emb": 256, "dim_pre": 512, "freq": 32},
             "final_loss": round(last_loss, 6),
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "bf16": bf,
             "wavenet": wn,
             "e2e": e2e, "frontend": fe,
         }

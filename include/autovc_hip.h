@@ -69,6 +69,15 @@ int autovc_gemm_f32(int M, int N, int K,
                     const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                     float* C, int64_t ldc, const float* bias1, const float* bias2,
                     int accumulate, int splits, float* workspace, hipStream_t stream);
+/* Same contract, bf16 compute (BASELINE config 3, "bf16 with fp32 master"): the fp32
+ * operands are rounded to bf16 (RNE) as they are staged, v_mfma_f32_32x32x16_bf16
+ * accumulates in fp32, C / bias / accumulate stay fp32 — the numerics of a torch.autocast
+ * bf16 matmul whose output is kept in fp32. */
+int autovc_gemm_bf16_f32(int M, int N, int K,
+                         const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
+                         const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
+                         float* C, int64_t ldc, const float* bias1, const float* bias2,
+                         int accumulate, int splits, float* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------- BatchNorm1d + act
  * Replaces nn.BatchNorm1d (train/eval) + F.relu / torch.tanh / identity after each

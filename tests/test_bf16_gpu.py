@@ -1,0 +1,97 @@
+"""bf16 compute mode (BASELINE config 3: bf16 matmul operands, fp32 accumulation, fp32
+master weights / optimizer / BatchNorm / losses).  The GEMM is checked exactly against
+fp64 products of the RNE-rounded operands (a bf16 x bf16 product is exact in fp32, so only
+the fp32 accumulation order differs); the training loss curve against fp32 (SURVEY §8d:
+within 5 % at matched steps over >= 100 steps)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().cpu().double()
+    b = b.detach().cpu().double()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+def r16(t):
+    return t.bfloat16().double()
+
+
+@pytest.mark.parametrize("M,N,K,at,bt", [(256, 128, 64, 0, 0), (300, 200, 36, 0, 1), (100, 260, 520, 1, 0),
+                                         (64, 80, 1024, 1, 1), (8192, 512, 2560, 0, 0), (512, 2560, 8192, 1, 1)])
+def test_gemm_bf16_layouts(cuda, M, N, K, at, bt):
+    from autovc_amd import functional as AF
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    Ad = (A.t() if at else A).contiguous().to(cuda)
+    Bd = (B if bt else B.t()).contiguous().to(cuda)
+    C = torch.empty(M, N, device=cuda)
+    with AF.precision("bf16"):
+        AF.gemm(M, N, K, Ad, M if at else K, at, Bd, N if bt else K, bt, C, N, bias1=bias.to(cuda))
+    ref = r16(A) @ r16(B) + bias.double()
+    assert rel(C, ref) < 2e-5
+    # and it is really bf16: the fp32-operand product differs by far more than that
+    assert rel(C, A.double() @ B.double() + bias.double()) > 1e-4
+
+
+def test_gemm_bf16_splitk_accumulate(cuda):
+    from autovc_amd import functional as AF
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(4096, 96, generator=g)
+    B = torch.randn(4096, 160, generator=g)
+    C0 = torch.randn(96, 160, generator=g)
+    C = C0.clone().to(cuda)
+    with AF.precision("bf16"):
+        AF.gemm(96, 160, 4096, A.to(cuda), 96, 1, B.to(cuda), 160, 1, C, 160, accumulate=True, splits=8)
+    assert rel(C, C0.double() + r16(A).t() @ r16(B)) < 2e-5
+
+
+def test_conv_bf16_fwd_bwd(cuda):
+    """Implicit-im2col conv under bf16: y from rounded (x, W), dX from rounded (dy, W),
+    dW from rounded (dy, x) — each checked against fp64 on exactly those operands."""
+    from autovc_amd import functional as AF
+    F = torch.nn.functional
+    torch.manual_seed(0)
+    Bn, T, Ci, Co = 3, 40, 36, 52
+    x = torch.randn(Bn, T, Ci)
+    W = torch.randn(Co, Ci, 5)
+    b = torch.randn(Co)
+    gy = torch.randn(Bn, T, Co)
+    xd, Wd, bd = (t.clone().to(cuda).requires_grad_() for t in (x, W, b))
+    with AF.precision("bf16"):
+        yd = AF.conv_only(xd, Wd, bd)
+        yd.backward(gy.to(cuda))
+
+    def conv(xx, ww):
+        return F.conv1d(xx.transpose(1, 2), ww, b.double(), padding=2).transpose(1, 2)
+    assert rel(yd, conv(r16(x), r16(W))) < 2e-5
+    xr = r16(x).requires_grad_()
+    conv(xr, r16(W)).backward(r16(gy))
+    assert rel(xd.grad, xr.grad) < 2e-5
+    Wr = r16(W).requires_grad_()
+    conv(r16(x), Wr).backward(r16(gy))
+    assert rel(Wd.grad, Wr.grad) < 2e-5
+
+
+def test_bf16_training_loss_tracks_fp32(cuda):
+    """100 Solver steps from the same weights and batch in fp32 and in bf16: the loss
+    curves agree within 5 % at every step."""
+    import bench
+    curves = {}
+    for prec in ("fp32", "bf16"):
+        torch.manual_seed(0)
+        solver = bench.make_solver(cuda, 16)
+        solver.precision = prec
+        solver.G.train()
+        x, e = bench.synthetic_batch(16, 128, cuda, 1234)
+        losses = []
+        for _ in range(100):
+            losses.append(solver.train_step(x, e)[0])
+        curves[prec] = torch.stack(losses).cpu().double()
+    r = (curves["bf16"] - curves["fp32"]).abs() / curves["fp32"]
+    assert float(r.max()) < 0.05, f"max rel loss gap {float(r.max()):.3f} at step {int(r.argmax())}"
+    assert float(curves["bf16"][-1]) < float(curves["bf16"][0])   # it trains
