@@ -73,16 +73,20 @@ struct OpTile {
   int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
   bool rowok;               // CK: the thread's row inside the operand
   // slot i of this thread -> (row r, k).  PAIRK (CK operands of the bf16 kernel): the
-  // thread's slots come in pairs at k, k + 1 of the same 4 rows, so they pack into bf16x2.
-  static_assert(!PAIRK || RK || (PER % 2 == 0 && BK % (2 * (NT / (ROWS / 4))) == 0), "k pairs");
+  // thread's slots come in pairs at k, k + 1 of the same 4 rows, so they pack into bf16x2;
+  // 8 consecutive lanes take 8 consecutive row quads (one 128-B global line) and the next
+  // 8 lanes the next k pair, so the packed LDS words of a wave spread over the banks
+  // (row-quad-major lanes put 32 lanes on 4 banks).
+  static_assert(!PAIRK || RK || (PER % 2 == 0 && (ROWS / 4) % 8 == 0 &&
+                                 BK / 2 == (NT / 8 / (ROWS / 32)) * (PER / 2)), "k pairs");
   __device__ __forceinline__ static void coords(int i, int& r, int& k) {
     const int e = threadIdx.x + i * NT;
     if (RK) { r = e / (BK / 4); k = 4 * (e % (BK / 4)); }
     else if (PAIRK) {
-      constexpr int C4 = ROWS / 4, KP = 2 * (NT / C4);
-      const int t = threadIdx.x;
-      k = (i >> 1) * KP + 2 * (t / C4) + (i & 1);
-      r = 4 * (t % C4);
+      constexpr int G8 = ROWS / 32;
+      const int t = threadIdx.x, rest = t >> 3;
+      r = 4 * ((t & 7) + 8 * (rest % G8));
+      k = 2 * (rest / G8 + (NT / 8 / G8) * (i >> 1)) + (i & 1);
     }
     else    { k = e / (ROWS / 4); r = 4 * (e % (ROWS / 4)); }
   }
@@ -530,8 +534,10 @@ void launch_gemm(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, in
   }
 }
 
-// bf16 tiles: 128x128 (4 waves of 64x64) once that grid fills the chip, else 64x64
-constexpr GemmShape kCfgBf16[] = {{0, 128, 128, 32}, {1, 64, 64, 32}};
+// bf16 tiles: 128x128 (4 waves of 64x64) once that grid fills the chip, else 64x64; BK 64:
+// with the MFMA work per stage 16x smaller than fp32's, the kernel waits on its operand
+// loads, so a stage keeps twice the bytes in flight (BK 32: conv fwd 67 us, LSTM dW 438 us)
+constexpr GemmShape kCfgBf16[] = {{0, 128, 128, 64}, {1, 64, 64, 64}};
 
 GemmShape pick_config_bf16(int M, int N, int splits) {
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
@@ -555,10 +561,10 @@ void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t s
                       Opnd ob, float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps,
                       float* slab) {
   if (id == 0)
-    launch_layouts_bf16<128, 128, 32, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
+    launch_layouts_bf16<128, 128, 64, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
                                               slab);
   else
-    launch_layouts_bf16<64, 64, 32, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
+    launch_layouts_bf16<64, 64, 64, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
                                             slab);
 }
 

@@ -300,6 +300,8 @@ def main():
     ap.add_argument("--no-wavenet", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-bf16", action="store_true")
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
+                    help="precision of the headline measurement (default fp32 = BASELINE config 2)")
     args = ap.parse_args()
 
     from autovc_amd import ddp
@@ -314,6 +316,7 @@ def main():
     if world > 1:
         ddp.make_data_parallel(solver)
     solver.G.train()
+    solver.precision = args.precision
     x, e = synthetic_batch(B, T, dev, 1234 + 2 * rank)
 
     for _ in range(args.warmup):
@@ -352,13 +355,13 @@ def main():
         return d, out
 
     bf = None
-    if not args.no_bf16:
+    if not args.no_bf16 and args.precision == "fp32":
         # BASELINE config 3 numerics (bf16 matmul operands, fp32 master/optimizer/BN/loss),
         # same solver and batch, after the fp32 measurement
         solver.precision = "bf16"
         timed_steps(max(2, args.warmup // 2))
         dtb, lb = timed_steps(args.steps)
-        solver.precision = "fp32"
+        solver.precision = args.precision
         bf = {"value": round(world * B * T * args.steps / dtb, 1), "unit": "mel-frames/s",
               "ms_per_step": round(dtb / args.steps * 1000, 3), "dtype": "bf16 MFMA operands, fp32 accumulate",
               "final_loss": round(float(lb[0].item()), 6),
@@ -387,7 +390,7 @@ def main():
             "metric": "mel-frames/sec Generator fwd+bwd", "value": round(value, 1), "unit": "mel-frames/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1000, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (clamped N(0.43,0.18) mels, unit-norm*0.8 emb)",
+            "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16", "data": "synthetic (clamped N(0.43,0.18) mels, unit-norm*0.8 emb)",
             "config": {"workload": "AutoVC Generator training step (solver_encoder.py), fwd+bwd+Adam",
                        "global_batch": B * world, "seq_len": T, "n_mels": 80, "parallelism": f"dp{world}",
                        "dim_neck": 32, "dim_emb": 256, "dim_pre": 512, "freq": 32},
