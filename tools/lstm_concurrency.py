@@ -61,6 +61,13 @@ def main():
     gpar = timeit(lambda: (chain(B, T, H, *bufs[0], s1), gemm(B * T, 4096, 1024, A, Wp, C, s2)))
     g4 = timeit(lambda: [gemm(B * T, 4096, 1024, A, Wp, C, s2) for _ in range(4)])
     g4par = timeit(lambda: (chain(B, T, H, *bufs[0], s1), [gemm(B * T, 4096, 1024, A, Wp, C, s2) for _ in range(4)]))
+    # stream priorities: the latency-bound chain on a high-priority stream, GEMMs low
+    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+    sh = torch.cuda.Stream(dev, priority=-1)
+    sl = torch.cuda.Stream(dev, priority=0)
+    gpar_p = timeit(lambda: (chain(B, T, H, *bufs[0], sh), gemm(B * T, 4096, 1024, A, Wp, C, sl)))
+    g4par_p = timeit(lambda: (chain(B, T, H, *bufs[0], sh), [gemm(B * T, 4096, 1024, A, Wp, C, sl) for _ in range(4)]))
+    print(f"priorities: chain hi || GEMM lo:  {gpar_p:.3f} ms ; chain hi || 4 GEMMs lo: {g4par_p:.3f} ms")
     print(f"one chain (128 steps, H=1024, B=64): {one:.3f} ms")
     print(f"two chains, one stream:               {seq:.3f} ms")
     print(f"two chains, two streams:              {par:.3f} ms")
