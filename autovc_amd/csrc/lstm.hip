@@ -59,7 +59,11 @@ __device__ __forceinline__ int swz(int sl, int r) { return (sl & ~15) | ((sl & 1
 // Two K segments: k < K1 reads the rows of (arow_of, brow_of), the next K2 those of
 // (arow2_of, brow2_of) — the stacked-layer step concatenates [input ; recurrent] this way
 // (K2 = 0: one segment).
-template <int KCH, int NW, int D, class AR, class BR, class AR2, class BR2>
+// BF: the rows hold bf16 (row pointers and K1/K2 still in 4-byte units: a 16-byte slot is
+// 8 bf16), and a 16-k sub-block of fp32 slots becomes one 32-k v_mfma_f32_16x16x32_bf16 —
+// lane group g's slot is exactly that instruction's k = 8g .. 8g+7 operand.  The staging,
+// swizzle and reduction are byte-for-byte those of the fp32 tile.
+template <int KCH, int NW, int D, bool BF = false, class AR, class BR, class AR2, class BR2>
 __device__ __forceinline__ f32x4 tile_gemm2(float* lds, AR arow_of, BR brow_of, int K1, AR2 arow2_of, BR2 brow2_of,
                                             int K2) {
   using C = Tile<KCH, NW, D>;
@@ -127,13 +131,22 @@ __device__ __forceinline__ f32x4 tile_gemm2(float* lds, AR arow_of, BR brow_of, 
           bv[s] = *reinterpret_cast<const f32x4*>(L + (TB + rb) * KCH + 4 * swz(sl, rb));
         }
         // MFMA local k index (lane>>4) <-> actual k = 16*sub + 4g + jj: same map for A and B
+        if constexpr (BF) {
 #pragma unroll
-        for (int s = 0; s < C::SUB; ++s)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            if (s & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][jj], bv[s][jj], acc1, 0, 0, 0);
-            else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][jj], bv[s][jj], acc0, 0, 0, 0);
+          for (int s = 0; s < C::SUB; ++s) {
+            const bf16x8 ab = __builtin_bit_cast(bf16x8, av[s]), bb = __builtin_bit_cast(bf16x8, bv[s]);
+            if (s & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, acc1, 0, 0, 0);
+            else acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, acc0, 0, 0, 0);
           }
+        } else {
+#pragma unroll
+          for (int s = 0; s < C::SUB; ++s)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              if (s & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][jj], bv[s][jj], acc1, 0, 0, 0);
+              else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][jj], bv[s][jj], acc0, 0, 0, 0);
+            }
+        }
       }
     }
   }
@@ -151,9 +164,9 @@ __device__ __forceinline__ f32x4 tile_gemm2(float* lds, AR arow_of, BR brow_of, 
   return acc;  // valid in waves 0..3 (quadrant q = wave)
 }
 
-template <int KCH, int NW, int D, class AR, class BR>
+template <int KCH, int NW, int D, bool BF = false, class AR, class BR>
 __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, int K) {
-  return tile_gemm2<KCH, NW, D>(lds, arow_of, brow_of, K, arow_of, brow_of, 0);
+  return tile_gemm2<KCH, NW, D, BF>(lds, arow_of, brow_of, K, arow_of, brow_of, 0);
 }
 
 // configuration used by the product kernels (chosen with tools/lstm_step_bench.hip)
@@ -177,6 +190,10 @@ struct StepArgs {
   float* c;                                  // (B, T, H) cell states
   float* gates;                              // (B, T, 4H) post-activation gates or null
   const float* gx2;                          // second bias added to gx (same strides) or null
+  // bf16 recurrences (precision "bf16"): W_hh rounded to bf16 (4H, H) and a bf16 copy of
+  // h, (B, T, H) contiguous, written by the epilogue and read by the next step's product
+  const __bf16* Wb;
+  __bf16* hb;
 };
 
 // One forward time step of a large-H layer, block (blockIdx.x, blockIdx.y) of grid
@@ -186,9 +203,11 @@ struct StepArgs {
 // h_t of this same launch wavefront (gx then holds only b_ih + b_hh, strides 0).
 // ABL != 0 only in the ablation build of tools/lstm_step_bench.hip (bit 0: every block
 // reads the same W_hh rows, bit 1: every lane reads the same h row) — never launched here.
-template <int ABL, int KCH_, int NW_, int D_>
-__device__ __forceinline__ void fwd_step_body(const StepArgs& a, int t, int tp, const float* xin, int64_t x_ldb,
-                                              int64_t x_ldt, const float* W_in, int K_in) {
+// BF: the recurrent (and stacked-input) products on bf16 copies (StepArgs::Wb / hb, the
+// input rows xin / W_in bf16 too), cell math and all fp32 outputs unchanged.
+template <int ABL, int KCH_, int NW_, int D_, bool BF = false>
+__device__ __forceinline__ void fwd_step_body(const StepArgs& a, int t, int tp, const void* xin, int64_t x_ldb,
+                                              int64_t x_ldt, const void* W_in, int K_in) {
   using C = Tile<KCH_, NW_, D_>;
   __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -211,20 +230,34 @@ __device__ __forceinline__ void fwd_step_body(const StepArgs& a, int t, int tp, 
     }
     if (tp >= 0) cp = a.c[(int64_t)b * a.T * H + (int64_t)tp * H + j];
   }
-  const int K_rec = tp >= 0 ? H : 0;
+  // K in 4-byte units (bf16 rows: half the elements)
+  const int K_rec = tp >= 0 ? (BF ? H / 2 : H) : 0;
+  const int K_in_u = BF ? K_in / 2 : K_in;
   auto arow_of = [&](int r) {
     const int b = (ABL & 2) ? 0 : min(b0 + r, a.B - 1);  // rows past B: any valid row, result unused
-    return a.h + (int64_t)b * a.h_ldb + (int64_t)max(tp, 0) * a.h_ldt;
+    if constexpr (BF) return reinterpret_cast<const float*>(a.hb + ((int64_t)b * a.T + max(tp, 0)) * H);
+    else return (const float*)(a.h + (int64_t)b * a.h_ldb + (int64_t)max(tp, 0) * a.h_ldt);
   };
   auto brow_of = [&](int r) {  // tile column r = gate*8 + unit
-    return a.W + (int64_t)((r >> 3) * H + ((ABL & 1) ? 0 : j0) + (r & 7)) * H;
+    const int64_t row = (r >> 3) * H + ((ABL & 1) ? 0 : j0) + (r & 7);
+    if constexpr (BF) return reinterpret_cast<const float*>(a.Wb + row * H);
+    else return a.W + row * H;
   };
-  auto xrow_of = [&](int r) { return xin + (int64_t)min(b0 + r, a.B - 1) * x_ldb + (int64_t)t * x_ldt; };
-  auto wrow_of = [&](int r) { return W_in + (int64_t)((r >> 3) * H + j0 + (r & 7)) * K_in; };
+  auto xrow_of = [&](int r) {
+    const int64_t off = (int64_t)min(b0 + r, a.B - 1) * x_ldb + (int64_t)t * x_ldt;
+    if constexpr (BF) return reinterpret_cast<const float*>(static_cast<const __bf16*>(xin) + off);
+    else return static_cast<const float*>(xin) + off;
+  };
+  auto wrow_of = [&](int r) {
+    const int64_t off = (int64_t)((r >> 3) * H + j0 + (r & 7)) * K_in;
+    if constexpr (BF) return reinterpret_cast<const float*>(static_cast<const __bf16*>(W_in) + off);
+    else return static_cast<const float*>(W_in) + off;
+  };
   float pre[4];
   {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (K_in + K_rec > 0) acc = tile_gemm2<KCH_, NW_, D_>(smem, xrow_of, wrow_of, K_in, arow_of, brow_of, K_rec);
+    if (K_in_u + K_rec > 0)
+      acc = tile_gemm2<KCH_, NW_, D_, BF>(smem, xrow_of, wrow_of, K_in_u, arow_of, brow_of, K_rec);
     __syncthreads();
     float* tile = smem;                                      // [32][33] after the chunk buffers are drained
     if (w < 4) {
@@ -241,16 +274,18 @@ __device__ __forceinline__ void fwd_step_body(const StepArgs& a, int t, int tp, 
   const float g_ = tanhf(pre[2] + gxv[2]), o_ = avc_sigmoid(pre[3] + gxv[3]);
   const float cn = f_ * cp + i_ * g_;
   a.c[(int64_t)b * a.T * H + (int64_t)t * H + j] = cn;
-  a.h[(int64_t)b * a.h_ldb + (int64_t)t * a.h_ldt + j] = o_ * tanhf(cn);
+  const float hn = o_ * tanhf(cn);
+  a.h[(int64_t)b * a.h_ldb + (int64_t)t * a.h_ldt + j] = hn;
+  if (BF) a.hb[((int64_t)b * a.T + t) * H + j] = (__bf16)hn;
   if (a.gates) {
     float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H;
     gs[0 * H + j] = i_; gs[1 * H + j] = f_; gs[2 * H + j] = g_; gs[3 * H + j] = o_;
   }
 }
 
-template <int ABL = 0, int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+template <int ABL = 0, int KCH_ = KCH, int NW_ = NWV, int D_ = DPF, bool BF = false>
 __global__ __launch_bounds__(64 * NW_) void lstm_fwd_step_kernel(StepArgs a, int t, int tp) {
-  fwd_step_body<ABL, KCH_, NW_, D_>(a, t, tp, nullptr, 0, 0, nullptr, 0);
+  fwd_step_body<ABL, KCH_, NW_, D_, BF>(a, t, tp, nullptr, 0, 0, nullptr, 0);
 }
 
 // Two stacked layers (nn.LSTM num_layers=2, decoder lstm2) as one launch per wavefront
@@ -261,14 +296,19 @@ __global__ __launch_bounds__(64 * NW_) void lstm_fwd_step_kernel(StepArgs a, int
 struct Stack2Args {
   StepArgs l0, l1;
   const float* W_ih1;   // (4H, H)
+  const __bf16* W_ih1b; // its bf16 copy (BF)
 };
 
-template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF, bool BF = false>
 __global__ __launch_bounds__(64 * NW_) void lstm2_fwd_step_kernel(Stack2Args a, int t) {
   if (blockIdx.z == 0) {
-    if (t < a.l0.T) fwd_step_body<0, KCH_, NW_, D_>(a.l0, t, t - 1, nullptr, 0, 0, nullptr, 0);
+    if (t < a.l0.T) fwd_step_body<0, KCH_, NW_, D_, BF>(a.l0, t, t - 1, nullptr, 0, 0, nullptr, 0);
   } else if (t >= 1) {
-    fwd_step_body<0, KCH_, NW_, D_>(a.l1, t - 1, t - 2, a.l0.h, a.l0.h_ldb, a.l0.h_ldt, a.W_ih1, a.l1.H);
+    if constexpr (BF)
+      fwd_step_body<0, KCH_, NW_, D_, true>(a.l1, t - 1, t - 2, a.l0.hb, (int64_t)a.l0.T * a.l0.H, a.l0.H,
+                                            a.W_ih1b, a.l1.H);
+    else
+      fwd_step_body<0, KCH_, NW_, D_>(a.l1, t - 1, t - 2, a.l0.h, a.l0.h_ldb, a.l0.h_ldt, a.W_ih1, a.l1.H);
   }
 }
 
@@ -284,6 +324,7 @@ struct BwdArgs {
   float* dG;                                   // (B,T,4H) out
   float* dc_state;                             // (B,H)
   float* P; int S;                             // (S,B,H) partials or null
+  __bf16* dGb;                                 // bf16 copy of dG (bf16 recurrences) or null
 };
 
 // Pointwise pass of one backward step: thread per (b, j).  Every operand is loaded
@@ -319,6 +360,11 @@ __global__ __launch_bounds__(256) void lstm_bwd_pointwise_kernel(BwdArgs a, int 
   d[H + j] = dc * cp * f_ * (1.f - f_);
   d[2 * H + j] = dc * i_ * (1.f - g_ * g_);
   d[3 * H + j] = dh * tc * o_ * (1.f - o_);
+  if (a.dGb) {
+    __bf16* db = a.dGb + ((int64_t)b * a.T + t) * 4 * H;
+    db[j] = (__bf16)d[j]; db[H + j] = (__bf16)d[H + j]; db[2 * H + j] = (__bf16)d[2 * H + j];
+    db[3 * H + j] = (__bf16)d[3 * H + j];
+  }
   a.dc_state[idx] = dc * f_;
 }
 
@@ -348,18 +394,20 @@ void launch_pointwise_any(int blocks, hipStream_t st, const BwdArgs& a, int t, i
 // fused variant — last-arriving split block runs the pointwise pass behind an agent-scope
 // release/acquire ticket — measured 13.8 us per step against 9.2 + 4.0 us for the two
 // launches: the serial partial read + fences cost more than the kernel boundary.)
-template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+// BF: dG / WT are the bf16 copies (passed as raw pointers, row lengths in bf16 elements).
+template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF, bool BF = false>
 __global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, int H, const float* dG, int t,
                                                                const float* WT, float* P) {
   using C = Tile<KCH_, NW_, D_>;
   __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j0 = blockIdx.x * TN, b0 = blockIdx.y * TB, s = blockIdx.z, S = gridDim.z;
-  const int K4 = 4 * H, ks = K4 / S, kb = s * ks;
+  // row length / split offsets in 4-byte units
+  const int K4 = BF ? 2 * H : 4 * H, ks = K4 / S, kb = s * ks;
   auto arow_of = [&](int r) { return dG + ((int64_t)min(b0 + r, B - 1) * T + t) * K4 + kb; };
   auto brow_of = [&](int r) { return WT + (int64_t)(j0 + r) * K4 + kb; };
   {
-    const f32x4 acc = tile_gemm<KCH_, NW_, D_>(smem, arow_of, brow_of, ks);
+    const f32x4 acc = tile_gemm<KCH_, NW_, D_, BF>(smem, arow_of, brow_of, ks);
     if (w >= 4) return;
     const int wi = w >> 1, wn = w & 1;
 #pragma unroll
@@ -680,5 +728,79 @@ extern "C" int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, i
   for (int i = 0; i < 2 * T; ++i) (void)hipEventDestroy(ev[i]);
   delete[] ev;
   *avg_us = (float)(tot / n * 1000.0);
+  return avc::kOk;
+}
+
+// ------------------------------------------------------------------ bf16 recurrences
+// precision "bf16" (BASELINE config 3): the recurrent products read bf16 copies of W
+// (RNE-rounded by the caller) and of h / dG (written by the step epilogues); cell math,
+// c, gates, h and dG stay fp32.  h is (B, T, H) contiguous.
+namespace {
+bool bf16_shape_ok(int B, int H) { return B > 0 && H > 0 && H % 128 == 0; }
+}
+
+extern "C" int autovc_lstm_fwd_bf16(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                                    const uint16_t* W_hh_b, float* h, uint16_t* h_b, float* c_all, float* gates,
+                                    int reverse, hipStream_t stream) {
+  AVC_CHECK_ARG(T > 0 && bf16_shape_ok(B, H), "autovc_lstm_fwd_bf16: bad dims B=%d T=%d H=%d (H %% 128 != 0)", B, T, H);
+  AVC_CHECK_ARG(gx && W_hh_b && h && h_b && c_all, "autovc_lstm_fwd_bf16: null pointer");
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_b) && AVC_ALIGNED16(h_b), "autovc_lstm_fwd_bf16: bf16 operands must be 16-byte aligned");
+  StepArgs a{B, T, H, gx, gx_ldb, gx_ldt, nullptr, h, (int64_t)T * H, H, c_all, gates, nullptr,
+             reinterpret_cast<const __bf16*>(W_hh_b), reinterpret_cast<__bf16*>(h_b)};
+  const dim3 grid(H / UT, (B + TB - 1) / TB);
+  for (int s = 0; s < T; ++s) {
+    const int t = reverse ? T - 1 - s : s;
+    const int tp = s == 0 ? -1 : (reverse ? t + 1 : t - 1);
+    hipLaunchKernelGGL((lstm_fwd_step_kernel<0, KCH, NWV, DPF, true>), grid, dim3(64 * NWV), 0, stream, a, t, tp);
+  }
+  AVC_CHECK_LAUNCH("autovc_lstm_fwd_bf16");
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm2_fwd_bf16(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                                     const uint16_t* W_hh0_b, const float* b_ih1, const float* b_hh1,
+                                     const uint16_t* W_ih1_b, const uint16_t* W_hh1_b, float* h0, uint16_t* h0_b,
+                                     float* c0, float* gates0, float* h1, uint16_t* h1_b, float* c1, float* gates1,
+                                     hipStream_t stream) {
+  AVC_CHECK_ARG(T > 0 && bf16_shape_ok(B, H), "autovc_lstm2_fwd_bf16: bad dims B=%d T=%d H=%d", B, T, H);
+  AVC_CHECK_ARG(gx0 && W_hh0_b && b_ih1 && b_hh1 && W_ih1_b && W_hh1_b && h0 && h0_b && c0 && h1 && h1_b && c1,
+                "autovc_lstm2_fwd_bf16: null pointer");
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh0_b) && AVC_ALIGNED16(W_ih1_b) && AVC_ALIGNED16(W_hh1_b) && AVC_ALIGNED16(h0_b) &&
+                AVC_ALIGNED16(h1_b), "autovc_lstm2_fwd_bf16: bf16 operands must be 16-byte aligned");
+  Stack2Args a{StepArgs{B, T, H, gx0, gx_ldb, gx_ldt, nullptr, h0, (int64_t)T * H, H, c0, gates0, nullptr,
+                        reinterpret_cast<const __bf16*>(W_hh0_b), reinterpret_cast<__bf16*>(h0_b)},
+               StepArgs{B, T, H, b_ih1, 0, 0, nullptr, h1, (int64_t)T * H, H, c1, gates1, b_hh1,
+                        reinterpret_cast<const __bf16*>(W_hh1_b), reinterpret_cast<__bf16*>(h1_b)},
+               nullptr, reinterpret_cast<const __bf16*>(W_ih1_b)};
+  const dim3 grid(H / UT, (B + TB - 1) / TB, 2);
+  for (int t = 0; t <= T; ++t)
+    hipLaunchKernelGGL((lstm2_fwd_step_kernel<KCH, NWV, DPF, true>), grid, dim3(64 * NWV), 0, stream, a, t);
+  AVC_CHECK_LAUNCH("autovc_lstm2_fwd_bf16");
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                                    const float* gates, const float* c_all, const uint16_t* W_hh_T_b, float* dG,
+                                    uint16_t* dG_b, int reverse, int splits, float* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(T > 0 && bf16_shape_ok(B, H), "autovc_lstm_bwd_bf16: bad dims");
+  AVC_CHECK_ARG((splits == 1 || splits == 2 || splits == 4 || splits == 8) && (2 * H) % (KCH * splits) == 0,
+                "autovc_lstm_bwd_bf16: splits must be 1, 2, 4 or 8 with 2H/splits a multiple of %d", KCH);
+  AVC_CHECK_ARG(gates && c_all && W_hh_T_b && dG && dG_b && workspace, "autovc_lstm_bwd_bf16: null pointer");
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_T_b) && AVC_ALIGNED16(dG_b), "autovc_lstm_bwd_bf16: alignment");
+  float* P = workspace;
+  float* dcs = workspace + (int64_t)splits * B * H;
+  BwdArgs a{B, T, H, dh_out, d_ldb, d_ldt, gates, c_all, dG, dcs, P, splits, reinterpret_cast<__bf16*>(dG_b)};
+  const int64_t BH = (int64_t)B * H;
+  const int pw_blocks = (int)((BH + 255) / 256);
+  const dim3 rgrid(H / TN, (B + TB - 1) / TB, splits);
+  for (int s = T - 1; s >= 0; --s) {
+    const int t = reverse ? T - 1 - s : s;
+    const int tp = s == 0 ? -1 : (reverse ? t + 1 : t - 1);
+    launch_pointwise_any(pw_blocks, stream, a, t, tp, s == T - 1);
+    if (s == 0) continue;
+    hipLaunchKernelGGL((lstm_bwd_rec_kernel<KCH, NWV, DPF, true>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
+                       reinterpret_cast<const float*>(dG_b), t, reinterpret_cast<const float*>(W_hh_T_b), P);
+  }
+  AVC_CHECK_LAUNCH("autovc_lstm_bwd_bf16");
   return avc::kOk;
 }

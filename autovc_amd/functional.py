@@ -386,8 +386,14 @@ class LSTMLayerFn(torch.autograd.Function):
         h = torch.empty((B, T, H), device=dev, dtype=torch.float32)
         c = torch.empty((B, T, H), device=dev, dtype=torch.float32)
         gates = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
-        _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
-                  h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), 0, _s())
+        if _bf16_rec(H):
+            hb = torch.empty((B, T, H), device=dev, dtype=torch.bfloat16)
+            Wb = _bf(W_hh)   # held until the launches are enqueued (stream-ordered reuse after)
+            _lib.call("autovc_lstm_fwd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),
+                      h.data_ptr(), hb.data_ptr(), c.data_ptr(), _p(gates), 0, _s())
+        else:
+            _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
+                      h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), 0, _s())
         ctx.save_for_backward(x, W_ih, W_hh, h, c, gates)
         ctx.params = (W_ih, W_hh, b_ih, b_hh)
         return h
@@ -396,6 +402,16 @@ class LSTMLayerFn(torch.autograd.Function):
     def backward(ctx, dh):
         x, W_ih, W_hh, h, c, gates = ctx.saved_tensors
         return _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, ctx.params, ctx.needs_input_grad[:5]) + (None,)
+
+
+def _bf16_rec(H):
+    """Recurrent products in bf16 under precision("bf16") (H a multiple of 128)."""
+    return _PRECISION[0] == "bf16" and H % 128 == 0
+
+
+def _bf(t):
+    """RNE bf16 copy (contiguous) of an fp32 weight for the bf16 recurrences."""
+    return t.detach().contiguous().to(torch.bfloat16)
 
 
 def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
@@ -414,8 +430,14 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     splits = 4 if (4 * H) % 256 == 0 else 1
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-    _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
-              WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
+    if _bf16_rec(H):
+        dGb = torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16)
+        WTb = _bf(WT)
+        _lib.call("autovc_lstm_bwd_bf16", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
+                  WTb.data_ptr(), dG.data_ptr(), dGb.data_ptr(), 0, splits, ws, _s())
+    else:
+        _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
+                  WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
     M = B * T
     dx = dWih = dWhh = dbih = dbhh = None
     if needs[1]:
@@ -458,9 +480,19 @@ class LSTM2StackFn(torch.autograd.Function):
         h0, c0, h1, c1 = (torch.empty((B, T, H), device=dev, dtype=torch.float32) for _ in range(4))
         g0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
         g1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
-        _lib.call("autovc_lstm2_fwd_f32", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W_hh0.data_ptr(),
-                  b_ih1.data_ptr(), b_hh1.data_ptr(), W_ih1.data_ptr(), W_hh1.data_ptr(), h0.data_ptr(),
-                  c0.data_ptr(), _p(g0), h1.data_ptr(), c1.data_ptr(), _p(g1), _s())
+        if _bf16_rec(H):
+            h0b, h1b = (torch.empty((B, T, H), device=dev, dtype=torch.bfloat16) for _ in range(2))
+            # the bf16 weight copies must be alive together (a temporary's block would be
+            # reused by the next conversion before the launches read it)
+            W0b, Wi1b, W1b = _bf(W_hh0), _bf(W_ih1), _bf(W_hh1)
+            _lib.call("autovc_lstm2_fwd_bf16", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W0b.data_ptr(),
+                      b_ih1.data_ptr(), b_hh1.data_ptr(), Wi1b.data_ptr(), W1b.data_ptr(),
+                      h0.data_ptr(), h0b.data_ptr(), c0.data_ptr(), _p(g0), h1.data_ptr(), h1b.data_ptr(),
+                      c1.data_ptr(), _p(g1), _s())
+        else:
+            _lib.call("autovc_lstm2_fwd_f32", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W_hh0.data_ptr(),
+                      b_ih1.data_ptr(), b_hh1.data_ptr(), W_ih1.data_ptr(), W_hh1.data_ptr(), h0.data_ptr(),
+                      c0.data_ptr(), _p(g0), h1.data_ptr(), c1.data_ptr(), _p(g1), _s())
         ctx.save_for_backward(x, W_ih0, W_hh0, h0, c0, g0, W_ih1, W_hh1, h1, c1, g1)
         ctx.params = ((W_ih0, W_hh0, b_ih0, b_hh0), (W_ih1, W_hh1, b_ih1, b_hh1))
         return h1

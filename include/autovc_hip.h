@@ -127,6 +127,23 @@ int autovc_lstm2_fwd_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, 
                          const float* W_hh0, const float* b_ih1, const float* b_hh1, const float* W_ih1,
                          const float* W_hh1, float* h0, float* c0, float* gates0, float* h1, float* c1,
                          float* gates1, hipStream_t stream);
+/* bf16 recurrences (precision "bf16", BASELINE config 3): as autovc_lstm_fwd_f32 /
+ * autovc_lstm2_fwd_f32 / autovc_lstm_bwd_f32, but the recurrent products read bf16
+ * (uint16_t bit patterns, RNE-rounded) copies of the weights — W_hh (4H,H), W_ih1 (4H,H),
+ * W_hh^T (H,4H) — and of h / dG, which the step kernels write alongside their fp32
+ * outputs (h_b (B,T,H), dG_b (B,T,4H)); cell math, c, gates, h, dG stay fp32.  h
+ * contiguous (B,T,H); H a multiple of 128. */
+int autovc_lstm_fwd_bf16(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                         const uint16_t* W_hh_b, float* h, uint16_t* h_b, float* c_all, float* gates,
+                         int reverse, hipStream_t stream);
+int autovc_lstm2_fwd_bf16(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                          const uint16_t* W_hh0_b, const float* b_ih1, const float* b_hh1,
+                          const uint16_t* W_ih1_b, const uint16_t* W_hh1_b, float* h0, uint16_t* h0_b,
+                          float* c0, float* gates0, float* h1, uint16_t* h1_b, float* c1, float* gates1,
+                          hipStream_t stream);
+int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                         const float* gates, const float* c_all, const uint16_t* W_hh_T_b, float* dG,
+                         uint16_t* dG_b, int reverse, int splits, float* workspace, hipStream_t stream);
 /* autovc_lstm_fwd_f32 with every step launch timed by its own dispatch events;
  * synchronises; *avg_us (HOST pointer) = mean kernel time of steps 1..T-1 (bench.py). */
 int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_ldb,

@@ -95,3 +95,36 @@ def test_bf16_training_loss_tracks_fp32(cuda):
     r = (curves["bf16"] - curves["fp32"]).abs() / curves["fp32"]
     assert float(r.max()) < 0.05, f"max rel loss gap {float(r.max()):.3f} at step {int(r.argmax())}"
     assert float(curves["bf16"][-1]) < float(curves["bf16"][0])   # it trains
+
+
+@pytest.mark.parametrize("B,T,I,H,stacked", [(64, 16, 320, 512, False), (9, 12, 512, 1024, False), (9, 12, 256, 512, True), (9, 12, 512, 1024, True)])
+def test_lstm_bf16_recurrence(cuda, B, T, I, H, stacked):
+    """bf16 recurrences (bf16 copies of h / W / dG in the recurrent products, fp32 cell
+    math): within bf16 rounding of the fp32 oracle, and genuinely different from fp32."""
+    from autovc_amd import functional as AF
+    from oracle import generator as og
+    torch.manual_seed(7)
+    s = 1 / H ** 0.5
+    nl = 2 if stacked else 1
+    shapes = [(4 * H, I), (4 * H, H), (4 * H,), (4 * H,)] + ([(4 * H, H), (4 * H, H), (4 * H,), (4 * H,)] if stacked else [])
+    ps = [(torch.rand(*sh) * 2 - 1).mul_(s).requires_grad_() for sh in shapes]
+    x = torch.randn(B, T, I, requires_grad=True)
+    h = x
+    for l in range(nl):
+        h = og.OracleGenerator._lstm_dir(h, *ps[4 * l:4 * l + 4], reverse=False)
+    gh = torch.randn_like(h)
+    h.backward(gh)
+    outs = {}
+    for prec in ("fp32", "bf16"):
+        xd = x.detach().to(cuda).requires_grad_()
+        pd = [p.detach().to(cuda).requires_grad_() for p in ps]
+        with AF.precision(prec):
+            hd = AF.LSTM2StackFn.apply(xd, *pd, True) if stacked else AF.LSTMLayerFn.apply(xd, *pd, True)
+            hd.backward(gh.to(cuda))
+        outs[prec] = (hd, xd.grad, [p.grad for p in pd])
+    hd, dx, dps = outs["bf16"]
+    assert rel(hd, h) < 3e-2, (rel(hd, h), rel(outs["fp32"][0], h))
+    assert rel(dx, x.grad) < 5e-2
+    for a, b in zip(dps, ps):
+        assert rel(a, b.grad) < 5e-2
+    assert rel(outs["bf16"][0], outs["fp32"][0]) > 1e-5
