@@ -493,6 +493,9 @@ constexpr GemmShape kCfg[] = {
 #define AVC_GEMM_FORCE_CFG -1
 #endif
 int g_force_cfg = AVC_GEMM_FORCE_CFG;  // tools/gemm_bench.hip overrides this
+// extra (unused) dynamic LDS per GEMM workgroup: caps how many GEMM workgroups share a CU
+// so that a latency-bound kernel on another stream still finds room (autovc_gemm_set_lds_pad)
+unsigned g_dyn_lds = 0;
 
 GemmShape pick_config(int M, int N, int K, int splits) {
   if (g_force_cfg >= 0) return kCfg[g_force_cfg];
@@ -510,7 +513,7 @@ template <int BM, int BN, int BK, int WM, int WN, bool PIPE = false>
 void launch_layouts(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                     float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE>), grid, dim3(NT), 0, st, M, N, K, \
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE>), grid, dim3(NT), g_dyn_lds, st, M, N, K, \
                                          oa, ob, C, ldc, b1, b2, acc, kps, slab)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
@@ -548,7 +551,7 @@ template <int BM, int BN, int BK, int WM, int WN>
 void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                          float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), 0, st, M, N, \
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), g_dyn_lds, st, M, N, \
                                          K, oa, ob, C, ldc, b1, b2, acc, kps, slab)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
@@ -641,4 +644,10 @@ extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
                                     int accumulate, int splits, float* workspace, hipStream_t stream) {
   return gemm_impl(true, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T, b_conv_C,
                    b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
+}
+
+extern "C" int autovc_gemm_set_lds_pad(int bytes) {
+  AVC_CHECK_ARG(bytes >= 0 && bytes <= 96 * 1024, "autovc_gemm_set_lds_pad: 0 <= bytes <= 96 KiB");
+  g_dyn_lds = (unsigned)bytes;
+  return avc::kOk;
 }

@@ -46,6 +46,8 @@ def allreduce_gradients(optimizer, bucket_bytes=64 << 20):
     world = dist.get_world_size()
     if world == 1:
         return
+    from .functional import join_grad_stream   # weight gradients may still be in flight
+    join_grad_stream()
     nb = max(1, bucket_bytes // 4)
     for flat in optimizer.flat_grads():
         for s in range(0, flat.numel(), nb):

@@ -9,6 +9,7 @@ read NTC through the GEMM's implicit im2col operand.
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 
@@ -50,7 +51,89 @@ class _Workspace:
 
 
 def _ws(device, nbytes, slot="main"):
+    # the gradient stream has scratch of its own (its GEMMs run beside the main stream's)
+    if _GRAD_STREAM_ACTIVE[0]:
+        slot = slot + "@grad"
     return _Workspace.get(device, nbytes, slot).data_ptr()
+
+
+# ---------------------------------------------------------------- gradient stream
+# Weight-gradient GEMMs (and the bias column sums next to them) are off the backward's
+# critical path: nothing reads them before the optimizer.  When a gradient lives in the
+# optimizer's flat buffer, its kernels go to a per-device side stream that first waits for
+# everything the main stream has issued so far (so its inputs exist), marks those inputs
+# as in use by the side stream (the caching allocator then keeps them until the side
+# stream is past them), and runs beside the main stream — the LSTM and BLSTM recurrences
+# there leave most of the chip idle.  Their fp32/bf16 GEMM workgroups carry an LDS pad
+# so that a recurrence step workgroup (37 KB LDS) still fits next to them on every CU
+# (tools/lstm_concurrency.py: a conv-GEMM batch beside a 128-step chain costs 0.46 ms
+# instead of 0.85 with the pad, 0.61 without).  FusedAdam.step (and join_grad_stream)
+# make the main stream wait before the gradients are read.  AVC_GRAD_STREAM=0 disables.
+_GRAD_STREAM_ON = os.environ.get("AVC_GRAD_STREAM", "1") != "0"
+_GRAD_STREAM_ACTIVE = [False]
+_GRAD_STREAMS: dict = {}
+GRAD_LDS_PAD = int(os.environ.get("AVC_GRAD_LDS_PAD", "20480"))
+
+
+def _grad_stream(dev):
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _GRAD_STREAMS.get(idx)
+    if st is None:
+        st = torch.cuda.Stream(torch.device("cuda", idx))
+        _GRAD_STREAMS[idx] = st
+    return st
+
+
+_GRAD_QUEUE: list = []
+
+
+def _grad_launch(dev, use, fn, *inputs):
+    """Queue the gradient launches `fn` for the side stream when `use` (the gradient is
+    accumulated into the flat buffer) and the side stream is enabled; else run them now.
+    Queued work is released at the next recurrence (_flush_grad_queue) so that it runs
+    beside a latency-bound chain rather than beside the main stream's own GEMMs (measured:
+    released immediately it only competed with them: 22.2 -> 22.9 ms/step)."""
+    if not (use and _GRAD_STREAM_ON):
+        fn()
+        return
+    _GRAD_QUEUE.append((dev, fn, inputs))
+
+
+def _flush_grad_queue():
+    """Issue every queued gradient launch on the side stream, ordered after all main-stream
+    work issued so far (their inputs), inputs marked as in use by the side stream."""
+    if not _GRAD_QUEUE:
+        return
+    items = list(_GRAD_QUEUE)
+    _GRAD_QUEUE.clear()
+    dev = items[0][0]
+    main = torch.cuda.current_stream(dev)
+    side = _grad_stream(dev)
+    side.wait_stream(main)
+    _GRAD_STREAM_ACTIVE[0] = True
+    _lib.call("autovc_gemm_set_lds_pad", GRAD_LDS_PAD)
+    try:
+        with torch.cuda.stream(side):
+            for _, fn, inputs in items:
+                for t in inputs:
+                    if t is not None:
+                        t.record_stream(side)
+                fn()
+    finally:
+        _lib.call("autovc_gemm_set_lds_pad", 0)
+        _GRAD_STREAM_ACTIVE[0] = False
+
+
+def join_grad_stream(dev=None):
+    """Release queued gradient work and make the current stream wait for the gradient
+    stream (before anything reads the gradients)."""
+    _flush_grad_queue()
+    if not _GRAD_STREAMS:
+        return
+    dev = dev or torch.device("cuda", torch.cuda.current_device())
+    st = _GRAD_STREAMS.get(dev.index if dev.index is not None else torch.cuda.current_device())
+    if st is not None:
+        torch.cuda.current_stream(dev).wait_stream(st)
 
 
 _PRECISION = ["fp32"]
@@ -174,14 +257,18 @@ def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None):
     padded = W is None or tuple(W.shape) != tuple(Wp.shape)
     if need_b:
         go = _GradOut(None if padded else b, (Cop,), dev)
-        colsum(dy.view(M, Cop), go.buf, accumulate=go.acc)
+        _grad_launch(dev, go.acc, lambda go=go: colsum(dy.view(M, Cop), go.buf, accumulate=go.acc), dy)
         db = go.result()
     if need_w:
-        dWf = torch.empty((Cop, KS * Cip), device=dev, dtype=torch.float32)
-        gemm(Cop, KS * Cip, M, dy, Cop, 1, x, Cip, 1, dWf, KS * Cip, b_conv=(T, Cip, -PAD),
-             splits=_splits_for(Cop, KS * Cip, M))
         go = _GradOut(None if padded else W, (Cop, Cip, KS), dev)
-        _lib.call("autovc_conv_unpack_grad_f32", Cop, Cip, KS, dWf.data_ptr(), go.buf.data_ptr(), int(go.acc), _s())
+
+        def dw(go=go):
+            dWf = torch.empty((Cop, KS * Cip), device=dev, dtype=torch.float32)
+            gemm(Cop, KS * Cip, M, dy, Cop, 1, x, Cip, 1, dWf, KS * Cip, b_conv=(T, Cip, -PAD),
+                 splits=_splits_for(Cop, KS * Cip, M))
+            _lib.call("autovc_conv_unpack_grad_f32", Cop, Cip, KS, dWf.data_ptr(), go.buf.data_ptr(), int(go.acc),
+                      _s())
+        _grad_launch(dev, go.acc, dw, dy, x)
         dW = go.result()
     if need_x:
         Wd = torch.empty((KS * Cop, Cip), device=dev, dtype=torch.float32)
@@ -352,12 +439,13 @@ class LinearFn(torch.autograd.Function):
         dx = dW = db = None
         if ctx.needs_input_grad[1]:
             go = _GradOut(W_param if Np == N else None, (Np, K), dev)
-            gemm(Np, K, M, dy, Np, 1, x, K, 1, go.buf, K, splits=_splits_for(Np, K, M), accumulate=go.acc)
+            _grad_launch(dev, go.acc, lambda go=go: gemm(Np, K, M, dy, Np, 1, x, K, 1, go.buf, K,
+                                                         splits=_splits_for(Np, K, M), accumulate=go.acc), dy, x)
             dW = go.result()
             dW = dW if (dW is None or Np == N) else dW[:N].contiguous()
         if ctx.has_b and ctx.needs_input_grad[2]:
             go = _GradOut(b_param if Np == N else None, (Np,), dev)
-            colsum(dy, go.buf, accumulate=go.acc)
+            _grad_launch(dev, go.acc, lambda go=go: colsum(dy, go.buf, accumulate=go.acc), dy)
             db = go.result()
             db = db if (db is None or Np == N) else db[:N].contiguous()
         if ctx.needs_input_grad[0]:
@@ -430,6 +518,7 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     splits = 4 if (4 * H) % 256 == 0 else 1
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+    _flush_grad_queue()   # queued weight gradients run beside this latency-bound recurrence
     if _bf16_rec(H):
         dGb = torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16)
         WTb = _bf(WT)
@@ -442,18 +531,20 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     dx = dWih = dWhh = dbih = dbhh = None
     if needs[1]:
         go = _GradOut(p_ih, W_ih.shape, dev)
-        gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I, splits=_splits_for(4 * H, I, M), accumulate=go.acc)
+        _grad_launch(dev, go.acc, lambda go=go: gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I,
+                                                     splits=_splits_for(4 * H, I, M), accumulate=go.acc), dG, x)
         dWih = go.result()
     if needs[2]:
         go = _GradOut(p_hh, W_hh.shape, dev)
-        gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
-             splits=_splits_for(4 * H, H, M), accumulate=go.acc)
+        _grad_launch(dev, go.acc, lambda go=go: gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
+                                                     splits=_splits_for(4 * H, H, M), accumulate=go.acc), dG, h)
         dWhh = go.result()
     if needs[3] or needs[4]:
         gi, gh = _GradOut(p_bih, (4 * H,), dev), _GradOut(p_bhh, (4 * H,), dev)
         if gi.acc != gh.acc:
             gi, gh = _GradOut(None, (4 * H,), dev), _GradOut(None, (4 * H,), dev)
-        colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc)
+        _grad_launch(dev, gi.acc, lambda gi=gi, gh=gh: colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc),
+                     dG)
         dbih, dbhh = gi.result(), gh.result()
     if needs[0]:
         dx = torch.empty_like(x)
@@ -546,6 +637,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         M = B * T
         dev = x.device
         dG = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32)
+        _flush_grad_queue()   # queued weight gradients run beside this latency-bound recurrence
         _lib.call("autovc_blstm_bwd_f32", B, T, H, 2, dh.data_ptr(), gates.data_ptr(), c.data_ptr(),
                   Whh_f.data_ptr(), Whh_b.data_ptr(), dG.data_ptr(), _s())
         grads = [None] * 10

@@ -81,6 +81,8 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        from .functional import join_grad_stream   # weight gradients may still be in flight
+        join_grad_stream()
         for group, f in zip(self.param_groups, self._flat):
             if f is None:
                 continue

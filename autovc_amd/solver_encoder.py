@@ -148,6 +148,7 @@ class Solver(object):
             g_loss, l_id, l_psnt, l_cd, x_psnt = self.compute_losses(x_real, emb_org)
             self.reset_grad()
             g_loss.backward()
+        AF.join_grad_stream()   # weight gradients (side stream) complete before they are read
         self._after_backward()
         self.g_optimizer.step()
         self._last_psnt = x_psnt

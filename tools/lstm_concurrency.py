@@ -68,6 +68,22 @@ def main():
     gpar_p = timeit(lambda: (chain(B, T, H, *bufs[0], sh), gemm(B * T, 4096, 1024, A, Wp, C, sl)))
     g4par_p = timeit(lambda: (chain(B, T, H, *bufs[0], sh), [gemm(B * T, 4096, 1024, A, Wp, C, sl) for _ in range(4)]))
     print(f"priorities: chain hi || GEMM lo:  {gpar_p:.3f} ms ; chain hi || 4 GEMMs lo: {g4par_p:.3f} ms")
+    # conv-shaped GEMMs (64x64 tiles, 36.9 KB LDS each: 4 per CU leave no room for a 37 KB
+    # step workgroup) with an LDS pad that caps them at 3 per CU
+    Xc = torch.randn(B * T, 2560, device=dev)
+    Wc = torch.randn(512, 2560, device=dev)
+    Cc = torch.empty(B * T, 512, device=dev)
+    conv4 = lambda st: [gemm(B * T, 512, 2560, Xc, Wc, Cc, st) for _ in range(4)]  # noqa: E731
+    c4 = timeit(lambda: conv4(s2))
+    c4par = timeit(lambda: (chain(B, T, H, *bufs[0], s1), conv4(s2)))
+    res = {}
+    for pad in (4096, 8192, 20480):
+        _lib.call("autovc_gemm_set_lds_pad", pad)
+        res[pad] = (timeit(lambda: conv4(s2)), timeit(lambda: (chain(B, T, H, *bufs[0], s1), conv4(s2))))
+    _lib.call("autovc_gemm_set_lds_pad", 0)
+    print(f"4 conv GEMMs alone {c4:.3f} ms; chain || 4 conv GEMMs {c4par:.3f} ms (sum {one + c4:.3f})")
+    for pad, (a_, b_) in res.items():
+        print(f"  LDS pad {pad:6d} B: 4 conv GEMMs alone {a_:.3f} ms; chain || them {b_:.3f} ms (sum {one + a_:.3f})")
     print(f"one chain (128 steps, H=1024, B=64): {one:.3f} ms")
     print(f"two chains, one stream:               {seq:.3f} ms")
     print(f"two chains, two streams:              {par:.3f} ms")
