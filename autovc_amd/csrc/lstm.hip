@@ -331,60 +331,76 @@ struct BwdArgs {
 // unconditionally before first use (optional operands are template switches, the previous
 // cell is read at a clamped step and masked): a load behind a runtime condition makes
 // hipcc wait vmcnt(0) per load, serialising a dozen HBM round trips.
+// Thread = 4 consecutive units of one batch row (float4 loads / stores), grid (H/256, B)
+// of 64-thread blocks: no 64-bit index division, and the bf16 dG copy comes from registers.
 template <int S, bool FIRST, bool HAS_DH>
-__global__ __launch_bounds__(256) void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t BH = (int64_t)a.B * a.H;
-  if (idx >= BH) return;
+__global__ __launch_bounds__(64) void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp) {
   const int H = a.H;
-  const int b = (int)(idx / H), j = (int)(idx % H);
-  const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H;
-  const float i_ = gs[j], f_ = gs[H + j], g_ = gs[2 * H + j], o_ = gs[3 * H + j];
-  const float cc = a.c[((int64_t)b * a.T + t) * H + j];
-  const float cpr = a.c[((int64_t)b * a.T + (tp >= 0 ? tp : t)) * H + j];
-  float dh = 0.f, dcs = 0.f;
-  if (HAS_DH) dh = a.dh_out[(int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j];
-  float p[S];
+  const int j = 4 * (blockIdx.x * 64 + threadIdx.x);
+  if (j >= H) return;
+  const int b = blockIdx.y;
+  const int64_t BH = (int64_t)a.B * H, bj = (int64_t)b * H + j;
+  auto ld4 = [](const float* p) { return *reinterpret_cast<const f32x4*>(p); };
+  const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H + j;
+  const f32x4 i_ = ld4(gs), f_ = ld4(gs + H), g_ = ld4(gs + 2 * H), o_ = ld4(gs + 3 * H);
+  const f32x4 cc = ld4(a.c + ((int64_t)b * a.T + t) * H + j);
+  const f32x4 cpr = ld4(a.c + ((int64_t)b * a.T + (tp >= 0 ? tp : t)) * H + j);
+  f32x4 dh = {0.f, 0.f, 0.f, 0.f}, dcs = {0.f, 0.f, 0.f, 0.f};
+  if (HAS_DH) dh = ld4(a.dh_out + (int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j);
+  f32x4 p[S];
   if (!FIRST) {
-    dcs = a.dc_state[idx];
+    dcs = ld4(a.dc_state + bj);
 #pragma unroll
-    for (int s = 0; s < S; ++s) p[s] = a.P[(int64_t)s * BH + idx];
+    for (int s = 0; s < S; ++s) p[s] = ld4(a.P + (int64_t)s * BH + bj);
 #pragma unroll
     for (int s = 0; s < S; ++s) dh += p[s];
   }
-  const float cp = tp >= 0 ? cpr : 0.f;
-  const float tc = tanhf(cc);
-  const float dc = dcs + dh * o_ * (1.f - tc * tc);
-  float* d = a.dG + ((int64_t)b * a.T + t) * 4 * H;
-  d[j] = dc * g_ * i_ * (1.f - i_);
-  d[H + j] = dc * cp * f_ * (1.f - f_);
-  d[2 * H + j] = dc * i_ * (1.f - g_ * g_);
-  d[3 * H + j] = dh * tc * o_ * (1.f - o_);
-  if (a.dGb) {
-    __bf16* db = a.dGb + ((int64_t)b * a.T + t) * 4 * H;
-    db[j] = (__bf16)d[j]; db[H + j] = (__bf16)d[H + j]; db[2 * H + j] = (__bf16)d[2 * H + j];
-    db[3 * H + j] = (__bf16)d[3 * H + j];
+  f32x4 di, df, dg, dO, dcn;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float cp = tp >= 0 ? cpr[e] : 0.f;
+    const float tc = tanhf(cc[e]);
+    const float dc = dcs[e] + dh[e] * o_[e] * (1.f - tc * tc);
+    di[e] = dc * g_[e] * i_[e] * (1.f - i_[e]);
+    df[e] = dc * cp * f_[e] * (1.f - f_[e]);
+    dg[e] = dc * i_[e] * (1.f - g_[e] * g_[e]);
+    dO[e] = dh[e] * tc * o_[e] * (1.f - o_[e]);
+    dcn[e] = dc * f_[e];
   }
-  a.dc_state[idx] = dc * f_;
+  float* d = a.dG + ((int64_t)b * a.T + t) * 4 * H + j;
+  *reinterpret_cast<f32x4*>(d) = di;
+  *reinterpret_cast<f32x4*>(d + H) = df;
+  *reinterpret_cast<f32x4*>(d + 2 * H) = dg;
+  *reinterpret_cast<f32x4*>(d + 3 * H) = dO;
+  if (a.dGb) {
+    __bf16* db = a.dGb + ((int64_t)b * a.T + t) * 4 * H + j;
+    auto cv = [](f32x4 v) { return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]}; };
+    *reinterpret_cast<bf16x4*>(db) = cv(di);
+    *reinterpret_cast<bf16x4*>(db + H) = cv(df);
+    *reinterpret_cast<bf16x4*>(db + 2 * H) = cv(dg);
+    *reinterpret_cast<bf16x4*>(db + 3 * H) = cv(dO);
+  }
+  *reinterpret_cast<f32x4*>(a.dc_state + bj) = dcn;
 }
 
 template <int S>
-void launch_pointwise(int blocks, hipStream_t st, const BwdArgs& a, int t, int tp, bool first) {
+void launch_pointwise(dim3 grid, hipStream_t st, const BwdArgs& a, int t, int tp, bool first) {
   if (first) {
-    if (a.dh_out) hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, true, true>), dim3(blocks), dim3(256), 0, st, a, t, tp);
-    else hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, true, false>), dim3(blocks), dim3(256), 0, st, a, t, tp);
+    if (a.dh_out) hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, true, true>), grid, dim3(64), 0, st, a, t, tp);
+    else hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, true, false>), grid, dim3(64), 0, st, a, t, tp);
   } else {
-    if (a.dh_out) hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, false, true>), dim3(blocks), dim3(256), 0, st, a, t, tp);
-    else hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, false, false>), dim3(blocks), dim3(256), 0, st, a, t, tp);
+    if (a.dh_out) hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, false, true>), grid, dim3(64), 0, st, a, t, tp);
+    else hipLaunchKernelGGL((lstm_bwd_pointwise_kernel<S, false, false>), grid, dim3(64), 0, st, a, t, tp);
   }
 }
 
-void launch_pointwise_any(int blocks, hipStream_t st, const BwdArgs& a, int t, int tp, bool first) {
+void launch_pointwise_any(int /*blocks*/, hipStream_t st, const BwdArgs& a, int t, int tp, bool first) {
+  const dim3 grid((a.H / 4 + 63) / 64, a.B);
   switch (a.S) {
-    case 1: launch_pointwise<1>(blocks, st, a, t, tp, first); break;
-    case 2: launch_pointwise<2>(blocks, st, a, t, tp, first); break;
-    case 4: launch_pointwise<4>(blocks, st, a, t, tp, first); break;
-    default: launch_pointwise<8>(blocks, st, a, t, tp, first); break;
+    case 1: launch_pointwise<1>(grid, st, a, t, tp, first); break;
+    case 2: launch_pointwise<2>(grid, st, a, t, tp, first); break;
+    case 4: launch_pointwise<4>(grid, st, a, t, tp, first); break;
+    default: launch_pointwise<8>(grid, st, a, t, tp, first); break;
   }
 }
 
@@ -640,6 +656,8 @@ extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int
   AVC_CHECK_ARG((splits == 1 || splits == 2 || splits == 4 || splits == 8) && (4 * H) % (64 * splits) == 0,
                 "autovc_lstm_bwd_f32: splits must be 1, 2, 4 or 8 and 4H must split into multiples of 64");
   AVC_CHECK_ARG(gates && c_all && W_hh_T && dG && workspace, "autovc_lstm_bwd_f32: null pointer");
+  AVC_CHECK_ARG(!dh_out || (d_ldb % 4 == 0 && d_ldt % 4 == 0 && AVC_ALIGNED16(dh_out)),
+                "autovc_lstm_bwd_f32: dh_out must be 16-byte aligned with strides %% 4 == 0");
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_T) && AVC_ALIGNED16(dG), "autovc_lstm_bwd_f32: W_hh_T/dG alignment");
   float* P = workspace;
   float* dcs = workspace + (int64_t)splits * B * H;
@@ -786,6 +804,8 @@ extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, in
   AVC_CHECK_ARG((splits == 1 || splits == 2 || splits == 4 || splits == 8) && (2 * H) % (KCH * splits) == 0,
                 "autovc_lstm_bwd_bf16: splits must be 1, 2, 4 or 8 with 2H/splits a multiple of %d", KCH);
   AVC_CHECK_ARG(gates && c_all && W_hh_T_b && dG && dG_b && workspace, "autovc_lstm_bwd_bf16: null pointer");
+  AVC_CHECK_ARG(!dh_out || (d_ldb % 4 == 0 && d_ldt % 4 == 0 && AVC_ALIGNED16(dh_out)),
+                "autovc_lstm_bwd_bf16: dh_out must be 16-byte aligned with strides %% 4 == 0");
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_T_b) && AVC_ALIGNED16(dG_b), "autovc_lstm_bwd_bf16: alignment");
   float* P = workspace;
   float* dcs = workspace + (int64_t)splits * B * H;
