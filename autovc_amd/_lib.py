@@ -41,7 +41,7 @@ sig("autovc_device_sync")
 sig("autovc_stft_mel_f32", c_ptr, c_ptr, c_ptr, c_int, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
     c_int, c_int, c_ptr, c_ptr)
 sig("autovc_gemm_workspace_floats", c_int, c_int, c_int)
-sig("autovc_gemm_set_lds_pad", c_int)
+sig("autovc_gemm_set_lds_reserve", c_int)
 sig("autovc_gemm_f32", c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,

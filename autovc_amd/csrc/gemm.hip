@@ -27,6 +27,7 @@
 // buffer, one barrier per stage; XCD-aware tile order.  Split-K writes fp32 slabs
 // reduced in k order by a second kernel (deterministic; no float atomics).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "../../include/autovc_hip.h"
@@ -487,15 +488,33 @@ constexpr GemmShape kCfg[] = {
     {6, 128, 64, 32},    // 4 waves of 64x32, BK 32, pipelined
     {7, 128, 128, 64},   // BK 64, pipelined (139 KB LDS, 1 block/CU)
     {8, 64, 64, 32},     // BK 32, pipelined
+    {9, 128, 128, 32},   // 8 waves of 64x32, pipelined (sweep candidate)
+    {10, 64, 64, 64},    // BK 64, pipelined (sweep candidate)
+    {11, 128, 64, 32},   // 8 waves of 32x32, pipelined (sweep candidate)
 };
 
 #ifndef AVC_GEMM_FORCE_CFG
 #define AVC_GEMM_FORCE_CFG -1
 #endif
 int g_force_cfg = AVC_GEMM_FORCE_CFG;  // tools/gemm_bench.hip overrides this
-// extra (unused) dynamic LDS per GEMM workgroup: caps how many GEMM workgroups share a CU
-// so that a latency-bound kernel on another stream still finds room (autovc_gemm_set_lds_pad)
-unsigned g_dyn_lds = 0;
+// LDS (bytes per CU) that GEMM launches leave free for a latency-bound kernel on another
+// stream (autovc_gemm_set_lds_reserve): each workgroup is padded with unused dynamic LDS
+// so that the largest count that still fits in 160 KiB - reserve is also the most that fit.
+unsigned g_lds_reserve = 0;
+constexpr unsigned kLdsPerCU = 160 * 1024;
+
+unsigned dyn_lds_for(unsigned static_bytes) {
+  if (g_lds_reserve == 0 || static_bytes == 0 || static_bytes + g_lds_reserve > kLdsPerCU) return 0;
+  unsigned n = (kLdsPerCU - g_lds_reserve) / static_bytes;
+  if (n > 8) n = 8;
+  const unsigned per = kLdsPerCU / (n + 1) + 256;   // n + 1 no longer fit
+  return per > static_bytes ? per - static_bytes : 0;
+}
+
+template <int BM, int BN, int BK, bool AR, bool BR>
+constexpr unsigned f32_lds_bytes() {
+  return 2u * 4u * ((AR ? BM * (BK + 4) : BK * (BM + 4)) + (BR ? BN * (BK + 4) : BK * (BN + 4)));
+}
 
 GemmShape pick_config(int M, int N, int K, int splits) {
   if (g_force_cfg >= 0) return kCfg[g_force_cfg];
@@ -503,6 +522,8 @@ GemmShape pick_config(int M, int N, int K, int splits) {
   // 128x128/BK32 once the 128-tile grid fills the chip >= 2x over (115-124 TF at
   // 8192x1024..4096); narrower unsplit outputs on 64x64/BK32 with pipelined fragment
   // reads (conv fwd/dX 105-109 TF); split-K weight gradients on 64x64/BK16 (92-99 TF).
+  // (8-wave tiles, cfg 9/11, won 5-7 % in the isolated sweep but nothing inside the step:
+  // 21.62 vs 21.52 ms, same box, alternating)
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
   if (t128 >= 512) return kCfg[2];
   if (splits > 1) return kCfg[3];
@@ -513,7 +534,8 @@ template <int BM, int BN, int BK, int WM, int WN, bool PIPE = false>
 void launch_layouts(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                     float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE>), grid, dim3(NT), g_dyn_lds, st, M, N, K, \
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE>), grid, dim3(NT), \
+                                         dyn_lds_for(f32_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, K, \
                                          oa, ob, C, ldc, b1, b2, acc, kps, slab)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
@@ -533,6 +555,9 @@ void launch_gemm(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, in
     case 6: launch_layouts<128, 64, 32, 64, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     case 7: launch_layouts<128, 128, 64, 64, 64, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     case 8: launch_layouts<64, 64, 32, 32, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 9: launch_layouts<128, 128, 32, 64, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 10: launch_layouts<64, 64, 64, 32, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 11: launch_layouts<128, 64, 32, 32, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     default: launch_layouts<64, 64, 16, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
   }
 }
@@ -551,7 +576,8 @@ template <int BM, int BN, int BK, int WM, int WN>
 void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                          float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), g_dyn_lds, st, M, N, \
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), \
+                                         dyn_lds_for(2u * 2u * (BM + BN) * (BK + 8)), st, M, N, \
                                          K, oa, ob, C, ldc, b1, b2, acc, kps, slab)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
@@ -646,8 +672,8 @@ extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
                    b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
 }
 
-extern "C" int autovc_gemm_set_lds_pad(int bytes) {
-  AVC_CHECK_ARG(bytes >= 0 && bytes <= 96 * 1024, "autovc_gemm_set_lds_pad: 0 <= bytes <= 96 KiB");
-  g_dyn_lds = (unsigned)bytes;
+extern "C" int autovc_gemm_set_lds_reserve(int bytes) {
+  AVC_CHECK_ARG(bytes >= 0 && bytes <= 96 * 1024, "autovc_gemm_set_lds_reserve: 0 <= bytes <= 96 KiB");
+  g_lds_reserve = (unsigned)bytes;
   return avc::kOk;
 }

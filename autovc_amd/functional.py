@@ -64,7 +64,7 @@ def _ws(device, nbytes, slot="main"):
 # everything the main stream has issued so far (so its inputs exist), marks those inputs
 # as in use by the side stream (the caching allocator then keeps them until the side
 # stream is past them), and runs beside the main stream — the LSTM and BLSTM recurrences
-# there leave most of the chip idle.  Their fp32 GEMM workgroups carry an LDS pad so that
+# there leave most of the chip idle.  Their fp32 GEMM workgroups carry LDS padding so that
 # a recurrence step workgroup (37 KB LDS) still fits next to them on every CU
 # (tools/lstm_concurrency.py: a conv-GEMM batch beside a 128-step chain costs 0.46 ms
 # instead of 0.85 with the pad, 0.61 without).  FusedAdam.step (and join_grad_stream)
@@ -72,10 +72,10 @@ def _ws(device, nbytes, slot="main"):
 _GRAD_STREAM_ON = os.environ.get("AVC_GRAD_STREAM", "1") != "0"
 _GRAD_STREAM_ACTIVE = [False]
 _GRAD_STREAMS: dict = {}
-# measured per precision (bench.py, same box, alternating): fp32 21.1 ms/step with a
-# 20 KB pad vs 21.9 without; bf16 13.1 without vs 13.3 with (its 128x128 tiles already
-# leave one GEMM workgroup per CU)
-GRAD_LDS_PAD = {"fp32": int(os.environ.get("AVC_GRAD_LDS_PAD", "20480")), "bf16": 0}
+# LDS left free per CU for the recurrence's step workgroup (37 KB) while side GEMMs run;
+# measured per precision (bench.py, same box, alternating): fp32 21.1 ms/step with room
+# kept vs 21.9 without; bf16 13.1 without vs 13.3 with (its 128x128 tiles run better 2/CU)
+GRAD_LDS_RESERVE = {"fp32": int(os.environ.get("AVC_GRAD_LDS_RESERVE", "38912")), "bf16": 0}
 
 
 def _grad_stream(dev):
@@ -114,7 +114,7 @@ def _flush_grad_queue():
     side = _grad_stream(dev)
     side.wait_stream(main)
     _GRAD_STREAM_ACTIVE[0] = True
-    _lib.call("autovc_gemm_set_lds_pad", GRAD_LDS_PAD[_PRECISION[0]])
+    _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[_PRECISION[0]])
     try:
         with torch.cuda.stream(side):
             for _, fn, inputs in items:
@@ -123,7 +123,7 @@ def _flush_grad_queue():
                         t.record_stream(side)
                 fn()
     finally:
-        _lib.call("autovc_gemm_set_lds_pad", 0)
+        _lib.call("autovc_gemm_set_lds_reserve", 0)
         _GRAD_STREAM_ACTIVE[0] = False
 
 

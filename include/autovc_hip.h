@@ -69,10 +69,10 @@ int autovc_gemm_f32(int M, int N, int K,
                     const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                     float* C, int64_t ldc, const float* bias1, const float* bias2,
                     int accumulate, int splits, float* workspace, hipStream_t stream);
-/* Extra dynamic LDS (bytes, 0 = none) per GEMM workgroup (fp32 and bf16) from now on: limits how
- * many GEMM workgroups share a CU so that a latency-bound kernel on another stream keeps a
- * slot (stream-concurrency experiments, tools/lstm_concurrency.py). */
-int autovc_gemm_set_lds_pad(int bytes);
+/* LDS bytes per CU that GEMM launches (fp32 and bf16) leave free from now on (0 = none):
+ * their workgroups are padded so that no more of them share a CU than fit beside that
+ * reserve — a latency-bound kernel on another stream keeps a slot on every CU. */
+int autovc_gemm_set_lds_reserve(int bytes);
 /* Same contract, bf16 compute (BASELINE config 3, "bf16 with fp32 master"): the fp32
  * operands are rounded to bf16 (RNE) as they are staged, v_mfma_f32_32x32x16_bf16
  * accumulates in fp32, C / bias / accumulate stay fp32 — the numerics of a torch.autocast

@@ -49,8 +49,8 @@ int main(int argc, char** argv) {
     ++ci;
     if (only_case >= 0 && ci != only_case) continue;
     printf("%-20s M=%5d N=%5d K=%5d s=%d :", c.name, c.M, c.N, c.K, c.splits);
-    for (int cfg = 2; cfg < 9; ++cfg) {
-      if (cfg == 5 || cfg == 6) continue;
+    for (int cfg = 2; cfg < 12; ++cfg) {
+      if (cfg == 5 || cfg == 7) continue;
       if (only_cfg >= 0 && cfg != only_cfg) continue;
       g_force_cfg = cfg;
       const int lda = c.at ? c.M : (c.aconv ? c.C : c.K);

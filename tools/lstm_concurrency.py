@@ -77,13 +77,13 @@ def main():
     c4 = timeit(lambda: conv4(s2))
     c4par = timeit(lambda: (chain(B, T, H, *bufs[0], s1), conv4(s2)))
     res = {}
-    for pad in (4096, 8192, 20480):
-        _lib.call("autovc_gemm_set_lds_pad", pad)
+    for pad in (38912, 49152):
+        _lib.call("autovc_gemm_set_lds_reserve", pad)
         res[pad] = (timeit(lambda: conv4(s2)), timeit(lambda: (chain(B, T, H, *bufs[0], s1), conv4(s2))))
-    _lib.call("autovc_gemm_set_lds_pad", 0)
+    _lib.call("autovc_gemm_set_lds_reserve", 0)
     print(f"4 conv GEMMs alone {c4:.3f} ms; chain || 4 conv GEMMs {c4par:.3f} ms (sum {one + c4:.3f})")
     for pad, (a_, b_) in res.items():
-        print(f"  LDS pad {pad:6d} B: 4 conv GEMMs alone {a_:.3f} ms; chain || them {b_:.3f} ms (sum {one + a_:.3f})")
+        print(f"  LDS reserve {pad:6d} B: 4 conv GEMMs alone {a_:.3f} ms; chain || them {b_:.3f} ms (sum {one + a_:.3f})")
     print(f"one chain (128 steps, H=1024, B=64): {one:.3f} ms")
     print(f"two chains, one stream:               {seq:.3f} ms")
     print(f"two chains, two streams:              {par:.3f} ms")
