@@ -505,8 +505,11 @@ constexpr unsigned kLdsPerCU = 160 * 1024;
 
 unsigned dyn_lds_for(unsigned static_bytes) {
   if (g_lds_reserve == 0 || static_bytes == 0 || static_bytes + g_lds_reserve > kLdsPerCU) return 0;
-  unsigned n = (kLdsPerCU - g_lds_reserve) / static_bytes;
+  // n workgroups of kLdsPerCU / (n + 1) + 256 bytes leave kLdsPerCU / (n + 1) - 256 free:
+  // n <= kLdsPerCU / reserve - 1, and n of the real size must fit beside the reserve
+  unsigned n = std::min((kLdsPerCU - g_lds_reserve) / static_bytes, kLdsPerCU / (g_lds_reserve + 256) - 1);
   if (n > 8) n = 8;
+  if (n == 0) return 0;
   const unsigned per = kLdsPerCU / (n + 1) + 256;   // n + 1 no longer fit
   return per > static_bytes ? per - static_bytes : 0;
 }
