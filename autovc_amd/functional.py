@@ -102,9 +102,10 @@ def _grad_launch(dev, use, fn, *inputs):
     _GRAD_QUEUE.append((dev, fn, inputs))
 
 
-def _flush_grad_queue():
+def _flush_grad_queue(beside_recurrence=True):
     """Issue every queued gradient launch on the side stream, ordered after all main-stream
-    work issued so far (their inputs), inputs marked as in use by the side stream."""
+    work issued so far (their inputs), inputs marked as in use by the side stream.  The
+    LDS reserve only pays beside a recurrence; the final flush (join) runs unpadded."""
     if not _GRAD_QUEUE:
         return
     items = list(_GRAD_QUEUE)
@@ -114,7 +115,7 @@ def _flush_grad_queue():
     side = _grad_stream(dev)
     side.wait_stream(main)
     _GRAD_STREAM_ACTIVE[0] = True
-    _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[_PRECISION[0]])
+    _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[_PRECISION[0]] if beside_recurrence else 0)
     try:
         with torch.cuda.stream(side):
             for _, fn, inputs in items:
@@ -130,7 +131,7 @@ def _flush_grad_queue():
 def join_grad_stream(dev=None):
     """Release queued gradient work and make the current stream wait for the gradient
     stream (before anything reads the gradients)."""
-    _flush_grad_queue()
+    _flush_grad_queue(beside_recurrence=False)
     if not _GRAD_STREAMS:
         return
     dev = dev or torch.device("cuda", torch.cuda.current_device())
