@@ -69,3 +69,28 @@ def test_optimizer_state_dict_roundtrip(cuda):
     s2.g_optimizer.load_state_dict(sd)
     for f1, f2 in zip(s.g_optimizer._flat, s2.g_optimizer._flat):
         assert torch.equal(f1["m"], f2["m"]) and torch.equal(f1["v"], f2["v"]) and f1["step"] == f2["step"]
+
+
+def test_grad_side_stream_bit_identical(cuda):
+    """Weight gradients on the side stream (released beside the recurrences) are the same
+    kernels in the same per-slice order: one Solver step with and without it gives
+    bit-identical parameters."""
+    import bench
+    from autovc_amd import functional as AF
+    out = []
+    prev = AF._GRAD_STREAM_ON
+    try:
+        for on in (True, False):
+            AF._GRAD_STREAM_ON = on
+            torch.manual_seed(0)
+            solver = bench.make_solver(cuda, 8)
+            solver.G.train()
+            x, e = bench.synthetic_batch(8, 128, cuda, 99)
+            for _ in range(2):
+                solver.train_step(x, e)
+            torch.cuda.synchronize()
+            out.append([f.clone() for f in solver.g_optimizer.flat_params()])
+    finally:
+        AF._GRAD_STREAM_ON = prev
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
