@@ -61,6 +61,8 @@ sig("autovc_lstm_fwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_pt
     c_ptr, c_ptr, c_int, c_ptr)
 sig("autovc_lstm2_fwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
+sig("autovc_lstm2_fwd_timed_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.POINTER(c_f32))
 sig("autovc_lstm_fwd_timed_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64,
     c_ptr, c_ptr, c_ptr, ctypes.POINTER(c_f32))
 sig("autovc_lstm_bwd_workspace_floats", c_int, c_int, c_int)

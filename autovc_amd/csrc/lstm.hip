@@ -824,3 +824,38 @@ extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, in
   AVC_CHECK_LAUNCH("autovc_lstm_bwd_bf16");
   return avc::kOk;
 }
+
+// The product's decoder-lstm2 launch (autovc_lstm2_fwd_f32's two-layer wavefront) with every
+// launch bracketed by its dispatch events; *avg_us (host) = mean over launches 2..T-1 (both
+// layers carry a recurrent product there).  bench.py's roofline of the dominant LSTM kernel.
+extern "C" int autovc_lstm2_fwd_timed_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                                          const float* W_hh0, const float* b_ih1, const float* b_hh1,
+                                          const float* W_ih1, const float* W_hh1, float* h0, float* c0,
+                                          float* gates0, float* h1, float* c1, float* gates1, hipStream_t stream,
+                                          float* avg_us) {
+  AVC_CHECK_ARG(T > 3 && lstm_shape_ok(B, H) && H % KCH == 0 && avg_us, "autovc_lstm2_fwd_timed_f32: bad args");
+  AVC_CHECK_ARG(gx0 && W_hh0 && b_ih1 && b_hh1 && W_ih1 && W_hh1 && h0 && c0 && h1 && c1,
+                "autovc_lstm2_fwd_timed_f32: null pointer");
+  Stack2Args a{StepArgs{B, T, H, gx0, gx_ldb, gx_ldt, W_hh0, h0, (int64_t)T * H, H, c0, gates0, nullptr},
+               StepArgs{B, T, H, b_ih1, 0, 0, W_hh1, h1, (int64_t)T * H, H, c1, gates1, b_hh1}, W_ih1};
+  const dim3 grid(H / UT, (B + TB - 1) / TB, 2);
+  hipEvent_t* ev = new hipEvent_t[2 * (T + 1)];
+  for (int i = 0; i < 2 * (T + 1); ++i) AVC_HIP(hipEventCreate(&ev[i]), "autovc_lstm2_fwd_timed_f32/event");
+  for (int t = 0; t <= T; ++t)
+    hipExtLaunchKernelGGL((lstm2_fwd_step_kernel<KCH, NWV, DPF>), grid, dim3(64 * NWV), 0, stream, ev[2 * t],
+                          ev[2 * t + 1], 0, a, t);
+  AVC_CHECK_LAUNCH("autovc_lstm2_fwd_timed_f32");
+  AVC_HIP(hipStreamSynchronize(stream), "autovc_lstm2_fwd_timed_f32/sync");
+  double tot = 0.0;
+  int n = 0;
+  for (int t = 2; t < T; ++t) {
+    float ms = 0.f;
+    AVC_HIP(hipEventElapsedTime(&ms, ev[2 * t], ev[2 * t + 1]), "autovc_lstm2_fwd_timed_f32/elapsed");
+    tot += ms;
+    ++n;
+  }
+  for (int i = 0; i < 2 * (T + 1); ++i) (void)hipEventDestroy(ev[i]);
+  delete[] ev;
+  *avg_us = (float)(tot / n * 1000.0);
+  return avc::kOk;
+}

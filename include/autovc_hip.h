@@ -148,6 +148,12 @@ int autovc_lstm2_fwd_bf16(int B, int T, int H, const float* gx0, int64_t gx_ldb,
 int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
                          const float* gates, const float* c_all, const uint16_t* W_hh_T_b, float* dG,
                          uint16_t* dG_b, int reverse, int splits, float* workspace, hipStream_t stream);
+/* autovc_lstm2_fwd_f32 with every launch timed by its own dispatch events; synchronises;
+ * *avg_us (HOST pointer) = mean kernel time of launches 2..T-1 (bench.py roofline). */
+int autovc_lstm2_fwd_timed_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                               const float* W_hh0, const float* b_ih1, const float* b_hh1, const float* W_ih1,
+                               const float* W_hh1, float* h0, float* c0, float* gates0, float* h1, float* c1,
+                               float* gates1, hipStream_t stream, float* avg_us);
 /* autovc_lstm_fwd_f32 with every step launch timed by its own dispatch events;
  * synchronises; *avg_us (HOST pointer) = mean kernel time of steps 1..T-1 (bench.py). */
 int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_ldb,

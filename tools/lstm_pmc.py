@@ -1,8 +1,9 @@
 """Workload for the PMC passes of the roofline `traffic` field (not part of the product):
-the decoder lstm2 layer-0 forward recurrence (B=64, T=128, H=1024), as bench.py times it.
-  rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_f -o run --output-format csv -- python tools/lstm_pmc.py
-  rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_w -o run --output-format csv -- python tools/lstm_pmc.py
-  python tools/pmc_summarize.py gpurun_out/pmc_f gpurun_out/pmc_w > profiles/lstm_step_pmc.json"""
+`single`: one H=1024 layer's forward recurrence (B=64, T=128) on lstm_fwd_step_kernel;
+`stack`: decoder lstm2's two-layer wavefront (lstm2_fwd_step_kernel), as bench.py times it.
+  rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_f -o run --output-format csv -- python tools/lstm_pmc.py stack
+  rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_w -o run --output-format csv -- python tools/lstm_pmc.py stack
+  python tools/pmc_summarize.py gpurun_out/pmc_f gpurun_out/pmc_w stack > profiles/lstm2_step_pmc.json"""
 import os
 import sys
 
@@ -19,8 +20,19 @@ gx = (torch.randn(B, T, 4 * H, generator=g) * 0.5).to(dev)
 h = torch.empty(B, T, H, device=dev)
 c = torch.empty(B, T, H, device=dev)
 gates = torch.empty(B, T, 4 * H, device=dev)
+MODE = sys.argv[1] if len(sys.argv) > 1 else "single"
+if MODE == "stack":
+    W1 = (torch.rand(4 * H, H, generator=g) * 2 - 1).div_(H ** 0.5).to(dev)
+    Wi1 = (torch.rand(4 * H, H, generator=g) * 2 - 1).div_(H ** 0.5).to(dev)
+    bi, bh = (torch.rand(4 * H, generator=g) * 0.2 - 0.1).to(dev), (torch.rand(4 * H, generator=g) * 0.2 - 0.1).to(dev)
+    h1, c1, g1 = torch.empty_like(h), torch.empty_like(c), torch.empty_like(gates)
 for _ in range(2):
-    _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(), h.data_ptr(),
-              T * H, H, c.data_ptr(), gates.data_ptr(), 0, _lib.stream_ptr(dev))
+    if MODE == "stack":
+        _lib.call("autovc_lstm2_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(), bi.data_ptr(),
+                  bh.data_ptr(), Wi1.data_ptr(), W1.data_ptr(), h.data_ptr(), c.data_ptr(), gates.data_ptr(),
+                  h1.data_ptr(), c1.data_ptr(), g1.data_ptr(), _lib.stream_ptr(dev))
+    else:
+        _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(), h.data_ptr(),
+                  T * H, H, c.data_ptr(), gates.data_ptr(), 0, _lib.stream_ptr(dev))
 torch.cuda.synchronize()
 print("ok", float(h[:, -1].abs().mean()))

@@ -9,11 +9,15 @@ import os
 import sys
 
 
+MODE = sys.argv[3] if len(sys.argv) > 3 else "single"
+KERNEL = "lstm2_fwd_step_kernel" if MODE == "stack" else "lstm_fwd_step_kernel"
+
+
 def per_dispatch(d, counter):
     rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "lstm_fwd_step_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+            if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
                 rows.append((int(r.get("Dispatch_Id", 0)), float(r["Counter_Value"])))
     rows.sort()
     return [v for _, v in rows]
@@ -22,12 +26,16 @@ def per_dispatch(d, counter):
 f = per_dispatch(sys.argv[1], "FETCH_SIZE")
 w = per_dispatch(sys.argv[2], "WRITE_SIZE")
 T = 128
-keep = lambda xs: [x for i, x in enumerate(xs) if i % T != 0]  # noqa: E731
+if MODE == "stack":   # T + 1 launches per sequence; 2..T-1 carry both layers' recurrent products
+    keep = lambda xs: [x for i, x in enumerate(xs) if 2 <= i % (T + 1) <= T - 1]  # noqa: E731
+else:
+    keep = lambda xs: [x for i, x in enumerate(xs) if i % T != 0]  # noqa: E731
 fa = sum(keep(f)) / max(1, len(keep(f)))
 wa = sum(keep(w)) / max(1, len(keep(w)))
-out = {"kernel": "lstm_fwd_step_kernel (decoder lstm2, H=1024, B=64)", "launches": len(f),
+out = {"kernel": ("lstm2_fwd_step_kernel (decoder lstm2, both layers, H=1024, B=64)" if MODE == "stack"
+                  else "lstm_fwd_step_kernel (H=1024, B=64)"), "launches": len(f),
        "fetch_size_kib_raw": round(fa, 1), "write_size_kib": round(wa, 1),
        "hbm_bytes_per_launch": int(round((2 * fa + wa) * 1024)),
        "correction": "FETCH_SIZE doubled (gfx950 reports half of wide streaming reads); WRITE_SIZE as is",
-       "source": "tools/lstm_pmc.py under rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)"}
+       "source": f"tools/lstm_pmc.py {MODE} under rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)"}
 print(json.dumps(out, indent=1))
