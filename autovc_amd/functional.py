@@ -102,10 +102,24 @@ def _grad_launch(dev, use, fn, *inputs):
     _GRAD_QUEUE.append((dev, fn, inputs))
 
 
-def _flush_grad_queue(beside_recurrence=True):
-    """Issue every queued gradient launch on the side stream, ordered after all main-stream
-    work issued so far (their inputs), inputs marked as in use by the side stream.  The
-    LDS reserve only pays beside a recurrence; the final flush (join) runs unpadded."""
+def _grad_mark(dev):
+    """Event on the main stream marking that every queued gradient launch's inputs exist;
+    taken just before a recurrence is enqueued, and handed to _flush_grad_queue after it,
+    so that the host launches the chain first (the side launches are Python-paced: issued
+    first they left the main stream idle for up to 1.3 ms) while the side stream still only
+    waits for the work before the chain."""
+    if not _GRAD_QUEUE:
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return ev
+
+
+def _flush_grad_queue(beside_recurrence=True, after=None):
+    """Issue every queued gradient launch on the side stream, ordered after `after` (an
+    event from _grad_mark) or else after all main-stream work issued so far (their
+    inputs), inputs marked as in use by the side stream.  The LDS reserve only pays beside
+    a recurrence; the final flush (join) runs unpadded."""
     if not _GRAD_QUEUE:
         return
     items = list(_GRAD_QUEUE)
@@ -113,7 +127,10 @@ def _flush_grad_queue(beside_recurrence=True):
     dev = items[0][0]
     main = torch.cuda.current_stream(dev)
     side = _grad_stream(dev)
-    side.wait_stream(main)
+    if after is not None:
+        side.wait_event(after)
+    else:
+        side.wait_stream(main)
     _GRAD_STREAM_ACTIVE[0] = True
     _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[_PRECISION[0]] if beside_recurrence else 0)
     try:
@@ -522,7 +539,7 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     splits = 4 if (4 * H) % 256 == 0 else 1
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-    _flush_grad_queue()   # queued weight gradients run beside this latency-bound recurrence
+    mark = _grad_mark(dev)   # queued weight gradients run beside this latency-bound recurrence
     if _bf16_rec(H):
         dGb = torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16)
         WTb = _bf(WT)
@@ -531,6 +548,7 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     else:
         _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
                   WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
+    _flush_grad_queue(after=mark)
     M = B * T
     dx = dWih = dWhh = dbih = dbhh = None
     if needs[1]:
@@ -641,9 +659,10 @@ class BLSTMLayerFn(torch.autograd.Function):
         M = B * T
         dev = x.device
         dG = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32)
-        _flush_grad_queue()   # queued weight gradients run beside this latency-bound recurrence
+        mark = _grad_mark(dev)   # queued weight gradients run beside this latency-bound recurrence
         _lib.call("autovc_blstm_bwd_f32", B, T, H, 2, dh.data_ptr(), gates.data_ptr(), c.data_ptr(),
                   Whh_f.data_ptr(), Whh_b.data_ptr(), dG.data_ptr(), _s())
+        _flush_grad_queue(after=mark)
         grads = [None] * 10
         dG2 = dG.view(M, 2 * G)
         for d, (iW, iH, iBi, iBh) in enumerate(((1, 2, 3, 4), (5, 6, 7, 8))):
