@@ -97,7 +97,8 @@ def test_bf16_training_loss_tracks_fp32(cuda):
     assert float(curves["bf16"][-1]) < float(curves["bf16"][0])   # it trains
 
 
-@pytest.mark.parametrize("B,T,I,H,stacked", [(64, 16, 320, 512, False), (9, 12, 512, 1024, False), (9, 12, 256, 512, True), (9, 12, 512, 1024, True)])
+@pytest.mark.parametrize("B,T,I,H,stacked", [(64, 16, 320, 512, False), (9, 12, 512, 1024, False), (9, 12, 256, 512, True),
+                                               (9, 12, 512, 1024, True), (5, 1, 64, 128, False), (3, 2, 64, 128, True)])
 def test_lstm_bf16_recurrence(cuda, B, T, I, H, stacked):
     """bf16 recurrences (bf16 copies of h / W / dG in the recurrent products, fp32 cell
     math): within bf16 rounding of the fp32 oracle, and genuinely different from fp32."""

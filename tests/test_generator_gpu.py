@@ -136,7 +136,7 @@ def test_lstm_layer_fwd_bwd(cuda, B, T, I, H):
         assert rel(a.grad, b.grad) < 1e-4
 
 
-@pytest.mark.parametrize("B,T,I,H", [(64, 16, 512, 1024), (3, 9, 320, 512)])
+@pytest.mark.parametrize("B,T,I,H", [(64, 16, 512, 1024), (3, 9, 320, 512), (2, 1, 64, 128), (33, 3, 64, 256)])
 def test_lstm2_stack_fwd_bwd(cuda, B, T, I, H):
     """Two stacked layers as one wavefront (autovc_lstm2_fwd_f32) vs two oracle layers."""
     from autovc_amd import functional as AF
