@@ -536,7 +536,12 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     dev = x.device
     WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
     _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
-    splits = 4 if (4 * H) % 256 == 0 else 1
+    # split-K of the recurrent product (same box, alternating): fp32 4 ways at H=1024 (256
+    # workgroups; 8 ways: +0.1 ms/step), 8 ways at H=512 (fills the chip: -0.15 ms); bf16
+    # 8 ways everywhere (half the bytes per workgroup: -0.15 ms).  AVC_LSTM_SPLITS overrides.
+    splits = int(os.environ.get("AVC_LSTM_SPLITS", "0")) or (8 if (H <= 512 or _bf16_rec(H)) else 4)
+    if (4 * H) % (64 * splits):
+        splits = 1
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
     mark = _grad_mark(dev)   # queued weight gradients run beside this latency-bound recurrence
