@@ -42,6 +42,11 @@ sig("autovc_stft_mel_f32", c_ptr, c_ptr, c_ptr, c_int, c_i64, c_ptr, c_ptr, c_pt
     c_int, c_int, c_ptr, c_ptr)
 sig("autovc_gemm_workspace_floats", c_int, c_int, c_int)
 sig("autovc_gemm_set_lds_reserve", c_int)
+sig("autovc_gemm_batched_f32", c_int, c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_int, c_ptr, c_i64, c_i64, c_int,
+    c_ptr, c_i64, c_i64, c_int, c_ptr)
+sig("autovc_wino5_weights_f32", c_int, c_int, c_ptr, c_int, c_ptr, c_ptr)
+sig("autovc_wino5_input_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr)
+sig("autovc_wino5_output_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_i64, c_ptr)
 sig("autovc_gemm_f32", c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,

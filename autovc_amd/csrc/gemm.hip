@@ -40,6 +40,12 @@ struct Opnd {
   int conv_T, conv_C, tap0;  // conv_T == 0: plain matrix
 };
 
+// Batched launch (c != 0): blockIdx.z is the batch index, the operands and C of batch z
+// start z * (a, b, c) floats further (no split-K then).
+struct Batch {
+  int64_t a, b, c;
+};
+
 // One operand tile (ROWS x BK) of a stage: staging map, LDS image and fragment reads.
 //   RK: LDS [ROWS][BK+4], staged as float4 along k, fragments read with ds_read_b128.
 //   CK: LDS [BK][ROWS+4], staged as float4 along rows (coalesced), fragments ds_read_b32.
@@ -217,7 +223,7 @@ template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool PIP
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
-    int k_per_split, float* __restrict__ slab) {
+    int k_per_split, float* __restrict__ slab, Batch bat) {
   constexpr int NWN = BN / WN;
   constexpr int NT = 64 * (BM / WM) * NWN;
   constexpr int TI = WM / 32, TJ = WN / 32;
@@ -235,8 +241,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
   const int xcd = L % 8, slot = L / 8, qq = nwg / 8, rr = nwg % 8;
   const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
   const int64_t m0 = (int64_t)(logical / nx) * BM, n0 = (int64_t)(logical % nx) * BN;
-  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
-  const int64_t kend = min((int64_t)K, kbeg + k_per_split);
+  if (bat.c) {
+    A.p += (int64_t)blockIdx.z * bat.a;
+    B.p += (int64_t)blockIdx.z * bat.b;
+    C += (int64_t)blockIdx.z * bat.c;
+  }
+  const int64_t kbeg = bat.c ? 0 : (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = bat.c ? (int64_t)K : min((int64_t)K, kbeg + k_per_split);
   const int nk = (int)((kend - kbeg + BK - 1) / BK);
 
   f32x16 acc[TI][TJ];
@@ -353,7 +364,7 @@ template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
-    int k_per_split, float* __restrict__ slab) {
+    int k_per_split, float* __restrict__ slab, Batch bat) {
   constexpr int NWN = BN / WN;
   constexpr int NT = 64 * (BM / WM) * NWN;
   constexpr int TI = WM / 32, TJ = WN / 32;
@@ -369,8 +380,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   const int xcd = L % 8, slot = L / 8, qq = nwg / 8, rr = nwg % 8;
   const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
   const int64_t m0 = (int64_t)(logical / nx) * BM, n0 = (int64_t)(logical % nx) * BN;
-  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
-  const int64_t kend = min((int64_t)K, kbeg + k_per_split);
+  if (bat.c) {
+    A.p += (int64_t)blockIdx.z * bat.a;
+    B.p += (int64_t)blockIdx.z * bat.b;
+    C += (int64_t)blockIdx.z * bat.c;
+  }
+  const int64_t kbeg = bat.c ? 0 : (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = bat.c ? (int64_t)K : min((int64_t)K, kbeg + k_per_split);
   const int nk = (int)((kend - kbeg + BK - 1) / BK);
 
   f32x16 acc[TI][TJ];
@@ -501,6 +517,7 @@ int g_force_cfg = AVC_GEMM_FORCE_CFG;  // tools/gemm_bench.hip overrides this
 // stream (autovc_gemm_set_lds_reserve): each workgroup is padded with unused dynamic LDS
 // so that the largest count that still fits in 160 KiB - reserve is also the most that fit.
 unsigned g_lds_reserve = 0;
+Batch g_batch = {0, 0, 0};   // set by gemm_impl for every launch (batched calls only non-zero)
 constexpr unsigned kLdsPerCU = 160 * 1024;
 
 unsigned dyn_lds_for(unsigned static_bytes) {
@@ -539,7 +556,7 @@ void launch_layouts(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, 
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
 #define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE>), grid, dim3(NT), \
                                          dyn_lds_for(f32_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, K, \
-                                         oa, ob, C, ldc, b1, b2, acc, kps, slab)
+                                         oa, ob, C, ldc, b1, b2, acc, kps, slab, g_batch)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
   else if (a_trans && !b_trans) AVC_L(false, true);
@@ -581,7 +598,7 @@ void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, in
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
 #define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), \
                                          dyn_lds_for(2u * 2u * (BM + BN) * (BK + 8)), st, M, N, \
-                                         K, oa, ob, C, ldc, b1, b2, acc, kps, slab)
+                                         K, oa, ob, C, ldc, b1, b2, acc, kps, slab, g_batch)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
   else if (a_trans && !b_trans) AVC_L(false, true);
@@ -606,7 +623,7 @@ extern "C" int64_t autovc_gemm_workspace_floats(int M, int N, int splits) {
   return splits > 1 ? (int64_t)splits * M * N : 0;
 }
 
-static int gemm_impl(bool bf16, int M, int N, int K,
+static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c_bs, int M, int N, int K,
                                const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
                                const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                float* C, int64_t ldc, const float* bias1, const float* bias2,
@@ -629,7 +646,12 @@ static int gemm_impl(bool bf16, int M, int N, int K,
   AVC_CHECK_ARG(4 * (a_ext + 2 * lda) < (int64_t)kOOB && 4 * (b_ext + 2 * ldb) < (int64_t)kOOB,
                 "autovc_gemm: operand extents must stay below 2 GiB");
   if (splits < 1) splits = 1;
-  const GemmShape cfg = bf16 ? pick_config_bf16(M, N, splits) : pick_config(M, N, K, splits);
+  AVC_CHECK_ARG(batch >= 1 && (batch == 1 || splits == 1), "autovc_gemm: batched calls cannot split K");
+  GemmShape cfg = bf16 ? pick_config_bf16(M, N, batch > 1 ? batch : splits) : pick_config(M, N, K, splits);
+  if (batch > 1 && !bf16) {   // batched: tile count x batch decides between 128x128 and 64x64
+    const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch;
+    cfg = t128 >= 512 ? kCfg[2] : kCfg[8];
+  }
   const int BKc = cfg.bk;
   int64_t kps = ((int64_t)K + splits - 1) / splits;
   kps = ((kps + BKc - 1) / BKc) * BKc;
@@ -639,7 +661,8 @@ static int gemm_impl(bool bf16, int M, int N, int K,
   Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0};
   Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0};
   float* slab = splits > 1 ? workspace : nullptr;
-  const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, splits);
+  const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, batch > 1 ? batch : splits);
+  g_batch = batch > 1 ? Batch{a_bs, b_bs, c_bs} : Batch{0, 0, 0};
   if (bf16)
     launch_gemm_bf16(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate,
                      (int)kps, slab);
@@ -662,8 +685,8 @@ extern "C" int autovc_gemm_f32(int M, int N, int K,
                                const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                float* C, int64_t ldc, const float* bias1, const float* bias2,
                                int accumulate, int splits, float* workspace, hipStream_t stream) {
-  return gemm_impl(false, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T, b_conv_C,
-                   b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
+  return gemm_impl(false, 1, 0, 0, 0, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T,
+                   b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
 }
 
 extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
@@ -671,12 +694,28 @@ extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
                                     const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                     float* C, int64_t ldc, const float* bias1, const float* bias2,
                                     int accumulate, int splits, float* workspace, hipStream_t stream) {
-  return gemm_impl(true, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T, b_conv_C,
-                   b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
+  return gemm_impl(true, 1, 0, 0, 0, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T,
+                   b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
 }
 
 extern "C" int autovc_gemm_set_lds_reserve(int bytes) {
   AVC_CHECK_ARG(bytes >= 0 && bytes <= 96 * 1024, "autovc_gemm_set_lds_reserve: 0 <= bytes <= 96 KiB");
   g_lds_reserve = (unsigned)bytes;
   return avc::kOk;
+}
+
+// batch independent GEMMs C_z = A_z B_z (z < batch) in one launch; operand / output z starts
+// z * (a_bstride, b_bstride, c_bstride) floats after the first (Winograd conv: 8 GEMMs)
+extern "C" int autovc_gemm_batched_f32(int batch, int M, int N, int K, const float* A, int64_t lda,
+                                       int64_t a_bstride, int a_trans, const float* B, int64_t ldb,
+                                       int64_t b_bstride, int b_trans, float* C, int64_t ldc, int64_t c_bstride,
+                                       int bf16, hipStream_t stream) {
+  AVC_CHECK_ARG(batch >= 1 && batch <= 65535 && (batch == 1 || c_bstride > 0),
+                "autovc_gemm_batched_f32: bad batch / strides");
+  AVC_CHECK_ARG(a_bstride % 4 == 0 && b_bstride % 4 == 0 && c_bstride >= 0,
+                "autovc_gemm_batched_f32: operand batch strides must be multiples of 4");
+  AVC_CHECK_ARG(4 * ((int64_t)batch * std::max(a_bstride, b_bstride)) < (int64_t)kOOB,
+                "autovc_gemm_batched_f32: batched operands must stay below 2 GiB");
+  return gemm_impl(bf16 != 0, batch, a_bstride, b_bstride, c_bstride, M, N, K, A, lda, a_trans, 0, 0, 0, B, ldb,
+                   b_trans, 0, 0, 0, C, ldc, nullptr, nullptr, 0, 1, nullptr, stream);
 }

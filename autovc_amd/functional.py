@@ -255,10 +255,43 @@ def _padded_weight(W, Cop, Cip):
     return Wp
 
 
+_WINOGRAD = os.environ.get("AVC_WINOGRAD", "1") != "0"
+
+
+def _wino_conv(x, Wp, bias, T, flip):
+    """Winograd F(4,5) conv (csrc/winograd.hip): flip=0 -> conv(x, W) + bias (B,T,Cop);
+    flip=1 -> the input-gradient correlation of x = dy (B,T,Cop) with W: (B,T,Cip)."""
+    B, _, Cin = x.shape
+    Cop, Cip, _ = Wp.shape
+    Cout = Cip if flip else Cop
+    nt = B * T // 4
+    dev = x.device
+    Wt = torch.empty((8, Cout, Cin), device=dev, dtype=torch.float32)
+    Xt = torch.empty((8, nt, Cin), device=dev, dtype=torch.float32)
+    Yt = torch.empty((8, nt, Cout), device=dev, dtype=torch.float32)
+    _lib.call("autovc_wino5_weights_f32", Cop, Cip, Wp.data_ptr(), int(flip), Wt.data_ptr(), _s())
+    _lib.call("autovc_wino5_input_f32", B, T, Cin, x.data_ptr(), x.stride(1), Xt.data_ptr(), _s())
+    _lib.call("autovc_gemm_batched_f32", 8, nt, Cout, Cin, Xt.data_ptr(), Cin, nt * Cin, 0, Wt.data_ptr(), Cin,
+              Cout * Cin, 0, Yt.data_ptr(), Cout, nt * Cout, 0, _s())
+    y = torch.empty((B, T, Cout), device=dev, dtype=torch.float32)
+    _lib.call("autovc_wino5_output_f32", B, T, Cout, Yt.data_ptr(), _p(bias), y.data_ptr(), Cout, _s())
+    return y
+
+
+def _wino_ok(T, *channels):
+    # fp32 only: rounding the TRANSFORMED operands to bf16 (coefficients up to 5.25 and 8)
+    # measured 1.6e-2 relative error vs 2e-5 for bf16 operands of the plain conv, so under
+    # precision("bf16") the conv stays the bf16 im2col GEMM (exact-operand semantics).
+    return _WINOGRAD and _PRECISION[0] == "fp32" and T % 4 == 0 and all(c % 4 == 0 for c in channels)
+
+
 def _conv_fwd(x, Wp, bp, T):
-    """y (B,T,Cop) = conv1d_k5p2(x (B,T,Cip)) + b as one implicit-im2col GEMM."""
+    """y (B,T,Cop) = conv1d_k5p2(x (B,T,Cip)) + b: Winograd F(4,5) (8 batched GEMMs) when T
+    is a multiple of 4, else one implicit-im2col GEMM."""
     B, _, Cip = x.shape
     Cop = Wp.shape[0]
+    if _wino_ok(T, Cip, Cop) and x.is_contiguous():
+        return _wino_conv(x, Wp, bp, T, 0)
     Wf = torch.empty((Cop, KS * Cip), device=x.device, dtype=torch.float32)
     _lib.call("autovc_conv_pack_f32", Cop, Cip, KS, Wp.data_ptr(), Wf.data_ptr(), 0, _s())
     y = torch.empty((B, T, Cop), device=x.device, dtype=torch.float32)
@@ -292,10 +325,13 @@ def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None):
         _grad_launch(dev, go.acc, dw, dy, x)
         dW = go.result()
     if need_x:
-        Wd = torch.empty((KS * Cop, Cip), device=dev, dtype=torch.float32)
-        _lib.call("autovc_conv_pack_f32", Cop, Cip, KS, Wp.data_ptr(), 0, Wd.data_ptr(), _s())
-        dx = torch.empty((B, T, Cip), device=dev, dtype=torch.float32)
-        gemm(M, Cip, KS * Cop, dy, Cop, 0, Wd, Cip, 1, dx, Cip, a_conv=(T, Cop, -PAD))
+        if _wino_ok(T, Cip, Cop) and dy.is_contiguous():
+            dx = _wino_conv(dy, Wp, None, T, 1)
+        else:
+            Wd = torch.empty((KS * Cop, Cip), device=dev, dtype=torch.float32)
+            _lib.call("autovc_conv_pack_f32", Cop, Cip, KS, Wp.data_ptr(), 0, Wd.data_ptr(), _s())
+            dx = torch.empty((B, T, Cip), device=dev, dtype=torch.float32)
+            gemm(M, Cip, KS * Cop, dy, Cop, 0, Wd, Cip, 1, dx, Cip, a_conv=(T, Cop, -PAD))
     return dx, dW, db
 
 
@@ -540,8 +576,10 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     # workgroups; 8 ways: +0.1 ms/step), 8 ways at H=512 (fills the chip: -0.15 ms); bf16
     # 8 ways everywhere (half the bytes per workgroup: -0.15 ms).  AVC_LSTM_SPLITS overrides.
     splits = int(os.environ.get("AVC_LSTM_SPLITS", "0")) or (8 if (H <= 512 or _bf16_rec(H)) else 4)
-    if (4 * H) % (64 * splits):
-        splits = 1
+    # the recurrent K (4H fp32 floats, 2H bf16 pairs) must cut into multiples of 64 per split
+    kdim = 2 * H if _bf16_rec(H) else 4 * H
+    while splits > 1 and kdim % (64 * splits):
+        splits //= 2
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
     mark = _grad_mark(dev)   # queued weight gradients run beside this latency-bound recurrence

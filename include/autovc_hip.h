@@ -83,6 +83,24 @@ int autovc_gemm_bf16_f32(int M, int N, int K,
                          float* C, int64_t ldc, const float* bias1, const float* bias2,
                          int accumulate, int splits, float* workspace, hipStream_t stream);
 
+/* batch independent GEMMs C_z = A_z B_z (same layouts as autovc_gemm_f32, plain operands,
+ * no bias/accumulate/split-K) in one launch; A_z / B_z / C_z start z * (a_bstride,
+ * b_bstride, c_bstride) floats after the first.  bf16 != 0: bf16 MFMA operands. */
+int autovc_gemm_batched_f32(int batch, int M, int N, int K, const float* A, int64_t lda, int64_t a_bstride,
+                            int a_trans, const float* B, int64_t ldb, int64_t b_bstride, int b_trans, float* C,
+                            int64_t ldc, int64_t c_bstride, int bf16, hipStream_t stream);
+
+/* ---------------------------------------------------------------- Winograd F(4,5) conv
+ * ConvNorm (Conv1d k=5, pad=2, model_vc_mel.py:20-38) as 8 batched GEMMs over 4-frame
+ * tiles (0.4 of the im2col multiply-adds).  weights: W (Co,Ci,5) -> out (8,Co,Ci) (flip=0)
+ * or (8,Ci,Co) with the kernel reversed (flip=1: the input-gradient correlation).  input:
+ * x (B,T,C) rows of ldx -> (8, B*T/4, C), zero outside each sequence.  output: (8,
+ * B*T/4, C) -> y (B,T,C) rows of ldy, + bias (nullable).  T and C multiples of 4. */
+int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip, float* out, hipStream_t stream);
+int autovc_wino5_input_f32(int B, int T, int C, const float* x, int64_t ldx, float* out, hipStream_t stream);
+int autovc_wino5_output_f32(int B, int T, int C, const float* Yt, const float* bias, float* y, int64_t ldy,
+                            hipStream_t stream);
+
 /* ---------------------------------------------------------------- BatchNorm1d + act
  * Replaces nn.BatchNorm1d (train/eval) + F.relu / torch.tanh / identity after each
  * ConvNorm (model_vc_mel.py:57,69,100,115,140,151,160,165,167).  y, z are (M=B*T, C)

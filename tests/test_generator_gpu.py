@@ -72,6 +72,27 @@ def test_conv_implicit_im2col_fwd_bwd(cuda):
     assert rel(xd.grad, x.grad) < 1e-5 and rel(Wd.grad, W.grad) < 1e-5 and rel(bd.grad, b.grad) < 1e-5
 
 
+@pytest.mark.parametrize("wino", [True, False])
+@pytest.mark.parametrize("B,T,Ci,Co", [(2, 4, 8, 12), (3, 8, 80, 512), (2, 128, 512, 512), (4, 42, 64, 32)])
+def test_conv_winograd_and_im2col(cuda, monkeypatch, wino, B, T, Ci, Co):
+    """ConvNorm fwd + input gradient through Winograd F(4,5) (T % 4 == 0) and through the
+    im2col GEMM (AVC_WINOGRAD=0, or T = 42), both against the fp64 conv: 1e-5 relative."""
+    from autovc_amd import functional as AF
+    monkeypatch.setattr(AF, "_WINOGRAD", wino)
+    g = torch.Generator().manual_seed(B * T + Ci)
+    x = torch.randn(B, T, Ci, generator=g, dtype=torch.float64, requires_grad=True)
+    W = (torch.randn(Co, Ci, 5, generator=g, dtype=torch.float64) / (5 * Ci) ** 0.5).requires_grad_()
+    b = torch.randn(Co, generator=g, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.conv1d(x.transpose(1, 2), W, b, padding=2).transpose(1, 2)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(gy)
+    xd, Wd, bd = (t.detach().float().to(cuda).requires_grad_() for t in (x, W, b))
+    yd = AF.conv_only(xd, Wd, bd)
+    yd.backward(gy.float().to(cuda))
+    assert rel(yd, y) < 1e-5 and rel(xd.grad, x.grad) < 1e-5
+    assert rel(Wd.grad, W.grad) < 1e-5 and rel(bd.grad, b.grad) < 1e-5
+
+
 def test_conv_padded_channels_513(cuda):
     """Channel counts % 4 != 0 (the 513/769-bin STFT generator) go through zero padding."""
     from autovc_amd import functional as AF
