@@ -47,6 +47,8 @@ sig("autovc_gemm_batched_f32", c_int, c_int, c_int, c_int, c_ptr, c_i64, c_i64, 
 sig("autovc_wino5_weights_f32", c_int, c_int, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_wino5_input_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr)
 sig("autovc_wino5_output_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_i64, c_ptr)
+sig("autovc_wino5_dy_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr)
+sig("autovc_wino5_wgrad_f32", c_int, c_int, c_ptr, c_ptr, c_int, c_ptr)
 sig("autovc_gemm_f32", c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,

@@ -112,6 +112,47 @@ __global__ __launch_bounds__(64) void wino_output_kernel(int T, int C, const flo
   }
 }
 
+// Weight gradient (the transpose of the forward algorithm): with
+//   dY~[i][tile][c] = sum_o AT[o][i] dy[4q+o][c]   and   X~ the forward's input transform,
+//   dW[co][ci][k]  = sum_i G[i][k] sum_tile dY~[i][tile][co] X~[i][tile][ci]
+// = 8 GEMMs over K = B*T/4 tiles (one batched launch) and a G^T combine.
+__global__ __launch_bounds__(64) void wino_dy_kernel(int T, int C, const float* __restrict__ dy, int64_t lddy,
+                                                     float* __restrict__ out, int64_t ntiles) {
+  const int c = 4 * (blockIdx.x * 64 + threadIdx.x);
+  if (c >= C) return;
+  const int64_t tile = blockIdx.y;
+  const int64_t b = tile / (T / 4);
+  const int q = (int)(tile % (T / 4));
+  f32x4 d[4];
+#pragma unroll
+  for (int o = 0; o < 4; ++o) d[o] = *reinterpret_cast<const f32x4*>(dy + (b * T + 4 * q + o) * lddy + c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+      if (kAT[o][i] != 0.f) v += kAT[o][i] * d[o];
+    *reinterpret_cast<f32x4*>(out + ((int64_t)i * ntiles + tile) * C + c) = v;
+  }
+}
+
+// dW (Co, Ci, 5) (=|+=) G^T M,  M (8, Co, Ci); the combine runs in double, rounds once
+__global__ void wino_wgrad_kernel(int64_t n, const float* __restrict__ Mt, float* __restrict__ dW, int acc) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    double m[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = Mt[(int64_t)i * n + e];
+    float* w = dW + e * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      double v = 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v += kG[i][k] * m[i];
+      w[k] = acc ? w[k] + (float)v : (float)v;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip, float* out, hipStream_t stream) {
@@ -145,5 +186,27 @@ extern "C" int autovc_wino5_output_f32(int B, int T, int C, const float* Yt, con
   hipLaunchKernelGGL(wino_output_kernel, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C, Yt,
                      bias, y, ldy, ntiles);
   AVC_CHECK_LAUNCH("autovc_wino5_output_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_wino5_dy_f32(int B, int T, int C, const float* dy, int64_t lddy, float* out,
+                                   hipStream_t stream) {
+  AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && lddy % 4 == 0 && dy && out,
+                "autovc_wino5_dy_f32: bad args (T and C multiples of 4)");
+  AVC_CHECK_ARG(AVC_ALIGNED16(dy) && AVC_ALIGNED16(out), "autovc_wino5_dy_f32: alignment");
+  const int64_t ntiles = (int64_t)B * T / 4;
+  hipLaunchKernelGGL(wino_dy_kernel, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C, dy, lddy,
+                     out, ntiles);
+  AVC_CHECK_LAUNCH("autovc_wino5_dy_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_wino5_wgrad_f32(int Co, int Ci, const float* Mt, float* dW, int accumulate,
+                                      hipStream_t stream) {
+  AVC_CHECK_ARG(Co > 0 && Ci > 0 && Mt && dW, "autovc_wino5_wgrad_f32: bad args");
+  const int64_t n = (int64_t)Co * Ci;
+  hipLaunchKernelGGL(wino_wgrad_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                     stream, n, Mt, dW, accumulate);
+  AVC_CHECK_LAUNCH("autovc_wino5_wgrad_f32");
   return avc::kOk;
 }

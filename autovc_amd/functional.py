@@ -88,6 +88,7 @@ def _grad_stream(dev):
 
 
 _GRAD_QUEUE: list = []
+_GRAD_PENDING: set = set()   # device indices whose side stream has work not yet joined
 
 
 def _grad_launch(dev, use, fn, *inputs):
@@ -99,7 +100,7 @@ def _grad_launch(dev, use, fn, *inputs):
     if not (use and _GRAD_STREAM_ON):
         fn()
         return
-    _GRAD_QUEUE.append((dev, fn, inputs))
+    _GRAD_QUEUE.append((dev, fn, inputs, _PRECISION[0]))   # run later under the same precision
 
 
 def _grad_mark(dev):
@@ -132,15 +133,19 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
     else:
         side.wait_stream(main)
     _GRAD_STREAM_ACTIVE[0] = True
-    _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[_PRECISION[0]] if beside_recurrence else 0)
+    _GRAD_PENDING.add(side.device.index)
+    prev_prec = _PRECISION[0]
+    _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0)
     try:
         with torch.cuda.stream(side):
-            for _, fn, inputs in items:
+            for _, fn, inputs, prec in items:
                 for t in inputs:
                     if t is not None:
                         t.record_stream(side)
+                _PRECISION[0] = prec
                 fn()
     finally:
+        _PRECISION[0] = prev_prec
         _lib.call("autovc_gemm_set_lds_reserve", 0)
         _GRAD_STREAM_ACTIVE[0] = False
 
@@ -149,12 +154,16 @@ def join_grad_stream(dev=None):
     """Release queued gradient work and make the current stream wait for the gradient
     stream (before anything reads the gradients)."""
     _flush_grad_queue(beside_recurrence=False)
-    if not _GRAD_STREAMS:
+    if not _GRAD_PENDING:
         return
     dev = dev or torch.device("cuda", torch.cuda.current_device())
-    st = _GRAD_STREAMS.get(dev.index if dev.index is not None else torch.cuda.current_device())
-    if st is not None:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _GRAD_STREAMS.get(idx)
+    if st is not None and idx in _GRAD_PENDING:
+        # only a side stream with work since the last join is waited on: inside a graph
+        # capture (autovc_amd.graph) the wait must be on work of the same capture
         torch.cuda.current_stream(dev).wait_stream(st)
+        _GRAD_PENDING.discard(idx)
 
 
 _PRECISION = ["fp32"]
@@ -278,6 +287,23 @@ def _wino_conv(x, Wp, bias, T, flip):
     return y
 
 
+def _wino_wgrad(x, dy, T, dW, acc):
+    """dW (Co,Ci,5) (+)= Winograd F(4,5) weight gradient of conv(x) against dy (B,T,Co):
+    dY~ and X~ transforms, 8 GEMMs over the B*T/4 tiles (M_i = dY~_i^T X~_i), G^T combine."""
+    B, _, Cin = x.shape
+    Cout = dy.shape[2]
+    nt = B * T // 4
+    dev = x.device
+    Xt = torch.empty((8, nt, Cin), device=dev, dtype=torch.float32)
+    Dt = torch.empty((8, nt, Cout), device=dev, dtype=torch.float32)
+    Mt = torch.empty((8, Cout, Cin), device=dev, dtype=torch.float32)
+    _lib.call("autovc_wino5_input_f32", B, T, Cin, x.data_ptr(), x.stride(1), Xt.data_ptr(), _s())
+    _lib.call("autovc_wino5_dy_f32", B, T, Cout, dy.data_ptr(), dy.stride(1), Dt.data_ptr(), _s())
+    _lib.call("autovc_gemm_batched_f32", 8, Cout, Cin, nt, Dt.data_ptr(), Cout, nt * Cout, 1, Xt.data_ptr(), Cin,
+              nt * Cin, 1, Mt.data_ptr(), Cin, Cout * Cin, 0, _s())
+    _lib.call("autovc_wino5_wgrad_f32", Cout, Cin, Mt.data_ptr(), dW.data_ptr(), int(acc), _s())
+
+
 def _wino_ok(T, *channels):
     # fp32 only: rounding the TRANSFORMED operands to bf16 (coefficients up to 5.25 and 8)
     # measured 1.6e-2 relative error vs 2e-5 for bf16 operands of the plain conv, so under
@@ -317,6 +343,9 @@ def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None):
         go = _GradOut(None if padded else W, (Cop, Cip, KS), dev)
 
         def dw(go=go):
+            if _wino_ok(T, Cip, Cop) and dy.is_contiguous() and x.is_contiguous():
+                _wino_wgrad(x, dy, T, go.buf, go.acc)
+                return
             dWf = torch.empty((Cop, KS * Cip), device=dev, dtype=torch.float32)
             gemm(Cop, KS * Cip, M, dy, Cop, 1, x, Cip, 1, dWf, KS * Cip, b_conv=(T, Cip, -PAD),
                  splits=_splits_for(Cop, KS * Cip, M))

@@ -1,0 +1,62 @@
+"""Whole-step HIP graphs for the Generator training step (not in the reference).
+
+`Solver.train_step` is ~1,900 kernel launches per B=64 step (two Generator passes, the
+LSTM/BLSTM recurrences one launch per time step, the backward with its side-stream weight
+gradients).  Issued eagerly from Python, the host falls behind the GPU in the short-kernel
+stretches (rocprof timeline: tools/trace_gaps.py).  `StepGraphs` captures the forward +
+backward (losses, zero_grad, autograd backward, the gradient side stream's fork and join)
+once per (input shapes, precision) into a `torch.cuda.CUDAGraph` (hipGraph) and replays it;
+the data-parallel all-reduce and the FusedAdam step stay eager after the replay, so the
+optimizer's host-side step count / lr schedule and RCCL are untouched.
+
+Replays run the same kernels on the same buffers in the same order as the eager step, so
+the losses and gradients are bit-identical to eager (tests/test_solver_gpu.py).  The
+warm-up pass before the capture (lazy workspaces) would add one BatchNorm running-stat
+update: those buffers are snapshotted and restored around it.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import functional as AF
+
+
+class StepGraphs:
+    def __init__(self, fn, module):
+        self.fn = fn            # fn(*inputs) -> tuple of device tensors
+        self.module = module    # holds the BatchNorm buffers the warm-up must not advance
+        self._graphs = {}
+
+    def _capture(self, inputs):
+        dev = inputs[0].device
+        static = [t.detach().clone() for t in inputs]
+        saved = [b.detach().clone() for b in self.module.buffers()]
+        cur = torch.cuda.current_stream(dev)
+        warm = torch.cuda.Stream(dev)
+        warm.wait_stream(cur)
+        with torch.cuda.stream(warm):
+            self.fn(*static)
+        cur.wait_stream(warm)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self.fn(*static)
+        with torch.no_grad():
+            for b, s in zip(self.module.buffers(), saved):
+                b.copy_(s)
+        return graph, static, out
+
+    def run(self, key, *inputs):
+        full_key = (key,) + tuple((tuple(t.shape), t.dtype, t.device) for t in inputs)
+        entry = self._graphs.get(full_key)
+        if entry is None:
+            entry = self._capture(inputs)
+            self._graphs[full_key] = entry
+        graph, static, out = entry
+        for s, t in zip(static, inputs):
+            if s.data_ptr() != t.data_ptr():
+                s.copy_(t)
+        graph.replay()
+        return out
+
+    def reset(self):
+        self._graphs.clear()

@@ -83,6 +83,10 @@ class Solver(object):
         # matmul precision of the step: "fp32" (BASELINE config 2) or "bf16" (config 3:
         # bf16 MFMA operands, fp32 master weights / Adam / BN / losses); not in the reference
         self.precision = getattr(config, "precision", "fp32")
+        # replay the forward+backward as a captured HIP graph (autovc_amd.graph); not in the
+        # reference.  Inputs of a new shape or precision capture a new graph.
+        self.hip_graph = bool(getattr(config, "hip_graph", False))
+        self._graphs = None
 
         self.path = "chkpnt_" + self.model_type + "_" + self.run_name + ".ckpt"
         self.file_exists = os.path.exists(self.path)
@@ -141,14 +145,26 @@ class Solver(object):
         g_loss = g_loss_id + g_loss_id_psnt + self.lambda_cd * g_loss_cd
         return g_loss, g_loss_id, g_loss_id_psnt, g_loss_cd, x_identic_psnt
 
-    def train_step(self, x_real, emb_org):
-        """Losses, zero_grad, backward, Adam (solver_encoder.py:226-300).  Returns device
-        scalars (g_loss, loss_id, loss_id_psnt, loss_cd); nothing synchronises."""
+    def _forward_backward(self, x_real, emb_org):
         with AF.precision(self.precision):
             g_loss, l_id, l_psnt, l_cd, x_psnt = self.compute_losses(x_real, emb_org)
             self.reset_grad()
             g_loss.backward()
         AF.join_grad_stream()   # weight gradients (side stream) complete before they are read
+        return g_loss, l_id, l_psnt, l_cd, x_psnt
+
+    def train_step(self, x_real, emb_org):
+        """Losses, zero_grad, backward, Adam (solver_encoder.py:226-300).  Returns device
+        scalars (g_loss, loss_id, loss_id_psnt, loss_cd); nothing synchronises.  With
+        `hip_graph` the forward+backward is a graph replay (its outputs are the graph's
+        static tensors, overwritten by the next step)."""
+        if self.hip_graph:
+            if self._graphs is None:
+                from .graph import StepGraphs
+                self._graphs = StepGraphs(self._forward_backward, self.G)
+            g_loss, l_id, l_psnt, l_cd, x_psnt = self._graphs.run(self.precision, x_real, emb_org)
+        else:
+            g_loss, l_id, l_psnt, l_cd, x_psnt = self._forward_backward(x_real, emb_org)
         self._after_backward()
         self.g_optimizer.step()
         self._last_psnt = x_psnt

@@ -322,6 +322,8 @@ def main():
     ap.add_argument("--no-wavenet", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-bf16", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="issue the step eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
                     help="precision of the headline measurement (default fp32 = BASELINE config 2)")
     args = ap.parse_args()
@@ -339,6 +341,7 @@ def main():
         ddp.make_data_parallel(solver)
     solver.G.train()
     solver.precision = args.precision
+    solver.hip_graph = not args.no_graph
     x, e = synthetic_batch(B, T, dev, 1234 + 2 * rank)
 
     for _ in range(args.warmup):
@@ -415,6 +418,7 @@ def main():
             "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16", "data": "synthetic (clamped N(0.43,0.18) mels, unit-norm*0.8 emb)",
             "config": {"workload": "AutoVC Generator training step (solver_encoder.py), fwd+bwd+Adam",
                        "global_batch": B * world, "seq_len": T, "n_mels": 80, "parallelism": f"dp{world}",
+                       "hip_graph": not args.no_graph,
                        "dim_neck": 32, "dim_emb": 256, "dim_pre": 512, "freq": 32},
             "final_loss": round(last_loss, 6),
             "roofline": roof, "cpu_baseline": cpu, "bf16": bf,

@@ -100,6 +100,11 @@ int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip, float* ou
 int autovc_wino5_input_f32(int B, int T, int C, const float* x, int64_t ldx, float* out, hipStream_t stream);
 int autovc_wino5_output_f32(int B, int T, int C, const float* Yt, const float* bias, float* y, int64_t ldy,
                             hipStream_t stream);
+/* Weight gradient: dy: dy (B,T,C) rows of lddy -> dY~ (8, B*T/4, C) (the output
+ * transform's transpose); with M_i = dY~_i^T X~_i (8 batched GEMMs over the tiles),
+ * wgrad: M (8,Co,Ci) -> dW (Co,Ci,5) = G^T M, accumulate != 0 adds into dW. */
+int autovc_wino5_dy_f32(int B, int T, int C, const float* dy, int64_t lddy, float* out, hipStream_t stream);
+int autovc_wino5_wgrad_f32(int Co, int Ci, const float* Mt, float* dW, int accumulate, hipStream_t stream);
 
 /* ---------------------------------------------------------------- BatchNorm1d + act
  * Replaces nn.BatchNorm1d (train/eval) + F.relu / torch.tanh / identity after each

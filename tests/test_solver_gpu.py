@@ -94,3 +94,34 @@ def test_grad_side_stream_bit_identical(cuda):
         AF._GRAD_STREAM_ON = prev
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_hip_graph_step_bit_identical(cuda, precision):
+    """Solver(hip_graph=True) replays the captured forward+backward: three steps (the first
+    captures) give bit-identical losses, parameters and BatchNorm running stats to eager,
+    and a second input batch of the same shape is picked up by the replay."""
+    import bench
+    res = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        solver = bench.make_solver(cuda, 8)
+        solver.G.train()
+        solver.precision = precision
+        solver.hip_graph = graph
+        xa, ea = bench.synthetic_batch(8, 128, cuda, 99)
+        xb, eb = bench.synthetic_batch(8, 128, cuda, 100)
+        losses = []
+        for x, e in ((xa, ea), (xb, eb), (xa, ea)):
+            out = solver.train_step(x, e)
+            losses.append(torch.stack([o.detach().reshape(()) for o in out]).clone())
+        torch.cuda.synchronize()
+        res.append((losses, [f.clone() for f in solver.g_optimizer.flat_params()],
+                    [b.clone() for b in solver.G.buffers()]))
+    (la, pa, ba), (lb, pb, bb) = res
+    for a, b in zip(la, lb):
+        assert torch.equal(a, b)
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+    for a, b in zip(ba, bb):
+        assert torch.equal(a, b)
