@@ -40,6 +40,8 @@ sig("autovc_abi_version")
 sig("autovc_device_sync")
 sig("autovc_stft_mel_f32", c_ptr, c_ptr, c_ptr, c_int, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
     c_int, c_int, c_ptr, c_ptr)
+sig("autovc_preprocess_f64", c_ptr, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_int,
+    c_ptr, c_ptr)
 sig("autovc_gemm_workspace_floats", c_int, c_int, c_int)
 sig("autovc_gemm_set_lds_reserve", c_int)
 sig("autovc_gemm_batched_f32", c_int, c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_int, c_ptr, c_i64, c_i64, c_int,

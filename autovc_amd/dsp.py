@@ -1,10 +1,12 @@
 """Host-side DSP constants and the GPU front-end entry (STFT + mel + log/clip).
 
-Host part (numpy/scipy, as in the reference):
-  make_spect.py:30-34  butter_highpass, make_spect.py:74-76 filtfilt + dither
-  make_spect.py:51     the Slaney mel basis (librosa 0.9.1 `filters.mel`, restated)
-GPU part (HIP, libautovc_hip.so `autovc_stft_mel_f32`):
-  make_spect.py:36-48 pySTFT + :79-86 mel projection, dB, clip
+Host part (constants only): make_spect.py:30-34 butter_highpass coefficients (+ scipy's
+  lfilter_zi initial state), make_spect.py:51 the Slaney mel basis (librosa 0.9.1
+  `filters.mel`, restated).  `preprocess` is the reference's host filtfilt + dither, kept
+  for callers that hold a RandomState object.
+GPU part (HIP, libautovc_hip.so):
+  make_spect.py:74-76  filtfilt + MT19937 dither, bit-exact (`autovc_preprocess_f64`)
+  make_spect.py:36-48  pySTFT + :79-86 mel projection, dB, clip (`autovc_stft_mel_f32`)
 """
 from __future__ import annotations
 
@@ -88,6 +90,70 @@ def preprocess(x: np.ndarray, prng: np.random.RandomState) -> np.ndarray:
     return y * 0.96 + (prng.rand(y.shape[0]) - 0.5) * 1e-06
 
 
+@functools.lru_cache(maxsize=None)
+def _filter_consts():
+    """(b, a, zi) of make_spect.py:30-34 as contiguous float64 host arrays; zi is
+    scipy.signal.lfilter_zi(b, a), the state filtfilt scales by each pass's first sample."""
+    from scipy import signal
+    b, a = butter_highpass()
+    zi = signal.lfilter_zi(b, a)
+    return tuple(np.ascontiguousarray(v, dtype=np.float64) for v in (b, a, zi))
+
+
+PADLEN = 3 * (ORDER + 1)   # scipy filtfilt's default padlen for this filter
+
+
+def preprocess_gpu(wavs, seeds=None, groups=None, device="cuda"):
+    """make_spect.py:74-76 on the GPU for a batch of utterances, bit-exact with scipy/numpy.
+
+    wavs   : list of 1-D raw utterances (float32 as load_wav returns them, or float64;
+             one dtype per batch, because numpy computes the odd extension in the input's
+             precision).  Each must be longer than 18 samples (scipy's ValueError).
+    seeds  : dither RandomState seeds, one per group; None = filtfilt only (no 0.96
+             scale, no dither).
+    groups : utterances per seed, consecutive in `wavs` (a speaker's sorted files share
+             one stream, make_spect.py:68-70); default one utterance per seed.
+    Returns (wav, lens): one float64 CUDA tensor with the utterances back to back, and
+    their lengths — the input of `stft_mel_packed`.
+    """
+    import torch
+    lens = [int(np.shape(w)[0]) for w in wavs]
+    if not lens:
+        return torch.empty(0, dtype=torch.float64, device=device), []
+    short = [n for n in lens if n <= PADLEN]
+    if short:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {PADLEN}.")
+    f32 = [(w.dtype == torch.float32) if torch.is_tensor(w) else (np.asarray(w).dtype == np.float32)
+           for w in wavs]
+    if any(f32) and not all(f32):
+        raise ValueError("preprocess_gpu: mix of float32 and float64 utterances in one batch")
+    dt = torch.float32 if f32[0] else torch.float64
+    parts = [w.to(device=device, dtype=dt).reshape(-1) if torch.is_tensor(w)
+             else torch.as_tensor(np.asarray(w, dtype=np.float32 if f32[0] else np.float64)).reshape(-1)
+             for w in wavs]
+    x = torch.cat([p.to(device, non_blocking=True) for p in parts])
+    off_h = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    woff = torch.from_numpy(off_h).to(device)
+    out = torch.empty(int(off_h[-1]), dtype=torch.float64, device=x.device)
+    b, a, zi = _filter_consts()
+    n_streams, soff, sd = 0, None, None
+    if seeds is not None:
+        groups = [1] * len(seeds) if groups is None else [int(g) for g in groups]
+        if len(groups) != len(seeds) or sum(groups) != len(lens) or min(groups) < 0:
+            raise ValueError("preprocess_gpu: groups must give one utterance count per seed, summing to len(wavs)")
+        gidx = np.concatenate([[0], np.cumsum(groups)]).astype(np.int64)
+        soff = torch.from_numpy(off_h[gidx]).to(device)
+        sd_h = np.asarray(seeds, dtype=np.int64)
+        if (sd_h < 0).any() or (sd_h > 0xFFFFFFFF).any():
+            raise ValueError("Seed must be between 0 and 2**32 - 1")
+        sd = torch.from_numpy(sd_h.astype(np.uint32).view(np.int32)).to(device)
+        n_streams = len(seeds)
+    _lib.call("autovc_preprocess_f64", _lib.ptr(x), 0 if f32[0] else 1, _lib.ptr(woff), len(lens),
+              b.ctypes.data, a.ctypes.data, zi.ctypes.data, ORDER, _lib.ptr(soff), _lib.ptr(sd), n_streams,
+              _lib.ptr(out), _lib.stream_ptr(out.device))
+    return out, lens
+
+
 def n_frames(n_samples: int) -> int:
     """Frames of pySTFT for a signal of n_samples (make_spect.py:41)."""
     return (n_samples + FFT_LENGTH - (FFT_LENGTH - HOP_LENGTH)) // HOP_LENGTH
@@ -120,10 +186,24 @@ def stft_mel(wavs, mode: str = "spmel", device="cuda", n_mels: int = 80):
     if len(wavs) == 0:
         return []
     lens = [int(w.shape[0]) for w in wavs]
-    frames = [n_frames(n) for n in lens]
     parts = [torch.as_tensor(np.asarray(w, dtype=np.float64)) if not torch.is_tensor(w)
              else w.to(torch.float64) for w in wavs]
     wav = torch.cat([p.reshape(-1).to(device, non_blocking=True) for p in parts])
+    return stft_mel_packed(wav, lens, mode, n_mels)
+
+
+def stft_mel_packed(wav, lens, mode: str = "spmel", n_mels: int = 80):
+    """`stft_mel` of utterances already back to back in one float64 CUDA tensor (the
+    output of `preprocess_gpu`): no host round trip between the two front-end stages."""
+    import torch
+    if mode not in ("spmel", "stft"):
+        raise ValueError(f"unknown front-end mode {mode!r}")
+    if len(lens) == 0:
+        return []
+    if wav.dtype != torch.float64 or not wav.is_cuda or wav.numel() != sum(lens):
+        raise ValueError("stft_mel_packed: wav must be a float64 CUDA tensor of sum(lens) samples")
+    device = wav.device
+    frames = [n_frames(n) for n in lens]
     woff = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int64, device=device)
     foff_h = np.concatenate([[0], np.cumsum(frames)])
     foff = torch.tensor(foff_h, dtype=torch.int64, device=device)
@@ -136,7 +216,7 @@ def stft_mel(wavs, mode: str = "spmel", device="cuda", n_mels: int = 80):
     else:
         lo = ln = off = w = None
         m = 1
-    _lib.call("autovc_stft_mel_f32", _lib.ptr(wav), _lib.ptr(woff), _lib.ptr(foff), len(wavs),
+    _lib.call("autovc_stft_mel_f32", _lib.ptr(wav), _lib.ptr(woff), _lib.ptr(foff), len(lens),
               total, _lib.ptr(lo), _lib.ptr(ln), _lib.ptr(off), _lib.ptr(w),
               n_mels if mode == "spmel" else 0, m, _lib.ptr(out), _lib.stream_ptr(out.device))
     return list(torch.split(out, frames, dim=0))

@@ -4,9 +4,11 @@ Same constructor (config with speaker_embed, model_type, main_dir), same directo
 walk (<main_dir>/wav48_silence_trimmed/<spk>/*, files containing 'mic1' skipped), same
 per-speaker RandomState(int(spk[1:])) dither stream consumed in sorted file order, same
 outputs (spmel: (T, 80) float32; stft: (513, T) float32, the reference's on-disk layout).
-Host: wav decode (16-bit PCM at 16 kHz; librosa.load's int16/32768), Butterworth filtfilt
-and dither (make_spect.py:72-76).  GPU: one fused STFT+mel launch per speaker
-(autovc_amd.dsp.stft_mel -> autovc_stft_mel_f32).
+Host: wav decode (16-bit PCM at 16 kHz; librosa.load's int16/32768).  GPU, per speaker:
+the Butterworth filtfilt and the RandomState dither of make_spect.py:74-76 in one call
+(autovc_amd.dsp.preprocess_gpu -> autovc_preprocess_f64, bit-exact with scipy/numpy), then
+one fused STFT+mel launch on the same device buffer (dsp.stft_mel_packed ->
+autovc_stft_mel_f32).
 """
 from __future__ import annotations
 
@@ -53,17 +55,18 @@ class Spect(object):
 
     def speaker(self, wav_paths, speaker):
         """All kept files of one speaker -> {name: array} (reference layouts)."""
-        prng = np.random.RandomState(int(speaker[1:]))
         names, wavs = [], []
         for p in sorted(wav_paths):
             fname = os.path.basename(p)
             if "mic1" in fname:
                 continue
-            wavs.append(dsp.preprocess(load_wav(p, self.fs), prng))
+            wavs.append(load_wav(p, self.fs))
             names.append(fname[:fname.rfind(".")])
         if self.model_type not in ("spmel", "stft"):
             raise NotImplementedError(f"model_type {self.model_type!r}: only 'spmel' and 'stft' are on the GPU path")
-        outs = dsp.stft_mel(wavs, self.model_type, device=self.device)
+        # one RandomState(int(spk[1:])) stream over the speaker's files in sorted order
+        wav, lens = dsp.preprocess_gpu(wavs, seeds=[int(speaker[1:])], groups=[len(wavs)], device=self.device)
+        outs = dsp.stft_mel_packed(wav, lens, self.model_type)
         res = {}
         for n, o in zip(names, outs):
             a = o.cpu().numpy()

@@ -3,8 +3,9 @@ wav -> STFT+mel (make_spect.py) -> Generator conversion (conversion.py) -> WaveN
 synthesis (vocoder.py / synthesis.wavegen).
 
 Stages and where they run:
-  spectrograms  host filtfilt + dither (make_spect.py:74-76, RandomState per utterance),
-                one fused STFT+mel launch for all utterances (autovc_stft_mel_f32)
+  spectrograms  filtfilt + dither (make_spect.py:74-76, RandomState per utterance) in one
+                launch pair (autovc_preprocess_f64), then one fused STFT+mel launch for all
+                utterances on the same device buffer (autovc_stft_mel_f32)
   convert       conversion.py:40-44,90-102: pad to a multiple of `freq`, eval forward with
                 (emb_org, emb_trg), drop the padding.  Utterances with the same padded length
                 run as one batch (eval BatchNorm and the LSTMs are per-row, so a batch equals
@@ -35,8 +36,8 @@ def pad_seq(x, base=32):
 def spectrograms(wavs, mode="spmel", device="cuda", seeds=None):
     """wavs: list of float arrays at 16 kHz -> list of (T, 80|513) device tensors."""
     seeds = seeds if seeds is not None else list(range(len(wavs)))
-    pre = [dsp.preprocess(np.asarray(w, np.float64), np.random.RandomState(s)) for w, s in zip(wavs, seeds)]
-    return dsp.stft_mel(pre, mode, device=device)
+    wav, lens = dsp.preprocess_gpu([np.asarray(w, np.float64) for w in wavs], seeds=list(seeds), device=device)
+    return dsp.stft_mel_packed(wav, lens, mode)
 
 
 def _mel_project(y):

@@ -224,14 +224,46 @@ def frontend_roofline(dev, n_utt=256):
         res[mode] = {"frames": fr, "kernel_ms": round(dt * 1e3, 3), "frames_per_s": round(fr / dt, 1),
                      "bytes_per_frame": bpf, "achieved": round(fr * bpf / dt / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(fr * bpf / dt / 1e9 / HBM_PEAK_GBS, 4)}
+    # filtfilt + dither (make_spect.py:74-76) of the same batch, one RandomState per
+    # utterance: latency-bound (a sequential IIR per utterance, bit-exact with scipy), so
+    # the figure is samples/s with all utterances in flight, not a bandwidth fraction.
+    ns = int(sum(lens))
+    seeds = list(range(n_utt))
+    dsp.preprocess_gpu(wavs, seeds=seeds, device=dev)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        dsp.preprocess_gpu(wavs, seeds=seeds, device=dev)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    dt = sorted(ts)[1]
+    n_cpu = 16
+    t0 = time.perf_counter()
+    for i in range(n_cpu):
+        fe_oracle_preprocess(wavs[i], np.random.RandomState(i))
+    dcpu = time.perf_counter() - t0
+    ns_cpu = int(sum(lens[:n_cpu]))
+    res["preprocess"] = {"utterances": n_utt, "samples": ns, "wall_ms_incl_h2d": round(dt * 1e3, 3),
+                         "samples_per_s": round(ns / dt, 1), "bound": "latency (sequential IIR per utterance)",
+                         "cpu_baseline": {"value": round(ns_cpu / dcpu, 1), "unit": "samples/s", "cores": 1,
+                                          "kind": "reference",
+                                          "sample": f"scipy.signal.filtfilt + RandomState.rand on {n_cpu} "
+                                                    f"utterances ({ns_cpu} samples), the reference's own host code"}}
     return res
 
 
+def fe_oracle_preprocess(w, prng):
+    from oracle import frontend as fe
+    return fe.preprocess(w, prng)
+
+
 def e2e_bench(dev, rank, world, per_rank=8):
-    """BASELINE config 5 / SURVEY §8d C5: 64 synthetic utterances sharded 8 per GPU; host
+    """BASELINE config 5 / SURVEY §8d C5: 64 synthetic utterances sharded 8 per GPU; GPU
     filtfilt + dither -> GPU 513-bin STFT -> GeneratorSTFT conversion (eval) -> projection
     to 80 mels (conversion.py:102) -> batched WaveNet synthesis.  Random-init weights (the
-    reference checkpoints are absent).  Timed per stage with the device synchronised."""
+    reference checkpoints are absent).  The spectrogram stage includes the GPU filtfilt +
+    dither (autovc_preprocess_f64).  Timed per stage with the device synchronised."""
     import numpy as np
     from autovc_amd import pipeline, synthesis
     from autovc_amd.model_vc_stft import GeneratorSTFT

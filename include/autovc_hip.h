@@ -54,6 +54,27 @@ int autovc_stft_mel_f32(const double* wav, const int64_t* wav_off, const int64_t
                         const int* mel_woff, const float* mel_w, int n_mels, int mode,
                         float* out, hipStream_t stream);
 
+/* Replaces make_spect.py:74 (scipy.signal.filtfilt of the make_spect.py:30-34 order-5
+ * Butterworth high-pass: odd extension of 18 samples, lfilter_zi initial states, direct
+ * form II transposed) and make_spect.py:76 (y * 0.96 + (RandomState(seed).rand(n) - 0.5)
+ * * 1e-06), bit-exact with scipy / numpy, for a batch of utterances.
+ *   x          : concatenated raw utterances, float32 (x_is_f64 = 0, what load_wav
+ *                returns; the odd extension is then computed in float32 like numpy) or
+ *                float64; every utterance must be longer than 18 samples (scipy raises)
+ *   wav_off    : [n_utt+1] int64 sample offsets (device)
+ *   b, a, zi   : HOST arrays, order+1 / order+1 / order doubles (butter + lfilter_zi);
+ *                order must be 5 and a[0] == 1
+ *   stream_off : [n_streams+1] int64 sample offsets of the dither streams (device): each
+ *                stream is one RandomState(seeds[s]) consumed over out[stream_off[s] ..
+ *                stream_off[s+1]) in order (a speaker's files in sorted order); seeds
+ *                (device, uint32).  n_streams = 0 skips the dither (filtfilt only).
+ *   out        : float64, same length as x (may not alias x)
+ */
+int autovc_preprocess_f64(const void* x, int x_is_f64, const int64_t* wav_off, int n_utt,
+                          const double* b, const double* a, const double* zi, int order,
+                          const int64_t* stream_off, const unsigned* seeds, int n_streams,
+                          double* out, hipStream_t stream);
+
 /* ---------------------------------------------------------------- GEMM (fp32 MFMA)
  * Replaces the ATen/cuDNN GEMMs behind nn.Conv1d (implicit im2col, model_vc_mel.py:28-38),
  * nn.LSTM input projections (model_vc_mel.py:61,90,104) and nn.Linear (:10,106), forward

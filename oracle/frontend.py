@@ -115,6 +115,63 @@ def preprocess(x, prng):
     return y * 0.96 + (prng.rand(y.shape[0]) - 0.5) * 1e-06
 
 
+# ---- operation-order restatements of the two preprocessing steps --------------------
+# The GPU kernel (autovc_amd/csrc/preprocess.hip) follows these loops exactly; they are
+# pinned against scipy / numpy themselves (tests/test_oracle_frontend.py), which shows
+# that a bit-exact GPU result is attainable (no reassociation anywhere).
+
+def lfilter_df2t(b, a, x, z):
+    """scipy.signal.lfilter inner loop (direct form II transposed, a[0] == 1), scalar
+    float64 in scipy's operation order: y = z0 + b0 x; z_i = (z_{i+1} + x b_{i+1}) - y a_{i+1};
+    z_last = x b_last - y a_last."""
+    z = [float(v) for v in z]
+    y = np.empty(len(x))
+    n = len(b)
+    for k, xn in enumerate(np.asarray(x, dtype=np.float64)):
+        yn = z[0] + b[0] * xn
+        for i in range(n - 2):
+            z[i] = z[i + 1] + xn * b[i + 1] - yn * a[i + 1]
+        z[n - 2] = xn * b[n - 1] - yn * a[n - 1]
+        y[k] = yn
+    return y
+
+
+def filtfilt_restated(x, b=None, a=None):
+    """scipy.signal.filtfilt(b, a, x) defaults (make_spect.py:74): odd extension of
+    padlen = 3*max(len(a), len(b)) samples computed in x's own dtype, lfilter_zi states
+    scaled by each pass's first sample, forward then backward pass."""
+    if b is None:
+        b, a = butter_highpass()
+    x = np.asarray(x)
+    n = 3 * max(len(a), len(b))
+    ext = np.concatenate((2 * x[0:1] - x[n:0:-1], x, 2 * x[-1:] - x[-2:-(n + 2):-1]))
+    zi = signal.lfilter_zi(b, a)
+    y = lfilter_df2t(b, a, ext, zi * ext[0:1])
+    y = lfilter_df2t(b, a, y[::-1], zi * y[-1:])
+    return y[::-1][n:-n]
+
+
+def mt19937_rand(seed, n):
+    """numpy RandomState(seed).rand(n): init_genrand seeding, the 624-word twist,
+    tempering, and random_sample's 53-bit doubles (a >> 5, b >> 6)."""
+    mt = [seed & 0xFFFFFFFF]
+    for i in range(1, 624):
+        mt.append((1812433253 * (mt[-1] ^ (mt[-1] >> 30)) + i) & 0xFFFFFFFF)
+    words = []
+    while len(words) < 2 * n:
+        for i in range(624):
+            y = (mt[i] & 0x80000000) | (mt[(i + 1) % 624] & 0x7FFFFFFF)
+            mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+        for v in mt:
+            v ^= v >> 11
+            v ^= (v << 7) & 0x9D2C5680
+            v ^= (v << 15) & 0xEFC60000
+            v ^= v >> 18
+            words.append(v & 0xFFFFFFFF)
+    w = np.asarray(words[: 2 * n], dtype=np.uint64)
+    return ((w[0::2] >> 5).astype(np.float64) * 67108864.0 + (w[1::2] >> 6)) / 9007199254740992.0
+
+
 def spmel_from_wav(wav, mel_basis=None):
     """make_spect.py:78-83 on an already preprocessed wav -> (T, 80) float32."""
     if mel_basis is None:

@@ -56,3 +56,21 @@ def test_frame_count_matches_reference():
     from autovc_amd import dsp
     for n in [600, 1000, 16000, 48000, 48001, 48255, 48256]:
         assert dsp.n_frames(n) == fe.py_stft(np.random.RandomState(0).rand(n)).shape[1] == n // 256 + 1
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_filtfilt_restatement_is_scipy_bit_exact(dtype):
+    """The operation order the GPU filtfilt follows (make_spect.py:74) equals scipy's."""
+    from scipy import signal
+    rs = np.random.RandomState(7)
+    b, a = fe.butter_highpass()
+    for n in (19, 20, 333, 3000):
+        x = rs.uniform(-0.6, 0.6, n).astype(dtype)
+        assert np.array_equal(fe.filtfilt_restated(x), signal.filtfilt(b, a, x)), n
+
+
+@pytest.mark.parametrize("seed", [0, 1, 225, 2**32 - 1])
+def test_mt19937_restatement_is_numpy_bit_exact(seed):
+    """make_spect.py:76's prng.rand(n), restated as the GPU dither computes it; 700 draws
+    cross two 624-word twists."""
+    assert np.array_equal(fe.mt19937_rand(seed, 700), np.random.RandomState(seed).rand(700))
