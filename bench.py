@@ -303,7 +303,7 @@ def e2e_bench(dev, rank, world, per_rank=8):
     audio_s = sum(len(w) for w in waves) / 16000.0
     assert all(len(w) == m.shape[0] * 256 and np.isfinite(w).all() for w, m in zip(waves, mels))
     n_total = per_rank * world
-    return {"workload": f"C5: {n_total} synthetic utterances ({per_rank} per GPU, 2.0-3.6 s), host filtfilt+dither "
+    return {"workload": f"C5: {n_total} synthetic utterances ({per_rank} per GPU, 2.0-3.6 s), HIP filtfilt+dither "
                         "-> HIP 513-bin STFT -> GeneratorSTFT conversion -> mel projection -> WaveNet",
             "utterances_per_s": round(n_total / s[3], 3), "rtf_node": round(audio_s * world / s[3], 3),
             "rank0_audio_s": round(audio_s, 2),
