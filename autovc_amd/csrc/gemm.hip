@@ -546,6 +546,15 @@ GemmShape pick_config(int M, int N, int K, int splits) {
   // 21.62 vs 21.52 ms, same box, alternating)
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
   if (t128 >= 512) return kCfg[2];
+  // deep-K outputs that fill the chip once with 128-tiles (the LSTM weight gradients,
+  // 4096 x 1024 over K = B*T = 8192, on the gradient side stream): 128x128/BK32 measured
+  // 17.86 vs 17.98 ms/step against 64x64 (tools/ab_gemm_bigk.sh; AVC_GEMM_BIGK=<cfg id>
+  // overrides, -1 = the 64x64 path)
+  static const int bigk = [] {
+    const char* e = getenv("AVC_GEMM_BIGK");
+    return e ? atoi(e) : 2;
+  }();
+  if (bigk >= 0 && bigk < (int)(sizeof(kCfg) / sizeof(kCfg[0])) && t128 >= 256 && K >= 4096) return kCfg[bigk];
   if (splits > 1) return kCfg[3];
   return kCfg[8];
 }
