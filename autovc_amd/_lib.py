@@ -26,7 +26,7 @@ c_ptr = ctypes.c_void_p
 _SIGS: dict[str, list] = {}
 _RESTYPES = {"autovc_last_error": ctypes.c_char_p,
              "autovc_gemm_workspace_floats": c_i64, "autovc_bn_workspace_bytes": c_i64,
-             "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
+             "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_lstm2_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
              "autovc_colsum_workspace_floats": c_i64, "autovc_wavenet_packed_floats": c_i64,
              "autovc_wavenet_workspace_bytes": c_i64}
 
@@ -77,6 +77,9 @@ sig("autovc_lstm_fwd_timed_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr
 sig("autovc_lstm_bwd_workspace_floats", c_int, c_int, c_int)
 sig("autovc_lstm_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
     c_int, c_int, c_ptr, c_ptr)
+sig("autovc_lstm2_bwd_workspace_floats", c_int, c_int, c_int)
+sig("autovc_lstm2_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_lstm_fwd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_int, c_ptr)
 sig("autovc_lstm2_fwd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,

@@ -334,7 +334,7 @@ struct BwdArgs {
 // Thread = 4 consecutive units of one batch row (float4 loads / stores), grid (H/256, B)
 // of 64-thread blocks: no 64-bit index division, and the bf16 dG copy comes from registers.
 template <int S, bool FIRST, bool HAS_DH>
-__global__ __launch_bounds__(64) void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp) {
+__device__ __forceinline__ void bwd_pointwise_body(const BwdArgs& a, int t, int tp) {
   const int H = a.H;
   const int j = 4 * (blockIdx.x * 64 + threadIdx.x);
   if (j >= H) return;
@@ -383,6 +383,27 @@ __global__ __launch_bounds__(64) void lstm_bwd_pointwise_kernel(BwdArgs a, int t
   *reinterpret_cast<f32x4*>(a.dc_state + bj) = dcn;
 }
 
+template <int S, bool FIRST, bool HAS_DH>
+__global__ __launch_bounds__(64) void lstm_bwd_pointwise_kernel(BwdArgs a, int t, int tp) {
+  bwd_pointwise_body<S, FIRST, HAS_DH>(a, t, tp);
+}
+
+// Both layers of a stacked pair (decoder lstm2) in one launch of the backward wavefront
+// (see autovc_lstm2_bwd_f32): blockIdx.z = 0 is layer 1 at step t1 (dh from above + its
+// S recurrent partials), z = 1 is layer 0 at step t0 = t1 + 1, whose dh is the sum of 2S
+// partials: S of its own recurrence and S of layer 1's input gradient dG1_t0 W_ih1.
+template <int S>
+__global__ __launch_bounds__(64) void lstm2_bwd_pointwise_kernel(BwdArgs a1, BwdArgs a0, int t1, int t0) {
+  if (blockIdx.z == 0) {
+    if (t1 < 0) return;
+    if (t1 == a1.T - 1) bwd_pointwise_body<S, true, true>(a1, t1, t1 - 1);
+    else bwd_pointwise_body<S, false, true>(a1, t1, t1 - 1);
+  } else {
+    if (t0 >= a0.T) return;
+    bwd_pointwise_body<2 * S, false, false>(a0, t0, t0 - 1);
+  }
+}
+
 template <int S>
 void launch_pointwise(dim3 grid, hipStream_t st, const BwdArgs& a, int t, int tp, bool first) {
   if (first) {
@@ -411,13 +432,13 @@ void launch_pointwise_any(int /*blocks*/, hipStream_t st, const BwdArgs& a, int 
 // release/acquire ticket — measured 13.8 us per step against 9.2 + 4.0 us for the two
 // launches: the serial partial read + fences cost more than the kernel boundary.)
 // BF: dG / WT are the bf16 copies (passed as raw pointers, row lengths in bf16 elements).
-template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF, bool BF = false>
-__global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, int H, const float* dG, int t,
-                                                               const float* WT, float* P) {
+template <int KCH_, int NW_, int D_, bool BF>
+__device__ __forceinline__ void bwd_rec_body(int B, int T, int H, const float* dG, int t, const float* WT, float* P,
+                                             int j0) {
   using C = Tile<KCH_, NW_, D_>;
   __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j0 = blockIdx.x * TN, b0 = blockIdx.y * TB, s = blockIdx.z, S = gridDim.z;
+  const int b0 = blockIdx.y * TB, s = blockIdx.z, S = gridDim.z;
   // row length / split offsets in 4-byte units
   const int K4 = BF ? 2 * H : 4 * H, ks = K4 / S, kb = s * ks;
   auto arow_of = [&](int r) { return dG + ((int64_t)min(b0 + r, B - 1) * T + t) * K4 + kb; };
@@ -431,6 +452,34 @@ __global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, in
       const int b = b0 + wi * 16 + 4 * (lane >> 4) + r;
       if (b < B) P[((int64_t)s * B + b) * H + j0 + wn * 16 + (lane & 15)] = acc[r];
     }
+  }
+}
+
+template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF, bool BF = false>
+__global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, int H, const float* dG, int t,
+                                                               const float* WT, float* P) {
+  bwd_rec_body<KCH_, NW_, D_, BF>(B, T, H, dG, t, WT, P, blockIdx.x * TN);
+}
+
+// Recurrent products of one backward wavefront launch of a stacked pair, grid
+// (3 H/32, ceil(B/32), S): x-tiles [0, H/32) = dG1_t1 W_hh1 (layer 1's own recurrence,
+// -> P1), [H/32, 2H/32) = dG1_t1 W_ih1 (its input gradient = layer 0's dh at t1, -> the
+// upper S slabs of PQ0), [2H/32, 3H/32) = dG0_t0 W_hh0 (-> the lower S slabs of PQ0).
+// W*T are the (H, 4H) transposes.  Out-of-range steps (t1 < 0, t0 >= T) exit.
+template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+__global__ __launch_bounds__(64 * NW_) void lstm2_bwd_rec_kernel(int B, int T, int H, const float* dG1,
+                                                                const float* dG0, int t1, int t0,
+                                                                const float* WT1, const float* WIT1,
+                                                                const float* WT0, float* P1, float* PQ0) {
+  const int nt = H / TN, prod = blockIdx.x / nt, j0 = (blockIdx.x % nt) * TN;
+  const int64_t slabs = (int64_t)gridDim.z * B * H;
+  if (prod < 2) {
+    if (t1 < 0) return;
+    if (prod == 0) bwd_rec_body<KCH_, NW_, D_, false>(B, T, H, dG1, t1, WT1, P1, j0);
+    else bwd_rec_body<KCH_, NW_, D_, false>(B, T, H, dG1, t1, WIT1, PQ0 + slabs, j0);
+  } else {
+    if (t0 >= T) return;
+    bwd_rec_body<KCH_, NW_, D_, false>(B, T, H, dG0, t0, WT0, PQ0, j0);
   }
 }
 
@@ -679,6 +728,52 @@ extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int
                          (const float*)dG, t, W_hh_T, P);
   }
   AVC_CHECK_LAUNCH("autovc_lstm_bwd_f32");
+  return avc::kOk;
+}
+
+extern "C" int64_t autovc_lstm2_bwd_workspace_floats(int B, int H, int splits) {
+  return (int64_t)(3 * splits + 2) * B * H;
+}
+
+// Backward of two stacked layers (decoder lstm2) as a one-step-lagged wavefront, the
+// mirror of autovc_lstm2_fwd_f32: launch pair s = 0..T runs layer 1 at t1 = T-1-s and
+// layer 0 at t0 = T-s.  Layer 1's input gradient dG1_t W_ih1 (layer 0's dh_t) is a third
+// product of the recurrent launch instead of a GEMM over all frames after layer 1 ends,
+// and layer 0 starts one step behind layer 1 instead of T steps.  Same per-element sums
+// as the unstacked path except that layer 0's dh_t adds its 2S partials in one order.
+extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                    const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                    const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
+                                    float* dG0, int splits, float* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H), "autovc_lstm2_bwd_f32: bad dims");
+  AVC_CHECK_ARG((splits == 2 || splits == 4) && (4 * H) % (KCH * splits) == 0,
+                "autovc_lstm2_bwd_f32: splits must be 2 or 4 with 4H a multiple of %d x splits", KCH);
+  AVC_CHECK_ARG(dh1_out && gates1 && c1 && gates0 && c0 && W_hh1_T && W_ih1_T && W_hh0_T && dG1 && dG0 && workspace,
+                "autovc_lstm2_bwd_f32: null pointer");
+  AVC_CHECK_ARG(d_ldb % 4 == 0 && d_ldt % 4 == 0 && AVC_ALIGNED16(dh1_out) && AVC_ALIGNED16(W_hh1_T) &&
+                AVC_ALIGNED16(W_ih1_T) && AVC_ALIGNED16(W_hh0_T) && AVC_ALIGNED16(dG1) && AVC_ALIGNED16(dG0),
+                "autovc_lstm2_bwd_f32: operands must be 16-byte aligned with strides %% 4 == 0");
+  const int64_t BH = (int64_t)B * H;
+  float* P1 = workspace;
+  float* PQ0 = P1 + splits * BH;            // [S slabs of layer 0's recurrence | S slabs of dG1 W_ih1]
+  float* dcs1 = PQ0 + 2 * splits * BH;
+  float* dcs0 = dcs1 + BH;
+  // layer 0's first processed step has no recurrent partials and no carried cell gradient
+  AVC_HIP(hipMemsetAsync(PQ0, 0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_f32");
+  AVC_HIP(hipMemsetAsync(dcs0, 0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_f32");
+  BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits};
+  BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits};
+  const dim3 pgrid((H / 4 + 63) / 64, B, 2);
+  const dim3 rgrid(3 * H / TN, (B + TB - 1) / TB, splits);
+  for (int s = 0; s <= T; ++s) {
+    const int t1 = T - 1 - s, t0 = T - s;
+    if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    else hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<2>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    if (s == T) break;
+    hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
+                       (const float*)dG1, (const float*)dG0, t1, t0, W_hh1_T, W_ih1_T, W_hh0_T, P1, PQ0);
+  }
+  AVC_CHECK_LAUNCH("autovc_lstm2_bwd_f32");
   return avc::kOk;
 }
 

@@ -621,6 +621,16 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
         _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
                   WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
     _flush_grad_queue(after=mark)
+    return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs)
+
+
+def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
+    """Parameter gradients (queued beside the next recurrence, into the flat gradient
+    buffer) and dx of one large-H layer from its gate gradients dG (B, T, 4H)."""
+    p_ih, p_hh, p_bih, p_bhh = params
+    B, T, I = x.shape
+    H = h.shape[2]
+    dev = x.device
     M = B * T
     dx = dWih = dWhh = dbih = dbhh = None
     if needs[1]:
@@ -629,7 +639,7 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
                                                      splits=_splits_for(4 * H, I, M), accumulate=go.acc), dG, x)
         dWih = go.result()
     if needs[2]:
-        go = _GradOut(p_hh, W_hh.shape, dev)
+        go = _GradOut(p_hh, (4 * H, H), dev)
         _grad_launch(dev, go.acc, lambda go=go: gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
                                                      splits=_splits_for(4 * H, H, M), accumulate=go.acc), dG, h)
         dWhh = go.result()
@@ -688,12 +698,44 @@ class LSTM2StackFn(torch.autograd.Function):
         n = ctx.needs_input_grad
         need0 = (n[0],) + tuple(n[1:5])
         need1 = (any(need0),) + tuple(n[5:9])
+        H = W_hh0.shape[1]
+        if (any(need0) and g0 is not None and g1 is not None and not _bf16_rec(H)
+                and os.environ.get("AVC_LSTM2_BWD", "1") != "0" and H % 64 == 0):
+            return LSTM2StackFn._backward_stacked(ctx, dh1, need0, need1)
         dh0, *grads1 = _lstm_layer_backward(dh1, h0, W_ih1, W_hh1, h1, c1, g1, ctx.params[1], need1)
         if dh0 is None:
             grads0 = [None] * 5
         else:
             grads0 = _lstm_layer_backward(dh0, x, W_ih0, W_hh0, h0, c0, g0, ctx.params[0], need0)
         return (grads0[0], *grads0[1:], *grads1, None)
+
+    @staticmethod
+    def _backward_stacked(ctx, dh1, need0, need1):
+        """Both recurrences as one backward wavefront (autovc_lstm2_bwd_f32): layer 0 runs
+        one step behind layer 1, and layer 1's input gradient dG1 W_ih1 is computed inside
+        its steps instead of by a GEMM over all frames between the two recurrences."""
+        x, W_ih0, W_hh0, h0, c0, g0, W_ih1, W_hh1, h1, c1, g1 = ctx.saved_tensors
+        dh1 = dh1.contiguous()
+        B, T, _ = x.shape
+        H = W_hh0.shape[1]
+        dev = x.device
+        WT1, WIT1, WT0 = (torch.empty((H, 4 * H), device=dev, dtype=torch.float32) for _ in range(3))
+        for W, WT in ((W_hh1, WT1), (W_ih1, WIT1), (W_hh0, WT0)):
+            _lib.call("autovc_transpose_f32", 4 * H, H, W.data_ptr(), WT.data_ptr(), _s())
+        splits = int(os.environ.get("AVC_LSTM2_SPLITS", "4"))
+        while splits > 2 and (4 * H) % (64 * splits):
+            splits //= 2
+        ws = _ws(dev, 4 * _lib.load().autovc_lstm2_bwd_workspace_floats(B, H, splits), "lstm")
+        dG1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+        dG0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+        mark = _grad_mark(dev)   # queued weight gradients run beside the recurrences
+        _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
+                  g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(), dG1.data_ptr(),
+                  dG0.data_ptr(), splits, ws, _s())
+        _flush_grad_queue(after=mark)
+        grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
+        grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)
+        return (grads0[0], *grads0[1:], *grads1[1:], None)
 
 
 class BLSTMLayerFn(torch.autograd.Function):

@@ -208,6 +208,18 @@ int64_t autovc_lstm_bwd_workspace_floats(int B, int H, int splits);
 int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
                         const float* gates, const float* c_all, const float* W_hh_T, float* dG,
                         int reverse, int splits, float* workspace, hipStream_t stream);
+/* Backward of the two stacked layers of decoder lstm2 (nn.LSTM(512, 1024, 2),
+ * model_vc_mel.py:104,118 — replaces torch's BPTT of both layers plus the input-gradient
+ * GEMM between them) as a one-step-lagged wavefront: 2(T+1) launches, layer 1's input
+ * gradient dG1_t W_ih1 computed inside its step as layer 0's dh_t.  W_*_T are the (H, 4H)
+ * transposes of W_hh1, W_ih1 (layer 1's input size is H) and W_hh0; dh1_out = dL/dh1;
+ * dG1 / dG0 out (B, T, 4H); splits 2 or 4; workspace of
+ * autovc_lstm2_bwd_workspace_floats floats.  fp32 only. */
+int64_t autovc_lstm2_bwd_workspace_floats(int B, int H, int splits);
+int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                         const float* gates1, const float* c1, const float* gates0, const float* c0,
+                         const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
+                         float* dG0, int splits, float* workspace, hipStream_t stream);
 int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
                          const float* W_hh_b, float* h, float* c_all, float* gates,
                          hipStream_t stream);

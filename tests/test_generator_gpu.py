@@ -180,6 +180,32 @@ def test_lstm2_stack_fwd_bwd(cuda, B, T, I, H):
         assert rel(a.grad, b.grad) < 1e-4
 
 
+@pytest.mark.parametrize("splits", ["2", "4"])
+def test_lstm2_stacked_backward_matches_layerwise(cuda, monkeypatch, splits):
+    """The backward wavefront (autovc_lstm2_bwd_f32) against the layer-by-layer backward
+    (two autovc_lstm_bwd_f32 recurrences + the input-gradient GEMM) at decoder lstm2's
+    size: the same sums up to the order of layer 0's dh partials."""
+    from autovc_amd import functional as AF
+    torch.manual_seed(6)
+    B, T, I, H = 64, 12, 512, 1024
+    s = 1 / H ** 0.5
+    x = torch.randn(B, T, I, device=cuda)
+    shapes = [(4 * H, I), (4 * H, H), (4 * H,), (4 * H,), (4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]
+    ps = [((torch.rand(*sh) * 2 - 1) * s).to(cuda) for sh in shapes]
+    gh = torch.randn(B, T, H, device=cuda)
+    grads = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("AVC_LSTM2_BWD", mode)
+        monkeypatch.setenv("AVC_LSTM2_SPLITS", splits)
+        xd = x.clone().requires_grad_()
+        pd = [p.clone().requires_grad_() for p in ps]
+        AF.LSTM2StackFn.apply(xd, *pd, True).backward(gh)
+        AF.join_grad_stream()
+        grads[mode] = [xd.grad] + [p.grad for p in pd]
+    for a, b in zip(grads["1"], grads["0"]):
+        assert rel(a, b) < 1e-5
+
+
 @pytest.mark.parametrize("B,T,I", [(64, 128, 512), (5, 7, 64), (9, 21, 64)])
 def test_blstm_layer_fwd_bwd(cuda, B, T, I):
     from autovc_amd import functional as AF
