@@ -8,8 +8,11 @@ user's metadata file in the reference layout [spk, emb, 'spk/file.npy', ...].
 
 Differences: spectrograms are loaded in-process (no multiprocessing.Manager),
 items stay on the host (the Solver moves each batch to the GPU with one non-blocking copy
-instead of a per-item .to(device), :69), and an optional rank/world pair shards speakers
-for data-parallel training.
+instead of a per-item .to(device), :69), and data-parallel training (rank/world) uses
+`SpeakerCropSampler`: every rank draws its batch from ALL speakers, with replacement, from
+a stream seeded by (seed, rank, epoch).  The reference's loader indexes speakers without
+replacement with drop_last (:96-101), so with the 7 bundled speakers any batch larger than
+7 yields zero batches; sharding those speakers over 8 ranks would leave each rank none.
 """
 from __future__ import annotations
 
@@ -53,14 +56,42 @@ class Utterances(data.Dataset):
         return self.num_tokens
 
 
-def get_loader(root_dir, batch_size=16, len_crop=128, model_type="spmel", num_workers=0, rank=None, world=None):
-    """data_loader.py:90-102 (shuffle, drop_last, seeded workers); rank/world optionally
-    shard the speakers across data-parallel ranks."""
+class SpeakerCropSampler(data.Sampler):
+    """Speaker indices for one data-parallel rank: `batches` batches of `batch_size`
+    speakers per epoch, drawn uniformly WITH replacement from all `n_speakers`, from
+    RandomState(seed + 1_000_003 * rank + 7_919 * epoch).  Ranks draw independent streams
+    (different crops of the same speakers), every epoch reshuffles (`set_epoch`, called by
+    Solver.train each time it re-creates the data iterator), and the stream is reproducible.
+    Default `batches` = max(1, n_speakers // (batch_size * world)): the reference's epoch
+    length (len // batch_size, drop_last) spread over the ranks, but never zero."""
+
+    def __init__(self, n_speakers, batch_size, rank=0, world=1, seed=0, batches=None):
+        if n_speakers <= 0 or batch_size <= 0 or world <= 0 or not 0 <= rank < world:
+            raise ValueError(f"SpeakerCropSampler: n_speakers={n_speakers} batch_size={batch_size} "
+                             f"rank={rank} world={world}")
+        self.n, self.bs, self.rank, self.world, self.seed = n_speakers, batch_size, rank, world, seed
+        self.batches = batches if batches is not None else max(1, n_speakers // (batch_size * world))
+        self.epoch = 0
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch)
+
+    def __iter__(self):
+        rs = np.random.RandomState((self.seed + 1_000_003 * self.rank + 7_919 * self.epoch) % (2 ** 32))
+        return iter(rs.randint(0, self.n, self.batches * self.bs).tolist())
+
+    def __len__(self):
+        return self.batches * self.bs
+
+
+def get_loader(root_dir, batch_size=16, len_crop=128, model_type="spmel", num_workers=0, rank=None, world=None,
+               seed=0):
+    """data_loader.py:90-102 (shuffle, drop_last, seeded workers).  With rank/world (and
+    world > 1) the batches come from a per-rank `SpeakerCropSampler` instead."""
     dataset = Utterances(root_dir, len_crop, model_type)
     sampler = None
     if world is not None and world > 1:
-        sampler = data.distributed.DistributedSampler(dataset, num_replicas=world, rank=rank, shuffle=True,
-                                                      drop_last=True)
+        sampler = SpeakerCropSampler(len(dataset), batch_size, rank or 0, world, seed)
     worker_init_fn = lambda x: np.random.seed((torch.initial_seed()) % (2 ** 32))  # noqa: E731
     return data.DataLoader(dataset=dataset, batch_size=batch_size, shuffle=sampler is None, sampler=sampler,
                            num_workers=num_workers, drop_last=True, worker_init_fn=worker_init_fn)

@@ -4,8 +4,19 @@ backend "nccl" (= RCCL on ROCm) over xGMI.
 The reference has no distributed code; the build shards utterances (crops)
 across ranks, keeps per-rank BatchNorm statistics (the reference semantics at B=64/GPU),
 and adds the one real exchange of the step: an all-reduce (mean) of the gradients.
-Because FusedAdam keeps every gradient in ONE contiguous buffer, the exchange is one
-bucketed collective over that buffer (no per-parameter calls), issued after backward.
+Because FusedAdam keeps every gradient in ONE contiguous buffer, the exchange is a few
+bucketed collectives over that buffer (no per-parameter calls).
+
+Overlap: the buckets are all-reduced asynchronously, and each bucket's Adam update is
+queued as soon as its collective is done (`reduce_and_step`), so the update of bucket i
+runs while bucket i+1 is still on the wire.  The forward+backward itself is replayed as
+one captured HIP graph (autovc_amd.graph): collectives are kept OUT of that graph (RCCL
+under stream capture is not exercised on the single-GPU boxes this build is tested on),
+which is why the exchange cannot start inside the backward in graph mode.
+
+Exchange precision: fp32 (113.7 MB per step) by default; `grad_dtype=torch.bfloat16`
+halves the bytes (56.8 MB) for BASELINE config 3 — the rank sum is then
+rounded to bf16 (the mean gradient loses the low 16 bits of its mantissa).
 """
 from __future__ import annotations
 
@@ -13,6 +24,8 @@ import os
 
 import torch
 import torch.distributed as dist
+
+DEFAULT_BUCKET_BYTES = 16 << 20
 
 
 def init_from_env(backend=None):
@@ -31,33 +44,86 @@ def init_from_env(backend=None):
     return dist.get_rank(), dist.get_world_size()
 
 
+def _world():
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size()
+
+
 def broadcast_parameters(optimizer, src=0):
     """Rank src's parameters (and nothing else) to every rank: one collective per flat buffer."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if _world() == 1:
         return
     for flat in optimizer.flat_params():
         dist.broadcast(flat, src)
 
 
-def allreduce_gradients(optimizer, bucket_bytes=64 << 20):
-    """Mean of the flat gradient buffers over all ranks, in buckets of bucket_bytes."""
-    if not (dist.is_available() and dist.is_initialized()):
-        return
-    world = dist.get_world_size()
+def _buckets(n, bucket_bytes):
+    nb = max(4, (bucket_bytes // 4) // 4 * 4)   # multiples of 4 floats: 16-byte aligned slices
+    return [(s, min(nb, n - s)) for s in range(0, n, nb)]
+
+
+def _issue(chunk, grad_dtype):
+    buf = chunk if grad_dtype is None or grad_dtype == chunk.dtype else chunk.to(grad_dtype)
+    return buf, dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True)
+
+
+def _finish(chunk, buf, work, world):
+    work.wait()
+    if buf is not chunk:
+        chunk.copy_(buf)
+    chunk.mul_(1.0 / world)
+
+
+def allreduce_gradients(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None):
+    """Mean of the flat gradient buffers over all ranks, in buckets of bucket_bytes (all
+    buckets in flight at once)."""
+    world = _world()
     if world == 1:
         return
     from .functional import join_grad_stream   # weight gradients may still be in flight
     join_grad_stream()
-    nb = max(1, bucket_bytes // 4)
+    pending = []
     for flat in optimizer.flat_grads():
-        for s in range(0, flat.numel(), nb):
-            chunk = flat[s:s + nb]
-            dist.all_reduce(chunk, op=dist.ReduceOp.SUM)
-            chunk.mul_(1.0 / world)
+        for s, c in _buckets(flat.numel(), bucket_bytes):
+            chunk = flat[s:s + c]
+            pending.append((chunk, *_issue(chunk, grad_dtype)))
+    for chunk, buf, work in pending:
+        _finish(chunk, buf, work, world)
 
 
-def make_data_parallel(solver):
-    """Attach gradient all-reduce to an autovc_amd Solver and sync its initial weights."""
+def reduce_and_step(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None):
+    """All-reduce (mean) + Adam, bucket by bucket: every bucket's collective is issued up
+    front; bucket i's update is queued on the compute stream once its collective is done,
+    overlapping the collectives of the later buckets.  Identical arithmetic to
+    allreduce_gradients() followed by optimizer.step() (Adam is elementwise)."""
+    world = _world()
+    optimizer.begin_step()          # joins the gradient side stream first
+    if world == 1:
+        for gi, f in enumerate(optimizer._flat):
+            if f is not None:
+                optimizer.update_range(gi, 0, f["p"].numel())
+        return
+    pending = []
+    for gi, f in enumerate(optimizer._flat):
+        if f is None:
+            continue
+        flat = f["g"]
+        for s, c in _buckets(flat.numel(), bucket_bytes):
+            chunk = flat[s:s + c]
+            pending.append((gi, s, c, chunk, *_issue(chunk, grad_dtype)))
+    for gi, s, c, chunk, buf, work in pending:
+        _finish(chunk, buf, work, world)
+        optimizer.update_range(gi, s, c)
+
+
+def make_data_parallel(solver, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None, overlap=True):
+    """Attach the gradient exchange to an autovc_amd Solver and sync its initial weights.
+    overlap=True: reduce_and_step (bucketed all-reduce interleaved with the Adam update);
+    overlap=False: allreduce_gradients after backward, then one Adam launch."""
     broadcast_parameters(solver.g_optimizer)
-    solver._after_backward = lambda: allreduce_gradients(solver.g_optimizer)
+    if overlap:
+        solver._optimizer_step = lambda: reduce_and_step(solver.g_optimizer, bucket_bytes, grad_dtype)
+    else:
+        solver._after_backward = lambda: allreduce_gradients(solver.g_optimizer, bucket_bytes, grad_dtype)
     return solver

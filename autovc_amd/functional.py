@@ -37,15 +37,26 @@ def _check(t, name):
 
 
 class _Workspace:
-    """Per-device scratch buffer reused by every op (one stream: ops never overlap)."""
+    """Per-device scratch buffer reused by every op (one stream: ops never overlap).
+
+    A slot that has to grow gets a new buffer, but the old one is never handed back to the
+    caching allocator: a captured step graph (autovc_amd.graph) keeps using the raw pointer
+    it was captured with, and replaying it into memory that now belongs to another tensor
+    would corrupt that tensor.  Slots grow geometrically, so the retired buffers cost at
+    most the size of the live one."""
     _bufs: dict = {}
+    _retired: list = []
 
     @classmethod
     def get(cls, device, nbytes, slot="main"):
         key = (device, slot)
         buf = cls._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(int(nbytes), 1) + 256, dtype=torch.uint8, device=device)
+            size = max(int(nbytes), 1) + 256
+            if buf is not None:
+                cls._retired.append(buf)
+                size = max(size, 2 * buf.numel())
+            buf = torch.empty(size, dtype=torch.uint8, device=device)
             cls._bufs[key] = buf
         return buf
 
@@ -722,9 +733,10 @@ class LSTM2StackFn(torch.autograd.Function):
         WT1, WIT1, WT0 = (torch.empty((H, 4 * H), device=dev, dtype=torch.float32) for _ in range(3))
         for W, WT in ((W_hh1, WT1), (W_ih1, WIT1), (W_hh0, WT0)):
             _lib.call("autovc_transpose_f32", 4 * H, H, W.data_ptr(), WT.data_ptr(), _s())
-        splits = int(os.environ.get("AVC_LSTM2_SPLITS", "4"))
-        while splits > 2 and (4 * H) % (64 * splits):
-            splits //= 2
+        # the stacked backward kernel is built for split-K 2 or 4 only (autovc_lstm2_bwd_f32)
+        splits = 4 if int(os.environ.get("AVC_LSTM2_SPLITS", "4")) >= 4 else 2
+        if (4 * H) % (64 * splits):
+            splits = 2
         ws = _ws(dev, 4 * _lib.load().autovc_lstm2_bwd_workspace_floats(B, H, splits), "lstm")
         dG1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         dG0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)

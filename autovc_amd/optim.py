@@ -81,21 +81,39 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self.begin_step()
+        for gi, f in enumerate(self._flat):
+            if f is not None:
+                self.update_range(gi, 0, f["p"].numel())
+        return loss
+
+    # -- split step (autovc_amd.ddp overlaps the gradient all-reduce of one bucket with the
+    #    update of the previous one): begin_step() once, then update_range() per slice
+    @torch.no_grad()
+    def begin_step(self):
         from .functional import join_grad_stream   # weight gradients may still be in flight
         join_grad_stream()
-        for group, f in zip(self.param_groups, self._flat):
+        for f in self._flat:
             if f is None:
                 continue
             self._reattach_grads(f)
             f["step"] += 1
-            b1, b2 = group["betas"]
-            bc1 = 1.0 - b1 ** f["step"]
-            bc2_sqrt = math.sqrt(1.0 - b2 ** f["step"])
-            _lib.call("autovc_adam_f32", f["p"].numel(), f["p"].data_ptr(), f["g"].data_ptr(),
-                      f["m"].data_ptr(), f["v"].data_ptr(), float(group["lr"]), float(b1), float(b2),
-                      float(group["eps"]), float(group["weight_decay"]), float(bc1), float(bc2_sqrt),
-                      _lib.stream_ptr(f["p"].device))
-        return loss
+
+    @torch.no_grad()
+    def update_range(self, group_index, start, count):
+        """Adam on flat elements [start, start + count) of one group (start a multiple of 4,
+        so every slice stays 16-byte aligned); the step count was advanced by begin_step."""
+        group, f = self.param_groups[group_index], self._flat[group_index]
+        if start % 4 or start < 0 or count <= 0 or start + count > f["p"].numel():
+            raise ValueError(f"FusedAdam.update_range: bad slice [{start}, {start + count})")
+        b1, b2 = group["betas"]
+        bc1 = 1.0 - b1 ** f["step"]
+        bc2_sqrt = math.sqrt(1.0 - b2 ** f["step"])
+        o = 4 * start
+        _lib.call("autovc_adam_f32", count, f["p"].data_ptr() + o, f["g"].data_ptr() + o,
+                  f["m"].data_ptr() + o, f["v"].data_ptr() + o, float(group["lr"]), float(b1), float(b2),
+                  float(group["eps"]), float(group["weight_decay"]), float(bc1), float(bc2_sqrt),
+                  _lib.stream_ptr(f["p"].device))
 
     def _reattach_grads(self, f):
         """If autograd replaced a .grad (e.g. zero_grad(set_to_none) by a caller), copy it

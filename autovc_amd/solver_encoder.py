@@ -33,6 +33,17 @@ from .model_vc_stft import GeneratorSTFT
 from .optim import FusedAdam
 
 
+def _rank():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def _barrier():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
+
+
 class _NoLogger:
     def log(self, *a, **k):
         pass
@@ -90,7 +101,7 @@ class Solver(object):
 
         self.path = "chkpnt_" + self.model_type + "_" + self.run_name + ".ckpt"
         self.file_exists = os.path.exists(self.path)
-        self.logger = _make_logger(config, self.file_exists)
+        self.logger = _make_logger(config, self.file_exists) if _rank() == 0 else _NoLogger()
 
         if not torch.cuda.is_available():
             raise RuntimeError("autovc_amd.Solver trains on the MI355X only (no CPU fallback)")
@@ -166,13 +177,18 @@ class Solver(object):
         else:
             g_loss, l_id, l_psnt, l_cd, x_psnt = self._forward_backward(x_real, emb_org)
         self._after_backward()
-        self.g_optimizer.step()
+        self._optimizer_step()
         self._last_psnt = x_psnt
         return g_loss, l_id, l_psnt, l_cd
 
     def _after_backward(self):
         """Hook for data-parallel gradient reduction (autovc_amd.ddp)."""
         return None
+
+    def _optimizer_step(self):
+        """Adam (solver_encoder.py:300); autovc_amd.ddp replaces it by the bucketed
+        all-reduce interleaved with per-bucket updates."""
+        self.g_optimizer.step()
 
     # ------------------------------------------------------------------ loop
     def train(self):
@@ -189,10 +205,15 @@ class Solver(object):
         self.G.train()
         self.logger.watch(self.G, log=None)
         data_iter = None
+        epoch = 0
         for i in range(i_start, self.num_iters):
             try:
                 x_real, emb_org = next(data_iter)
             except Exception:  # reference: bare except re-creates the iterator (:212-216)
+                sampler = getattr(data_loader, "sampler", None)
+                if hasattr(sampler, "set_epoch"):   # data-parallel sampler: reshuffle per epoch
+                    sampler.set_epoch(epoch)
+                epoch += 1
                 data_iter = iter(data_loader)
                 x_real, emb_org = next(data_iter)
             x_real = x_real.to(self.device, non_blocking=True)
@@ -226,8 +247,13 @@ class Solver(object):
                     save_name = "chkpnt_" + self.model_type + "_" + self.run_name + "_resumed.ckpt"
                 else:
                     save_name = "chkpnt_" + self.model_type + "_" + self.run_name + ".ckpt"
-                torch.save(state, save_name)
-                self.logger.log({"i": i, "lr": lr, "g_loss": g_loss.item(), "g_loss_id": loss["G/loss_id"],
-                                 "g_loss_id_psnt": loss["G/loss_id_psnt"], "g_loss_cd": loss["G/loss_cd"],
-                                 "g_loss_SISNR": float("nan")})
+                # data-parallel: the ranks hold identical weights; only rank 0 writes the file
+                # and logs, and every rank waits until it is complete (a resume reads it)
+                rank0 = _rank() == 0
+                if rank0:
+                    torch.save(state, save_name)
+                    self.logger.log({"i": i, "lr": lr, "g_loss": g_loss.item(), "g_loss_id": loss["G/loss_id"],
+                                     "g_loss_id_psnt": loss["G/loss_id_psnt"], "g_loss_cd": loss["G/loss_cd"],
+                                     "g_loss_SISNR": float("nan")})
+                _barrier()
         return self

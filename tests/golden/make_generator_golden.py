@@ -162,5 +162,58 @@ def main(out_path=os.path.join(HERE, "generator_golden.npz")):
     print("wrote", out_path, {k: getattr(v, "shape", None) for k, v in out.items()})
 
 
+def _reference_steps(ref_mel, sd, xt, et, dtype, threads, n_steps):
+    """The reference Generator + the Solver's loss composition (solver_encoder.py:228-243,
+    293-300) + torch Adam, in `dtype` on `threads` intra-op threads.  Returns (per-step
+    losses (n,3), first-step gradient slices (n_params, N_SLICE) in float64)."""
+    torch.set_num_threads(threads)
+    G = ref_mel.Generator(32, 256, 512, 32)
+    G.load_state_dict(sd)
+    G = G.to(dtype).train()
+    x, e = xt.to(dtype), et.to(dtype)
+    opt = torch.optim.Adam(G.parameters(), 1e-4)
+    hist, gslice = [], None
+    for _ in range(n_steps):
+        x_id, x_psnt, code = G(x, e, e)
+        l_id = torch.nn.functional.mse_loss(x.squeeze(), x_id.squeeze())
+        l_psnt = torch.nn.functional.mse_loss(x, x_psnt.squeeze())
+        l_cd = torch.nn.functional.l1_loss(code, G(x_psnt, e, None))
+        opt.zero_grad()
+        (l_id + l_psnt + l_cd).backward()
+        if gslice is None:
+            gslice = np.stack([np.pad(p.grad.detach().double().flatten()[:N_SLICE].numpy(),
+                                      (0, max(0, N_SLICE - p.numel()))) for p in G.parameters()])
+        opt.step()
+        hist.append([l_id.item(), l_psnt.item(), l_cd.item()])
+    return np.array(hist), gslice
+
+
+def main_spread(out_path=os.path.join(HERE, "generator_spread.npz")):
+    """The reference's OWN numerical spread, used to set the trajectory and gradient-slice
+    tolerances from evidence instead of by hand:
+      traj_f64 / grad_slice_f64 — the reference Generator run in float64 (the closest thing
+                                  to the exact answer the reference can give),
+      traj_t1                   — the reference in float32 on ONE intra-op thread (the golden
+                                  solver_traj ran on 8): same code, another reduction order."""
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    _stub_modules()
+    sys.path.insert(0, REF)
+    import model_vc_mel as ref_mel  # reference
+    g = np.load(os.path.join(HERE, "generator_golden.npz"))
+    xt, et = torch.from_numpy(g["x"]), torch.from_numpy(g["emb"])
+    sd = deterministic_state_dict(ref_mel.Generator(32, 256, 512, 32).state_dict())
+    traj_f64, gs64 = _reference_steps(ref_mel, sd, xt, et, torch.float64, 8, 10)
+    traj_t1, _ = _reference_steps(ref_mel, sd, xt, et, torch.float32, 1, 10)
+    traj_t8, gs32 = _reference_steps(ref_mel, sd, xt, et, torch.float32, 8, 1)
+    assert np.array_equal(traj_t8[0], g["solver_traj"][0]) or np.allclose(traj_t8[0], g["solver_traj"][0], rtol=1e-6)
+    np.savez_compressed(out_path, traj_f64=traj_f64, traj_t1=traj_t1, grad_slice_f64=gs64,
+                        grad_slice_f32_check=gs32)
+    print("wrote", out_path)
+
+
 if __name__ == "__main__":
-    main()
+    if "--spread" in sys.argv:
+        main_spread()
+    else:
+        main()

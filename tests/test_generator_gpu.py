@@ -8,6 +8,7 @@ import torch
 
 from conftest import GOLDEN
 from oracle import generator as og
+from parity_tol import check_grad_slices
 
 pytestmark = pytest.mark.gpu
 G = np.load(os.path.join(GOLDEN, "generator_golden.npz"))
@@ -309,6 +310,9 @@ def test_one_training_step_grads_vs_reference_golden(cuda):
             assert abs(gn - G["grad_norm"][i]) < 1e-6, n
         else:
             assert abs(gn - G["grad_norm"][i]) <= 1e-2 * G["grad_norm"][i], (n, gn, G["grad_norm"][i])
+    # elementwise: first 64 gradient elements of every tensor vs the reference's float32 and
+    # float64 backward (tests/parity_tol.py; pre-BN conv biases |g| <= 1e-6)
+    check_grad_slices({n: p.grad.detach().cpu().numpy() for n, p in params.items()})
     bufs = dict(g.named_buffers())
     got = np.concatenate([bufs[k].float().flatten().cpu().numpy() for k in G["step1_buffer_names"]])
     assert rel(got, G["step1_buffers"]) < FWD_TOL  # encoder BN updated twice, decoder/postnet once

@@ -6,7 +6,9 @@ Tolerances: forward <= 1e-4 rel (max-abs / max); one-step gradient
 <= 1e-2 rel per tensor (the reference's own fp32 noise is ~1e-3, F8) except pre-BN conv
 biases whose true gradient is 0 (compared absolutely); Adam step 1 moves each parameter
 by ~lr*sign(grad), so parameters are compared at 2.01e-4 abs with near-all elements
-exact to 1e-6; loss trajectory: step 1 <= 1e-4 rel, steps 2-10 see check_trajectory."""
+exact to 1e-6; first-step gradients ELEMENTWISE against the reference's float32 and
+float64 gradient slices (tests/parity_tol.py); loss trajectory: step 1 <= 1e-4 rel, steps
+2-10 within max(5 %, 2 x the reference's own spread) (parity_tol.check_trajectory)."""
 import os
 
 import numpy as np
@@ -15,6 +17,7 @@ import torch
 
 from conftest import GOLDEN
 from oracle import generator as og
+from parity_tol import check_grad_slices, check_trajectory
 
 G = np.load(os.path.join(GOLDEN, "generator_golden.npz"))
 FWD_TOL = 1e-4
@@ -70,6 +73,7 @@ def test_one_step_grads_adam_and_running_stats():
             assert abs(g.norm().item() - G["grad_norm"][i]) < 1e-6, n
             continue
         assert abs(g.norm().item() - G["grad_norm"][i]) <= 1e-2 * G["grad_norm"][i] + 1e-9, n
+    check_grad_slices(grads)
     diffs = []
     for i, n in enumerate(names):
         v = P[n].flatten()[:64].numpy()
@@ -106,16 +110,6 @@ def test_solver_trajectory_matches_reference_solver_train():
     traj = np.array(hist)
     assert rel(traj[0], G["solver_traj"][0]) < 1e-4
     check_trajectory(traj, G["solver_traj"])
-
-
-def check_trajectory(traj, ref):
-    """Steps 2-10: reconstruction losses within 5 %, the content-code L1 loss within 15 %.
-    L_cd is an L1 of two nearly equal code sets; its sign-driven Adam updates amplify
-    rounding: an fp64 restatement of the same 10 steps differs from the reference's fp32
-    run by 7 % on L_cd at steps 5-10 (and < 0.3 % on the other two)."""
-    traj, ref = np.asarray(traj), np.asarray(ref)
-    assert np.all(np.abs(traj[:, :2] - ref[:, :2]) <= 0.05 * np.abs(ref[:, :2])), (traj, ref)
-    assert np.all(np.abs(traj[:, 2] - ref[:, 2]) <= 0.15 * np.abs(ref[:, 2])), (traj, ref)
 
 
 def test_stft_variant_513_bins():

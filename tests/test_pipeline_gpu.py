@@ -87,3 +87,72 @@ def test_stft_model_output_projected_to_mels(cuda):
     ref = y.cpu().double() @ torch.from_numpy(dsp.mel_basis().T).double()
     assert got.shape == (37, 80)
     assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_c5_chain_513_bins_24_layer_wavenet_vs_oracles(cuda):
+    """BASELINE config 5 exactly as specified, on 2 synthetic utterances,
+    every stage against its oracle on the same inputs:
+      HIP filtfilt + dither  (make_spect.py:74-76)      vs scipy/numpy             bit-exact
+      HIP 513-bin STFT       (make_spect.py:78,84-86)   vs oracle.frontend         <= 1e-4 abs
+      GeneratorSTFT eval     (model_vc_stft.py:7-53, conversion.py:40-44,90-100)
+                                                        vs oracle.generator        <= 1e-4 rel
+      mel_basis projection   (conversion.py:102)        vs float64 numpy           <= 1e-5 rel
+      24-layer r9y9 WaveNet  (synthesis.py:44-73), 512 samples per utterance, free-running
+                                                        vs oracle.wavenet          <= 1e-4 abs
+    """
+    from autovc_amd import dsp, pipeline
+    from autovc_amd.model_vc_stft import GeneratorSTFT
+    from autovc_amd.wavenet import WaveNet
+    wavs = _wavs(2, seed=21)
+    # stage 1: preprocessing, bit-exact with the reference's host libraries
+    wav, lens = dsp.preprocess_gpu([np.asarray(w, np.float64) for w in wavs], seeds=[0, 1], device=cuda)
+    pre = [fe.preprocess(np.asarray(w, np.float64), np.random.RandomState(i)) for i, w in enumerate(wavs)]
+    got_pre = wav.cpu().numpy()
+    assert list(lens) == [len(p) for p in pre]
+    assert np.array_equal(got_pre, np.concatenate(pre))
+    # stage 2: 513-bin STFT (frame-major; the reference stores it (513, T))
+    specs = dsp.stft_mel_packed(wav, lens, "stft")
+    for i in range(2):
+        ref = fe.stft_from_wav(pre[i]).T
+        assert specs[i].shape == ref.shape and specs[i].shape[1] == 513
+        assert np.abs(specs[i].cpu().numpy() - ref).max() <= 1e-4
+    # stage 3+4: GeneratorSTFT conversion (eval) and the mel projection
+    P = og.make_weights(prefix="model.", n_in=513, n_out=513)
+    G = GeneratorSTFT(32, 256, 512, 32)
+    G.load_state_dict(P)
+    G = G.to(cuda).eval()
+    g = torch.Generator().manual_seed(21)
+    e = torch.randn(2, 256, generator=g)
+    e = e / e.norm(dim=1, keepdim=True) * 0.8
+    mels = pipeline.convert(G, specs, e.to(cuda), e.flip(0).to(cuda))
+    ref_gen = og.OracleGenerator(P, prefix="model.", training=False)
+    basis = dsp.mel_basis().T.astype(np.float64)                      # (513, 80)
+    for i in range(2):
+        x, len_pad = pipeline.pad_seq(specs[i].cpu().numpy())
+        with torch.no_grad():
+            _, psnt, _ = ref_gen.forward(torch.from_numpy(x[None]), e[i:i + 1], e.flip(0)[i:i + 1])
+        y513 = psnt[0, 0, : specs[i].shape[0]].double().numpy()
+        ref = y513 @ basis
+        assert mels[i].shape == (specs[i].shape[0], 80)
+        err = np.abs(mels[i].cpu().double().numpy() - ref).max() / np.abs(ref).max()
+        assert err < 1e-4, (i, err)
+    # stage 5: the 24-layer / 4-stack r9y9 WaveNet, 512 samples (2 conditioning frames)
+    hp = ow.HPARAMS
+    assert hp["layers"] == 24 and hp["stacks"] == 4 and hp["residual_channels"] == 512
+    V = WaveNet(out_channels=hp["out_channels"], layers=hp["layers"], stacks=hp["stacks"],
+                residual_channels=hp["residual_channels"], gate_channels=hp["gate_channels"],
+                skip_out_channels=hp["skip_out_channels"], kernel_size=hp["kernel_size"],
+                cin_channels=hp["cin_channels"], upsample_conditional_features=True,
+                upsample_scales=list(hp["upsample_scales"]), scalar_input=True, legacy=True)
+    V.make_generation_fast_()
+    W = ow.make_weights(hp, 4322)
+    V.load_state_dict(W)
+    V = V.to(cuda).eval()
+    c = torch.stack([m[:2].t() for m in mels]).contiguous()          # (2, 80, 2) conditioning
+    seed = 31337
+    y = V.generate(c, seed=seed, log_scale_min=ow.HPARAMS["log_scale_min"])
+    o = ow.OracleWaveNet(W, hp)
+    u = ow.philox_uniforms(seed, [0, 1], 0, 512)
+    y_ref = o.incremental(o.upsample(c.cpu()), 512, uniforms=u)
+    assert y.shape == (2, 512)
+    assert (y.double().cpu() - y_ref).abs().max().item() < 1e-4

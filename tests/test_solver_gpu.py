@@ -44,7 +44,7 @@ def test_adam_step_matches_reference(cuda):
 
 
 def test_ten_step_trajectory_matches_reference_solver(cuda):
-    from test_oracle_generator import check_trajectory
+    from parity_tol import check_trajectory
     s = _solver()
     x = torch.from_numpy(G["x"]).to(cuda)
     e = torch.from_numpy(G["emb"]).to(cuda)
@@ -125,3 +125,37 @@ def test_hip_graph_step_bit_identical(cuda, precision):
         assert torch.equal(a, b)
     for a, b in zip(ba, bb):
         assert torch.equal(a, b)
+
+
+def test_graph_replay_survives_workspace_growth(cuda):
+    """A graph captured at a small shape keeps the raw pointers of the shared scratch
+    workspace; capturing a larger shape grows that workspace.  The first graph's replay must
+    still be bit-identical to eager and must not write into memory that now belongs to other
+    tensors (the retired workspace buffers are kept alive, functional._Workspace)."""
+    import bench
+    from autovc_amd.graph import StepGraphs
+    g = og_build_eval(cuda)
+
+    def fn(x, e):
+        with torch.no_grad():
+            return tuple(g(x, e, e))
+
+    sg = StepGraphs(fn, g)
+    x8, e8 = bench.synthetic_batch(8, 128, cuda, 3)
+    x64, e64 = bench.synthetic_batch(64, 128, cuda, 4)
+    ref8 = [t.clone() for t in fn(x8, e8)]
+    first = [t.clone() for t in sg.run("f", x8, e8)]
+    sg.run("f", x64, e64)                       # bigger scratch: the workspace slots grow
+    canary = torch.full((32 << 20,), 3.0, device=cuda)
+    again = sg.run("f", x8, e8)
+    torch.cuda.synchronize()
+    for a, b, r in zip(first, again, ref8):
+        assert torch.equal(a, r) and torch.equal(b, r)
+    assert bool((canary == 3.0).all())
+
+
+def og_build_eval(cuda):
+    from autovc_amd.model_vc_mel import Generator
+    g = Generator(32, 256, 512, 32)
+    g.load_state_dict(og.make_weights())
+    return g.to(cuda).eval()
