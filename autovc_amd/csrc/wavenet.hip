@@ -44,12 +44,19 @@
 
 namespace {
 
+// Diagnostic ablations of the step kernels (tools/wn_ablate.sh builds them into a separate
+// library; the product build is WN_ABLATE 0): 1 = step index a constant (no dependent
+// counter load), 2 = 1 + no activation loads, 3 = 1 + no weight loads, 4 = 1 + no residual
+// wave work, 5 = every step kernel returns at once (launch boundaries only), 6 = 2+3+4,
+// 7 = 1 + no cross-lane reduction.  Outputs are meaningless unless WN_ABLATE == 0.
+#ifndef WN_ABLATE
+#define WN_ABLATE 0
+#endif
+
 constexpr float kSqrtHalf = 0.70710677f;  // float(math.sqrt(0.5))
 constexpr int kBT = 8;                    // utterances per batch tile
 constexpr int kMaxNO = 32;                // MoL head width limit (3 x up to 10 mixtures)
 constexpr int kCtrSlots = 128;
-constexpr int kMaxResid = 4;              // residual rows per layer workgroup: R/H + S/H
-constexpr int kGateWaves = 7;             // waves per layer workgroup on the GEMV (1792 = 7 chunks of 256)
 
 struct WnArgs {
   int B, T, R, G, S, NO, K, RING, n_layers, lps, Tch, legacy, n_kern;
@@ -183,6 +190,7 @@ __device__ inline f32x4 ld4(const float* p) { return *reinterpret_cast<const f32
 // step index: a kernel argument for direct launches (targ >= 0), else (graph replay) the
 // counter slot the previous kernel wrote
 __device__ inline int read_step(const WnArgs& a, int slot, int next_delta, int targ) {
+  if (WN_ABLATE != 0) return a.T - 1;
   if (targ >= 0) return targ;
   const int t = a.ctr[slot];
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[slot + 1 == a.n_kern ? 0 : slot + 1] = t + next_delta;
@@ -196,7 +204,7 @@ __device__ inline int read_step(const WnArgs& a, int slot, int next_delta, int t
 
 // MoL parameters of step tp = tp1 - 1 (from h1) for the batch tile, then the input of
 // step tp1.  Runs on the whole workgroup (NW waves).  Writes s_in[b].
-template <int NW>
+template <int NW, int UB>
 __device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_mol, float* s_in) {
   constexpr int MAXR = (kMaxNO + NW - 1) / NW;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -205,15 +213,15 @@ __device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_
   const float* b2 = W2 + (int64_t)a.NO * a.S;
   const int tp = tp1 - 1;
   if (tp >= 0) {
-    float acc[MAXR][kBT];
+    float acc[MAXR][UB];
 #pragma unroll
     for (int q = 0; q < MAXR; ++q)
 #pragma unroll
-      for (int b = 0; b < kBT; ++b) acc[q][b] = 0.f;
+      for (int b = 0; b < UB; ++b) acc[q][b] = 0.f;
     for (int k = lane * 4; k < a.S; k += 256) {
-      f32x4 h[kBT];
+      f32x4 h[UB];
 #pragma unroll
-      for (int b = 0; b < kBT; ++b) h[b] = ld4(a.h1 + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + k);
+      for (int b = 0; b < UB; ++b) h[b] = ld4(a.h1 + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + k);
       f32x4 w[MAXR];
 #pragma unroll
       for (int q = 0; q < MAXR; ++q) {
@@ -223,14 +231,14 @@ __device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_
 #pragma unroll
       for (int q = 0; q < MAXR; ++q)
 #pragma unroll
-        for (int b = 0; b < kBT; ++b) acc[q][b] = dot4(w[q], h[b], acc[q][b]);
+        for (int b = 0; b < UB; ++b) acc[q][b] = dot4(w[q], h[b], acc[q][b]);
     }
 #pragma unroll
     for (int q = 0; q < MAXR; ++q) {
       const int r = wave + q * NW;
       if (r < a.NO) {  // wave-uniform
-        const float v = wave_reduce_multi<kBT>(acc[q], lane);
-        if ((lane & 7) == 0) s_mol[(lane >> 3) * kMaxNO + r] = v + b2[r];
+        const float v = wave_reduce_multi<UB>(acc[q], lane);
+        if ((lane & (64 / UB - 1)) == 0) s_mol[(lane / (64 / UB)) * kMaxNO + r] = v + b2[r];
       }
     }
   }
@@ -256,68 +264,113 @@ __device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_
   __syncthreads();
 }
 
-// x_(l-1)(t) chunk for the current-tap fold: from the ring, or (l-1 == 0) first_conv(input)
-__device__ __forceinline__ void load_xprev(const WnArgs& a, int lprev, int t, int b0, int nb, int i,
-                                           const float* s_in, f32x4 (&x)[kBT]) {
-  if (lprev == 0) {
-    const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
-#pragma unroll
-    for (int b = 0; b < kBT; ++b) {
-      const float in_v = s_in ? s_in[b] : a.yin[(int64_t)(b0 + (b < nb ? b : 0)) * a.T + t];
-      x[b][0] = in_v * fw[0] + fb[0];
-      x[b][1] = in_v * fw[1] + fb[1];
-      x[b][2] = in_v * fw[2] + fb[2];
-      x[b][3] = in_v * fw[3] + fb[3];
-    }
-  } else {
-    const float* xr = a.ring + (((int64_t)lprev * a.RING + (t & (a.RING - 1))) * a.B + b0) * a.R + i;
-#pragma unroll
-    for (int b = 0; b < kBT; ++b) x[b] = ld4(xr + (int64_t)(b < nb ? b : 0) * a.R);
-  }
-}
+// layer(l): one workgroup per kRP gate pairs (o, o + G/2) and kUB utterances: 2*kRP gate rows
+// x kUB utterances per workgroup (4 x 4 reads fewer operand bytes per CU than 2 rows x 8
+// utterances: (rows + utterances) x K floats; the per-CU operand fill bounds the launch).
+// Waves 0..kGW-1 split the GEMV's KX inputs in 256-float chunks (no chunk straddles a
+// segment: R, H % 256 == 0); for l >= 1 waves kGW..kGW+kRW-1 do layer l-1's residual rows
+// (R/H rows of x_l(t) and S/H skip rows per gate pair) with every operand they need, the
+// skip accumulator and the residual input included, loaded at kernel start.  Loads that
+// do not depend on the step (weights, biases, the skip accumulator) are issued before the
+// step counter is read.
+constexpr int kRP = 2;                    // gate pairs per workgroup
+constexpr int kUB = 4;                    // utterances per workgroup
+constexpr int kGW = 7;                    // gate waves (KX = 1792 = 7 chunks of 256 for r9y9)
+constexpr int kRW = 2;                    // residual waves
+constexpr int kResRows = 4;               // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
+constexpr int kLayerThreads = 64 * (kGW + kRW);
 
-// layer(l): one workgroup per gate pair (o, o + G/2) and batch tile.  Waves 0..NW-1 split the
-// GEMV's KX inputs in 256-float chunks (no chunk straddles a segment: R, H % 256 == 0);
-// for l >= 1 wave NW does layer l-1's residual rows (R/H of x_l(t) and S/H skip rows per
-// workgroup).
-template <int NW, bool L0>
-__global__ __launch_bounds__(64 * (NW + 1)) void wn_layer_kernel(WnArgs a, int layer, int slot, int targ) {
-  __shared__ float s_mol[L0 ? kBT * kMaxNO : 1];
-  __shared__ float s_in[kBT];
-  __shared__ float s_red[NW][2 * kBT];
-  const int t = read_step(a, slot, 0, targ);
+template <bool L0>
+__global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int layer, int slot, int targ) {
+  __shared__ float s_mol[L0 ? kUB * kMaxNO : 1];
+  __shared__ float s_in[kUB];
+  __shared__ float s_red[kGW][2 * kRP * kUB];
+  if (WN_ABLATE == 5) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b0 = blockIdx.y * kBT;
-  const int nb = min(kBT, a.B - b0);
+  const int b0 = blockIdx.y * kUB;
+  const int nb = min(kUB, a.B - b0);
   const int H = a.G / 2;
-  const int o = blockIdx.x;
-  // the conditioning pre-activations (HBM, written by the chunk GEMM) are fetched first so
-  // their latency hides under the GEMV instead of trailing it
-  float pre_a = 0.f, pre_b = 0.f;
-  if ((int)threadIdx.x < nb) {
-    const float* pre = a.pre + ((int64_t)(t % a.Tch) * a.B + b0 + threadIdx.x) * ((int64_t)a.n_layers * a.G) +
-                       (int64_t)layer * a.G;
-    pre_a = pre[o];
-    pre_b = pre[o + H];
-  }
-  if (L0) sample_stage<NW + 1>(a, t, b0, nb, s_mol, s_in);
+  const int o0 = blockIdx.x * kRP;          // first gate pair of the workgroup
   const int KX = gate_width(a);
-  const int KT = (a.K - 1) * a.R;              // end of the ring taps
+  const int KT = (a.K - 1) * a.R;           // end of the ring taps
   const float* base = layer_base(a, layer);
-  const int d = 1 << (layer % a.lps);
-  if (wave < NW) {
-    const float* wa = base + (int64_t)o * KX;
-    const float* wb = base + (int64_t)(o + H) * KX;
-    const float* gprev = L0 ? nullptr : gbuf_of(a, layer - 1);
-    float acc[2 * kBT];
+  // ---- step-independent loads first: this wave's first weight chunk / residual operands
+  f32x4 w0[2 * kRP];
+  const int c0 = wave;
+  if (wave < kGW && c0 * 256 < KX) {
 #pragma unroll
-    for (int j = 0; j < 2 * kBT; ++j) acc[j] = 0.f;
-    for (int c = wave; c * 256 < KX; c += NW) {
+    for (int r = 0; r < 2 * kRP; ++r) {
+      const int row = o0 + (r >> 1) + (r & 1) * H;
+      if ((WN_ABLATE == 3 || WN_ABLATE == 6) && !L0) w0[r] = f32x4{0.01f * lane, 0.f, 0.f, 0.f};
+      else w0[r] = ld4(base + (int64_t)row * KX + c0 * 256 + lane * 4);
+    }
+  }
+  const int rx = a.R / H, nrp = rx + a.S / H;            // residual rows per gate pair
+  const int lp = layer - 1;
+  const float* pbase = L0 ? nullptr : layer_base(a, lp) + (int64_t)a.G * KX;
+  const float* pbias = L0 ? nullptr : pbase + (int64_t)(a.R + a.S) * H;
+  const int rwave = wave - kGW;
+  int rrow[kResRows];
+  f32x4 rw[kResRows];
+  float rbias = 0.f, rskip = 0.f;
+  // after the butterfly, lane L (L % (64/(kResRows*kUB)) == 0) holds sum index L/4 = q*kUB + b
+  const int my_q = (lane >> 2) / kUB, my_b = (lane >> 2) % kUB;
+  const int my_gb = b0 + (my_b < nb ? my_b : 0);
+  const bool resid = !L0 && rwave >= 0 && WN_ABLATE != 4 && WN_ABLATE != 6;
+  if (resid) {
+#pragma unroll
+    for (int q = 0; q < kResRows; ++q) {
+      int j = rwave + q * kRW;                            // residual row index in the workgroup
+      if (j >= kRP * nrp) j = 0;                          // padding rows: computed and dropped
+      const int p = j / nrp, jj = j - p * nrp;
+      rrow[q] = jj < rx ? (o0 + p) * rx + jj : a.R + (o0 + p) * (nrp - rx) + (jj - rx);
+      rw[q] = ld4(pbase + (int64_t)rrow[q] * H + lane * 4);   // H == 256: one chunk per lane
+    }
+    int myrow = rrow[0];
+#pragma unroll
+    for (int q = 1; q < kResRows; ++q) if (q == my_q) myrow = rrow[q];
+    rbias = pbias[myrow];
+    if (myrow >= a.R) rskip = a.skip[(int64_t)my_gb * a.S + (myrow - a.R)];
+  }
+  // ---- the step, and everything addressed by it
+  const int t = read_step(a, slot, 0, targ);
+  float pre_v = 0.f;            // conditioning pre-activation of (gate row, utterance) threadIdx.x
+  if ((int)threadIdx.x < 2 * kRP * kUB) {
+    const int r = threadIdx.x / kUB, b = threadIdx.x % kUB;
+    const int row = o0 + (r >> 1) + (r & 1) * H;
+    pre_v = a.pre[((int64_t)(t % a.Tch) * a.B + b0 + (b < nb ? b : 0)) * ((int64_t)a.n_layers * a.G) +
+                  (int64_t)layer * a.G + row];
+  }
+  float rres = 0.f;
+  const int slot_t = t & (a.RING - 1);
+  if (resid) {
+    int myrow = rrow[0];
+#pragma unroll
+    for (int q = 1; q < kResRows; ++q) if (q == my_q) myrow = rrow[q];
+    if (myrow < a.R)
+      rres = lp == 0 ? a.yin[(int64_t)my_gb * a.T + t] * a.packed[myrow] + a.packed[a.R + myrow]
+                     : a.ring[(((int64_t)lp * a.RING + slot_t) * a.B + my_gb) * a.R + myrow];
+  }
+  if (L0) sample_stage<kGW + kRW, kUB>(a, t, b0, nb, s_mol, s_in);
+  const int d = 1 << (layer % a.lps);
+  auto urow = [&](int b) { return (int64_t)(b0 + (b < nb ? b : 0)); };
+  if (wave < kGW) {
+    const float* gprev = L0 ? nullptr : gbuf_of(a, layer - 1);
+    float acc[2 * kRP * kUB];
+#pragma unroll
+    for (int j = 0; j < 2 * kRP * kUB; ++j) acc[j] = 0.f;
+    for (int c = c0; c * 256 < KX; c += kGW) {
       const int kc = c * 256;
       const int k = kc + lane * 4;
-      const f32x4 va = ld4(wa + k), vb = ld4(wb + k);   // weights do not depend on the step: issue first
-      f32x4 x[kBT];
-      if (kc < KT) {                           // ring taps 0..K-2 of x_l
+      f32x4 w[2 * kRP];
+#pragma unroll
+      for (int r = 0; r < 2 * kRP; ++r)
+        w[r] = c == c0 ? w0[r] : ld4(base + (int64_t)(o0 + (r >> 1) + (r & 1) * H) * KX + k);
+      f32x4 x[kUB];
+      if ((WN_ABLATE == 2 || WN_ABLATE == 6) && !L0) {
+#pragma unroll
+        for (int b = 0; b < kUB; ++b) x[b] = f32x4{0.5f, 0.25f, 0.f, (float)b};
+      } else if (kc < KT) {                    // ring taps 0..K-2 of x_l
         const int tap = kc / a.R;
         const int tau = t - (a.K - 1 - tap) * d;
         if (tau < 0) continue;                 // wave-uniform: zero history before the first sample
@@ -325,109 +378,104 @@ __global__ __launch_bounds__(64 * (NW + 1)) void wn_layer_kernel(WnArgs a, int l
         if (L0) {
           const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
 #pragma unroll
-          for (int b = 0; b < kBT; ++b) {
-            const float in_v = a.yin[(int64_t)(b0 + (b < nb ? b : 0)) * a.T + tau];
+          for (int b = 0; b < kUB; ++b) {
+            const float in_v = a.yin[urow(b) * a.T + tau];
             x[b][0] = in_v * fw[0] + fb[0];
             x[b][1] = in_v * fw[1] + fb[1];
             x[b][2] = in_v * fw[2] + fb[2];
             x[b][3] = in_v * fw[3] + fb[3];
           }
         } else {
-          const float* xr = a.ring + (((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B + b0) * a.R + i;
+          const float* xr = a.ring + ((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B * a.R + i;
 #pragma unroll
-          for (int b = 0; b < kBT; ++b) x[b] = ld4(xr + (int64_t)(b < nb ? b : 0) * a.R);
+          for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
         }
       } else if (kc < KT + H) {                // g_(l-1) (layer 0: zero weights, skipped)
         if (L0) continue;
         const int j = k - KT;
 #pragma unroll
-        for (int b = 0; b < kBT; ++b) x[b] = ld4(gprev + (int64_t)(b0 + (b < nb ? b : 0)) * H + j);
+        for (int b = 0; b < kUB; ++b) x[b] = ld4(gprev + urow(b) * H + j);
       } else {                                 // current tap: x_(l-1)(t) (layer 0: x_0(t))
         const int i = k - KT - H;
-        load_xprev(a, L0 ? 0 : layer - 1, t, b0, nb, i, L0 ? s_in : nullptr, x);
-      }
+        if (L0) {
+          const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
 #pragma unroll
-      for (int b = 0; b < kBT; ++b) {
-        acc[b] = dot4(va, x[b], acc[b]);
-        acc[kBT + b] = dot4(vb, x[b], acc[kBT + b]);
-      }
-    }
-    const float s = wave_reduce_multi<2 * kBT>(acc, lane);
-    if ((lane & 3) == 0) s_red[wave][lane >> 2] = s;
-  } else if (!L0) {
-    // layer l-1's residual rows: x_l(t) rows [o*R/H, (o+1)*R/H) and skip rows [o*S/H, ...).
-    // All loads of the wave (g once, every row's weights and residual) are issued before the
-    // first reduction: this wave is on the launch's critical path.
-    const int lp = layer - 1;
-    const float* pbase = layer_base(a, lp) + (int64_t)a.G * KX;
-    const float* bias = pbase + (int64_t)(a.R + a.S) * H;
-    const float* gprev = gbuf_of(a, lp);
-    const int rx = a.R / H, nr = rx + a.S / H;   // <= kMaxResid (host check)
-    const int slot_t = t & (a.RING - 1);
-    const int bl = (lane >> 3) < nb ? (lane >> 3) : 0;
-    const int gbl = b0 + bl;
-    int rows[kMaxResid];
-    float res[kMaxResid], bsv[kMaxResid];
+          for (int b = 0; b < kUB; ++b) {
+            const float in_v = s_in[b];
+            x[b][0] = in_v * fw[0] + fb[0];
+            x[b][1] = in_v * fw[1] + fb[1];
+            x[b][2] = in_v * fw[2] + fb[2];
+            x[b][3] = in_v * fw[3] + fb[3];
+          }
+        } else if (layer - 1 == 0) {
+          const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
 #pragma unroll
-    for (int q = 0; q < kMaxResid; ++q) {
-      const int qq = q < nr ? q : 0;
-      rows[q] = qq < rx ? o * rx + qq : a.R + o * (nr - rx) + (qq - rx);
-      bsv[q] = bias[rows[q]];
-      res[q] = 0.f;
-      if (rows[q] < a.R)
-        res[q] = lp == 0 ? a.yin[(int64_t)gbl * a.T + t] * a.packed[rows[q]] + a.packed[a.R + rows[q]]
-                         : a.ring[(((int64_t)lp * a.RING + slot_t) * a.B + gbl) * a.R + rows[q]];
-    }
-    float acc[kMaxResid][kBT];
-#pragma unroll
-    for (int q = 0; q < kMaxResid; ++q)
-#pragma unroll
-      for (int b = 0; b < kBT; ++b) acc[q][b] = 0.f;
-    for (int k = lane * 4; k < H; k += 256) {
-      f32x4 g[kBT], wv[kMaxResid];
-#pragma unroll
-      for (int b = 0; b < kBT; ++b) g[b] = ld4(gprev + (int64_t)(b0 + (b < nb ? b : 0)) * H + k);
-#pragma unroll
-      for (int q = 0; q < kMaxResid; ++q) wv[q] = ld4(pbase + (int64_t)rows[q] * H + k);
-#pragma unroll
-      for (int q = 0; q < kMaxResid; ++q)
-#pragma unroll
-        for (int b = 0; b < kBT; ++b) acc[q][b] = dot4(wv[q], g[b], acc[q][b]);
-    }
-    const int b = lane >> 3;
-#pragma unroll
-    for (int q = 0; q < kMaxResid; ++q) {
-      const float v0 = wave_reduce_multi<kBT>(acc[q], lane);
-      if (q < nr && (lane & 7) == 0 && b < nb) {
-        const int gb = b0 + b;
-        const int row = rows[q];
-        const float v = v0 + bsv[q];
-        if (row < a.R) {
-          a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gb) * a.R + row] = (v + res[q]) * kSqrtHalf;
+          for (int b = 0; b < kUB; ++b) {
+            const float in_v = a.yin[urow(b) * a.T + t];
+            x[b][0] = in_v * fw[0] + fb[0];
+            x[b][1] = in_v * fw[1] + fb[1];
+            x[b][2] = in_v * fw[2] + fb[2];
+            x[b][3] = in_v * fw[3] + fb[3];
+          }
         } else {
-          float* sp = a.skip + (int64_t)gb * a.S + (row - a.R);
-          if (lp == 0) *sp = v;
-          else *sp = a.legacy ? (*sp + v) * kSqrtHalf : (*sp + v);
+          const float* xr = a.ring + ((int64_t)(layer - 1) * a.RING + slot_t) * a.B * a.R + i;
+#pragma unroll
+          for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
         }
+      }
+#pragma unroll
+      for (int r = 0; r < 2 * kRP; ++r)
+#pragma unroll
+        for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w[r], x[b], acc[r * kUB + b]);
+    }
+    const float s = WN_ABLATE == 7 ? acc[lane & 15] : wave_reduce_multi<2 * kRP * kUB>(acc, lane);
+    if ((lane & (64 / (2 * kRP * kUB) - 1)) == 0) s_red[wave][lane / (64 / (2 * kRP * kUB))] = s;
+  } else if (resid) {
+    // layer l-1's residual rows: x_l(t) and skip rows of this workgroup's gate pairs
+    const float* gprev = gbuf_of(a, lp);
+    f32x4 g[kUB];
+#pragma unroll
+    for (int b = 0; b < kUB; ++b) g[b] = ld4(gprev + urow(b) * H + lane * 4);
+    float acc[kResRows * kUB];
+#pragma unroll
+    for (int q = 0; q < kResRows; ++q)
+#pragma unroll
+      for (int b = 0; b < kUB; ++b) acc[q * kUB + b] = dot4(rw[q], g[b], 0.f);
+    const float v0 = wave_reduce_multi<kResRows * kUB>(acc, lane);
+    const int j = rwave + my_q * kRW;
+    if ((lane & 3) == 0 && j < kRP * nrp && my_b < nb) {
+      int row = rrow[0];
+#pragma unroll
+      for (int q = 1; q < kResRows; ++q) if (q == my_q) row = rrow[q];
+      const int gb = b0 + my_b;
+      const float v = v0 + rbias;
+      if (row < a.R) {
+        a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gb) * a.R + row] = (v + rres) * kSqrtHalf;
+      } else {
+        float* sp = a.skip + (int64_t)gb * a.S + (row - a.R);
+        if (lp == 0) *sp = v;
+        else *sp = a.legacy ? (rskip + v) * kSqrtHalf : (rskip + v);
       }
     }
   }
+  // pre-activations: lane r*kUB + b of wave 0 holds gate row r's; the pair's two rows are
+  // fetched by whole-wave shuffles (every lane active) before the final branch
+  const int fp = (lane / kUB) % kRP, fb = lane % kUB;
+  const float pre_a = __shfl(pre_v, (2 * fp) * kUB + fb);
+  const float pre_b = __shfl(pre_v, (2 * fp + 1) * kUB + fb);
   __syncthreads();
-  if ((int)threadIdx.x < nb) {
-    const int b = threadIdx.x;
-    float za = 0.f, zb = 0.f;
+  if ((int)threadIdx.x < kRP * kUB && fb < nb) {
+    float za = pre_a, zb = pre_b;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) { za += s_red[w][b]; zb += s_red[w][kBT + b]; }
-    const int gb = b0 + b;
-    za += pre_a;
-    zb += pre_b;
-    gbuf_of(a, layer)[(int64_t)gb * H + o] = tanhf(za) * avc_sigmoid(zb);
+    for (int w = 0; w < kGW; ++w) { za += s_red[w][(2 * fp) * kUB + fb]; zb += s_red[w][(2 * fp + 1) * kUB + fb]; }
+    gbuf_of(a, layer)[(int64_t)(b0 + fb) * H + o0 + fp] = tanhf(za) * avc_sigmoid(zb);
   }
 }
 
 // tail: the last layer's skip rows, one wave per row.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, int targ) {
+  if (WN_ABLATE == 5) return;
   const int t = read_step(a, slot, 0, targ);
   (void)t;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -465,6 +513,7 @@ __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, in
 // head: h1 = relu(W1 relu(skips) + b1); advances the step counter.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, int targ) {
+  if (WN_ABLATE == 5) return;
   read_step(a, slot, 1, targ);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
@@ -499,7 +548,7 @@ __global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, in
 __global__ __launch_bounds__(256) void wn_final_sample_kernel(WnArgs a, int tp1) {
   __shared__ float s_mol[kBT * kMaxNO];
   const int b0 = blockIdx.y * kBT;
-  sample_stage<4>(a, tp1, b0, min(kBT, a.B - b0), s_mol, nullptr);
+  sample_stage<4, kBT>(a, tp1, b0, min(kBT, a.B - b0), s_mol, nullptr);
 }
 
 __global__ void wn_set_ctr_kernel(int* ctr, int t) { ctr[0] = t; }
@@ -568,10 +617,10 @@ hipStream_t g_capture_stream[64] = {};
 int enqueue_step(const WnArgs& a, hipStream_t s, int targ) {
   const int H = a.G / 2;
   const int nbt = (a.B + kBT - 1) / kBT;
-  constexpr int NT = 64 * (kGateWaves + 1);
+  const dim3 lgrid(H / kRP, (a.B + kUB - 1) / kUB);
   for (int l = 0; l < a.n_layers; ++l) {
-    if (l == 0) hipLaunchKernelGGL((wn_layer_kernel<kGateWaves, true>), dim3(H, nbt), dim3(NT), 0, s, a, 0, 0, targ);
-    else hipLaunchKernelGGL((wn_layer_kernel<kGateWaves, false>), dim3(H, nbt), dim3(NT), 0, s, a, l, l, targ);
+    if (l == 0) hipLaunchKernelGGL((wn_layer_kernel<true>), lgrid, dim3(kLayerThreads), 0, s, a, 0, 0, targ);
+    else hipLaunchKernelGGL((wn_layer_kernel<false>), lgrid, dim3(kLayerThreads), 0, s, a, l, l, targ);
   }
   hipLaunchKernelGGL((wn_tail_kernel<4>), dim3((a.S + 3) / 4, nbt), dim3(256), 0, s, a, a.n_layers, targ);
   hipLaunchKernelGGL((wn_head_kernel<4>), dim3((a.S + 3) / 4, nbt), dim3(256), 0, s, a, a.n_layers + 1, targ);
@@ -677,8 +726,10 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
                     taps >= 1,
                 "%s: bad layer structure layers=%d per_stack=%d taps=%d", fn, n_layers, layers_per_stack, taps);
   AVC_CHECK_ARG(R > 0 && R % 256 == 0 && G > 0 && G % 512 == 0 && S > 0 && S % 256 == 0 &&
-                    R % (G / 2) == 0 && S % (G / 2) == 0 && (R + S) / (G / 2) <= kMaxResid && taps >= 2,
-                "%s: need R, G/2, S multiples of 256 with G/2 dividing R and S, taps >= 2 (R=%d, G/2=%d, S=%d)", fn,
+                    R % (G / 2) == 0 && S % (G / 2) == 0 && G / 2 == 256 &&
+                    kRP * ((R + S) / (G / 2)) <= kRW * kResRows && taps >= 2,
+                "%s: need G/2 == 256, R and S multiples of 256 with (R + S) / (G/2) <= %d, taps >= 2 "
+                "(R=%d, G/2=%d, S=%d)", fn, kRW * kResRows / kRP,
                 R, G / 2, S);
   AVC_CHECK_ARG(n_out % 3 == 0 && n_out / 3 >= 1 && n_out / 3 <= 10 && n_out <= kMaxNO,
                 "%s: out_channels %d is not 3 x (1..10) logistic mixtures", fn, n_out);

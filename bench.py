@@ -104,6 +104,92 @@ def lstm_roofline(solver, B, T, dev):
                              "frac": round(a1 / HBM_PEAK_GBS, 4)}}
 
 
+def blstm_roofline(dev, B, T, H=32):
+    """The encoder BLSTM recurrence (model_vc_mel.py:61,72-73; blstm_fwd/bwd_kernel: one
+    launch per layer covers all T steps of both directions) priced with SURVEY §8d's
+    formula: per step and direction W_hh (4H x H) + gates_x (B x 4H) + h read, c read+write,
+    h write (B x H each) = 82 KB at H=32, B=64 -> x T x 2 directions per launch.  Timed with
+    events on the launch stream (one kernel per call), median of 5."""
+    from autovc_amd import _lib
+    g = torch.Generator().manual_seed(11)
+    gx = (torch.randn(B, T, 8 * H, generator=g) * 0.5).to(dev)
+    Wf, Wb = ((torch.rand(4 * H, H, generator=g) * 2 - 1).div_(H ** 0.5).to(dev) for _ in range(2))
+    h = torch.empty(B, T, 2 * H, device=dev)
+    c = torch.empty(B, T, 2 * H, device=dev)
+    gates = torch.empty(B, T, 8 * H, device=dev)
+    dh = torch.randn(B, T, 2 * H, generator=g).to(dev)
+    dG = torch.empty(B, T, 8 * H, device=dev)
+    st = _lib.stream_ptr(dev)
+    fwd = lambda: _lib.call("autovc_blstm_fwd_f32", B, T, H, 2, gx.data_ptr(), Wf.data_ptr(), Wb.data_ptr(),  # noqa: E731
+                            h.data_ptr(), c.data_ptr(), gates.data_ptr(), st)
+    bwd = lambda: _lib.call("autovc_blstm_bwd_f32", B, T, H, 2, dh.data_ptr(), gates.data_ptr(), c.data_ptr(),  # noqa: E731
+                            Wf.data_ptr(), Wb.data_ptr(), dG.data_ptr(), st)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        return sorted(ts)[2]
+
+    per_step_dir = 4 * H * H * 4 + B * 4 * H * 4 + 4 * B * H * 4
+    nbytes = per_step_dir * T * 2
+    out = {"kernel": f"blstm_fwd_kernel (encoder BLSTM layer, H={H}, B={B}, T={T}, both directions per launch)",
+           "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "bytes_per_launch": nbytes,
+           "bytes_per_step_direction": per_step_dir, "traffic": None}
+    for name, fn in (("fwd", fwd), ("bwd", bwd)):
+        us = timed(fn)
+        a = nbytes / (us * 1e-6) / 1e9
+        out[name] = {"avg_launch_us": round(us, 2), "achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBS, 4)}
+    out["achieved"], out["frac"] = out["fwd"]["achieved"], out["fwd"]["frac"]
+    out["note"] = ("latency-bound: 128 dependent steps per launch; the 82 KB per step-direction the formula "
+                   "counts fit in L2/LDS, so HBM never limits this kernel (SURVEY §8d expects << 40 %)")
+    return out
+
+
+def step_roofline(B, ms_per_step, precision="fp32"):
+    """Whole-step MFMA fraction: algorithmic FLOPs (convs, LSTMs, linear
+    fwd + bwd, the second encoder pass; 24.60 GFLOP per sample) / step time / peak."""
+    flop = 24.60e9 * B
+    peak = 157.3 if precision == "fp32" else 2500.0
+    tf = flop / (ms_per_step * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(tf / peak, 4), "flop_per_step": flop,
+            "note": f"{precision} dense MFMA peak (MI355X_MICROARCH.md); FLOPs = 2 x MACs of convs/LSTMs/linear, "
+                    "fwd+bwd, both encoder passes (SURVEY §8d C2)"}
+
+
+def cpu_share():
+    """(threads this process may run on, physical cores of the host).  On the GPU box the
+    process is given a share of the host (16 CPUs per GPU); os.cpu_count() shows the whole
+    machine."""
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:     # the box's per-job CPU share (16 per GPU)
+        allowed = min(allowed, int(env))
+    phys = set()
+    try:
+        pid = core = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+                phys.add((pid, core))
+    except OSError:
+        pass
+    return allowed, len(phys) or (os.cpu_count() or 1)
+
+
 def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=True):
     """BASELINE config 4 / SURVEY §8d C4: r9y9 WaveNet (24 layers, 512 residual channels),
     8 utterances x 128 conditioning frames (32,768 samples = 2.048 s each) synthesised in one
@@ -131,14 +217,21 @@ def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=
                                                        model.out_channels)
     step_bytes = 4 * packed
     achieved = step_bytes * T / dt / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "wavenet_pmc.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_sample_step")
     out = {"workload": f"r9y9 WaveNet incremental synthesis, {n_utt} utterances x {T} samples (16 kHz), fp32",
            "samples_per_s": round(n_utt * T / dt, 1), "rtf_aggregate": round(n_utt * T / dt / 16000.0, 3),
            "rtf_per_stream": round(T / 16000.0 / dt, 3), "wall_s": round(dt, 3),
            "us_per_sample_step": round(dt / T * 1e6, 2),
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "bytes_per_step": step_bytes,
-                        "note": "weight-streaming convention: packed per-step weights once per sample step"}}
+                        "note": "weight-streaming convention: packed per-step weights once per sample step; "
+                                "traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per sample step summed over its "
+                                "launches (profiles/wavenet_pmc.json)"}}
     if cpu:
         out["cpu_baseline"] = wavenet_cpu_baseline(n_utt, seconds_cpu)
         out["vs_cpu_baseline"] = round(out["samples_per_s"] / out["cpu_baseline"]["value"], 1)
@@ -149,7 +242,7 @@ def wavenet_cpu_baseline(n_utt, seconds):
     """oracle/wavenet.py (fp32 torch CPU ops, the reference's own per-step structure) on a
     bounded number of sample steps of the same batch."""
     from oracle import wavenet as ow
-    threads = min(16, os.cpu_count() or 1)
+    threads, _ = cpu_share()
     torch.set_num_threads(threads)
     hp = ow.HPARAMS
     o = ow.OracleWaveNet(ow.make_weights(hp), hp, dtype=torch.float32)
@@ -327,10 +420,22 @@ def e2e_bench(dev, rank, world, per_rank=8):
 
 def cpu_baseline(B, T, seconds=15.0):
     """The oracle's CPU restatement of the same training step (fused torch CPU LSTM, conv1d,
-    batch_norm, Adam — the reference's own CPU ops), timed on this host."""
-    from oracle import generator as og
-    threads = min(16, os.cpu_count() or 1)
+    batch_norm, Adam — the reference's own CPU ops), timed on this host on every CPU this
+    process may use (the GPU box gives a job a 16-CPU share of the host; the host's
+    physical core count is stated beside it).  Also the BASELINE config-1 shape (B=2)."""
+    threads, phys = cpu_share()
     torch.set_num_threads(threads)
+    out = _cpu_step(B, T, threads, seconds)
+    out["host_physical_cores"] = phys
+    c1 = _cpu_step(2, T, threads, seconds / 3)
+    out["c1"] = {"value": c1["value"], "unit": "mel-frames/s", "cores": threads, "kind": "port",
+                 "sample": c1["sample"].replace("oracle training steps", "oracle training steps (BASELINE config 1 "
+                                                "shape: batch 2)")}
+    return out
+
+
+def _cpu_step(B, T, threads, seconds):
+    from oracle import generator as og
     P = og.make_weights()
     params = [v for k, v in P.items() if v.dtype == torch.float32 and "running_" not in k]
     for v in params:
@@ -438,9 +543,10 @@ def main():
               "final_loss": round(float(lb[0].item()), 6),
               "note": "BASELINE config 3 precision; the headline value above is config 2 (fp32)"}
 
-    roof = None
+    roof = blstm = None
     if not args.no_roofline and rank == 0:
         roof = lstm_roofline(solver, B, T, dev)
+        blstm = blstm_roofline(dev, B, T)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(B, T)
@@ -467,12 +573,15 @@ def main():
                        "hip_graph": not args.no_graph,
                        "dim_neck": 32, "dim_emb": 256, "dim_pre": 512, "freq": 32},
             "final_loss": round(last_loss, 6),
-            "roofline": roof, "cpu_baseline": cpu, "bf16": bf,
+            "roofline": roof, "blstm_roofline": blstm,
+            "step_roofline": step_roofline(B, dt / args.steps * 1000, args.precision),
+            "cpu_baseline": cpu, "bf16": bf,
             "wavenet": wn,
             "e2e": e2e, "frontend": fe,
         }
         if cpu:
             line["vs_cpu_baseline"] = round(value / cpu["value"], 2)
+            line["vs_cpu_baseline_c1"] = round(value / cpu["c1"]["value"], 2)
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.barrier()
