@@ -279,6 +279,65 @@ constexpr int kGW = 7;                    // gate waves (KX = 1792 = 7 chunks of
 constexpr int kRW = 2;                    // residual waves
 constexpr int kResRows = 4;               // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
 constexpr int kLayerThreads = 64 * (kGW + kRW);
+constexpr int kTailWaves = 2;             // tail / head: one wave per output row
+
+// MoL head output of the previous step for the utterance tile, in two halves so that its
+// loads (W2 rows, h1) are issued at kernel start: the first reads this wave's W2 rows and
+// h1 chunk (S == 256: one 4-float chunk per lane), the second reduces them into s_mol.
+constexpr int kMolRows = (kMaxNO + kGW + kRW - 1) / (kGW + kRW);   // W2 rows per wave
+
+__device__ __forceinline__ void mol_load(const WnArgs& a, int wave, int lane, int b0, int nb,
+                                         f32x4 (&mw)[kMolRows], f32x4 (&mh)[kUB]) {
+  const float* W2 = head_base(a) + (int64_t)a.S * a.S + a.S;
+#pragma unroll
+  for (int q = 0; q < kMolRows; ++q) {
+    const int r = wave + q * (kGW + kRW);
+    mw[q] = ld4(W2 + (int64_t)(r < a.NO ? r : 0) * a.S + lane * 4);
+  }
+#pragma unroll
+  for (int b = 0; b < kUB; ++b) mh[b] = ld4(a.h1 + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + lane * 4);
+}
+
+// s_mol <- MoL parameters of step tp1 - 1; then s_in <- the input of step tp1 (sampled, or
+// the teacher value); block 0 of the tile records the sample and the input.
+__device__ void mol_finish(const WnArgs& a, int tp1, int wave, int lane, int b0, int nb, const f32x4 (&mw)[kMolRows],
+                           const f32x4 (&mh)[kUB], float* s_mol, float* s_in) {
+  const int tp = tp1 - 1;
+  if (tp >= 0) {
+    const float* b2 = head_base(a) + (int64_t)a.S * a.S + a.S + (int64_t)a.NO * a.S;
+#pragma unroll
+    for (int q = 0; q < kMolRows; ++q) {
+      const int r = wave + q * (kGW + kRW);
+      float acc[kUB];
+#pragma unroll
+      for (int b = 0; b < kUB; ++b) acc[b] = dot4(mw[q], mh[b], 0.f);
+      if (r < a.NO) {  // wave-uniform
+        const float v = wave_reduce_multi<kUB>(acc, lane);
+        if ((lane & (64 / kUB - 1)) == 0) s_mol[(lane / (64 / kUB)) * kMaxNO + r] = v + b2[r];
+      }
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nb) {
+    const int b = threadIdx.x;
+    const int gb = b0 + b;
+    float in_v = 0.f;
+    float smp = 0.f;
+    if (tp >= 0) smp = mol_sample(s_mol + b * kMaxNO, a.NO / 3, tp, a.utt_base + gb, a);
+    if (a.teacher != nullptr && tp1 < a.teacher_len) in_v = a.teacher[(int64_t)gb * a.teacher_len + tp1];
+    else if (tp >= 0) in_v = smp;
+    s_in[b] = in_v;
+    if (blockIdx.x == 0) {
+      if (tp1 < a.T) a.yin[(int64_t)gb * a.T + tp1] = in_v;
+      if (tp >= 0) {
+        a.y_out[(int64_t)gb * a.T + tp] = smp;
+        if (a.mol_out)
+          for (int j = 0; j < a.NO; ++j) a.mol_out[((int64_t)gb * a.T + tp) * a.NO + j] = s_mol[b * kMaxNO + j];
+      }
+    }
+  }
+  __syncthreads();
+}
 
 template <bool L0>
 __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int layer, int slot, int targ) {
@@ -294,128 +353,178 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   const int KX = gate_width(a);
   const int KT = (a.K - 1) * a.R;           // end of the ring taps
   const float* base = layer_base(a, layer);
-  // ---- step-independent loads first: this wave's first weight chunk / residual operands
-  f32x4 w0[2 * kRP];
+  const float* gprev = L0 ? nullptr : gbuf_of(a, layer - 1);
+  auto urow = [&](int b) { return (int64_t)(b0 + (b < nb ? b : 0)); };
+  auto wrow = [&](int r) { return o0 + (r >> 1) + (r & 1) * H; };   // gate row r of the workgroup
+
+  // ---------------- prologue part 1: every load that does not depend on the step
+  // gate waves: the first chunk's weights (and, for the g_(l-1) chunk, its inputs: gbuf is
+  // addressed by the layer only)
   const int c0 = wave;
-  if (wave < kGW && c0 * 256 < KX) {
+  const bool gate = wave < kGW && c0 * 256 < KX;
+  const int kc0 = c0 * 256;
+  const int cat0 = kc0 < KT ? 0 : (kc0 < KT + H ? 1 : 2);    // 0 ring taps, 1 g_(l-1), 2 current tap
+  f32x4 w0[2 * kRP], x0[kUB], fw0 = {}, fb0 = {};
+  if (gate) {
 #pragma unroll
     for (int r = 0; r < 2 * kRP; ++r) {
-      const int row = o0 + (r >> 1) + (r & 1) * H;
       if ((WN_ABLATE == 3 || WN_ABLATE == 6) && !L0) w0[r] = f32x4{0.01f * lane, 0.f, 0.f, 0.f};
-      else w0[r] = ld4(base + (int64_t)row * KX + c0 * 256 + lane * 4);
+      else w0[r] = ld4(base + (int64_t)wrow(r) * KX + kc0 + lane * 4);
+    }
+    if (cat0 == 1 && !L0) {
+#pragma unroll
+      for (int b = 0; b < kUB; ++b) x0[b] = ld4(gprev + urow(b) * H + (kc0 - KT) + lane * 4);
+    }
+    if ((L0 && cat0 != 1) || (!L0 && layer == 1 && cat0 == 2)) {     // x_0 = first_conv(input)
+      const int i = (cat0 == 0 ? kc0 % a.R : kc0 - KT - H) + lane * 4;
+      fw0 = ld4(a.packed + i);
+      fb0 = ld4(a.packed + a.R + i);
     }
   }
+  // residual waves (layer l-1's x_l(t) and skip rows): weights, biases, skip accumulator, g
   const int rx = a.R / H, nrp = rx + a.S / H;            // residual rows per gate pair
   const int lp = layer - 1;
   const float* pbase = L0 ? nullptr : layer_base(a, lp) + (int64_t)a.G * KX;
   const float* pbias = L0 ? nullptr : pbase + (int64_t)(a.R + a.S) * H;
   const int rwave = wave - kGW;
-  int rrow[kResRows];
-  f32x4 rw[kResRows];
-  float rbias = 0.f, rskip = 0.f;
-  // after the butterfly, lane L (L % (64/(kResRows*kUB)) == 0) holds sum index L/4 = q*kUB + b
+  const bool resid = !L0 && rwave >= 0 && WN_ABLATE != 4 && WN_ABLATE != 6;
+  // after the butterfly, lane L (L % 4 == 0) holds sum index L/4 = q*kUB + b
   const int my_q = (lane >> 2) / kUB, my_b = (lane >> 2) % kUB;
   const int my_gb = b0 + (my_b < nb ? my_b : 0);
-  const bool resid = !L0 && rwave >= 0 && WN_ABLATE != 4 && WN_ABLATE != 6;
+  f32x4 rw[kResRows], rg[kUB];
+  int myrow = 0;
+  float rbias = 0.f, rskip = 0.f;
   if (resid) {
 #pragma unroll
     for (int q = 0; q < kResRows; ++q) {
       int j = rwave + q * kRW;                            // residual row index in the workgroup
       if (j >= kRP * nrp) j = 0;                          // padding rows: computed and dropped
       const int p = j / nrp, jj = j - p * nrp;
-      rrow[q] = jj < rx ? (o0 + p) * rx + jj : a.R + (o0 + p) * (nrp - rx) + (jj - rx);
-      rw[q] = ld4(pbase + (int64_t)rrow[q] * H + lane * 4);   // H == 256: one chunk per lane
+      const int row = jj < rx ? (o0 + p) * rx + jj : a.R + (o0 + p) * (nrp - rx) + (jj - rx);
+      rw[q] = ld4(pbase + (int64_t)row * H + lane * 4);   // H == 256: one chunk per lane
+      if (q == my_q) myrow = row;
     }
-    int myrow = rrow[0];
 #pragma unroll
-    for (int q = 1; q < kResRows; ++q) if (q == my_q) myrow = rrow[q];
+    for (int b = 0; b < kUB; ++b) rg[b] = ld4(gbuf_of(a, lp) + urow(b) * H + lane * 4);
     rbias = pbias[myrow];
     if (myrow >= a.R) rskip = a.skip[(int64_t)my_gb * a.S + (myrow - a.R)];
   }
-  // ---- the step, and everything addressed by it
+  // layer 0: the MoL head of the previous step (weights and h1)
+  f32x4 mw[kMolRows], mh[kUB];
+  if (L0) mol_load(a, wave, lane, b0, nb, mw, mh);
+
+  // ---------------- prologue part 2: the step, and every load addressed by it
   const int t = read_step(a, slot, 0, targ);
+  const int slot_t = t & (a.RING - 1);
+  const int d = 1 << (layer % a.lps);
   float pre_v = 0.f;            // conditioning pre-activation of (gate row, utterance) threadIdx.x
   if ((int)threadIdx.x < 2 * kRP * kUB) {
     const int r = threadIdx.x / kUB, b = threadIdx.x % kUB;
-    const int row = o0 + (r >> 1) + (r & 1) * H;
-    pre_v = a.pre[((int64_t)(t % a.Tch) * a.B + b0 + (b < nb ? b : 0)) * ((int64_t)a.n_layers * a.G) +
-                  (int64_t)layer * a.G + row];
+    pre_v = a.pre[((int64_t)(t % a.Tch) * a.B + urow(b)) * ((int64_t)a.n_layers * a.G) + (int64_t)layer * a.G + wrow(r)];
   }
   float rres = 0.f;
-  const int slot_t = t & (a.RING - 1);
-  if (resid) {
-    int myrow = rrow[0];
+  if (resid && myrow < a.R)
+    rres = lp == 0 ? a.yin[(int64_t)my_gb * a.T + t] * a.packed[myrow] + a.packed[a.R + myrow]
+                   : a.ring[(((int64_t)lp * a.RING + slot_t) * a.B + my_gb) * a.R + myrow];
+  // first chunk's step-addressed inputs; `live0` false = the chunk contributes nothing
+  bool live0 = gate;
+  if (gate) {
+    if ((WN_ABLATE == 2 || WN_ABLATE == 6) && !L0) {
 #pragma unroll
-    for (int q = 1; q < kResRows; ++q) if (q == my_q) myrow = rrow[q];
-    if (myrow < a.R)
-      rres = lp == 0 ? a.yin[(int64_t)my_gb * a.T + t] * a.packed[myrow] + a.packed[a.R + myrow]
-                     : a.ring[(((int64_t)lp * a.RING + slot_t) * a.B + my_gb) * a.R + myrow];
+      for (int b = 0; b < kUB; ++b) x0[b] = f32x4{0.5f, 0.25f, 0.f, (float)b};
+    } else if (cat0 == 0) {                      // ring taps 0..K-2 of x_l
+      const int tap = kc0 / a.R;
+      const int tau = t - (a.K - 1 - tap) * d;
+      live0 = tau >= 0;                          // zero history before the first sample
+      if (live0) {
+        if (L0) {
+#pragma unroll
+          for (int b = 0; b < kUB; ++b) {
+            const float in_v = a.yin[urow(b) * a.T + tau];
+            x0[b] = f32x4{in_v * fw0[0] + fb0[0], in_v * fw0[1] + fb0[1], in_v * fw0[2] + fb0[2],
+                          in_v * fw0[3] + fb0[3]};
+          }
+        } else {
+          const float* xr = a.ring + ((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B * a.R +
+                            (kc0 - tap * a.R) + lane * 4;
+#pragma unroll
+          for (int b = 0; b < kUB; ++b) x0[b] = ld4(xr + urow(b) * a.R);
+        }
+      }
+    } else if (cat0 == 1) {
+      live0 = !L0;                               // layer 0: zero weights there, skipped
+    } else if (!L0) {                            // current tap x_(l-1)(t)
+      if (layer == 1) {
+#pragma unroll
+        for (int b = 0; b < kUB; ++b) {
+          const float in_v = a.yin[urow(b) * a.T + t];
+          x0[b] = f32x4{in_v * fw0[0] + fb0[0], in_v * fw0[1] + fb0[1], in_v * fw0[2] + fb0[2],
+                        in_v * fw0[3] + fb0[3]};
+        }
+      } else {
+        const float* xr = a.ring + ((int64_t)(layer - 1) * a.RING + slot_t) * a.B * a.R + (kc0 - KT - H) + lane * 4;
+#pragma unroll
+        for (int b = 0; b < kUB; ++b) x0[b] = ld4(xr + urow(b) * a.R);
+      }
+    }
   }
-  if (L0) sample_stage<kGW + kRW, kUB>(a, t, b0, nb, s_mol, s_in);
-  const int d = 1 << (layer % a.lps);
-  auto urow = [&](int b) { return (int64_t)(b0 + (b < nb ? b : 0)); };
+
+  // ---------------- layer 0: sample the previous step's output; its x_0(t) is the current tap
+  if (L0) {
+    mol_finish(a, t, wave, lane, b0, nb, mw, mh, s_mol, s_in);
+    if (gate && cat0 == 2) {
+#pragma unroll
+      for (int b = 0; b < kUB; ++b) {
+        const float in_v = s_in[b];
+        x0[b] = f32x4{in_v * fw0[0] + fb0[0], in_v * fw0[1] + fb0[1], in_v * fw0[2] + fb0[2], in_v * fw0[3] + fb0[3]};
+      }
+    }
+  }
+
+  // ---------------- gate GEMV (first chunk from the prologue; further chunks only when KX > kGW*256)
   if (wave < kGW) {
-    const float* gprev = L0 ? nullptr : gbuf_of(a, layer - 1);
     float acc[2 * kRP * kUB];
 #pragma unroll
     for (int j = 0; j < 2 * kRP * kUB; ++j) acc[j] = 0.f;
-    for (int c = c0; c * 256 < KX; c += kGW) {
-      const int kc = c * 256;
-      const int k = kc + lane * 4;
-      f32x4 w[2 * kRP];
+    if (live0) {
 #pragma unroll
       for (int r = 0; r < 2 * kRP; ++r)
-        w[r] = c == c0 ? w0[r] : ld4(base + (int64_t)(o0 + (r >> 1) + (r & 1) * H) * KX + k);
-      f32x4 x[kUB];
-      if ((WN_ABLATE == 2 || WN_ABLATE == 6) && !L0) {
 #pragma unroll
-        for (int b = 0; b < kUB; ++b) x[b] = f32x4{0.5f, 0.25f, 0.f, (float)b};
-      } else if (kc < KT) {                    // ring taps 0..K-2 of x_l
+        for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w0[r], x0[b], acc[r * kUB + b]);
+    }
+    for (int c = c0 + kGW; c * 256 < KX; c += kGW) {
+      const int kc = c * 256;
+      const int k = kc + lane * 4;
+      f32x4 x[kUB];
+      if (kc < KT) {
         const int tap = kc / a.R;
         const int tau = t - (a.K - 1 - tap) * d;
-        if (tau < 0) continue;                 // wave-uniform: zero history before the first sample
+        if (tau < 0) continue;
         const int i = k - tap * a.R;
         if (L0) {
           const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
 #pragma unroll
           for (int b = 0; b < kUB; ++b) {
             const float in_v = a.yin[urow(b) * a.T + tau];
-            x[b][0] = in_v * fw[0] + fb[0];
-            x[b][1] = in_v * fw[1] + fb[1];
-            x[b][2] = in_v * fw[2] + fb[2];
-            x[b][3] = in_v * fw[3] + fb[3];
+            x[b] = f32x4{in_v * fw[0] + fb[0], in_v * fw[1] + fb[1], in_v * fw[2] + fb[2], in_v * fw[3] + fb[3]};
           }
         } else {
           const float* xr = a.ring + ((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B * a.R + i;
 #pragma unroll
           for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
         }
-      } else if (kc < KT + H) {                // g_(l-1) (layer 0: zero weights, skipped)
+      } else if (kc < KT + H) {
         if (L0) continue;
-        const int j = k - KT;
 #pragma unroll
-        for (int b = 0; b < kUB; ++b) x[b] = ld4(gprev + urow(b) * H + j);
-      } else {                                 // current tap: x_(l-1)(t) (layer 0: x_0(t))
+        for (int b = 0; b < kUB; ++b) x[b] = ld4(gprev + urow(b) * H + (k - KT));
+      } else {
         const int i = k - KT - H;
-        if (L0) {
+        if (L0 || layer == 1) {
           const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
 #pragma unroll
           for (int b = 0; b < kUB; ++b) {
-            const float in_v = s_in[b];
-            x[b][0] = in_v * fw[0] + fb[0];
-            x[b][1] = in_v * fw[1] + fb[1];
-            x[b][2] = in_v * fw[2] + fb[2];
-            x[b][3] = in_v * fw[3] + fb[3];
-          }
-        } else if (layer - 1 == 0) {
-          const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
-#pragma unroll
-          for (int b = 0; b < kUB; ++b) {
-            const float in_v = a.yin[urow(b) * a.T + t];
-            x[b][0] = in_v * fw[0] + fb[0];
-            x[b][1] = in_v * fw[1] + fb[1];
-            x[b][2] = in_v * fw[2] + fb[2];
-            x[b][3] = in_v * fw[3] + fb[3];
+            const float in_v = L0 ? s_in[b] : a.yin[urow(b) * a.T + t];
+            x[b] = f32x4{in_v * fw[0] + fb[0], in_v * fw[1] + fb[1], in_v * fw[2] + fb[2], in_v * fw[3] + fb[3]};
           }
         } else {
           const float* xr = a.ring + ((int64_t)(layer - 1) * a.RING + slot_t) * a.B * a.R + i;
@@ -424,35 +533,30 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
         }
       }
 #pragma unroll
-      for (int r = 0; r < 2 * kRP; ++r)
+      for (int r = 0; r < 2 * kRP; ++r) {
+        const f32x4 w = ld4(base + (int64_t)wrow(r) * KX + k);
 #pragma unroll
-        for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w[r], x[b], acc[r * kUB + b]);
+        for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w, x[b], acc[r * kUB + b]);
+      }
     }
     const float s = WN_ABLATE == 7 ? acc[lane & 15] : wave_reduce_multi<2 * kRP * kUB>(acc, lane);
     if ((lane & (64 / (2 * kRP * kUB) - 1)) == 0) s_red[wave][lane / (64 / (2 * kRP * kUB))] = s;
   } else if (resid) {
-    // layer l-1's residual rows: x_l(t) and skip rows of this workgroup's gate pairs
-    const float* gprev = gbuf_of(a, lp);
-    f32x4 g[kUB];
-#pragma unroll
-    for (int b = 0; b < kUB; ++b) g[b] = ld4(gprev + urow(b) * H + lane * 4);
+    // layer l-1's residual rows: x_l(t) -> ring l, skip rows -> the skip accumulator
     float acc[kResRows * kUB];
 #pragma unroll
     for (int q = 0; q < kResRows; ++q)
 #pragma unroll
-      for (int b = 0; b < kUB; ++b) acc[q * kUB + b] = dot4(rw[q], g[b], 0.f);
+      for (int b = 0; b < kUB; ++b) acc[q * kUB + b] = dot4(rw[q], rg[b], 0.f);
     const float v0 = wave_reduce_multi<kResRows * kUB>(acc, lane);
     const int j = rwave + my_q * kRW;
     if ((lane & 3) == 0 && j < kRP * nrp && my_b < nb) {
-      int row = rrow[0];
-#pragma unroll
-      for (int q = 1; q < kResRows; ++q) if (q == my_q) row = rrow[q];
       const int gb = b0 + my_b;
       const float v = v0 + rbias;
-      if (row < a.R) {
-        a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gb) * a.R + row] = (v + rres) * kSqrtHalf;
+      if (myrow < a.R) {
+        a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gb) * a.R + myrow] = (v + rres) * kSqrtHalf;
       } else {
-        float* sp = a.skip + (int64_t)gb * a.S + (row - a.R);
+        float* sp = a.skip + (int64_t)gb * a.S + (myrow - a.R);
         if (lp == 0) *sp = v;
         else *sp = a.legacy ? (rskip + v) * kSqrtHalf : (rskip + v);
       }
@@ -472,23 +576,24 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   }
 }
 
-// tail: the last layer's skip rows, one wave per row.
+// tail: the last layer's skip rows, one wave per row.  Every operand (weights, g, the skip
+// accumulator) is loaded before the step counter is touched (the tail only forwards it).
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, int targ) {
   if (WN_ABLATE == 5) return;
-  const int t = read_step(a, slot, 0, targ);
-  (void)t;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
   const int H = a.G / 2;
   const int lp = a.n_layers - 1;
-  const int srow = blockIdx.x * NW + wave;
-  if (srow >= a.S) return;
+  const int srow = min(blockIdx.x * NW + wave, a.S - 1);
   const int row = a.R + srow;
   const float* pbase = layer_base(a, lp) + (int64_t)a.G * gate_width(a);
   const float* bias = pbase + (int64_t)(a.R + a.S) * H;
   const float* gprev = gbuf_of(a, lp);
+  const int bl = (lane >> 3) < nb ? (lane >> 3) : 0;
+  const float bv = bias[row];
+  const float sk = a.skip[(int64_t)(b0 + bl) * a.S + srow];
   float acc[kBT];
 #pragma unroll
   for (int b = 0; b < kBT; ++b) acc[b] = 0.f;
@@ -500,28 +605,28 @@ __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, in
 #pragma unroll
     for (int b = 0; b < kBT; ++b) acc[b] = dot4(wv, g[b], acc[b]);
   }
+  read_step(a, slot, 0, targ);
   const float s = wave_reduce_multi<kBT>(acc, lane);
-  if ((lane & 7) != 0) return;
+  if ((lane & 7) != 0 || blockIdx.x * NW + wave >= a.S) return;
   const int b = lane >> 3;
   if (b >= nb) return;
   float* sp = a.skip + (int64_t)(b0 + b) * a.S + srow;
-  const float v = s + bias[row];
+  const float v = s + bv;
   if (lp == 0) *sp = v;
-  else *sp = a.legacy ? (*sp + v) * kSqrtHalf : (*sp + v);
+  else *sp = a.legacy ? (sk + v) * kSqrtHalf : (sk + v);
 }
 
 // head: h1 = relu(W1 relu(skips) + b1); advances the step counter.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, int targ) {
   if (WN_ABLATE == 5) return;
-  read_step(a, slot, 1, targ);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
-  const int row = blockIdx.x * NW + wave;
-  if (row >= a.S) return;
+  const int row = min(blockIdx.x * NW + wave, a.S - 1);
   const float* W1 = head_base(a);
   const float* b1 = W1 + (int64_t)a.S * a.S;
+  const float bv = b1[row];
   float acc[kBT];
 #pragma unroll
   for (int b = 0; b < kBT; ++b) acc[b] = 0.f;
@@ -537,11 +642,12 @@ __global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, in
       acc[b] = dot4(wv, x[b], acc[b]);
     }
   }
+  read_step(a, slot, 1, targ);
   const float s = wave_reduce_multi<kBT>(acc, lane);
-  if ((lane & 7) != 0) return;
+  if ((lane & 7) != 0 || blockIdx.x * NW + wave >= a.S) return;
   const int b = lane >> 3;
   if (b >= nb) return;
-  a.h1[(int64_t)(b0 + b) * a.S + row] = fmaxf(s + b1[row], 0.f);
+  a.h1[(int64_t)(b0 + b) * a.S + row] = fmaxf(s + bv, 0.f);
 }
 
 // Sample the last output (step T-1) after the final head.
@@ -622,8 +728,10 @@ int enqueue_step(const WnArgs& a, hipStream_t s, int targ) {
     if (l == 0) hipLaunchKernelGGL((wn_layer_kernel<true>), lgrid, dim3(kLayerThreads), 0, s, a, 0, 0, targ);
     else hipLaunchKernelGGL((wn_layer_kernel<false>), lgrid, dim3(kLayerThreads), 0, s, a, l, l, targ);
   }
-  hipLaunchKernelGGL((wn_tail_kernel<4>), dim3((a.S + 3) / 4, nbt), dim3(256), 0, s, a, a.n_layers, targ);
-  hipLaunchKernelGGL((wn_head_kernel<4>), dim3((a.S + 3) / 4, nbt), dim3(256), 0, s, a, a.n_layers + 1, targ);
+  hipLaunchKernelGGL((wn_tail_kernel<kTailWaves>), dim3((a.S + kTailWaves - 1) / kTailWaves, nbt),
+                     dim3(64 * kTailWaves), 0, s, a, a.n_layers, targ);
+  hipLaunchKernelGGL((wn_head_kernel<kTailWaves>), dim3((a.S + kTailWaves - 1) / kTailWaves, nbt),
+                     dim3(64 * kTailWaves), 0, s, a, a.n_layers + 1, targ);
   AVC_CHECK_LAUNCH("autovc_wavenet_generate_f32");
   return avc::kOk;
 }
@@ -726,9 +834,9 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
                     taps >= 1,
                 "%s: bad layer structure layers=%d per_stack=%d taps=%d", fn, n_layers, layers_per_stack, taps);
   AVC_CHECK_ARG(R > 0 && R % 256 == 0 && G > 0 && G % 512 == 0 && S > 0 && S % 256 == 0 &&
-                    R % (G / 2) == 0 && S % (G / 2) == 0 && G / 2 == 256 &&
+                    R % (G / 2) == 0 && S % (G / 2) == 0 && G / 2 == 256 && S == 256 &&
                     kRP * ((R + S) / (G / 2)) <= kRW * kResRows && taps >= 2,
-                "%s: need G/2 == 256, R and S multiples of 256 with (R + S) / (G/2) <= %d, taps >= 2 "
+                "%s: need G/2 == S == 256, R a multiple of 256 with (R + S) / (G/2) <= %d, taps >= 2 "
                 "(R=%d, G/2=%d, S=%d)", fn, kRW * kResRows / kRP,
                 R, G / 2, S);
   AVC_CHECK_ARG(n_out % 3 == 0 && n_out / 3 >= 1 && n_out / 3 <= 10 && n_out <= kMaxNO,
