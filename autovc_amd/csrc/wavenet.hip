@@ -48,7 +48,9 @@ namespace {
 // library; the product build is WN_ABLATE 0): 1 = step index a constant (no dependent
 // counter load), 2 = 1 + no activation loads, 3 = 1 + no weight loads, 4 = 1 + no residual
 // wave work, 5 = every step kernel returns at once (launch boundaries only), 6 = 2+3+4,
-// 7 = 1 + no cross-lane reduction.  Outputs are meaningless unless WN_ABLATE == 0.
+// 7 = 1 + no cross-lane reduction, 8 = layer kernels l >= 1 return at once, 9 = every layer
+// kernel returns at once, 10 = tail and head return at once.  Outputs are meaningless
+// unless WN_ABLATE == 0.
 #ifndef WN_ABLATE
 #define WN_ABLATE 0
 #endif
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   __shared__ float s_mol[L0 ? kUB * kMaxNO : 1];
   __shared__ float s_in[kUB];
   __shared__ float s_red[kGW][2 * kRP * kUB];
-  if (WN_ABLATE == 5) return;
+  if (WN_ABLATE == 5 || WN_ABLATE == 9 || (WN_ABLATE == 8 && !L0)) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kUB;
   const int nb = min(kUB, a.B - b0);
@@ -580,7 +582,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
 // accumulator) is loaded before the step counter is touched (the tail only forwards it).
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, int targ) {
-  if (WN_ABLATE == 5) return;
+  if (WN_ABLATE == 5 || WN_ABLATE == 10) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
@@ -619,7 +621,7 @@ __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, in
 // head: h1 = relu(W1 relu(skips) + b1); advances the step counter.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, int targ) {
-  if (WN_ABLATE == 5) return;
+  if (WN_ABLATE == 5 || WN_ABLATE == 10) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -17,7 +18,7 @@ struct Args { const float* in; float* out; const float* w; const int* ctr; int f
 // (the same region for every workgroup), `w_floats` floats of a stable weight buffer (a
 // different slice per workgroup), reduces, and one lane per workgroup writes 4 floats.
 template <int NT>
-__global__ __launch_bounds__(NT) void chain_kernel(Args a) {
+__device__ __forceinline__ void chain_body(const Args& a) {
   const int lane = threadIdx.x;
   int off = 0;
   if (a.use_ctr) off = a.ctr[0] & 1;
@@ -44,7 +45,13 @@ __global__ __launch_bounds__(NT) void chain_kernel(Args a) {
     *reinterpret_cast<f4*>(a.out + (size_t)blockIdx.x * per + k) = f4{t, t, t, t};
 }
 
+template <int NT>
+__global__ __launch_bounds__(NT) void chain_kernel(Args a) { chain_body<NT>(a); }
+
 __global__ void empty_kernel(Args) {}
+// a second symbol with identical code: does switching kernels cost more than repeating one?
+template <int NT>
+__global__ __launch_bounds__(NT) void chain_kernel_b(Args a) { chain_body<NT>(a); }
 
 template <int NT>
 float run(int variant, int fresh, int wfl, int use_ctr, float* b0, float* b1, const float* w, const int* ctr,
@@ -56,6 +63,8 @@ float run(int variant, int fresh, int wfl, int use_ctr, float* b0, float* b1, co
     for (int l = 0; l < L; ++l) {
       Args a{(l & 1) ? b1 : b0, (l & 1) ? b0 : b1, w, ctr, fresh, wfl, use_ctr};
       if (variant == 0) hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(NT), 0, st, a);
+      else if (variant == 2 && (l & 1)) hipLaunchKernelGGL(chain_kernel_b<NT>, dim3(256), dim3(NT), 0, st, a);
+      else if (variant == 3 && (l & 1)) hipLaunchKernelGGL(chain_kernel<128>, dim3(128), dim3(128), 0, st, a);
       else hipLaunchKernelGGL(chain_kernel<NT>, dim3(256), dim3(NT), 0, st, a);
     }
   hipStreamEndCapture(st, &g);
@@ -86,6 +95,11 @@ int main() {
   printf("us per launch, 256 workgroups, chains of 26 x 64 launches in one graph\n");
   printf("empty 256 thr      : %6.2f\n", run<256>(0, 0, 0, 0, b0, b1, w, ctr, st));
   printf("empty 576 thr      : %6.2f\n", run<576>(0, 0, 0, 0, b0, b1, w, ctr, st));
+  printf("alternating symbols (576 thr, fresh 4096 B, weights 16384 B): same %6.2f  two symbols %6.2f  "
+         "every other launch 128x128 threads %6.2f\n",
+         run<576>(1, 1024, 4096, 0, b0, b1, w, ctr, st), run<576>(2, 1024, 4096, 0, b0, b1, w, ctr, st),
+         run<576>(3, 1024, 4096, 0, b0, b1, w, ctr, st));
+  if (getenv("CHAIN_ALT_ONLY")) return 0;
   const int fr[] = {0, 16, 1024, 4096, 8192, 16384};
   const int wf[] = {0, 4096, 8192};
   for (int nt = 0; nt < 2; ++nt)

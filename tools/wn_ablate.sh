@@ -4,7 +4,7 @@
 #   run   (on the GPU box):           bash tools/wn_ablate.sh run  > gpurun_out/wn_ablate.txt
 set -o pipefail
 cd "$(dirname "$0")/.."
-MODES="1 2 3 4 5 6 7"
+MODES="${WN_MODES:-1 2 3 4 5 6 7 8 9 10}"
 if [ "$1" = build ]; then
   mkdir -p tools/build
   objs=$(ls autovc_amd/csrc/build/*.o | grep -v '/wavenet.o$')
