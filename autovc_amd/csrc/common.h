@@ -57,6 +57,17 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Accurate (ocml) expf/tanhf: the LSTM parity bar is 1e-4 rel vs torch CPU.
 __device__ __forceinline__ float avc_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Short-latency forms for the latency-bound small-H recurrence (encoder BLSTM: 128 dependent
+// steps per launch, where ocml's branchy tanhf and IEEE division dominated a step):
+// v_exp_f32 + v_rcp_f32, a few ulp; tanh via 1 - 2 / (e^{2x} + 1) (absolute error ~1e-7 near
+// 0, exact limits +-1).
+__device__ __forceinline__ float avc_sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float avc_tanh_fast(float x) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
+}
+
 // x + x[lane ^ M] inside each quad of lanes (M = 1 or 2): DPP quad_perm, VALU only
 template <int M>
 __device__ __forceinline__ float avc_quad_xor_add(float x) {

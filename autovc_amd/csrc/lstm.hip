@@ -551,9 +551,10 @@ __global__ __launch_bounds__(kThreads) void blstm_fwd_kernel(int B, int T, const
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[q] = avc_quad_xor_add<2>(avc_quad_xor_add<1>(acc[q]));
-      const float i_ = avc_sigmoid(acc[0]), f_ = avc_sigmoid(acc[1]), g_ = tanhf(acc[2]), o_ = avc_sigmoid(acc[3]);
+      const float i_ = avc_sigmoid_fast(acc[0]), f_ = avc_sigmoid_fast(acc[1]), g_ = avc_tanh_fast(acc[2]);
+      const float o_ = avc_sigmoid_fast(acc[3]);
       c = f_ * c + i_ * g_;
-      const float h = o_ * tanhf(c);
+      const float h = o_ * avc_tanh_fast(c);
       if (ks == 0) hs[cur ^ 1][bl][j] = h;
       if (own && s < T) {
         const int64_t o = ((int64_t)b * T + t) * HO + dir * SH + j;
@@ -618,7 +619,7 @@ __global__ __launch_bounds__(kThreads) void blstm_bwd_kernel(int B, int T, const
       const float i_ = o.g[0], f_ = o.g[1], g_ = o.g[2], o_ = o.g[3];
       const float dh = dhr + o.dh;
       const float cp = s == T - 1 ? 0.f : o.cp;   // the forward's first step: c_prev = 0
-      const float tc = tanhf(o.cc);
+      const float tc = avc_tanh_fast(o.cc);
       const float dc = dcs + dh * o_ * (1.f - tc * tc);
       const float di = dc * g_ * i_ * (1.f - i_);
       const float df = dc * cp * f_ * (1.f - f_);

@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TF = 157.3   # dense fp32 MFMA (= vector) peak (MI355X_MICROARCH.md)
 
 
 def synthetic_batch(B, T, dev, seed):
@@ -87,21 +88,33 @@ def lstm_roofline(solver, B, T, dev):
     bytes2 = 2 * per_layer_step
     achieved = bytes2 / (us2 * 1e-6) / 1e9
     a1 = per_layer_step / (us1 * 1e-6) / 1e9
+    # per launch: layer 0's recurrent product (B x 4H x H) and layer 1's input + recurrent
+    # products (B x 4H x 2H), 2 FLOP per MAC
+    flop2 = 2 * B * 4 * H * H * 3
+    tf = flop2 / (us2 * 1e-6) / 1e12
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "lstm2_step_pmc.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
-    return {"kernel": "lstm2_fwd_step_kernel (decoder lstm2: both layers per launch, H=1024, B=64)", "bound": "hbm",
-            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "bytes_per_launch": bytes2, "avg_launch_us": round(us2, 3),
-            "note": ("traffic (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/lstm2_step_pmc.json) includes the "
-                     "16.8 MB W_ih1 read of the fused layer-1 input projection and the per-XCD h re-reads, "
-                     "which the algorithmic bytes leave out"),
+    ridge = MFMA_F32_PEAK_TF * 1e12 / (HBM_PEAK_GBS * 1e9)
+    return {"kernel": "lstm2_fwd_step_kernel (decoder lstm2: both layers per launch, H=1024, B=64)", "bound": "mfma",
+            "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
+            "frac": round(tf / MFMA_F32_PEAK_TF, 4), "traffic": traffic,
+            "flop_per_launch": flop2, "bytes_per_launch": bytes2, "avg_launch_us": round(us2, 3),
+            "arithmetic_intensity": round(flop2 / bytes2, 1), "ridge_flop_per_byte": round(ridge, 1),
+            "hbm": {"convention": "SURVEY 8d weight-streaming bytes (W_hh, gates_x, h/c per layer-step), x 2 layers",
+                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4)},
+            "note": ("bound = mfma: the launch's arithmetic intensity over the 8d algorithmic bytes is above the fp32 "
+                     "ridge point (157.3 TF / 8 TB/s), so the fp32 MFMA peak is its roofline; the 8d HBM "
+                     "convention figure is reported under 'hbm'.  traffic (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                     "profiles/lstm2_step_pmc.json) includes the 16.8 MB W_ih1 read of the fused layer-1 input "
+                     "projection and the per-XCD h re-reads, which the algorithmic bytes leave out"),
             "single_layer": {"kernel": "lstm_fwd_step_kernel (H=1024, B=64)", "bytes_per_launch": per_layer_step,
-                             "avg_launch_us": round(us1, 3), "achieved": round(a1, 1),
-                             "frac": round(a1 / HBM_PEAK_GBS, 4)}}
+                             "avg_launch_us": round(us1, 3), "hbm_achieved": round(a1, 1),
+                             "hbm_frac": round(a1 / HBM_PEAK_GBS, 4),
+                             "mfma_frac": round(2 * B * 4 * H * H / (us1 * 1e-6) / 1e12 / MFMA_F32_PEAK_TF, 4)}}
 
 
 def blstm_roofline(dev, B, T, H=32):
@@ -157,7 +170,7 @@ def step_roofline(B, ms_per_step, precision="fp32"):
     """Whole-step MFMA fraction: algorithmic FLOPs (convs, LSTMs, linear
     fwd + bwd, the second encoder pass; 24.60 GFLOP per sample) / step time / peak."""
     flop = 24.60e9 * B
-    peak = 157.3 if precision == "fp32" else 2500.0
+    peak = MFMA_F32_PEAK_TF if precision == "fp32" else 2500.0
     tf = flop / (ms_per_step * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(tf / peak, 4), "flop_per_step": flop,
