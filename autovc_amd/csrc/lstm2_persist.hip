@@ -1,0 +1,424 @@
+// Decoder lstm2 forward (nn.LSTM(512, 1024, num_layers=2), model_vc_mel.py:104,118) as ONE
+// persistent, weight-stationary launch for gfx950.
+//
+// The per-step launch (lstm.hip, lstm2_fwd_step_kernel) re-streams every weight row of both
+// layers into every CU at every step: 768 KB of operands per CU per step (W_hh0, W_ih1,
+// W_hh1 and the h rows, 32 x 1024 fp32 each), which bounds the step at ~24 us — the CU's
+// operand fill, not the MFMA (10.2 us of fp32 MFMA per CU at peak).  Here each of the 256
+// workgroups (one per CU) owns the same 32 batch rows x 32 gate columns (8 hidden units x 4
+// gates) of BOTH layers for the whole sequence and keeps their weights on the CU:
+//   W_ih1, W_hh1 tile rows  -> VGPRs (128 floats per lane: the MFMA B fragments)
+//   W_hh0 tile rows         -> LDS (128 KB, k-blocked [k/4][col][4]: conflict-free b128 reads)
+// so a step streams only the h rows (h0_{t-1}, shared by both layers, and h1_{t-2}): 256 KB
+// per CU.  Steps are separated by an XCD-hierarchical grid barrier instead of a launch
+// boundary (MI355X_MICROARCH.md price list: barrier-xcd).
+//
+// Iteration t (t = 0..T) is the same wavefront as the per-step launch: layer 0 at step t
+// (input h0_{t-1}), layer 1 at step t-1 (inputs h0_{t-1}, h1_{t-2}).  v_mfma_f32_32x32x2_f32
+// (exact fp32), one wave per SIMD (512 VGPRs: 256 of weights, two 8-deep h prefetch windows):
+// wave w takes k in [256w, 256w + 256) of both h0_{t-1} (layer 0 with B from LDS, layer 1's
+// input product with B = W_ih1 from VGPRs) and h1_{t-2} (layer 1's recurrent product, B =
+// W_hh1 from VGPRs).  Each lane half takes 128 consecutive k (lane h: k0 + 128h + i for
+// MFMA i), so a lane's weights and its h fragments are contiguous in memory; the h rows come
+// from a k-blocked copy [t][H/4][B][4] the epilogues write beside h (512 B contiguous per
+// half-wave).  The 4 waves' partial tiles are summed through LDS in fixed order, then the
+// cell update (v_exp / v_rcp sigmoid and tanh).
+//
+// Inter-workgroup visibility (cdna_hip_programming.md Guideline 16, the write-through form of
+// MI355X_MICROARCH.md "Valid forms", first row of its table): the only bytes handed between
+// workgroups are the k-blocked h copies; they are stored sc1 (write-through), every wave
+// waits vmcnt(0), the workgroup barrier, then ONE lane adds to its XCC's arrival counter
+// (agent-scope atomic); the XCC's last arriver adds to the top counter, whose last arriver
+// stores the generation word every workgroup polls (sc1 loads); every load of the handed-off
+// bytes is an sc1 buffer load, so no release / acquire fence is needed.  Every k-blocked row
+// is written once per call (fresh addresses).  Every spin is bounded by s_memrealtime; a
+// timeout sets an error word and every workgroup exits.
+#include "common.h"
+#include "../../include/autovc_hip.h"
+
+#include <hip/hip_runtime.h>
+
+// Diagnostic ablations (tools/lp_ablate.sh builds them into separate libraries; the product
+// build is LP_ABLATE 0): 1 = no grid barrier, 2 = no products, 3 = products without the h
+// loads (constant operands), 4 = no epilogue (no reduction, cell update or stores).
+#ifndef LP_ABLATE
+#define LP_ABLATE 0
+#endif
+// W_ih1 tile in LDS beside W_hh0 (1) or in VGPRs beside W_hh1 (0); h groups in flight per stream
+#ifndef LP_W1_LDS
+#define LP_W1_LDS 1
+#endif
+#ifndef LP_PWIN
+#define LP_PWIN 3
+#endif
+
+namespace {
+
+constexpr int PB = 64;             // batch rows per tile (all of them)
+constexpr int PU = 4;              // hidden units per tile (x 4 gates = 16 columns)
+constexpr int PC = 4 * PU;         // tile columns
+constexpr int PNW = 4;             // waves per workgroup (one per SIMD)
+constexpr int PNT = 64 * PNW;
+constexpr int PH = 1024;           // hidden size this kernel is built for
+constexpr int PKW = PH / PNW;      // k per wave and segment (256)
+constexpr int PKL = PKW / 4;       // k per lane group (64: lane group l / 16 of the MFMA)
+constexpr int PGR = PKL / 4;       // 4-k groups per lane (16)
+constexpr int PRB = PB / 16;       // 16-row blocks of the tile (4)
+constexpr int PWIN = LP_PWIN;      // h groups in flight per stream
+constexpr int RED_LD = PC + 1;     // padded row of a 64 x 16 partial tile in LDS
+constexpr int RED_SLOT = PB * RED_LD;
+constexpr int LDS_W0 = (PH / 4) * PC * 4;          // floats: W_hh0 tile [k/4][16][4]
+constexpr int LDS_W1 = LP_W1_LDS ? LDS_W0 : 0;     // floats: W_ih1 tile, same layout
+constexpr int RED_LAYERS = LP_W1_LDS ? 1 : 2;      // partial tiles of one layer at a time, or both
+constexpr int LDS_RED = RED_LAYERS * PNW * RED_SLOT;
+constexpr int LDS_MISC = 16;                       // floats: broadcast words
+constexpr int LDS_BYTES = 4 * (LDS_W0 + LDS_W1 + LDS_RED + LDS_MISC);
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+
+// barrier block: one 128-B line per word (ints)
+constexpr int L = 32;
+constexpr int BAR_CENSUS = 0;      // 16 lines: workgroups per XCC
+constexpr int BAR_START = 16;      // 1 line: workgroups arrived at the start
+constexpr int BAR_ARRIVE = 17;     // 16 lines: per-XCC arrivals (cumulative)
+constexpr int BAR_TOP = 33;        // 1 line: XCC leaders arrived (cumulative)
+constexpr int BAR_GEN = 34;        // 16 lines: per-XCC generation released
+constexpr int BAR_ERR = 50;        // 1 line: timeout / error code
+constexpr int BAR_LINES = 52;
+constexpr int64_t BAR_BYTES = BAR_LINES * L * 4;
+
+struct PArgs {
+  int B, T, H;
+  const float* gx0;
+  int64_t gx_ldb, gx_ldt;
+  const float* W_hh0;
+  const float* b_ih1;
+  const float* b_hh1;
+  const float* W_ih1;
+  const float* W_hh1;
+  float *h0, *c0, *g0, *h1, *c1, *g1;
+  float* hk0;                      // k-blocked h0: [t][H/4][B][4]
+  float* hk1;                      // k-blocked h1
+  int* bar;
+  int timeout_ticks;               // s_memrealtime ticks (100 MHz) before a spin gives up
+};
+
+__device__ __forceinline__ int ld_rlx(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int add_rlx(int* p, int v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// spin until *p >= target or the deadline passes (returns false on timeout, after
+// recording it); one lane polls, s_sleep between polls
+__device__ __noinline__ bool wait_ge(int* p, int target, int* err, int timeout_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (ld_rlx(p) < target) {
+    if (ld_rlx(err) != 0) return false;
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)timeout_ticks) {
+      st_rlx(err, 1);
+      return false;
+    }
+  }
+  return true;
+}
+
+// Grid barrier number `gen` (0, 1, ...).  Called by every thread; returns false if any
+// workgroup timed out (then every workgroup leaves the kernel).
+__device__ __forceinline__ bool grid_sync(const PArgs& a, int* misc, int gen) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's stores are in L2
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int xcc = misc[0], mine = misc[1], nx = misc[2];
+    bool ok = true;
+    const int old = add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
+    if (old == mine * (gen + 1) - 1) {                    // last of this XCC
+      const int top = add_rlx(a.bar + BAR_TOP * L, 1);
+      if (top == nx * (gen + 1) - 1)                      // last XCC: open every XCC's gate
+        for (int x = 0; x < 16; ++x) st_rlx(a.bar + (BAR_GEN + x) * L, gen + 1);
+    }
+    ok = wait_ge(a.bar + (BAR_GEN + xcc) * L, gen + 1, a.bar + BAR_ERR * L, a.timeout_ticks);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)
+    misc[3] = ok ? 0 : 1;
+  }
+  __syncthreads();
+  return misc[3] == 0;
+}
+
+// per-step cell update of one (batch row b, unit j) from its 4 gate pre-activations
+__device__ __forceinline__ void cell(const float (&pre)[4], float cp, float* c_out, float* h_out, float* g_out,
+                                    float* hk_out, int64_t H) {
+  const float i_ = avc_sigmoid_fast(pre[0]), f_ = avc_sigmoid_fast(pre[1]);
+  const float g_ = avc_tanh_fast(pre[2]), o_ = avc_sigmoid_fast(pre[3]);
+  const float cn = f_ * cp + i_ * g_;
+  const float hn = o_ * avc_tanh_fast(cn);
+  *c_out = cn;
+  *h_out = hn;
+  __hip_atomic_store(hk_out, hn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: handed off
+  if (g_out) { g_out[0] = i_; g_out[H] = f_; g_out[2 * H] = g_; g_out[3 * H] = o_; }
+}
+
+// acc[rb] (16 x 16 MFMA tiles of the 64 x 16 tile) -> LDS partial slot: C/D map of
+// v_mfma_f32_16x16x4f32: col = lane & 15, row = 4 (lane >> 4) + r
+__device__ __forceinline__ void put_tile(float* slot, const f32x4 (&acc)[PRB], int lane) {
+#pragma unroll
+  for (int rb = 0; rb < PRB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slot[(16 * rb + 4 * (lane >> 4) + r) * RED_LD + (lane & 15)] = acc[rb][r];
+}
+
+// One iteration's products of a wave over its k range: S0 = stream h0_{t-1} (layer 1 input
+// product, B = W_ih1 fragments in VGPRs; L0: also layer 0, B = W_hh0 from LDS), S1 = stream
+// h1_{t-2} (layer 1 recurrent product, B = W_hh1 fragments in VGPRs).  Lane l: MFMA k slot
+// l >> 4 covers k = kbase + 64 (l >> 4) + i, row block rb's A row 16 rb + (l & 15).
+template <bool S0, bool L0, bool S1>
+__device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const float* __restrict__ hk1_t,
+                                          const float (&wi)[LP_W1_LDS ? 1 : PKL], const float (&wh)[PKL], const float* W0,
+                                          const float* W1, int kb0,
+                                          int B, int lane, f32x4 (&acc1)[PRB], f32x4 (&acc0)[PRB]) {
+  // group g, row block rb: f32x4 at hk[kb0 + g][16 rb + (lane & 15)][0..3]; sc1 buffer loads
+  // (every load of the handed-off rows bypasses L1: no acquire fence needed)
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hk0_t), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r1 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hk1_t), (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t off0 = (uint32_t)((kb0 * B + (lane & 15)) * 16);
+  const uint32_t gstride = (uint32_t)B * 16;
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int g, int rb) {
+    if (LP_ABLATE == 3) return f32x4{0.5f, 0.25f, (float)g, (float)rb};
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off0 + g * gstride + rb * 256, 0, 16));
+  };
+  f32x4 a0[PWIN][PRB], a1[PWIN][PRB];
+#pragma unroll
+  for (int g = 0; g < PWIN; ++g)
+#pragma unroll
+    for (int rb = 0; rb < PRB; ++rb) {
+      if (S0) a0[g][rb] = ld(r0, g, rb);
+      if (S1) a1[g][rb] = ld(r1, g, rb);
+    }
+  const float* w0p = W0 + (kb0 * PC + (lane & 15)) * 4;
+  const float* w1p = W1 + (kb0 * PC + (lane & 15)) * 4;
+#pragma unroll
+  for (int g = 0; g < PGR; ++g) {
+    f32x4 x0[PRB], x1[PRB];
+#pragma unroll
+    for (int rb = 0; rb < PRB; ++rb) {
+      x0[rb] = a0[g % PWIN][rb];
+      x1[rb] = a1[g % PWIN][rb];
+    }
+    if (g + PWIN < PGR) {
+#pragma unroll
+      for (int rb = 0; rb < PRB; ++rb) {
+        if (S0) a0[g % PWIN][rb] = ld(r0, g + PWIN, rb);
+        if (S1) a1[g % PWIN][rb] = ld(r1, g + PWIN, rb);
+      }
+    }
+    f32x4 bv0 = {}, bv1 = {};
+    if (L0) bv0 = *reinterpret_cast<const f32x4*>(w0p + g * PC * 4);
+    if (LP_W1_LDS && S0) bv1 = *reinterpret_cast<const f32x4*>(w1p + g * PC * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int rb = 0; rb < PRB; ++rb) {
+        if (S0) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], LP_W1_LDS ? bv1[q] : wi[LP_W1_LDS ? 0 : 4 * g + q],
+                                                                acc1[rb], 0, 0, 0);
+        if (S1) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[rb][q], wh[4 * g + q], acc1[rb], 0, 0, 0);
+        if (L0) acc0[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], bv0[q], acc0[rb], 0, 0, 0);
+      }
+  }
+}
+
+__global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* W0 = lds;                          // [H/4][16][4]
+  float* W1 = lds + LDS_W0;                 // [H/4][16][4] (LP_W1_LDS)
+  float* red = W1 + LDS_W1;                 // layer 1: slots 0..3, layer 0: slots 4..7 (or reused)
+  int* misc = reinterpret_cast<int*>(red + LDS_RED);
+  const int H = PH, B = a.B, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j0 = blockIdx.x * PU;
+  auto grow = [&](int col) { return (col >> 2) * H + j0 + (col & 3); };   // tile column -> gate row
+
+  // ---- start: census of workgroups per XCC (the barrier's groups)
+  if (tid == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 15;
+    add_rlx(a.bar + (BAR_CENSUS + xcc) * L, 1);
+    add_rlx(a.bar + BAR_START * L, 1);
+    const bool ok = wait_ge(a.bar + BAR_START * L, gridDim.x, a.bar + BAR_ERR * L, a.timeout_ticks);
+    int nx = 0;
+    for (int x = 0; x < 16; ++x) nx += ld_rlx(a.bar + (BAR_CENSUS + x) * L) > 0;
+    misc[0] = (int)xcc;
+    misc[1] = ld_rlx(a.bar + (BAR_CENSUS + xcc) * L);
+    misc[2] = nx;
+    misc[3] = ok ? 0 : 1;
+  }
+  // ---- weights: W_hh0 tile -> LDS (k-blocked), W_ih1 / W_hh1 fragments -> VGPRs
+  for (int e = tid; e < (H / 4) * PC; e += PNT) {
+    const int kb = e / PC, col = e % PC;
+    *reinterpret_cast<f32x4*>(W0 + e * 4) = *reinterpret_cast<const f32x4*>(a.W_hh0 + (int64_t)grow(col) * H + kb * 4);
+    if (LP_W1_LDS)
+      *reinterpret_cast<f32x4*>(W1 + e * 4) =
+          *reinterpret_cast<const f32x4*>(a.W_ih1 + (int64_t)grow(col) * H + kb * 4);
+  }
+  const int kbase = wave * PKW + PKL * (lane >> 4);          // this lane's first k
+  const int kb0 = kbase / 4;
+  float wi[LP_W1_LDS ? 1 : PKL], wh[PKL];
+  {
+    const float* si = (LP_W1_LDS ? a.W_hh1 : a.W_ih1) + (int64_t)grow(lane & 15) * H + kbase;
+    const float* sh = a.W_hh1 + (int64_t)grow(lane & 15) * H + kbase;
+#pragma unroll
+    for (int g = 0; g < PGR; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(si + 4 * g);
+      if (!LP_W1_LDS) { wi[4 * g] = v[0]; wi[4 * g + 1] = v[1]; wi[4 * g + 2] = v[2]; wi[4 * g + 3] = v[3]; }
+      const f32x4 u = *reinterpret_cast<const f32x4*>(sh + 4 * g);
+      wh[4 * g] = u[0]; wh[4 * g + 1] = u[1]; wh[4 * g + 2] = u[2]; wh[4 * g + 3] = u[3];
+    }
+  }
+  __syncthreads();
+  if (misc[3] != 0) return;
+
+  // epilogue ownership: thread e owns (batch row e / 4, unit j0 + e % 4) of both layers
+  const int eb = tid >> 2, ej = j0 + (tid & 3), eu = tid & 3;
+  const bool eown = eb < B;
+  float bias1[4] = {0.f, 0.f, 0.f, 0.f};
+  if (eown)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bias1[g] = a.b_ih1[g * H + ej] + a.b_hh1[g * H + ej];
+  const int64_t BH = (int64_t)B * H;
+
+  for (int t = 0; t <= T; ++t) {
+    const bool l0 = t < T, l1 = t >= 1;
+    // epilogue operands of this iteration (latency hidden under the products)
+    float gxv[4] = {0.f, 0.f, 0.f, 0.f}, cp0 = 0.f, cp1 = 0.f;
+    if (eown) {
+      if (l0) {
+        const float* g = a.gx0 + (int64_t)eb * a.gx_ldb + (int64_t)t * a.gx_ldt;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gxv[q] = g[q * H + ej];
+        if (t >= 1) cp0 = a.c0[((int64_t)eb * T + t - 1) * H + ej];
+      }
+      if (t >= 2) cp1 = a.c1[((int64_t)eb * T + t - 2) * H + ej];
+    }
+    f32x4 acc1[PRB] = {}, acc0[PRB] = {};
+    const float* hk0 = a.hk0 + (int64_t)(t >= 1 ? t - 1 : 0) * BH;   // h0_{t-1}
+    const float* hk1 = a.hk1 + (int64_t)(t >= 2 ? t - 2 : 0) * BH;   // h1_{t-2}
+    if (LP_ABLATE == 2 || t == 0) {                                  // h0_{-1} = 0: no products
+    } else if (t == 1) {                                             // h1_{-1} = 0
+      gemm_wave<true, true, false>(hk0, hk1, wi, wh, W0, W1, kb0, B, lane, acc1, acc0);
+    } else if (t < T) {
+      gemm_wave<true, true, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, lane, acc1, acc0);
+    } else {                                                         // t == T: layer 1 only
+      gemm_wave<true, false, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, lane, acc1, acc0);
+    }
+    if (LP_ABLATE != 4) {
+      // the 4 waves' partial tiles summed through LDS in fixed order
+      auto sum = [&](int layer, int g) {
+        const float* r = red + layer * PNW * RED_SLOT + eb * RED_LD + g * PU + eu;
+        return ((r[0] + r[RED_SLOT]) + r[2 * RED_SLOT]) + r[3 * RED_SLOT];
+      };
+      constexpr int L0SLOT = RED_LAYERS - 1;                         // layer 0's slots
+      put_tile(red + wave * RED_SLOT, acc1, lane);
+      if (!LP_W1_LDS) put_tile(red + (L0SLOT * PNW + wave) * RED_SLOT, acc0, lane);
+      __syncthreads();
+      if (eown) {
+        if (l1) {                                                    // layer 1 at step t - 1
+          float pre[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + bias1[g];
+          const int t1 = t - 1;
+          const int64_t o = ((int64_t)eb * T + t1) * H + ej;
+          cell(pre, t1 >= 1 ? cp1 : 0.f, a.c1 + o, a.h1 + o,
+               a.g1 ? a.g1 + ((int64_t)eb * T + t1) * 4 * H + ej : nullptr,
+               a.hk1 + (int64_t)t1 * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3), H);
+        }
+      }
+      if (LP_W1_LDS) {                                               // slots reused for layer 0
+        __syncthreads();
+        put_tile(red + wave * RED_SLOT, acc0, lane);
+        __syncthreads();
+      }
+      if (eown) {
+        if (l0) {                                                    // layer 0 at step t
+          float pre[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) pre[g] = sum(L0SLOT, g) + gxv[g];
+          const int64_t o = ((int64_t)eb * T + t) * H + ej;
+          cell(pre, cp0, a.c0 + o, a.h0 + o, a.g0 ? a.g0 + ((int64_t)eb * T + t) * 4 * H + ej : nullptr,
+               a.hk0 + (int64_t)t * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3), H);
+        }
+      }
+    } else if (wave == 0 && acc1[0][0] == 12345.f && acc0[1][1] == 12345.f) {
+      a.h0[0] = 0.f;                                                  // keep the products live
+    }
+    if (LP_ABLATE == 1) __syncthreads();
+    else if (t < T && !grid_sync(a, misc, t)) return;
+  }
+}
+
+int g_cus = -1;
+
+}  // namespace
+
+extern "C" int64_t autovc_lstm2_persist_workspace_bytes(int B, int T, int H) {
+  if (B <= 0 || T <= 0 || H != PH) return -1;
+  return BAR_BYTES + 2 * (int64_t)T * B * H * 4;
+}
+
+extern "C" int autovc_lstm2_persist_supported(int B, int H) {
+  if (H != PH || B != PB) return 0;
+  if (g_cus < 0) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
+    int per = 0;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(lstm2_persist_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm2_persist_kernel, PNT, LDS_BYTES) != hipSuccess ||
+        per < 1)
+      g_cus = 0;
+    else
+      g_cus = p.multiProcessorCount;
+  }
+  // every workgroup must be resident at once: one per CU, no more workgroups than CUs
+  return H / PU <= g_cus ? 1 : 0;
+}
+
+extern "C" int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                                            const float* W_hh0, const float* b_ih1, const float* b_hh1,
+                                            const float* W_ih1, const float* W_hh1, float* h0, float* c0,
+                                            float* gates0, float* h1, float* c1, float* gates1, void* workspace,
+                                            hipStream_t stream) {
+  static const char* fn = "autovc_lstm2_fwd_persist_f32";
+  AVC_CHECK_ARG(T > 0 && autovc_lstm2_persist_supported(B, H),
+                "%s: unsupported shape B=%d H=%d on this device (needs H=%d, B=%d, one CU per workgroup)", fn,
+                B, H, PH, PB);
+  AVC_CHECK_ARG(gx0 && W_hh0 && b_ih1 && b_hh1 && W_ih1 && W_hh1 && h0 && c0 && h1 && c1 && workspace,
+                "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh0) && AVC_ALIGNED16(W_ih1) && AVC_ALIGNED16(W_hh1) && AVC_ALIGNED16(workspace),
+                "%s: weights / workspace must be 16-byte aligned", fn);
+  PArgs a;
+  a.B = B; a.T = T; a.H = H;
+  a.gx0 = gx0; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt;
+  a.W_hh0 = W_hh0; a.b_ih1 = b_ih1; a.b_hh1 = b_hh1; a.W_ih1 = W_ih1; a.W_hh1 = W_hh1;
+  a.h0 = h0; a.c0 = c0; a.g0 = gates0; a.h1 = h1; a.c1 = c1; a.g1 = gates1;
+  a.bar = static_cast<int*>(workspace);
+  a.hk0 = reinterpret_cast<float*>(static_cast<char*>(workspace) + BAR_BYTES);
+  a.hk1 = a.hk0 + (int64_t)T * B * H;
+  a.timeout_ticks = 20000000;   // 200 ms of s_memrealtime (100 MHz) per wait
+  AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
+  hipLaunchKernelGGL(lstm2_persist_kernel, dim3(H / PU), dim3(PNT), LDS_BYTES, stream, a);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+
+// 0 = the last call's barriers completed, else a timeout was recorded (synchronises)
+extern "C" int autovc_lstm2_persist_status(const void* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(workspace != nullptr, "autovc_lstm2_persist_status: null workspace");
+  int err = 0;
+  AVC_HIP(hipMemcpyAsync(&err, static_cast<const int*>(workspace) + BAR_ERR * L, sizeof(int), hipMemcpyDeviceToHost,
+                         stream), "autovc_lstm2_persist_status");
+  AVC_HIP(hipStreamSynchronize(stream), "autovc_lstm2_persist_status");
+  return err;
+}

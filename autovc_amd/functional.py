@@ -667,6 +667,16 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
     return dx, dWih, dWhh, dbih, dbhh
 
 
+# decoder lstm2 forward as ONE persistent weight-stationary launch (csrc/lstm2_persist.hip)
+# where the shape and device allow it (H = 1024, one CU per 32 x 32 tile); AVC_LSTM2_PERSIST=0
+# selects the per-step launches
+_PERSIST_ON = os.environ.get("AVC_LSTM2_PERSIST", "0") != "0"
+
+
+def lstm2_persistent(B, H):
+    return _PERSIST_ON and bool(_lib.load().autovc_lstm2_persist_supported(B, H))
+
+
 class LSTM2StackFn(torch.autograd.Function):
     """Two stacked unidirectional large-H layers (decoder lstm2 = nn.LSTM(512, 1024, 2),
     model_vc_mel.py:104,118).  Forward: one GEMM for the layer-0 input projection, then
@@ -695,6 +705,11 @@ class LSTM2StackFn(torch.autograd.Function):
                       b_ih1.data_ptr(), b_hh1.data_ptr(), Wi1b.data_ptr(), W1b.data_ptr(),
                       h0.data_ptr(), h0b.data_ptr(), c0.data_ptr(), _p(g0), h1.data_ptr(), h1b.data_ptr(),
                       c1.data_ptr(), _p(g1), _s())
+        elif lstm2_persistent(B, H):
+            ws = _ws(dev, _lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), "lstm2p")
+            _lib.call("autovc_lstm2_fwd_persist_f32", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W_hh0.data_ptr(),
+                      b_ih1.data_ptr(), b_hh1.data_ptr(), W_ih1.data_ptr(), W_hh1.data_ptr(), h0.data_ptr(),
+                      c0.data_ptr(), _p(g0), h1.data_ptr(), c1.data_ptr(), _p(g1), ws, _s())
         else:
             _lib.call("autovc_lstm2_fwd_f32", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W_hh0.data_ptr(),
                       b_ih1.data_ptr(), b_hh1.data_ptr(), W_ih1.data_ptr(), W_hh1.data_ptr(), h0.data_ptr(),

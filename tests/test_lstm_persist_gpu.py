@@ -1,0 +1,70 @@
+"""Decoder lstm2 forward as one persistent, weight-stationary launch
+(autovc_lstm2_fwd_persist_f32, csrc/lstm2_persist.hip) against the per-step wavefront
+launches (autovc_lstm2_fwd_f32), which the Generator tests pin to the reference: same
+inputs, every output (h0, c0, gates0, h1, c1, gates1) within fp32 summation-order noise,
+no barrier timeout, and graph replay identical to a direct call."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(B, T, H, dev, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    s = 1.0 / H ** 0.5
+    W = [((torch.rand(4 * H, H, generator=g) * 2 - 1) * s).to(dev) for _ in range(3)]
+    b1, b2 = ((torch.rand(4 * H, generator=g) * 0.2 - 0.1).to(dev) for _ in range(2))
+    gx = (torch.randn(B, T, 4 * H, generator=g) * 0.5).to(dev)
+    return gx, W, b1, b2
+
+
+def _run(name, B, T, H, gx, W, b1, b2, dev, ws=None):
+    from autovc_amd import _lib
+    outs = [torch.full((B, T, H), float("nan"), device=dev) for _ in range(4)]
+    gts = [torch.full((B, T, 4 * H), float("nan"), device=dev) for _ in range(2)]
+    h0, c0, h1, c1 = outs
+    g0, g1 = gts
+    args = [B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W[0].data_ptr(), b1.data_ptr(), b2.data_ptr(),
+            W[1].data_ptr(), W[2].data_ptr(), h0.data_ptr(), c0.data_ptr(), g0.data_ptr(), h1.data_ptr(),
+            c1.data_ptr(), g1.data_ptr()]
+    if ws is not None:
+        args.append(ws.data_ptr())
+    _lib.call(name, *args, _lib.stream_ptr(dev))
+    torch.cuda.synchronize()
+    return h0, c0, g0, h1, c1, g1
+
+
+def _supported(B, H):
+    from autovc_amd import _lib
+    return bool(_lib.load().autovc_lstm2_persist_supported(B, H))
+
+
+@pytest.mark.parametrize("T", [3, 128])
+def test_persistent_matches_per_step_launches(cuda, T):
+    from autovc_amd import _lib
+    B, H = 64, 1024
+    if not _supported(B, H):
+        pytest.skip("persistent lstm2 needs one CU per workgroup on this device")
+    gx, W, b1, b2 = _inputs(B, T, H, cuda)
+    ref = _run("autovc_lstm2_fwd_f32", B, T, H, gx, W, b1, b2, cuda)
+    ws = torch.empty(_lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), dtype=torch.uint8, device=cuda)
+    got = _run("autovc_lstm2_fwd_persist_f32", B, T, H, gx, W, b1, b2, cuda, ws)
+    assert _lib.load().autovc_lstm2_persist_status(ws.data_ptr(), _lib.stream_ptr(cuda)) == 0
+    for name, a, r in zip(["h0", "c0", "gates0", "h1", "c1", "gates1"], got, ref):
+        assert bool(torch.isfinite(a).all()), name
+        err = (a.double() - r.double()).abs().max().item() / max(r.abs().max().item(), 1e-30)
+        assert err < 2e-5, (name, err)
+    # a second call into the same workspace (barrier words re-zeroed) is identical
+    again = _run("autovc_lstm2_fwd_persist_f32", B, T, H, gx, W, b1, b2, cuda, ws)
+    for a, b in zip(got, again):
+        assert torch.equal(a, b)
+
+
+def test_persistent_unsupported_shape_rejected(cuda):
+    from autovc_amd import _lib
+    assert not _supported(2, 1024) and not _supported(64, 512)
+    gx, W, b1, b2 = _inputs(2, 4, 1024, cuda)
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=cuda)
+    with pytest.raises(ValueError):
+        _run("autovc_lstm2_fwd_persist_f32", 2, 4, 1024, gx, W, b1, b2, cuda, ws)
