@@ -2,27 +2,32 @@
 // persistent, weight-stationary launch for gfx950.
 //
 // The per-step launch (lstm.hip, lstm2_fwd_step_kernel) re-streams every weight row of both
-// layers into every CU at every step: 768 KB of operands per CU per step (W_hh0, W_ih1,
-// W_hh1 and the h rows, 32 x 1024 fp32 each), which bounds the step at ~24 us — the CU's
-// operand fill, not the MFMA (10.2 us of fp32 MFMA per CU at peak).  Here each of the 256
-// workgroups (one per CU) owns the same 32 batch rows x 32 gate columns (8 hidden units x 4
-// gates) of BOTH layers for the whole sequence and keeps their weights on the CU:
-//   W_ih1, W_hh1 tile rows  -> VGPRs (128 floats per lane: the MFMA B fragments)
-//   W_hh0 tile rows         -> LDS (128 KB, k-blocked [k/4][col][4]: conflict-free b128 reads)
-// so a step streams only the h rows (h0_{t-1}, shared by both layers, and h1_{t-2}): 256 KB
-// per CU.  Steps are separated by an XCD-hierarchical grid barrier instead of a launch
-// boundary (MI355X_MICROARCH.md price list: barrier-xcd).
+// layers into every CU at every step, which bounds the step at ~24 us (the CU's operand fill,
+// not the MFMA: 10.2 us of fp32 MFMA per CU at peak).  Here each of the 256 workgroups (one
+// per CU) owns all 64 batch rows x 16 gate columns (4 hidden units x 4 gates) of BOTH layers
+// for the whole sequence and keeps their weights on the CU:
+//   W_hh0, W_ih1 tile rows -> LDS (64 KB each, k-blocked [k/4][col][4]: conflict-free b128 reads)
+//   W_hh1 tile rows        -> VGPRs (64 floats per lane: the MFMA B fragments)
+// so a step streams only the h rows (h0_{t-1}, shared by both layers, and h1_{t-2}): 512 KB
+// per CU, L2-served.  Steps are separated by an XCD-hierarchical grid barrier instead of a
+// launch boundary (MI355X_MICROARCH.md price list: barrier-xcd).
 //
 // Iteration t (t = 0..T) is the same wavefront as the per-step launch: layer 0 at step t
-// (input h0_{t-1}), layer 1 at step t-1 (inputs h0_{t-1}, h1_{t-2}).  v_mfma_f32_32x32x2_f32
-// (exact fp32), one wave per SIMD (512 VGPRs: 256 of weights, two 8-deep h prefetch windows):
-// wave w takes k in [256w, 256w + 256) of both h0_{t-1} (layer 0 with B from LDS, layer 1's
-// input product with B = W_ih1 from VGPRs) and h1_{t-2} (layer 1's recurrent product, B =
-// W_hh1 from VGPRs).  Each lane half takes 128 consecutive k (lane h: k0 + 128h + i for
-// MFMA i), so a lane's weights and its h fragments are contiguous in memory; the h rows come
-// from a k-blocked copy [t][H/4][B][4] the epilogues write beside h (512 B contiguous per
-// half-wave).  The 4 waves' partial tiles are summed through LDS in fixed order, then the
-// cell update (v_exp / v_rcp sigmoid and tanh).
+// (input h0_{t-1}), layer 1 at step t-1 (inputs h0_{t-1}, h1_{t-2}).  v_mfma_f32_16x16x4_f32
+// (exact fp32), one wave per SIMD: wave w takes k in [256w, 256w + 256) of h0_{t-1} (layer 0,
+// B = W_hh0 from LDS; layer 1's input product, B = W_ih1 from LDS) and h1_{t-2} (layer 1's
+// recurrent product, B = W_hh1 from VGPRs).  MFMA k slot s = lane / 16 takes the 64
+// consecutive k from k0 + 64 s, so a lane's weights and its h fragments are contiguous; the h
+// rows come from a k-blocked copy [t][H/4][B][4] the epilogues write beside h (256 B
+// contiguous per 16 lanes).  The 4 waves' partial tiles are summed through LDS in fixed order,
+// then the cell update (v_exp / v_rcp sigmoid and tanh).
+//
+// Measured (profiles/r02/lstm2_persist_ab.txt, B=64 T=128): 23.9 us per iteration against
+// 23.7 for the per-step launches, so it stays opt-in.  Ablations: no grid barrier 21.0, no
+// products 8.0 (barrier + epilogue), products without the h loads 14.8.  The h stream is the
+// limiter: 512 KB per CU per iteration at the L2-shared per-CU fill rate (66-73 GB/s,
+// MI355X_MICROARCH.md "Indexed rows") is 7.3 us that the one-wave-per-SIMD MFMA stream does
+// not hide; prefetch depth 2/3/4 groups measured 24.5/23.9/25.1.
 //
 // Inter-workgroup visibility (cdna_hip_programming.md Guideline 16, the write-through form of
 // MI355X_MICROARCH.md "Valid forms", first row of its table): the only bytes handed between
