@@ -61,7 +61,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)kOOB, 0x00020000);
 }
 
-template <bool RK, int ROWS, int BK, int NT, bool PAIRK = false>
+template <bool RK, int ROWS, int BK, int NT>
 struct OpTile {
   static constexpr int LD = RK ? BK + 4 : ROWS + 4;
   static constexpr int FLOATS = RK ? ROWS * LD : BK * LD;
@@ -79,22 +79,10 @@ struct OpTile {
   int tap, kmod;            // conv: RK: k / C, k % C (advancing); CK: q / C (fixed)
   int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
   bool rowok;               // CK: the thread's row inside the operand
-  // slot i of this thread -> (row r, k).  PAIRK (CK operands of the bf16 kernel): the
-  // thread's slots come in pairs at k, k + 1 of the same 4 rows, so they pack into bf16x2;
-  // 8 consecutive lanes take 8 consecutive row quads (one 128-B global line) and the next
-  // 8 lanes the next k pair, so the packed LDS words of a wave spread over the banks
-  // (row-quad-major lanes put 32 lanes on 4 banks).
-  static_assert(!PAIRK || RK || (PER % 2 == 0 && (ROWS / 4) % 8 == 0 &&
-                                 BK / 2 == (NT / 8 / (ROWS / 32)) * (PER / 2)), "k pairs");
+  // slot i of this thread -> (row r, k)
   __device__ __forceinline__ static void coords(int i, int& r, int& k) {
     const int e = threadIdx.x + i * NT;
     if (RK) { r = e / (BK / 4); k = 4 * (e % (BK / 4)); }
-    else if (PAIRK) {
-      constexpr int G8 = ROWS / 32;
-      const int t = threadIdx.x, rest = t >> 3;
-      r = 4 * ((t & 7) + 8 * (rest % G8));
-      k = 2 * (rest / G8 + (NT / 8 / G8) * (i >> 1)) + (i & 1);
-    }
     else    { k = e / (ROWS / 4); r = 4 * (e % (ROWS / 4)); }
   }
   __device__ __forceinline__ void init(const Opnd& o, int64_t r0, int64_t kbeg, int64_t R) {
@@ -169,30 +157,30 @@ struct OpTile {
       *reinterpret_cast<f32x4*>(lds + (RK ? r * LD + k : k * LD + r)) = v[i];
     }
   }
-  // bf16 image [row][LDB] (k contiguous) for the bf16 MFMA: RK slots as one 8-byte write,
-  // CK slot pairs (k, k + 1) as four packed bf16x2 words
+  // bf16 image [row][LDB] (k contiguous) of an RK operand: each slot as one 8-byte write
   template <int LDB>
   __device__ __forceinline__ void store_bf16(__bf16* lds) const {
-    if (RK) {
+    static_assert(RK, "CK operands use store_bf16_kr");
 #pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        int r, k;
-        coords(i, r, k);
-        const bf16x4 b = {(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
-        *reinterpret_cast<bf16x4*>(lds + r * LDB + k) = b;
-      }
-    } else {
-      static_assert(PAIRK, "CK bf16 staging needs k pairs");
+    for (int i = 0; i < PER; ++i) {
+      int r, k;
+      coords(i, r, k);
+      const bf16x4 b = {(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
+      *reinterpret_cast<bf16x4*>(lds + r * LDB + k) = b;
+    }
+  }
+  // bf16 image [k][ROWS + 32] (rows contiguous) of a CK operand: each slot's 4 rows as one
+  // 8-byte write (a wave writes whole k rows: conflict-free); read back transposed with
+  // ds_read_b64_tr_b16 (frag_tr below).  The 32-element pad makes the k-row stride 16 dwords
+  // mod 64, so the 4 k rows one 32-lane half reads sit on disjoint banks.
+  static constexpr int LDK = ROWS + 32;
+  __device__ __forceinline__ void store_bf16_kr(__bf16* lds) const {
 #pragma unroll
-      for (int i = 0; i < PER; i += 2) {
-        int r, k;
-        coords(i, r, k);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const bf16x2 b = {(__bf16)v[i][jj], (__bf16)v[i + 1][jj]};
-          *reinterpret_cast<bf16x2*>(lds + (r + jj) * LDB + k) = b;
-        }
-      }
+    for (int i = 0; i < PER; ++i) {
+      int r, k;
+      coords(i, r, k);
+      const bf16x4 b = {(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
+      *reinterpret_cast<bf16x4*>(lds + k * LDK + r) = b;
     }
   }
   // fragment values of MFMAs p = 4g .. 4g+3 (k = h*BK/2 + p) for tile row `row`
@@ -369,9 +357,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   constexpr int NT = 64 * (BM / WM) * NWN;
   constexpr int TI = WM / 32, TJ = WN / 32;
   constexpr int LDB = BK + 8;
-  using TA = OpTile<A_RK, BM, BK, NT, true>;
-  using TBt = OpTile<B_RK, BN, BK, NT, true>;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2][(BM + BN) * LDB];
+  using TA = OpTile<A_RK, BM, BK, NT>;
+  using TBt = OpTile<B_RK, BN, BK, NT>;
+  // RK operands: [row][BK + 8] images read with ds_read_b128; CK operands: [k][rows + 32]
+  // images read with ds_read_b64_tr_b16
+  constexpr int A_EL = A_RK ? BM * LDB : BK * TA::LDK;
+  constexpr int B_EL = B_RK ? BN * LDB : BK * TBt::LDK;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2][A_EL + B_EL];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / NWN, wc = wave % NWN;
@@ -401,15 +393,34 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   TBt sb;
   sa.init(A, m0, kbeg, M);
   sb.init(B, n0, kbeg, N);
+  auto stage = [&](__bf16* img) {
+    if constexpr (A_RK) sa.template store_bf16<LDB>(img);
+    else sa.store_bf16_kr(img);
+    if constexpr (B_RK) sb.template store_bf16<LDB>(img + A_EL);
+    else sb.store_bf16_kr(img + A_EL);
+  };
   if (nk > 0) {
     sa.load(A, kend);
     sb.load(B, kend);
-    sa.template store_bf16<LDB>(smem[0]);
-    sb.template store_bf16<LDB>(smem[0] + BM * LDB);
+    stage(smem[0]);
   }
   __syncthreads();
 
   const int h = lane >> 5, li = lane & 31;
+  // transposed-read lane map (T10): lane 16g + 4q + p supplies k row 8h + q (+4) and rows
+  // 16 (g & 1) + 4p .. +3 of the 32-row block; it receives row (lane & 31)'s 8 k values
+  const int tr_off = ((lane >> 2) & 3) + 8 * h;               // k row within the 16-k step
+  const int tr_row = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  auto frag_tr = [&](const __bf16* img, int LDK, int row0, int ks) {
+    const __bf16* p0 = img + (ks * 16 + tr_off) * LDK + row0 + tr_row;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(p0 + 4 * LDK));
+    const s16x4 w[2] = {lo, hi};
+    return __builtin_bit_cast(bf16x8, w);
+  };
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) {
@@ -417,26 +428,25 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
       sb.load(B, kend);
     }
     const __bf16* As = smem[buf];
-    const __bf16* Bs = smem[buf] + BM * LDB;
+    const __bf16* Bs = smem[buf] + A_EL;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 fa[TI], fb[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8*>(As + (wr * WM + i * 32 + li) * LDB + ks * 16 + 8 * h);
+        fa[i] = A_RK ? *reinterpret_cast<const bf16x8*>(As + (wr * WM + i * 32 + li) * LDB + ks * 16 + 8 * h)
+                     : frag_tr(As, TA::LDK, wr * WM + i * 32, ks);
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (wc * WN + j * 32 + li) * LDB + ks * 16 + 8 * h);
+        fb[j] = B_RK ? *reinterpret_cast<const bf16x8*>(Bs + (wc * WN + j * 32 + li) * LDB + ks * 16 + 8 * h)
+                     : frag_tr(Bs, TBt::LDK, wc * WN + j * 32, ks);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) {
-      sa.template store_bf16<LDB>(smem[buf ^ 1]);
-      sb.template store_bf16<LDB>(smem[buf ^ 1] + BM * LDB);
-    }
+    if (kt + 1 < nk) stage(smem[buf ^ 1]);
     __syncthreads();
   }
 
@@ -594,11 +604,49 @@ void launch_gemm(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, in
 // bf16 tiles: 128x128 (4 waves of 64x64) once that grid fills the chip, else 64x64; BK 64:
 // with the MFMA work per stage 16x smaller than fp32's, the kernel waits on its operand
 // loads, so a stage keeps twice the bytes in flight (BK 32: conv fwd 67 us, LSTM dW 438 us)
-constexpr GemmShape kCfgBf16[] = {{0, 128, 128, 64}, {1, 64, 64, 64}};
+constexpr GemmShape kCfgBf16[] = {
+    {0, 128, 128, 64},   // 4 waves of 64x64
+    {1, 64, 64, 64},     // 4 waves of 32x32
+    {2, 256, 128, 64},   // 8 waves of 64x64 (one workgroup per CU)
+    {3, 256, 256, 64},   // 8 waves of 128x64 (one workgroup per CU)
+    {4, 256, 256, 32},   // 8 waves of 128x64, BK 32
+};
+int g_force_cfg_bf16 = -1;   // tools/gemm_bf16_bench.hip overrides these
+int g_force_splits_bf16 = 0;
 
 GemmShape pick_config_bf16(int M, int N, int splits) {
+  if (g_force_cfg_bf16 >= 0) return kCfgBf16[g_force_cfg_bf16];
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
   return t128 >= 256 ? kCfgBf16[0] : kCfgBf16[1];
+}
+
+// Large bf16 GEMMs: one workgroup per CU on 256-row tiles, split-K chosen here so that about
+// one wave of 256 workgroups runs (tools/gemm_bf16_bench.hip, round 2, bf16-exact operands
+// = the fp32 result): 256x256/BK32 when the tile grid times a split of <= 4 fills the chip with
+// >= 1024 k per split (LSTM dW 4096x1024x8192: 4 splits, 128 us vs 221 for 128x128 unsplit;
+// LSTM dX 8192x1024x4096: 2 splits, 127 vs 132), else 256x128 with <= 4 splits of >= 512 k
+// (conv fwd/dX 8192x512x2560: 2 splits, 57 vs 68 us; conv dW 512x2560x8192: 4 splits, 79 vs
+// 87 for 128x128 at 4), and 256x128 unsplit for grids of >= 256 such tiles (LSTM input
+// projections 8192x4096x1024: 151 us).  Smaller outputs keep the caller's split and the
+// 128x128 / 64x64 tiles.
+struct PlanBf16 { int cfg, splits; };
+PlanBf16 plan_bf16(int M, int N, int K, int requested) {
+  const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  const int64_t t2 = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
+  if (t2 >= 256) return {2, 1};
+  for (int s = 1; s <= 4; ++s)
+    if (t256 * s >= 224 && t256 * s <= 288 && K / s >= 1024) return {4, s};
+  if (t2 >= 16) {
+    int s = (int)std::max<int64_t>(1, std::min<int64_t>(4, (256 + t2 / 2) / t2));
+    while (s > 1 && K / s < 512) --s;
+    return {2, s};
+  }
+  return {-1, requested};
+}
+
+template <int BM, int BN, int BK, bool AR, bool BR>
+constexpr unsigned bf16_lds_bytes() {
+  return 2u * 2u * ((AR ? BM * (BK + 8) : BK * (BM + 32)) + (BR ? BN * (BK + 8) : BK * (BN + 32)));
 }
 
 template <int BM, int BN, int BK, int WM, int WN>
@@ -606,7 +654,7 @@ void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, in
                          float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
 #define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), \
-                                         dyn_lds_for(2u * 2u * (BM + BN) * (BK + 8)), st, M, N, \
+                                         dyn_lds_for(bf16_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, \
                                          K, oa, ob, C, ldc, b1, b2, acc, kps, slab, g_batch)
   if (!a_trans && !b_trans) AVC_L(true, true);
   else if (!a_trans && b_trans) AVC_L(true, false);
@@ -618,12 +666,13 @@ void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, in
 void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa,
                       Opnd ob, float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps,
                       float* slab) {
-  if (id == 0)
-    launch_layouts_bf16<128, 128, 64, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
-                                              slab);
-  else
-    launch_layouts_bf16<64, 64, 64, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps,
-                                            slab);
+  switch (id) {
+    case 0: launch_layouts_bf16<128, 128, 64, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 2: launch_layouts_bf16<256, 128, 64, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 3: launch_layouts_bf16<256, 256, 64, 128, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 4: launch_layouts_bf16<256, 256, 32, 128, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    default: launch_layouts_bf16<64, 64, 64, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+  }
 }
 
 }  // namespace
@@ -655,8 +704,21 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   AVC_CHECK_ARG(4 * (a_ext + 2 * lda) < (int64_t)kOOB && 4 * (b_ext + 2 * ldb) < (int64_t)kOOB,
                 "autovc_gemm: operand extents must stay below 2 GiB");
   if (splits < 1) splits = 1;
+  if (bf16 && g_force_splits_bf16 > 0 && batch == 1) splits = g_force_splits_bf16;
   AVC_CHECK_ARG(batch >= 1 && (batch == 1 || splits == 1), "autovc_gemm: batched calls cannot split K");
+  if (bf16 && batch == 1 && g_force_cfg_bf16 < 0) {
+    const PlanBf16 pl = plan_bf16(M, N, K, splits);
+    if (pl.cfg >= 0) {
+      AVC_CHECK_ARG(pl.splits <= splits || workspace,
+                    "autovc_gemm_bf16_f32: split-K plan needs the workspace of autovc_gemm_bf16_splits");
+      splits = pl.splits;
+    }
+  }
   GemmShape cfg = bf16 ? pick_config_bf16(M, N, batch > 1 ? batch : splits) : pick_config(M, N, K, splits);
+  if (bf16 && batch == 1 && g_force_cfg_bf16 < 0) {
+    const PlanBf16 pl = plan_bf16(M, N, K, splits);
+    if (pl.cfg >= 0) cfg = kCfgBf16[pl.cfg];
+  }
   if (batch > 1 && !bf16) {   // batched: tile count x batch decides between 128x128 and 64x64
     const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch;
     cfg = t128 >= 512 ? kCfg[2] : kCfg[8];
@@ -705,6 +767,12 @@ extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
                                     int accumulate, int splits, float* workspace, hipStream_t stream) {
   return gemm_impl(true, 1, 0, 0, 0, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T,
                    b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
+}
+
+extern "C" int autovc_gemm_bf16_splits(int M, int N, int K, int requested) {
+  if (M <= 0 || N <= 0 || K <= 0) return requested < 1 ? 1 : requested;
+  const PlanBf16 pl = plan_bf16(M, N, K, requested < 1 ? 1 : requested);
+  return pl.splits;
 }
 
 extern "C" int autovc_gemm_set_lds_reserve(int bytes) {

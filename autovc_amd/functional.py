@@ -207,6 +207,8 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
     ac = a_conv or (0, 0, 0)
     bc = b_conv or (0, 0, 0)
     ws = 0
+    if _PRECISION[0] == "bf16":   # the library plans large bf16 GEMMs' split-K itself
+        splits = _lib.load().autovc_gemm_bf16_splits(M, N, K, splits)
     if splits > 1:
         ws = _ws(C.device, 4 * _lib.load().autovc_gemm_workspace_floats(M, N, splits), "gemm")
     fn = "autovc_gemm_bf16_f32" if _PRECISION[0] == "bf16" else "autovc_gemm_f32"

@@ -103,6 +103,11 @@ int autovc_gemm_bf16_f32(int M, int N, int K,
                          const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                          float* C, int64_t ldc, const float* bias1, const float* bias2,
                          int accumulate, int splits, float* workspace, hipStream_t stream);
+/* The split-K count autovc_gemm_bf16_f32 uses for this shape when the caller asks for
+ * `requested` splits: large outputs run one workgroup per CU on 256-row tiles with the
+ * library's own split (so the workspace must be autovc_gemm_workspace_floats(M, N, returned
+ * value) floats), smaller ones keep `requested`. */
+int autovc_gemm_bf16_splits(int M, int N, int K, int requested);
 
 /* batch independent GEMMs C_z = A_z B_z (same layouts as autovc_gemm_f32, plain operands,
  * no bias/accumulate/split-K) in one launch; A_z / B_z / C_z start z * (a_bstride,

@@ -20,7 +20,13 @@ def r16(t):
 
 
 @pytest.mark.parametrize("M,N,K,at,bt", [(256, 128, 64, 0, 0), (300, 200, 36, 0, 1), (100, 260, 520, 1, 0),
-                                         (64, 80, 1024, 1, 1), (8192, 512, 2560, 0, 0), (512, 2560, 8192, 1, 1)])
+                                         (64, 80, 1024, 1, 1), (8192, 512, 2560, 0, 0), (512, 2560, 8192, 1, 1),
+                                         # the library-planned 256-row tiles: LSTM dW (256x256, 4
+                                         # splits), dX (256x256, 2), input projection (256x128,
+                                         # unsplit), and ragged edges on 256x128 with 4 splits
+                                         (4096, 1024, 8192, 1, 1), (8192, 1024, 4096, 0, 1),
+                                         (8192, 4096, 1024, 0, 0), (1000, 700, 3000, 1, 0),
+                                         (777, 1028, 2048, 0, 1)])
 def test_gemm_bf16_layouts(cuda, M, N, K, at, bt):
     from autovc_amd import functional as AF
     g = torch.Generator().manual_seed(M + N + K)
