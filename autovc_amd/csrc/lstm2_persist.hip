@@ -54,7 +54,12 @@
 #define LP_W1_LDS 1
 #endif
 #ifndef LP_PWIN
-#define LP_PWIN 3
+#define LP_PWIN 1
+#endif
+// waves per workgroup: 4 (one per SIMD) or 8 (two per SIMD: one wave's MFMAs run while the
+// other waits for its h loads)
+#ifndef LP_NW
+#define LP_NW 8
 #endif
 
 namespace {
@@ -62,22 +67,26 @@ namespace {
 constexpr int PB = 64;             // batch rows per tile (all of them)
 constexpr int PU = 4;              // hidden units per tile (x 4 gates = 16 columns)
 constexpr int PC = 4 * PU;         // tile columns
-constexpr int PNW = 4;             // waves per workgroup (one per SIMD)
+constexpr int PNW = LP_NW;         // waves per workgroup
 constexpr int PNT = 64 * PNW;
 constexpr int PH = 1024;           // hidden size this kernel is built for
-constexpr int PKW = PH / PNW;      // k per wave and segment (256)
+constexpr int PRH = PNW == 16 ? 2 : 1;   // row halves: 16 waves = 8 k ranges x 2 row halves
+constexpr int PKWN = PNW / PRH;    // k ranges
+constexpr int PKW = PH / PKWN;     // k per wave and segment
 constexpr int PKL = PKW / 4;       // k per lane group (64: lane group l / 16 of the MFMA)
 constexpr int PGR = PKL / 4;       // 4-k groups per lane (16)
 constexpr int PRB = PB / 16;       // 16-row blocks of the tile (4)
+constexpr int PRBW = PRB / PRH;    // 16-row blocks per wave
 constexpr int PWIN = LP_PWIN;      // h groups in flight per stream
 constexpr int RED_LD = PC + 1;     // padded row of a 64 x 16 partial tile in LDS
 constexpr int RED_SLOT = PB * RED_LD;
 constexpr int LDS_W0 = (PH / 4) * PC * 4;          // floats: W_hh0 tile [k/4][16][4]
 constexpr int LDS_W1 = LP_W1_LDS ? LDS_W0 : 0;     // floats: W_ih1 tile, same layout
 constexpr int RED_LAYERS = LP_W1_LDS ? 1 : 2;      // partial tiles of one layer at a time, or both
-constexpr int LDS_RED = RED_LAYERS * PNW * RED_SLOT;
-constexpr int LDS_MISC = 16;                       // floats: broadcast words
-constexpr int LDS_BYTES = 4 * (LDS_W0 + LDS_W1 + LDS_RED + LDS_MISC);
+constexpr int NSLOT = 4;                            // partial-tile slots per layer
+static_assert(PNW == 4 || ((PNW == 8 || PNW == 16) && LP_W1_LDS), "8/16 waves: W_ih1 in LDS, shared slots");
+constexpr int LDS_RED = RED_LAYERS * NSLOT * RED_SLOT;
+constexpr int LDS_BYTES = 4 * (LDS_W0 + LDS_W1 + LDS_RED);
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
 // barrier block: one 128-B line per word (ints)
@@ -130,11 +139,12 @@ __device__ __noinline__ bool wait_ge(int* p, int target, int* err, int timeout_t
 
 // Grid barrier number `gen` (0, 1, ...).  Called by every thread; returns false if any
 // workgroup timed out (then every workgroup leaves the kernel).
-__device__ __forceinline__ bool grid_sync(const PArgs& a, int* misc, int gen) {
+// xcc / mine / nx: this workgroup's XCC, the workgroups on it and the XCCs in use (held by
+// thread 0); *status: an LDS word broadcasting the outcome to the workgroup
+__device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int nx, int* status, int gen) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's stores are in L2
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int xcc = misc[0], mine = misc[1], nx = misc[2];
     bool ok = true;
     const int old = add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
     if (old == mine * (gen + 1) - 1) {                    // last of this XCC
@@ -144,32 +154,51 @@ __device__ __forceinline__ bool grid_sync(const PArgs& a, int* misc, int gen) {
     }
     ok = wait_ge(a.bar + (BAR_GEN + xcc) * L, gen + 1, a.bar + BAR_ERR * L, a.timeout_ticks);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)
-    misc[3] = ok ? 0 : 1;
+    *status = ok ? 0 : 1;
   }
   __syncthreads();
-  return misc[3] == 0;
+  return *status == 0;
 }
 
 // per-step cell update of one (batch row b, unit j) from its 4 gate pre-activations
-__device__ __forceinline__ void cell(const float (&pre)[4], float cp, float* c_out, float* h_out, float* g_out,
-                                    float* hk_out, int64_t H) {
-  const float i_ = avc_sigmoid_fast(pre[0]), f_ = avc_sigmoid_fast(pre[1]);
-  const float g_ = avc_tanh_fast(pre[2]), o_ = avc_sigmoid_fast(pre[3]);
-  const float cn = f_ * cp + i_ * g_;
-  const float hn = o_ * avc_tanh_fast(cn);
-  *c_out = cn;
-  *h_out = hn;
-  __hip_atomic_store(hk_out, hn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: handed off
-  if (g_out) { g_out[0] = i_; g_out[H] = f_; g_out[2 * H] = g_; g_out[3 * H] = o_; }
+// Only the k-blocked h copy is handed to other workgroups, so only it is stored before the
+// grid barrier (sc1, write-through); h, c and the gates are kept in registers and stored
+// after the barrier, under the next iteration's products (the barrier's vmcnt(0) then waits
+// for the hand-off stores alone).  The cell state is carried in registers, never re-read.
+struct CellOut { float c, h, i, f, g, o; };
+
+__device__ __forceinline__ CellOut cell(const float (&pre)[4], float cp, float* hk_out) {
+  CellOut r;
+  r.i = avc_sigmoid_fast(pre[0]);
+  r.f = avc_sigmoid_fast(pre[1]);
+  r.g = avc_tanh_fast(pre[2]);
+  r.o = avc_sigmoid_fast(pre[3]);
+  r.c = r.f * cp + r.i * r.g;
+  r.h = r.o * avc_tanh_fast(r.c);
+  __hip_atomic_store(hk_out, r.h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: handed off
+  return r;
+}
+
+__device__ __forceinline__ void cell_store(const CellOut& r, float* c_out, float* h_out, float* g_out, int64_t H) {
+  *c_out = r.c;
+  *h_out = r.h;
+  if (g_out) { g_out[0] = r.i; g_out[H] = r.f; g_out[2 * H] = r.g; g_out[3 * H] = r.o; }
 }
 
 // acc[rb] (16 x 16 MFMA tiles of the 64 x 16 tile) -> LDS partial slot: C/D map of
 // v_mfma_f32_16x16x4f32: col = lane & 15, row = 4 (lane >> 4) + r
-__device__ __forceinline__ void put_tile(float* slot, const f32x4 (&acc)[PRB], int lane) {
+__device__ __forceinline__ void put_tile(float* slot, const f32x4 (&acc)[PRBW], int rb0, int lane) {
 #pragma unroll
-  for (int rb = 0; rb < PRB; ++rb)
+  for (int rb = 0; rb < PRBW; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) slot[(16 * rb + 4 * (lane >> 4) + r) * RED_LD + (lane & 15)] = acc[rb][r];
+    for (int r = 0; r < 4; ++r) slot[(16 * (rb0 + rb) + 4 * (lane >> 4) + r) * RED_LD + (lane & 15)] = acc[rb][r];
+}
+
+__device__ __forceinline__ void add_tile(float* slot, const f32x4 (&acc)[PRBW], int rb0, int lane) {
+#pragma unroll
+  for (int rb = 0; rb < PRBW; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slot[(16 * (rb0 + rb) + 4 * (lane >> 4) + r) * RED_LD + (lane & 15)] += acc[rb][r];
 }
 
 // One iteration's products of a wave over its k range: S0 = stream h0_{t-1} (layer 1 input
@@ -180,24 +209,24 @@ template <bool S0, bool L0, bool S1>
 __device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const float* __restrict__ hk1_t,
                                           const float (&wi)[LP_W1_LDS ? 1 : PKL], const float (&wh)[PKL], const float* W0,
                                           const float* W1, int kb0,
-                                          int B, int lane, f32x4 (&acc1)[PRB], f32x4 (&acc0)[PRB]) {
+                                          int B, int rb0, int lane, f32x4 (&acc1)[PRBW], f32x4 (&acc0)[PRBW]) {
   // group g, row block rb: f32x4 at hk[kb0 + g][16 rb + (lane & 15)][0..3]; sc1 buffer loads
   // (every load of the handed-off rows bypasses L1: no acquire fence needed)
   const __amdgpu_buffer_rsrc_t r0 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hk0_t), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t r1 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hk1_t), (short)0, 0x7fffffff, 0x00020000);
-  const uint32_t off0 = (uint32_t)((kb0 * B + (lane & 15)) * 16);
+  const uint32_t off0 = (uint32_t)((kb0 * B + 16 * rb0 + (lane & 15)) * 16);
   const uint32_t gstride = (uint32_t)B * 16;
   auto ld = [&](__amdgpu_buffer_rsrc_t r, int g, int rb) {
     if (LP_ABLATE == 3) return f32x4{0.5f, 0.25f, (float)g, (float)rb};
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off0 + g * gstride + rb * 256, 0, 16));
   };
-  f32x4 a0[PWIN][PRB], a1[PWIN][PRB];
+  f32x4 a0[PWIN][PRBW], a1[PWIN][PRBW];
 #pragma unroll
   for (int g = 0; g < PWIN; ++g)
 #pragma unroll
-    for (int rb = 0; rb < PRB; ++rb) {
+    for (int rb = 0; rb < PRBW; ++rb) {
       if (S0) a0[g][rb] = ld(r0, g, rb);
       if (S1) a1[g][rb] = ld(r1, g, rb);
     }
@@ -205,15 +234,15 @@ __device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const
   const float* w1p = W1 + (kb0 * PC + (lane & 15)) * 4;
 #pragma unroll
   for (int g = 0; g < PGR; ++g) {
-    f32x4 x0[PRB], x1[PRB];
+    f32x4 x0[PRBW], x1[PRBW];
 #pragma unroll
-    for (int rb = 0; rb < PRB; ++rb) {
+    for (int rb = 0; rb < PRBW; ++rb) {
       x0[rb] = a0[g % PWIN][rb];
       x1[rb] = a1[g % PWIN][rb];
     }
     if (g + PWIN < PGR) {
 #pragma unroll
-      for (int rb = 0; rb < PRB; ++rb) {
+      for (int rb = 0; rb < PRBW; ++rb) {
         if (S0) a0[g % PWIN][rb] = ld(r0, g + PWIN, rb);
         if (S1) a1[g % PWIN][rb] = ld(r1, g + PWIN, rb);
       }
@@ -224,7 +253,7 @@ __device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int rb = 0; rb < PRB; ++rb) {
+      for (int rb = 0; rb < PRBW; ++rb) {
         if (S0) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], LP_W1_LDS ? bv1[q] : wi[LP_W1_LDS ? 0 : 4 * g + q],
                                                                 acc1[rb], 0, 0, 0);
         if (S1) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[rb][q], wh[4 * g + q], acc1[rb], 0, 0, 0);
@@ -238,7 +267,9 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
   float* W0 = lds;                          // [H/4][16][4]
   float* W1 = lds + LDS_W0;                 // [H/4][16][4] (LP_W1_LDS)
   float* red = W1 + LDS_W1;                 // layer 1: slots 0..3, layer 0: slots 4..7 (or reused)
-  int* misc = reinterpret_cast<int*>(red + LDS_RED);
+  // broadcast word: the pad column of slot 0's row 0, never written by put_tile / add_tile
+  int* status = reinterpret_cast<int*>(red + PC);
+  int xcc_id = 0, xcc_wgs = 0, xcc_n = 0;
   const int H = PH, B = a.B, T = a.T;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j0 = blockIdx.x * PU;
@@ -254,10 +285,10 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
     const bool ok = wait_ge(a.bar + BAR_START * L, gridDim.x, a.bar + BAR_ERR * L, a.timeout_ticks);
     int nx = 0;
     for (int x = 0; x < 16; ++x) nx += ld_rlx(a.bar + (BAR_CENSUS + x) * L) > 0;
-    misc[0] = (int)xcc;
-    misc[1] = ld_rlx(a.bar + (BAR_CENSUS + xcc) * L);
-    misc[2] = nx;
-    misc[3] = ok ? 0 : 1;
+    xcc_id = (int)xcc;
+    xcc_wgs = ld_rlx(a.bar + (BAR_CENSUS + xcc) * L);
+    xcc_n = nx;
+    *status = ok ? 0 : 1;
   }
   // ---- weights: W_hh0 tile -> LDS (k-blocked), W_ih1 / W_hh1 fragments -> VGPRs
   for (int e = tid; e < (H / 4) * PC; e += PNT) {
@@ -267,7 +298,8 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
       *reinterpret_cast<f32x4*>(W1 + e * 4) =
           *reinterpret_cast<const f32x4*>(a.W_ih1 + (int64_t)grow(col) * H + kb * 4);
   }
-  const int kbase = wave * PKW + PKL * (lane >> 4);          // this lane's first k
+  const int kw = wave % PKWN, rb0 = (wave / PKWN) * PRBW;    // k range, first row block
+  const int kbase = kw * PKW + PKL * (lane >> 4);             // this lane's first k
   const int kb0 = kbase / 4;
   float wi[LP_W1_LDS ? 1 : PKL], wh[PKL];
   {
@@ -282,7 +314,7 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
     }
   }
   __syncthreads();
-  if (misc[3] != 0) return;
+  if (*status != 0) return;
 
   // epilogue ownership: thread e owns (batch row e / 4, unit j0 + e % 4) of both layers
   const int eb = tid >> 2, ej = j0 + (tid & 3), eu = tid & 3;
@@ -292,40 +324,61 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) bias1[g] = a.b_ih1[g * H + ej] + a.b_hh1[g * H + ej];
   const int64_t BH = (int64_t)B * H;
+  CellOut out0 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, out1 = out0;   // c carried from step to step
+  // the previous iteration's outputs (layer 0 at step t0, layer 1 at step t0 - 1)
+  auto store_outputs = [&](int t0) {
+    if (!eown) return;
+    if (t0 >= 1) {
+      const int t1 = t0 - 1;
+      const int64_t o = ((int64_t)eb * T + t1) * H + ej;
+      cell_store(out1, a.c1 + o, a.h1 + o, a.g1 ? a.g1 + ((int64_t)eb * T + t1) * 4 * H + ej : nullptr, H);
+    }
+    if (t0 < T) {
+      const int64_t o = ((int64_t)eb * T + t0) * H + ej;
+      cell_store(out0, a.c0 + o, a.h0 + o, a.g0 ? a.g0 + ((int64_t)eb * T + t0) * 4 * H + ej : nullptr, H);
+    }
+  };
 
   for (int t = 0; t <= T; ++t) {
     const bool l0 = t < T, l1 = t >= 1;
+    if (t >= 1) store_outputs(t - 1);
     // epilogue operands of this iteration (latency hidden under the products)
-    float gxv[4] = {0.f, 0.f, 0.f, 0.f}, cp0 = 0.f, cp1 = 0.f;
-    if (eown) {
-      if (l0) {
-        const float* g = a.gx0 + (int64_t)eb * a.gx_ldb + (int64_t)t * a.gx_ldt;
+    float gxv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (eown && l0) {
+      const float* g = a.gx0 + (int64_t)eb * a.gx_ldb + (int64_t)t * a.gx_ldt;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) gxv[q] = g[q * H + ej];
-        if (t >= 1) cp0 = a.c0[((int64_t)eb * T + t - 1) * H + ej];
-      }
-      if (t >= 2) cp1 = a.c1[((int64_t)eb * T + t - 2) * H + ej];
+      for (int q = 0; q < 4; ++q) gxv[q] = g[q * H + ej];
     }
-    f32x4 acc1[PRB] = {}, acc0[PRB] = {};
+    f32x4 acc1[PRBW] = {}, acc0[PRBW] = {};
     const float* hk0 = a.hk0 + (int64_t)(t >= 1 ? t - 1 : 0) * BH;   // h0_{t-1}
     const float* hk1 = a.hk1 + (int64_t)(t >= 2 ? t - 2 : 0) * BH;   // h1_{t-2}
     if (LP_ABLATE == 2 || t == 0) {                                  // h0_{-1} = 0: no products
     } else if (t == 1) {                                             // h1_{-1} = 0
-      gemm_wave<true, true, false>(hk0, hk1, wi, wh, W0, W1, kb0, B, lane, acc1, acc0);
+      gemm_wave<true, true, false>(hk0, hk1, wi, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
     } else if (t < T) {
-      gemm_wave<true, true, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, lane, acc1, acc0);
+      gemm_wave<true, true, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
     } else {                                                         // t == T: layer 1 only
-      gemm_wave<true, false, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, lane, acc1, acc0);
+      gemm_wave<true, false, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
     }
     if (LP_ABLATE != 4) {
       // the 4 waves' partial tiles summed through LDS in fixed order
       auto sum = [&](int layer, int g) {
-        const float* r = red + layer * PNW * RED_SLOT + eb * RED_LD + g * PU + eu;
+        const float* r = red + layer * NSLOT * RED_SLOT + eb * RED_LD + g * PU + eu;
         return ((r[0] + r[RED_SLOT]) + r[2 * RED_SLOT]) + r[3 * RED_SLOT];
       };
       constexpr int L0SLOT = RED_LAYERS - 1;                         // layer 0's slots
-      put_tile(red + wave * RED_SLOT, acc1, lane);
-      if (!LP_W1_LDS) put_tile(red + (L0SLOT * PNW + wave) * RED_SLOT, acc0, lane);
+      // more than 4 waves: wave w < 4 stores its tile into slot w, then waves 4..7 add into
+      // slots 0..3, then waves 8..11, ... (fixed order)
+      auto reduce_put = [&](float* slots, const f32x4 (&acc)[PRBW]) {
+        if (kw < 4) put_tile(slots + (kw & 3) * RED_SLOT, acc, rb0, lane);
+#pragma unroll
+        for (int ph = 1; ph < PKWN / 4; ++ph) {
+          __syncthreads();
+          if (kw / 4 == ph) add_tile(slots + (kw & 3) * RED_SLOT, acc, rb0, lane);
+        }
+      };
+      reduce_put(red, acc1);
+      if (!LP_W1_LDS) put_tile(red + (L0SLOT * NSLOT + wave) * RED_SLOT, acc0, 0, lane);
       __syncthreads();
       if (eown) {
         if (l1) {                                                    // layer 1 at step t - 1
@@ -333,15 +386,12 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + bias1[g];
           const int t1 = t - 1;
-          const int64_t o = ((int64_t)eb * T + t1) * H + ej;
-          cell(pre, t1 >= 1 ? cp1 : 0.f, a.c1 + o, a.h1 + o,
-               a.g1 ? a.g1 + ((int64_t)eb * T + t1) * 4 * H + ej : nullptr,
-               a.hk1 + (int64_t)t1 * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3), H);
+          out1 = cell(pre, out1.c, a.hk1 + (int64_t)t1 * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3));
         }
       }
       if (LP_W1_LDS) {                                               // slots reused for layer 0
         __syncthreads();
-        put_tile(red + wave * RED_SLOT, acc0, lane);
+        reduce_put(red, acc0);
         __syncthreads();
       }
       if (eown) {
@@ -349,17 +399,16 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
           float pre[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) pre[g] = sum(L0SLOT, g) + gxv[g];
-          const int64_t o = ((int64_t)eb * T + t) * H + ej;
-          cell(pre, cp0, a.c0 + o, a.h0 + o, a.g0 ? a.g0 + ((int64_t)eb * T + t) * 4 * H + ej : nullptr,
-               a.hk0 + (int64_t)t * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3), H);
+          out0 = cell(pre, out0.c, a.hk0 + (int64_t)t * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3));
         }
       }
     } else if (wave == 0 && acc1[0][0] == 12345.f && acc0[1][1] == 12345.f) {
       a.h0[0] = 0.f;                                                  // keep the products live
     }
     if (LP_ABLATE == 1) __syncthreads();
-    else if (t < T && !grid_sync(a, misc, t)) return;
+    else if (t < T && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, status, t)) return;
   }
+  store_outputs(T);                                                  // layer 1 at step T - 1
 }
 
 int g_cus = -1;

@@ -669,10 +669,11 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
     return dx, dWih, dWhh, dbih, dbhh
 
 
-# decoder lstm2 forward as ONE persistent weight-stationary launch (csrc/lstm2_persist.hip)
-# where the shape and device allow it (H = 1024, one CU per 32 x 32 tile); AVC_LSTM2_PERSIST=0
-# selects the per-step launches
-_PERSIST_ON = os.environ.get("AVC_LSTM2_PERSIST", "0") != "0"
+# decoder lstm2 forward (fp32) as ONE persistent weight-stationary launch
+# (csrc/lstm2_persist.hip) where the shape and device allow it (H = 1024, B = 64, one
+# workgroup per CU): 20.3 vs 23.7 us per wavefront iteration (profiles/r02/lstm2_persist_ab.txt);
+# AVC_LSTM2_PERSIST=0 selects the per-step launches
+_PERSIST_ON = os.environ.get("AVC_LSTM2_PERSIST", "1") != "0"
 
 
 def lstm2_persistent(B, H):

@@ -50,12 +50,14 @@ def make_solver(dev, B):
 
 
 def lstm_roofline(solver, B, T, dev):
-    """The dominant LSTM kernel of the forward — decoder lstm2's two-layer wavefront launch
-    (lstm2_fwd_step_kernel, what the Generator runs) — timed per launch with dispatch
-    events and priced with SURVEY §8d's algorithmic bytes per layer-step (x 2 layers; the
-    W_ih1 read of the fused layer-1 input projection is NOT counted).  The single-layer
-    step kernel (lstm1's, here at lstm2's size) is reported alongside."""
-    from autovc_amd import _lib
+    """The dominant LSTM kernel of the forward — decoder lstm2's two-layer recurrence as the
+    Generator runs it: the persistent weight-stationary launch (lstm2_persist_kernel, one
+    launch per sequence) when functional.lstm2_persistent(B, H), else the per-step wavefront
+    launch (lstm2_fwd_step_kernel).  Timed with events on the launch stream; FLOPs = the
+    recurrent MACs of both layers (layer 1's input product included), x 2; SURVEY §8d's
+    algorithmic bytes per layer-step are reported under 'hbm'.  The per-step launch and the
+    single-layer step kernel are reported alongside."""
+    from autovc_amd import _lib, functional as AF
     import ctypes
     lstm = solver.G.decoder.lstm2
     H = lstm.hidden_size
@@ -75,46 +77,68 @@ def lstm_roofline(solver, B, T, dev):
         return sorted(xs)[1]
 
     st = _lib.stream_ptr(dev)
-    us2 = med(lambda: _lib.call("autovc_lstm2_fwd_timed_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H,
-                                P["weight_hh_l0"].data_ptr(), P["bias_ih_l1"].data_ptr(), P["bias_hh_l1"].data_ptr(),
-                                P["weight_ih_l1"].data_ptr(), P["weight_hh_l1"].data_ptr(), h0.data_ptr(),
-                                c0.data_ptr(), g0.data_ptr(), h1.data_ptr(), c1.data_ptr(), g1.data_ptr(), st,
-                                ctypes.byref(avg)))
+    args = [B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, P["weight_hh_l0"].data_ptr(), P["bias_ih_l1"].data_ptr(),
+            P["bias_hh_l1"].data_ptr(), P["weight_ih_l1"].data_ptr(), P["weight_hh_l1"].data_ptr(), h0.data_ptr(),
+            c0.data_ptr(), g0.data_ptr(), h1.data_ptr(), c1.data_ptr(), g1.data_ptr()]
+    us2 = med(lambda: _lib.call("autovc_lstm2_fwd_timed_f32", *args, st, ctypes.byref(avg)))
     us1 = med(lambda: _lib.call("autovc_lstm_fwd_timed_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H,
                                 P["weight_hh_l0"].data_ptr(), h0.data_ptr(), T * H, H, c0.data_ptr(), g0.data_ptr(),
                                 st, ctypes.byref(avg)))
     # per layer-step: W_hh (4H x H fp32) + gates_x (B x 4H) + h read, c read+write, h write (B x H each)
     per_layer_step = 4 * H * H * 4 + B * 4 * H * 4 + 4 * B * H * 4
-    bytes2 = 2 * per_layer_step
-    achieved = bytes2 / (us2 * 1e-6) / 1e9
-    a1 = per_layer_step / (us1 * 1e-6) / 1e9
-    # per launch: layer 0's recurrent product (B x 4H x H) and layer 1's input + recurrent
-    # products (B x 4H x 2H), 2 FLOP per MAC
+    # per wavefront step: layer 0's recurrent product (B x 4H x H) and layer 1's input +
+    # recurrent products (B x 4H x 2H), 2 FLOP per MAC
     flop2 = 2 * B * 4 * H * H * 3
-    tf = flop2 / (us2 * 1e-6) / 1e12
+    ridge = MFMA_F32_PEAK_TF * 1e12 / (HBM_PEAK_GBS * 1e9)
+    step_launch = {"kernel": "lstm2_fwd_step_kernel (per-step wavefront launch)", "avg_launch_us": round(us2, 3),
+                   "mfma_frac": round(flop2 / (us2 * 1e-6) / 1e12 / MFMA_F32_PEAK_TF, 4),
+                   "hbm_frac": round(2 * per_layer_step / (us2 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    persistent = AF.lstm2_persistent(B, H)
+    if persistent:
+        ws = torch.empty(_lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), dtype=torch.uint8, device=dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        xs = []
+        for _ in range(4):
+            e0.record()
+            _lib.call("autovc_lstm2_fwd_persist_f32", *args, ws.data_ptr(), st)
+            e1.record()
+            torch.cuda.synchronize()
+            xs.append(e0.elapsed_time(e1) * 1e3)
+        launch_us = sorted(xs[1:])[1]
+        flop_launch, bytes_launch = flop2 * T, 2 * per_layer_step * T
+        kernel = "lstm2_persist_kernel (decoder lstm2 forward, both layers, whole sequence per launch, H=1024, B=64)"
+        pmc_file = "lstm2_persist_pmc.json"
+    else:
+        launch_us, flop_launch, bytes_launch = us2, flop2, 2 * per_layer_step
+        kernel = "lstm2_fwd_step_kernel (decoder lstm2: both layers per launch, H=1024, B=64)"
+        pmc_file = "lstm2_step_pmc.json"
+    tf = flop_launch / (launch_us * 1e-6) / 1e12
+    achieved = bytes_launch / (launch_us * 1e-6) / 1e9
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "lstm2_step_pmc.json")
+    pmc = os.path.join(ROOT, "profiles", pmc_file)
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
-    ridge = MFMA_F32_PEAK_TF * 1e12 / (HBM_PEAK_GBS * 1e9)
-    return {"kernel": "lstm2_fwd_step_kernel (decoder lstm2: both layers per launch, H=1024, B=64)", "bound": "mfma",
-            "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
-            "frac": round(tf / MFMA_F32_PEAK_TF, 4), "traffic": traffic,
-            "flop_per_launch": flop2, "bytes_per_launch": bytes2, "avg_launch_us": round(us2, 3),
-            "arithmetic_intensity": round(flop2 / bytes2, 1), "ridge_flop_per_byte": round(ridge, 1),
-            "hbm": {"convention": "SURVEY 8d weight-streaming bytes (W_hh, gates_x, h/c per layer-step), x 2 layers",
-                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4)},
-            "note": ("bound = mfma: the launch's arithmetic intensity over the 8d algorithmic bytes is above the fp32 "
-                     "ridge point (157.3 TF / 8 TB/s), so the fp32 MFMA peak is its roofline; the 8d HBM "
-                     "convention figure is reported under 'hbm'.  traffic (PMC FETCH_SIZE x2 + WRITE_SIZE, "
-                     "profiles/lstm2_step_pmc.json) includes the 16.8 MB W_ih1 read of the fused layer-1 input "
-                     "projection and the per-XCD h re-reads, which the algorithmic bytes leave out"),
-            "single_layer": {"kernel": "lstm_fwd_step_kernel (H=1024, B=64)", "bytes_per_launch": per_layer_step,
-                             "avg_launch_us": round(us1, 3), "hbm_achieved": round(a1, 1),
-                             "hbm_frac": round(a1 / HBM_PEAK_GBS, 4),
-                             "mfma_frac": round(2 * B * 4 * H * H / (us1 * 1e-6) / 1e12 / MFMA_F32_PEAK_TF, 4)}}
+    out = {"kernel": kernel, "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
+           "frac": round(tf / MFMA_F32_PEAK_TF, 4), "traffic": traffic,
+           "flop_per_launch": flop_launch, "bytes_per_launch": bytes_launch, "avg_launch_us": round(launch_us, 3),
+           "arithmetic_intensity": round(flop2 / (2 * per_layer_step), 1), "ridge_flop_per_byte": round(ridge, 1),
+           "hbm": {"convention": "SURVEY 8d weight-streaming bytes (W_hh, gates_x, h/c per layer-step), x 2 layers",
+                   "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(achieved / HBM_PEAK_GBS, 4)},
+           "note": ("bound = mfma: the arithmetic intensity over the 8d algorithmic bytes is above the fp32 ridge "
+                    "point (157.3 TF / 8 TB/s), so the fp32 MFMA peak is the roofline; the 8d HBM convention figure "
+                    "is reported under 'hbm'.  traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
+                    f"(profiles/{pmc_file})"),
+           "step_launch": step_launch,
+           "single_layer": {"kernel": "lstm_fwd_step_kernel (H=1024, B=64)", "bytes_per_launch": per_layer_step,
+                            "avg_launch_us": round(us1, 3),
+                            "hbm_achieved": round(per_layer_step / (us1 * 1e-6) / 1e9, 1),
+                            "hbm_frac": round(per_layer_step / (us1 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                            "mfma_frac": round(2 * B * 4 * H * H / (us1 * 1e-6) / 1e12 / MFMA_F32_PEAK_TF, 4)}}
+    if persistent:
+        out["us_per_wavefront_step"] = round(launch_us / (T + 1), 3)
+    return out
 
 
 def blstm_roofline(dev, B, T, H=32):

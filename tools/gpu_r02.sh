@@ -17,6 +17,9 @@ for STEP in ${1//,/ }; do
            timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/wnpmc_w -o run --output-format csv -- python tools/wn_pmc.py 1 > gpurun_out/wnpmc_w.log 2>&1 && \
            python tools/wn_pmc_summarize.py gpurun_out/wnpmc_f gpurun_out/wnpmc_w 256 > gpurun_out/wavenet_pmc.json && \
            rm -f gpurun_out/wnpmc_f/*/*.csv.bak ;;
+    lppmc) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/lppmc_f -o run --output-format csv -- python tools/lstm_pmc.py persist > gpurun_out/lppmc_f.log 2>&1 && \
+           timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/lppmc_w -o run --output-format csv -- python tools/lstm_pmc.py persist > gpurun_out/lppmc_w.log 2>&1 && \
+           python tools/pmc_summarize.py gpurun_out/lppmc_f gpurun_out/lppmc_w persist > gpurun_out/lstm2_persist_pmc.json ;;
     wnsweep) timeout -k 10 600 python tools/wavenet_bench.py 16 8 > gpurun_out/wnsweep.log 2>&1 ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac

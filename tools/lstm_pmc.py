@@ -1,7 +1,9 @@
 """Workload for the PMC passes of the roofline `traffic` field (not part of the product):
 `single`: one H=1024 layer's forward recurrence (B=64, T=128) on lstm_fwd_step_kernel;
 `stack`: decoder lstm2's two-layer wavefront (lstm2_fwd_step_kernel), as bench.py times it;
-`stackbwd`: its backward wavefront (lstm2_bwd_rec_kernel, autovc_lstm2_bwd_f32, split-K 4).
+`stackbwd`: its backward wavefront (lstm2_bwd_rec_kernel, autovc_lstm2_bwd_f32, split-K 4);
+`persist`: the persistent weight-stationary lstm2 forward (lstm2_persist_kernel, one launch
+  per sequence, what the Generator runs at B=64).
   rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_f -o run --output-format csv -- python tools/lstm_pmc.py stack
   rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_w -o run --output-format csv -- python tools/lstm_pmc.py stack
   python tools/pmc_summarize.py gpurun_out/pmc_f gpurun_out/pmc_w stack > profiles/lstm2_step_pmc.json"""
@@ -22,7 +24,7 @@ h = torch.empty(B, T, H, device=dev)
 c = torch.empty(B, T, H, device=dev)
 gates = torch.empty(B, T, 4 * H, device=dev)
 MODE = sys.argv[1] if len(sys.argv) > 1 else "single"
-if MODE == "stack":
+if MODE in ("stack", "persist"):
     W1 = (torch.rand(4 * H, H, generator=g) * 2 - 1).div_(H ** 0.5).to(dev)
     Wi1 = (torch.rand(4 * H, H, generator=g) * 2 - 1).div_(H ** 0.5).to(dev)
     bi, bh = (torch.rand(4 * H, generator=g) * 0.2 - 0.1).to(dev), (torch.rand(4 * H, generator=g) * 0.2 - 0.1).to(dev)
@@ -39,6 +41,12 @@ for _ in range(2):
         _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
                   g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(), dG1.data_ptr(),
                   dG0.data_ptr(), 4, ws.data_ptr(), _lib.stream_ptr(dev))
+    elif MODE == "persist":
+        if "ws" not in globals():
+            ws = torch.empty(_lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), dtype=torch.uint8, device=dev)
+        _lib.call("autovc_lstm2_fwd_persist_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(),
+                  bi.data_ptr(), bh.data_ptr(), Wi1.data_ptr(), W1.data_ptr(), h.data_ptr(), c.data_ptr(),
+                  gates.data_ptr(), h1.data_ptr(), c1.data_ptr(), g1.data_ptr(), ws.data_ptr(), _lib.stream_ptr(dev))
     elif MODE == "stack":
         _lib.call("autovc_lstm2_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(), bi.data_ptr(),
                   bh.data_ptr(), Wi1.data_ptr(), W1.data_ptr(), h.data_ptr(), c.data_ptr(), gates.data_ptr(),
