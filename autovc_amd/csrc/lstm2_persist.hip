@@ -49,10 +49,7 @@
 #ifndef LP_ABLATE
 #define LP_ABLATE 0
 #endif
-// W_ih1 tile in LDS beside W_hh0 (1) or in VGPRs beside W_hh1 (0); h groups in flight per stream
-#ifndef LP_W1_LDS
-#define LP_W1_LDS 1
-#endif
+// h groups in flight per stream
 #ifndef LP_PWIN
 #define LP_PWIN 1
 #endif
@@ -69,25 +66,29 @@ constexpr int PU = 4;              // hidden units per tile (x 4 gates = 16 colu
 constexpr int PC = 4 * PU;         // tile columns
 constexpr int PNW = LP_NW;         // waves per workgroup
 constexpr int PNT = 64 * PNW;
-constexpr int PH = 1024;           // hidden size this kernel is built for
 constexpr int PRH = PNW == 16 ? 2 : 1;   // row halves: 16 waves = 8 k ranges x 2 row halves
 constexpr int PKWN = PNW / PRH;    // k ranges
-constexpr int PKW = PH / PKWN;     // k per wave and segment
-constexpr int PKL = PKW / 4;       // k per lane group (64: lane group l / 16 of the MFMA)
-constexpr int PGR = PKL / 4;       // 4-k groups per lane (16)
 constexpr int PRB = PB / 16;       // 16-row blocks of the tile (4)
 constexpr int PRBW = PRB / PRH;    // 16-row blocks per wave
 constexpr int PWIN = LP_PWIN;      // h groups in flight per stream
 constexpr int RED_LD = PC + 1;     // padded row of a 64 x 16 partial tile in LDS
 constexpr int RED_SLOT = PB * RED_LD;
-constexpr int LDS_W0 = (PH / 4) * PC * 4;          // floats: W_hh0 tile [k/4][16][4]
-constexpr int LDS_W1 = LP_W1_LDS ? LDS_W0 : 0;     // floats: W_ih1 tile, same layout
-constexpr int RED_LAYERS = LP_W1_LDS ? 1 : 2;      // partial tiles of one layer at a time, or both
-constexpr int NSLOT = 4;                            // partial-tile slots per layer
-static_assert(PNW == 4 || ((PNW == 8 || PNW == 16) && LP_W1_LDS), "8/16 waves: W_ih1 in LDS, shared slots");
-constexpr int LDS_RED = RED_LAYERS * NSLOT * RED_SLOT;
-constexpr int LDS_BYTES = 4 * (LDS_W0 + LDS_W1 + LDS_RED);
-static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+constexpr int NSLOT = 4;                            // partial-tile slots (one layer at a time)
+static_assert(PNW == 4 || PNW == 8 || PNW == 16, "waves per workgroup");
+constexpr int LDS_RED = NSLOT * RED_SLOT;
+
+// per hidden size HH: k per wave and segment, k per MFMA lane group, 4-k groups per lane,
+// floats of one k-blocked [k/4][16][4] weight tile in LDS
+template <int HH>
+struct PK {
+  static constexpr int KW = HH / PKWN, KL = KW / 4, GR = KL / 4, W = (HH / 4) * PC * 4;
+};
+// LDS floats of a launch: W_hh0 (+ W_ih1 for the stacked pair) and the partial-tile slots
+template <int HH, bool TWO>
+constexpr int lds_bytes() {
+  return 4 * (PK<HH>::W * (TWO ? 2 : 1) + LDS_RED);
+}
+static_assert(lds_bytes<1024, true>() <= 160 * 1024, "LDS budget");
 
 // barrier block: one 128-B line per word (ints)
 constexpr int L = 32;
@@ -110,6 +111,7 @@ struct PArgs {
   const float* W_ih1;
   const float* W_hh1;
   float *h0, *c0, *g0, *h1, *c1, *g1;
+  int64_t h0_ldb, h0_ldt;          // h0 strides (single layer: the caller's; stacked: T*H, H)
   float* hk0;                      // k-blocked h0: [t][H/4][B][4]
   float* hk1;                      // k-blocked h1
   int* bar;
@@ -201,14 +203,13 @@ __device__ __forceinline__ void add_tile(float* slot, const f32x4 (&acc)[PRBW], 
     for (int r = 0; r < 4; ++r) slot[(16 * (rb0 + rb) + 4 * (lane >> 4) + r) * RED_LD + (lane & 15)] += acc[rb][r];
 }
 
-// One iteration's products of a wave over its k range: S0 = stream h0_{t-1} (layer 1 input
-// product, B = W_ih1 fragments in VGPRs; L0: also layer 0, B = W_hh0 from LDS), S1 = stream
-// h1_{t-2} (layer 1 recurrent product, B = W_hh1 fragments in VGPRs).  Lane l: MFMA k slot
+// One iteration's products of a wave over its k range of stream h0_{t-1}: S0 = layer 1's input
+// product (B = W_ih1 from LDS), L0 = layer 0's recurrent product (B = W_hh0 from LDS); S1 =
+// stream h1_{t-2}, layer 1's recurrent product (B = W_hh1 fragments in VGPRs).  Lane l: MFMA k slot
 // l >> 4 covers k = kbase + 64 (l >> 4) + i, row block rb's A row 16 rb + (l & 15).
-template <bool S0, bool L0, bool S1>
+template <int KL, bool S0, bool L0, bool S1>
 __device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const float* __restrict__ hk1_t,
-                                          const float (&wi)[LP_W1_LDS ? 1 : PKL], const float (&wh)[PKL], const float* W0,
-                                          const float* W1, int kb0,
+                                          const float (&wh)[KL], const float* W0, const float* W1, int kb0,
                                           int B, int rb0, int lane, f32x4 (&acc1)[PRBW], f32x4 (&acc0)[PRBW]) {
   // group g, row block rb: f32x4 at hk[kb0 + g][16 rb + (lane & 15)][0..3]; sc1 buffer loads
   // (every load of the handed-off rows bypasses L1: no acquire fence needed)
@@ -227,50 +228,54 @@ __device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const
   for (int g = 0; g < PWIN; ++g)
 #pragma unroll
     for (int rb = 0; rb < PRBW; ++rb) {
-      if (S0) a0[g][rb] = ld(r0, g, rb);
+      if (S0 || L0) a0[g][rb] = ld(r0, g, rb);
       if (S1) a1[g][rb] = ld(r1, g, rb);
     }
   const float* w0p = W0 + (kb0 * PC + (lane & 15)) * 4;
   const float* w1p = W1 + (kb0 * PC + (lane & 15)) * 4;
 #pragma unroll
-  for (int g = 0; g < PGR; ++g) {
+  for (int g = 0; g < KL / 4; ++g) {
     f32x4 x0[PRBW], x1[PRBW];
 #pragma unroll
     for (int rb = 0; rb < PRBW; ++rb) {
       x0[rb] = a0[g % PWIN][rb];
       x1[rb] = a1[g % PWIN][rb];
     }
-    if (g + PWIN < PGR) {
+    if (g + PWIN < KL / 4) {
 #pragma unroll
       for (int rb = 0; rb < PRBW; ++rb) {
-        if (S0) a0[g % PWIN][rb] = ld(r0, g + PWIN, rb);
+        if (S0 || L0) a0[g % PWIN][rb] = ld(r0, g + PWIN, rb);
         if (S1) a1[g % PWIN][rb] = ld(r1, g + PWIN, rb);
       }
     }
     f32x4 bv0 = {}, bv1 = {};
     if (L0) bv0 = *reinterpret_cast<const f32x4*>(w0p + g * PC * 4);
-    if (LP_W1_LDS && S0) bv1 = *reinterpret_cast<const f32x4*>(w1p + g * PC * 4);
+    if (S0) bv1 = *reinterpret_cast<const f32x4*>(w1p + g * PC * 4);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int rb = 0; rb < PRBW; ++rb) {
-        if (S0) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], LP_W1_LDS ? bv1[q] : wi[LP_W1_LDS ? 0 : 4 * g + q],
-                                                                acc1[rb], 0, 0, 0);
+        if (S0) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], bv1[q], acc1[rb], 0, 0, 0);
         if (S1) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[rb][q], wh[4 * g + q], acc1[rb], 0, 0, 0);
         if (L0) acc0[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], bv0[q], acc0[rb], 0, 0, 0);
       }
   }
 }
 
-__global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
+// TWO: the stacked pair (decoder lstm2); else one layer (decoder lstm1), whose "layer 0" is
+// that layer and whose iteration t is its step t (no lag, T iterations).
+template <int HH, bool TWO>
+__global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
+  constexpr int KW = PK<HH>::KW, KL = PK<HH>::KL, GR = PK<HH>::GR;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* W0 = lds;                          // [H/4][16][4]
-  float* W1 = lds + LDS_W0;                 // [H/4][16][4] (LP_W1_LDS)
-  float* red = W1 + LDS_W1;                 // layer 1: slots 0..3, layer 0: slots 4..7 (or reused)
+  float* W1 = lds + PK<HH>::W;              // [H/4][16][4] (TWO)
+  float* red = W1 + (TWO ? PK<HH>::W : 0);  // partial-tile slots, one layer at a time
   // broadcast word: the pad column of slot 0's row 0, never written by put_tile / add_tile
   int* status = reinterpret_cast<int*>(red + PC);
   int xcc_id = 0, xcc_wgs = 0, xcc_n = 0;
-  const int H = PH, B = a.B, T = a.T;
+  constexpr int H = HH;
+  const int B = a.B, T = a.T;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j0 = blockIdx.x * PU;
   auto grow = [&](int col) { return (col >> 2) * H + j0 + (col & 3); };   // tile column -> gate row
@@ -294,21 +299,18 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
   for (int e = tid; e < (H / 4) * PC; e += PNT) {
     const int kb = e / PC, col = e % PC;
     *reinterpret_cast<f32x4*>(W0 + e * 4) = *reinterpret_cast<const f32x4*>(a.W_hh0 + (int64_t)grow(col) * H + kb * 4);
-    if (LP_W1_LDS)
+    if (TWO)
       *reinterpret_cast<f32x4*>(W1 + e * 4) =
           *reinterpret_cast<const f32x4*>(a.W_ih1 + (int64_t)grow(col) * H + kb * 4);
   }
   const int kw = wave % PKWN, rb0 = (wave / PKWN) * PRBW;    // k range, first row block
-  const int kbase = kw * PKW + PKL * (lane >> 4);             // this lane's first k
+  const int kbase = kw * KW + KL * (lane >> 4);               // this lane's first k
   const int kb0 = kbase / 4;
-  float wi[LP_W1_LDS ? 1 : PKL], wh[PKL];
-  {
-    const float* si = (LP_W1_LDS ? a.W_hh1 : a.W_ih1) + (int64_t)grow(lane & 15) * H + kbase;
+  float wh[KL] = {};
+  if (TWO) {
     const float* sh = a.W_hh1 + (int64_t)grow(lane & 15) * H + kbase;
 #pragma unroll
-    for (int g = 0; g < PGR; ++g) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(si + 4 * g);
-      if (!LP_W1_LDS) { wi[4 * g] = v[0]; wi[4 * g + 1] = v[1]; wi[4 * g + 2] = v[2]; wi[4 * g + 3] = v[3]; }
+    for (int g = 0; g < GR; ++g) {
       const f32x4 u = *reinterpret_cast<const f32x4*>(sh + 4 * g);
       wh[4 * g] = u[0]; wh[4 * g + 1] = u[1]; wh[4 * g + 2] = u[2]; wh[4 * g + 3] = u[3];
     }
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
   const int eb = tid >> 2, ej = j0 + (tid & 3), eu = tid & 3;
   const bool eown = eb < B;
   float bias1[4] = {0.f, 0.f, 0.f, 0.f};
-  if (eown)
+  if (TWO && eown)
 #pragma unroll
     for (int g = 0; g < 4; ++g) bias1[g] = a.b_ih1[g * H + ej] + a.b_hh1[g * H + ej];
   const int64_t BH = (int64_t)B * H;
@@ -328,19 +330,21 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
   // the previous iteration's outputs (layer 0 at step t0, layer 1 at step t0 - 1)
   auto store_outputs = [&](int t0) {
     if (!eown) return;
-    if (t0 >= 1) {
+    if (TWO && t0 >= 1) {
       const int t1 = t0 - 1;
       const int64_t o = ((int64_t)eb * T + t1) * H + ej;
       cell_store(out1, a.c1 + o, a.h1 + o, a.g1 ? a.g1 + ((int64_t)eb * T + t1) * 4 * H + ej : nullptr, H);
     }
     if (t0 < T) {
       const int64_t o = ((int64_t)eb * T + t0) * H + ej;
-      cell_store(out0, a.c0 + o, a.h0 + o, a.g0 ? a.g0 + ((int64_t)eb * T + t0) * 4 * H + ej : nullptr, H);
+      cell_store(out0, a.c0 + o, a.h0 + (int64_t)eb * a.h0_ldb + (int64_t)t0 * a.h0_ldt + ej,
+                 a.g0 ? a.g0 + ((int64_t)eb * T + t0) * 4 * H + ej : nullptr, H);
     }
   };
 
-  for (int t = 0; t <= T; ++t) {
-    const bool l0 = t < T, l1 = t >= 1;
+  const int last = TWO ? T : T - 1;                                 // final iteration
+  for (int t = 0; t <= last; ++t) {
+    const bool l0 = t < T, l1 = TWO && t >= 1;
     if (t >= 1) store_outputs(t - 1);
     // epilogue operands of this iteration (latency hidden under the products)
     float gxv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -353,12 +357,14 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
     const float* hk0 = a.hk0 + (int64_t)(t >= 1 ? t - 1 : 0) * BH;   // h0_{t-1}
     const float* hk1 = a.hk1 + (int64_t)(t >= 2 ? t - 2 : 0) * BH;   // h1_{t-2}
     if (LP_ABLATE == 2 || t == 0) {                                  // h0_{-1} = 0: no products
+    } else if (!TWO) {
+      gemm_wave<KL, false, true, false>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
     } else if (t == 1) {                                             // h1_{-1} = 0
-      gemm_wave<true, true, false>(hk0, hk1, wi, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+      gemm_wave<KL, true, true, false>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
     } else if (t < T) {
-      gemm_wave<true, true, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+      gemm_wave<KL, true, true, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
     } else {                                                         // t == T: layer 1 only
-      gemm_wave<true, false, true>(hk0, hk1, wi, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+      gemm_wave<KL, true, false, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
     }
     if (LP_ABLATE != 4) {
       // the 4 waves' partial tiles summed through LDS in fixed order
@@ -366,7 +372,6 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
         const float* r = red + layer * NSLOT * RED_SLOT + eb * RED_LD + g * PU + eu;
         return ((r[0] + r[RED_SLOT]) + r[2 * RED_SLOT]) + r[3 * RED_SLOT];
       };
-      constexpr int L0SLOT = RED_LAYERS - 1;                         // layer 0's slots
       // more than 4 waves: wave w < 4 stores its tile into slot w, then waves 4..7 add into
       // slots 0..3, then waves 8..11, ... (fixed order)
       auto reduce_put = [&](float* slots, const f32x4 (&acc)[PRBW]) {
@@ -377,28 +382,25 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
           if (kw / 4 == ph) add_tile(slots + (kw & 3) * RED_SLOT, acc, rb0, lane);
         }
       };
-      reduce_put(red, acc1);
-      if (!LP_W1_LDS) put_tile(red + (L0SLOT * NSLOT + wave) * RED_SLOT, acc0, 0, lane);
-      __syncthreads();
-      if (eown) {
-        if (l1) {                                                    // layer 1 at step t - 1
+      if (TWO) {
+        reduce_put(red, acc1);
+        __syncthreads();
+        if (eown && l1) {                                            // layer 1 at step t - 1
           float pre[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + bias1[g];
           const int t1 = t - 1;
           out1 = cell(pre, out1.c, a.hk1 + (int64_t)t1 * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3));
         }
+        __syncthreads();                                             // slots reused for layer 0
       }
-      if (LP_W1_LDS) {                                               // slots reused for layer 0
-        __syncthreads();
-        reduce_put(red, acc0);
-        __syncthreads();
-      }
+      reduce_put(red, acc0);
+      __syncthreads();
       if (eown) {
         if (l0) {                                                    // layer 0 at step t
           float pre[4];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) pre[g] = sum(L0SLOT, g) + gxv[g];
+          for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + gxv[g];
           out0 = cell(pre, out0.c, a.hk0 + (int64_t)t * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3));
         }
       }
@@ -406,37 +408,53 @@ __global__ __launch_bounds__(PNT, 1) void lstm2_persist_kernel(PArgs a) {
       a.h0[0] = 0.f;                                                  // keep the products live
     }
     if (LP_ABLATE == 1) __syncthreads();
-    else if (t < T && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, status, t)) return;
+    else if (t < last && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, status, t)) return;
   }
-  store_outputs(T);                                                  // layer 1 at step T - 1
+  store_outputs(last);                                               // the final iteration's outputs
 }
 
 int g_cus = -1;
 
+// one workgroup of the <HH, TWO> kernel must fit on a CU, and every workgroup must be resident
+// at once: no more workgroups (HH / PU) than CUs
+template <int HH, bool TWO>
+bool persist_fits() {
+  static int per = -1;
+  if (per < 0) {
+    per = 0;
+    const void* k = reinterpret_cast<const void*>(lstm_persist_kernel<HH, TWO>);
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<HH, TWO>()) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_persist_kernel<HH, TWO>, PNT,
+                                                     lds_bytes<HH, TWO>()) != hipSuccess)
+      per = 0;
+  }
+  if (g_cus < 0) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    g_cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
+                ? p.multiProcessorCount : 0;
+  }
+  return per >= 1 && HH / PU <= g_cus;
+}
+
+template <int HH, bool TWO>
+void launch_persist(PArgs& a, void* workspace, hipStream_t stream) {
+  a.bar = static_cast<int*>(workspace);
+  a.hk0 = reinterpret_cast<float*>(static_cast<char*>(workspace) + BAR_BYTES);
+  a.hk1 = TWO ? a.hk0 + (int64_t)a.T * a.B * HH : nullptr;
+  a.timeout_ticks = 20000000;   // 200 ms of s_memrealtime (100 MHz) per wait
+  hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO>()), stream, a);
+}
+
 }  // namespace
 
 extern "C" int64_t autovc_lstm2_persist_workspace_bytes(int B, int T, int H) {
-  if (B <= 0 || T <= 0 || H != PH) return -1;
+  if (B <= 0 || T <= 0 || H != 1024) return -1;
   return BAR_BYTES + 2 * (int64_t)T * B * H * 4;
 }
 
 extern "C" int autovc_lstm2_persist_supported(int B, int H) {
-  if (H != PH || B != PB) return 0;
-  if (g_cus < 0) {
-    int dev = 0;
-    hipDeviceProp_t p;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
-    int per = 0;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(lstm2_persist_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm2_persist_kernel, PNT, LDS_BYTES) != hipSuccess ||
-        per < 1)
-      g_cus = 0;
-    else
-      g_cus = p.multiProcessorCount;
-  }
-  // every workgroup must be resident at once: one per CU, no more workgroups than CUs
-  return H / PU <= g_cus ? 1 : 0;
+  return (H == 1024 && B == PB && persist_fits<1024, true>()) ? 1 : 0;
 }
 
 extern "C" int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
@@ -446,8 +464,8 @@ extern "C" int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx
                                             hipStream_t stream) {
   static const char* fn = "autovc_lstm2_fwd_persist_f32";
   AVC_CHECK_ARG(T > 0 && autovc_lstm2_persist_supported(B, H),
-                "%s: unsupported shape B=%d H=%d on this device (needs H=%d, B=%d, one CU per workgroup)", fn,
-                B, H, PH, PB);
+                "%s: unsupported shape B=%d H=%d on this device (needs H=1024, B=%d, one CU per workgroup)", fn,
+                B, H, PB);
   AVC_CHECK_ARG(gx0 && W_hh0 && b_ih1 && b_hh1 && W_ih1 && W_hh1 && h0 && c0 && h1 && c1 && workspace,
                 "%s: null pointer", fn);
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh0) && AVC_ALIGNED16(W_ih1) && AVC_ALIGNED16(W_hh1) && AVC_ALIGNED16(workspace),
@@ -457,12 +475,43 @@ extern "C" int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx
   a.gx0 = gx0; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt;
   a.W_hh0 = W_hh0; a.b_ih1 = b_ih1; a.b_hh1 = b_hh1; a.W_ih1 = W_ih1; a.W_hh1 = W_hh1;
   a.h0 = h0; a.c0 = c0; a.g0 = gates0; a.h1 = h1; a.c1 = c1; a.g1 = gates1;
-  a.bar = static_cast<int*>(workspace);
-  a.hk0 = reinterpret_cast<float*>(static_cast<char*>(workspace) + BAR_BYTES);
-  a.hk1 = a.hk0 + (int64_t)T * B * H;
-  a.timeout_ticks = 20000000;   // 200 ms of s_memrealtime (100 MHz) per wait
+  a.h0_ldb = (int64_t)T * H; a.h0_ldt = H;
   AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
-  hipLaunchKernelGGL(lstm2_persist_kernel, dim3(H / PU), dim3(PNT), LDS_BYTES, stream, a);
+  launch_persist<1024, true>(a, workspace, stream);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+
+extern "C" int64_t autovc_lstm_persist_workspace_bytes(int B, int T, int H) {
+  if (B <= 0 || T <= 0 || (H != 512 && H != 1024)) return -1;
+  return BAR_BYTES + (int64_t)T * B * H * 4;
+}
+
+extern "C" int autovc_lstm_persist_supported(int B, int H) {
+  if (B != PB) return 0;
+  if (H == 512) return persist_fits<512, false>() ? 1 : 0;
+  if (H == 1024) return persist_fits<1024, false>() ? 1 : 0;
+  return 0;
+}
+
+extern "C" int autovc_lstm_fwd_persist_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                                           const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                                           float* gates, void* workspace, hipStream_t stream) {
+  static const char* fn = "autovc_lstm_fwd_persist_f32";
+  AVC_CHECK_ARG(T > 0 && autovc_lstm_persist_supported(B, H),
+                "%s: unsupported shape B=%d H=%d on this device (needs H=512 or 1024, B=%d)", fn, B, H, PB);
+  AVC_CHECK_ARG(gx && W_hh && h && c_all && workspace, "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh) && AVC_ALIGNED16(workspace), "%s: weights / workspace must be 16-byte aligned",
+                fn);
+  PArgs a = {};
+  a.B = B; a.T = T; a.H = H;
+  a.gx0 = gx; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt;
+  a.W_hh0 = W_hh;
+  a.h0 = h; a.c0 = c_all; a.g0 = gates;
+  a.h0_ldb = h_ldb; a.h0_ldt = h_ldt;
+  AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
+  if (H == 512) launch_persist<512, false>(a, workspace, stream);
+  else launch_persist<1024, false>(a, workspace, stream);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
 }

@@ -578,6 +578,10 @@ class LSTMLayerFn(torch.autograd.Function):
             Wb = _bf(W_hh)   # held until the launches are enqueued (stream-ordered reuse after)
             _lib.call("autovc_lstm_fwd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),
                       h.data_ptr(), hb.data_ptr(), c.data_ptr(), _p(gates), 0, _s())
+        elif lstm_persistent(B, H):
+            ws = _ws(dev, _lib.load().autovc_lstm_persist_workspace_bytes(B, T, H), "lstmp")
+            _lib.call("autovc_lstm_fwd_persist_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
+                      h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), ws, _s())
         else:
             _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
                       h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), 0, _s())
@@ -678,6 +682,17 @@ _PERSIST_ON = os.environ.get("AVC_LSTM2_PERSIST", "1") != "0"
 
 def lstm2_persistent(B, H):
     return _PERSIST_ON and bool(_lib.load().autovc_lstm2_persist_supported(B, H))
+
+
+# the single-layer recurrence (decoder lstm1, H = 512) the same way — opt-in
+# (AVC_LSTM_PERSIST=1): at H = 512 the grid barrier costs what the launch boundary did
+# (6.58 vs 6.75 us per step, profiles/r02/lstm_persist_ab.txt; 16.47-16.50 vs 16.49-16.55 ms
+# per training step), so the per-step launches and their cell arithmetic stay the default
+_PERSIST1_ON = os.environ.get("AVC_LSTM_PERSIST", "0") != "0"
+
+
+def lstm_persistent(B, H):
+    return _PERSIST1_ON and bool(_lib.load().autovc_lstm_persist_supported(B, H))
 
 
 class LSTM2StackFn(torch.autograd.Function):

@@ -204,20 +204,30 @@ int autovc_lstm2_fwd_timed_f32(int B, int T, int H, const float* gx0, int64_t gx
                                const float* W_hh1, float* h0, float* c0, float* gates0, float* h1, float* c1,
                                float* gates1, hipStream_t stream, float* avg_us);
 /* autovc_lstm2_fwd_f32 as ONE persistent, weight-stationary launch (csrc/lstm2_persist.hip):
- * each workgroup (one per CU) keeps its 32 gate columns of W_ih1 / W_hh1 in VGPRs and of
- * W_hh0 in LDS for the whole sequence; the T + 1 wavefront iterations are separated by an
+ * each workgroup (one per CU, 8 waves) owns all B = 64 rows x 16 gate columns (4 hidden
+ * units) of both layers and keeps their W_hh0 / W_ih1 tiles in LDS and W_hh1 fragments in
+ * VGPRs for the whole sequence; the T + 1 wavefront iterations are separated by an
  * XCD-hierarchical grid barrier.  Same arguments and outputs as autovc_lstm2_fwd_f32
  * (model_vc_mel.py:104,118) plus a workspace of autovc_lstm2_persist_workspace_bytes bytes
- * (barrier words + k-blocked copies of h0 / h1), 16-byte aligned.  Only where
- * autovc_lstm2_persist_supported(B, H) (H = 1024, B % 32 == 0, (B/32)(H/8) workgroups all
- * resident at once); else -1.  Every spin is bounded: autovc_lstm2_persist_status(workspace,
- * stream) (synchronising) returns non-zero if the last call's barriers timed out. */
+ * (barrier words + k-blocked copies of h0 / h1), 16-byte aligned, re-initialised by every
+ * call.  Only where autovc_lstm2_persist_supported(B, H) (H = 1024, B = 64, H/4 workgroups
+ * all resident at once); else -1.  Every spin is bounded: autovc_lstm2_persist_status(
+ * workspace, stream) (synchronising) returns non-zero if the last call's barriers timed out. */
 int64_t autovc_lstm2_persist_workspace_bytes(int B, int T, int H);
 int autovc_lstm2_persist_supported(int B, int H);
 int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
                                  const float* W_hh0, const float* b_ih1, const float* b_hh1,
                                  const float* W_ih1, const float* W_hh1, float* h0, float* c0, float* gates0,
                                  float* h1, float* c1, float* gates1, void* workspace, hipStream_t stream);
+/* One large-H layer (decoder lstm1, model_vc_mel.py:90,111) the same way: arguments and
+ * outputs of autovc_lstm_fwd_f32 (forward direction) plus a workspace of
+ * autovc_lstm_persist_workspace_bytes bytes; H = 512 or 1024, B = 64
+ * (autovc_lstm_persist_supported); autovc_lstm2_persist_status reads its barrier words too. */
+int64_t autovc_lstm_persist_workspace_bytes(int B, int T, int H);
+int autovc_lstm_persist_supported(int B, int H);
+int autovc_lstm_fwd_persist_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                                const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                                float* gates, void* workspace, hipStream_t stream);
 int autovc_lstm2_persist_status(const void* workspace, hipStream_t stream);
 /* autovc_lstm_fwd_f32 with every step launch timed by its own dispatch events;
  * synchronises; *avg_us (HOST pointer) = mean kernel time of steps 1..T-1 (bench.py). */

@@ -68,3 +68,39 @@ def test_persistent_unsupported_shape_rejected(cuda):
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=cuda)
     with pytest.raises(ValueError):
         _run("autovc_lstm2_fwd_persist_f32", 2, 4, 1024, gx, W, b1, b2, cuda, ws)
+
+
+@pytest.mark.parametrize("H,T", [(512, 3), (512, 128), (1024, 17)])
+def test_single_layer_persistent_matches_per_step_launches(cuda, H, T):
+    """autovc_lstm_fwd_persist_f32 (decoder lstm1's recurrence as one launch) against the
+    per-step launches of autovc_lstm_fwd_f32, h written into a strided buffer."""
+    from autovc_amd import _lib
+    B = 64
+    if not _lib.load().autovc_lstm_persist_supported(B, H):
+        pytest.skip("persistent lstm needs one CU per workgroup on this device")
+    g = torch.Generator().manual_seed(H + T)
+    W = ((torch.rand(4 * H, H, generator=g) * 2 - 1) / H ** 0.5).to(cuda)
+    gx = (torch.randn(B, T, 4 * H, generator=g) * 0.5).to(cuda)
+    st = _lib.stream_ptr(cuda)
+
+    def run(persist):
+        hbuf = torch.full((B, T, H + 8), float("nan"), device=cuda)       # row stride T*(H+8)
+        c = torch.full((B, T, H), float("nan"), device=cuda)
+        gates = torch.full((B, T, 4 * H), float("nan"), device=cuda)
+        if persist:
+            ws = torch.empty(_lib.load().autovc_lstm_persist_workspace_bytes(B, T, H), dtype=torch.uint8, device=cuda)
+            _lib.call("autovc_lstm_fwd_persist_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(),
+                      hbuf.data_ptr(), T * (H + 8), H + 8, c.data_ptr(), gates.data_ptr(), ws.data_ptr(), st)
+            assert _lib.load().autovc_lstm2_persist_status(ws.data_ptr(), st) == 0
+        else:
+            _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(),
+                      hbuf.data_ptr(), T * (H + 8), H + 8, c.data_ptr(), gates.data_ptr(), 0, st)
+        torch.cuda.synchronize()
+        return hbuf, c, gates
+
+    ref, got = run(False), run(True)
+    assert bool(torch.isnan(got[0][:, :, H:]).all())                        # pad columns untouched
+    for name, a, r in zip(["h", "c", "gates"], (got[0][:, :, :H], got[1], got[2]), (ref[0][:, :, :H], ref[1], ref[2])):
+        assert bool(torch.isfinite(a).all()), name
+        err = (a.double() - r.double()).abs().max().item() / max(r.abs().max().item(), 1e-30)
+        assert err < 2e-5, (name, err)
