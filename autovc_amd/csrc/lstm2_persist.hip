@@ -84,9 +84,9 @@ struct PK {
   static constexpr int KW = HH / PKWN, KL = KW / 4, GR = KL / 4, W = (HH / 4) * PC * 4;
 };
 // LDS floats of a launch: W_hh0 (+ W_ih1 for the stacked pair) and the partial-tile slots
-template <int HH, bool TWO>
+template <int HH, bool TWO, bool BF = false>
 constexpr int lds_bytes() {
-  return 4 * (PK<HH>::W * (TWO ? 2 : 1) + LDS_RED);
+  return (BF ? 2 : 4) * PK<HH>::W * (TWO ? 2 : 1) + 4 * LDS_RED;
 }
 static_assert(lds_bytes<1024, true>() <= 160 * 1024, "LDS budget");
 
@@ -114,6 +114,10 @@ struct PArgs {
   int64_t h0_ldb, h0_ldt;          // h0 strides (single layer: the caller's; stacked: T*H, H)
   float* hk0;                      // k-blocked h0: [t][H/4][B][4]
   float* hk1;                      // k-blocked h1
+  // bf16 variant (precision("bf16"), numerics of autovc_lstm2_fwd_bf16): RNE weight copies,
+  // and bf16 hand-off copies of h blocked by 8: [t][H/8][B][8]
+  const __bf16 *W0b, *Wi1b, *W1b;
+  __bf16 *hk0b, *hk1b;
   int* bar;
   int timeout_ticks;               // s_memrealtime ticks (100 MHz) before a spin gives up
 };
@@ -169,7 +173,7 @@ __device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int
 // for the hand-off stores alone).  The cell state is carried in registers, never re-read.
 struct CellOut { float c, h, i, f, g, o; };
 
-__device__ __forceinline__ CellOut cell(const float (&pre)[4], float cp, float* hk_out) {
+__device__ __forceinline__ CellOut cell(const float (&pre)[4], float cp) {
   CellOut r;
   r.i = avc_sigmoid_fast(pre[0]);
   r.f = avc_sigmoid_fast(pre[1]);
@@ -177,8 +181,28 @@ __device__ __forceinline__ CellOut cell(const float (&pre)[4], float cp, float* 
   r.o = avc_sigmoid_fast(pre[3]);
   r.c = r.f * cp + r.i * r.g;
   r.h = r.o * avc_tanh_fast(r.c);
-  __hip_atomic_store(hk_out, r.h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: handed off
   return r;
+}
+
+// the hand-off copy of h (sc1 write-through stores).  fp32: one dword per (row, unit) at
+// [H/4][B][4]; bf16: the 4 units of a row held by 4 consecutive lanes are gathered into the
+// first of them and stored as one 8-byte word at [H/8][B][8] (every lane of the wave calls)
+template <bool BF>
+__device__ __forceinline__ void handoff(float h, float* hk, __bf16* hkb, int B, int eb, int ej, int lane) {
+  if constexpr (!BF) {
+    __hip_atomic_store(hk + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3), h, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    const __bf16 hb = (__bf16)h;
+    const int v = (int)__builtin_bit_cast(unsigned short, hb);
+    const int q0 = lane & ~3;
+    const unsigned long long w = (unsigned long long)(unsigned)(__shfl(v, q0, 64) | (__shfl(v, q0 + 1, 64) << 16)) |
+                                 ((unsigned long long)(unsigned)(__shfl(v, q0 + 2, 64) |
+                                                                 (__shfl(v, q0 + 3, 64) << 16)) << 32);
+    if ((lane & 3) == 0)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(hkb + ((int64_t)(ej >> 3) * B + eb) * 8 + (ej & 7)), w,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 __device__ __forceinline__ void cell_store(const CellOut& r, float* c_out, float* h_out, float* g_out, int64_t H) {
@@ -262,15 +286,70 @@ __device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const
   }
 }
 
+// bf16 products (v_mfma_f32_16x16x32_bf16): lane l supplies rows 16 rb + (l & 15) and the 8
+// k of block k8 = k8_0 + 4 s (8 (l >> 4) within the 32-k step s) of the bf16 hand-off copy,
+// B fragments from the bf16 LDS tiles [H/8][16][8] (W_hh0, W_ih1) or VGPRs (W_hh1).
+template <int NS, bool S0, bool L0, bool S1>
+__device__ __forceinline__ void gemm_wave_bf(const __bf16* __restrict__ hk0_t, const __bf16* __restrict__ hk1_t,
+                                             const bf16x8 (&wh)[NS], const __bf16* W0, const __bf16* W1, int k8_0,
+                                             int B, int rb0, int lane, f32x4 (&acc1)[PRBW], f32x4 (&acc0)[PRBW]) {
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(hk0_t), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r1 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(hk1_t), (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t off0 = (uint32_t)((k8_0 * B + 16 * rb0 + (lane & 15)) * 16);
+  const uint32_t sstride = (uint32_t)B * 64;          // 4 k8 blocks per 32-k step
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int st, int rb) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off0 + st * sstride + rb * 256, 0, 16));
+  };
+  bf16x8 a0[PRBW], a1[PRBW];
+#pragma unroll
+  for (int rb = 0; rb < PRBW; ++rb) {
+    if (S0 || L0) a0[rb] = ld(r0, 0, rb);
+    if (S1) a1[rb] = ld(r1, 0, rb);
+  }
+  const __bf16* w0p = W0 + (k8_0 * PC + (lane & 15)) * 8;
+  const __bf16* w1p = W1 + (k8_0 * PC + (lane & 15)) * 8;
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    bf16x8 x0[PRBW], x1[PRBW];
+#pragma unroll
+    for (int rb = 0; rb < PRBW; ++rb) {
+      x0[rb] = a0[rb];
+      x1[rb] = a1[rb];
+    }
+    if (st + 1 < NS) {
+#pragma unroll
+      for (int rb = 0; rb < PRBW; ++rb) {
+        if (S0 || L0) a0[rb] = ld(r0, st + 1, rb);
+        if (S1) a1[rb] = ld(r1, st + 1, rb);
+      }
+    }
+    bf16x8 bv0 = {}, bv1 = {};
+    if (L0) bv0 = *reinterpret_cast<const bf16x8*>(w0p + st * 4 * PC * 8);
+    if (S0) bv1 = *reinterpret_cast<const bf16x8*>(w1p + st * 4 * PC * 8);
+#pragma unroll
+    for (int rb = 0; rb < PRBW; ++rb) {
+      if (S0) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0[rb], bv1, acc1[rb], 0, 0, 0);
+      if (S1) acc1[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[rb], wh[st], acc1[rb], 0, 0, 0);
+      if (L0) acc0[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0[rb], bv0, acc0[rb], 0, 0, 0);
+    }
+  }
+}
+
 // TWO: the stacked pair (decoder lstm2); else one layer (decoder lstm1), whose "layer 0" is
 // that layer and whose iteration t is its step t (no lag, T iterations).
-template <int HH, bool TWO>
+// BF: bf16 weights and hand-off copies (the products' numerics of autovc_lstm2_fwd_bf16);
+// cell math, c, h, gates fp32 either way.
+template <int HH, bool TWO, bool BF = false>
 __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
-  constexpr int KW = PK<HH>::KW, KL = PK<HH>::KL, GR = PK<HH>::GR;
+  constexpr int KW = PK<HH>::KW, KL = PK<HH>::KL, GR = PK<HH>::GR, NS = KW / 32;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* W0 = lds;                          // [H/4][16][4]
-  float* W1 = lds + PK<HH>::W;              // [H/4][16][4] (TWO)
-  float* red = W1 + (TWO ? PK<HH>::W : 0);  // partial-tile slots, one layer at a time
+  float* W0 = lds;                          // fp32 [H/4][16][4]
+  float* W1 = lds + PK<HH>::W;              // fp32 [H/4][16][4] (TWO)
+  __bf16* W0b = reinterpret_cast<__bf16*>(lds);             // bf16 [H/8][16][8]
+  __bf16* W1b = W0b + PK<HH>::W;                            // bf16 [H/8][16][8] (TWO)
+  float* red = lds + (BF ? PK<HH>::W / 2 : PK<HH>::W) * (TWO ? 2 : 1);   // partial-tile slots
   // broadcast word: the pad column of slot 0's row 0, never written by put_tile / add_tile
   int* status = reinterpret_cast<int*>(red + PC);
   int xcc_id = 0, xcc_wgs = 0, xcc_n = 0;
@@ -295,8 +374,16 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
     xcc_n = nx;
     *status = ok ? 0 : 1;
   }
-  // ---- weights: W_hh0 tile -> LDS (k-blocked), W_ih1 / W_hh1 fragments -> VGPRs
-  for (int e = tid; e < (H / 4) * PC; e += PNT) {
+  // ---- weights: W_hh0 (and W_ih1) tiles -> LDS (k-blocked), W_hh1 fragments -> VGPRs
+  if (BF) {
+    for (int e = tid; e < (H / 8) * PC; e += PNT) {
+      const int kb = e / PC, col = e % PC;
+      *reinterpret_cast<bf16x8*>(W0b + e * 8) = *reinterpret_cast<const bf16x8*>(a.W0b + (int64_t)grow(col) * H + kb * 8);
+      if (TWO)
+        *reinterpret_cast<bf16x8*>(W1b + e * 8) =
+            *reinterpret_cast<const bf16x8*>(a.Wi1b + (int64_t)grow(col) * H + kb * 8);
+    }
+  } else for (int e = tid; e < (H / 4) * PC; e += PNT) {
     const int kb = e / PC, col = e % PC;
     *reinterpret_cast<f32x4*>(W0 + e * 4) = *reinterpret_cast<const f32x4*>(a.W_hh0 + (int64_t)grow(col) * H + kb * 4);
     if (TWO)
@@ -307,7 +394,13 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
   const int kbase = kw * KW + KL * (lane >> 4);               // this lane's first k
   const int kb0 = kbase / 4;
   float wh[KL] = {};
-  if (TWO) {
+  bf16x8 whb[NS] = {};
+  const int k8_0 = (kw * KW) / 8 + (lane >> 4);              // bf16: this lane's first k block
+  if (TWO && BF) {
+#pragma unroll
+    for (int st = 0; st < NS; ++st)
+      whb[st] = *reinterpret_cast<const bf16x8*>(a.W1b + (int64_t)grow(lane & 15) * H + 8 * (k8_0 + 4 * st));
+  } else if (TWO) {
     const float* sh = a.W_hh1 + (int64_t)grow(lane & 15) * H + kbase;
 #pragma unroll
     for (int g = 0; g < GR; ++g) {
@@ -356,15 +449,19 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
     f32x4 acc1[PRBW] = {}, acc0[PRBW] = {};
     const float* hk0 = a.hk0 + (int64_t)(t >= 1 ? t - 1 : 0) * BH;   // h0_{t-1}
     const float* hk1 = a.hk1 + (int64_t)(t >= 2 ? t - 2 : 0) * BH;   // h1_{t-2}
+    const __bf16* hk0b = a.hk0b + (int64_t)(t >= 1 ? t - 1 : 0) * BH;
+    const __bf16* hk1b = a.hk1b + (int64_t)(t >= 2 ? t - 2 : 0) * BH;
     if (LP_ABLATE == 2 || t == 0) {                                  // h0_{-1} = 0: no products
-    } else if (!TWO) {
-      gemm_wave<KL, false, true, false>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
-    } else if (t == 1) {                                             // h1_{-1} = 0
-      gemm_wave<KL, true, true, false>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
-    } else if (t < T) {
-      gemm_wave<KL, true, true, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
-    } else {                                                         // t == T: layer 1 only
-      gemm_wave<KL, true, false, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+    } else if constexpr (BF) {
+      if (!TWO) gemm_wave_bf<NS, false, true, false>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
+      else if (t == 1) gemm_wave_bf<NS, true, true, false>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
+      else if (t < T) gemm_wave_bf<NS, true, true, true>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
+      else gemm_wave_bf<NS, true, false, true>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
+    } else {
+      if (!TWO) gemm_wave<KL, false, true, false>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+      else if (t == 1) gemm_wave<KL, true, true, false>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+      else if (t < T) gemm_wave<KL, true, true, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+      else gemm_wave<KL, true, false, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);   // t == T
     }
     if (LP_ABLATE != 4) {
       // the 4 waves' partial tiles summed through LDS in fixed order
@@ -385,24 +482,24 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
       if (TWO) {
         reduce_put(red, acc1);
         __syncthreads();
-        if (eown && l1) {                                            // layer 1 at step t - 1
+        if (wave < 4 && l1) {                                        // layer 1 at step t - 1 (eown)
           float pre[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + bias1[g];
           const int t1 = t - 1;
-          out1 = cell(pre, out1.c, a.hk1 + (int64_t)t1 * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3));
+          out1 = cell(pre, out1.c);
+          handoff<BF>(out1.h, a.hk1 + (int64_t)t1 * BH, a.hk1b + (int64_t)t1 * BH, B, eb, ej, lane);
         }
         __syncthreads();                                             // slots reused for layer 0
       }
       reduce_put(red, acc0);
       __syncthreads();
-      if (eown) {
-        if (l0) {                                                    // layer 0 at step t
-          float pre[4];
+      if (wave < 4 && l0) {                                          // layer 0 at step t (eown)
+        float pre[4];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + gxv[g];
-          out0 = cell(pre, out0.c, a.hk0 + (int64_t)t * BH + ((int64_t)(ej >> 2) * B + eb) * 4 + (ej & 3));
-        }
+        for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + gxv[g];
+        out0 = cell(pre, out0.c);
+        handoff<BF>(out0.h, a.hk0 + (int64_t)t * BH, a.hk0b + (int64_t)t * BH, B, eb, ej, lane);
       }
     } else if (wave == 0 && acc1[0][0] == 12345.f && acc0[1][1] == 12345.f) {
       a.h0[0] = 0.f;                                                  // keep the products live
@@ -417,15 +514,15 @@ int g_cus = -1;
 
 // one workgroup of the <HH, TWO> kernel must fit on a CU, and every workgroup must be resident
 // at once: no more workgroups (HH / PU) than CUs
-template <int HH, bool TWO>
+template <int HH, bool TWO, bool BF = false>
 bool persist_fits() {
   static int per = -1;
   if (per < 0) {
     per = 0;
-    const void* k = reinterpret_cast<const void*>(lstm_persist_kernel<HH, TWO>);
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<HH, TWO>()) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_persist_kernel<HH, TWO>, PNT,
-                                                     lds_bytes<HH, TWO>()) != hipSuccess)
+    const void* k = reinterpret_cast<const void*>(lstm_persist_kernel<HH, TWO, BF>);
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<HH, TWO, BF>()) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_persist_kernel<HH, TWO, BF>, PNT,
+                                                     lds_bytes<HH, TWO, BF>()) != hipSuccess)
       per = 0;
   }
   if (g_cus < 0) {
@@ -437,13 +534,16 @@ bool persist_fits() {
   return per >= 1 && HH / PU <= g_cus;
 }
 
-template <int HH, bool TWO>
+template <int HH, bool TWO, bool BF = false>
 void launch_persist(PArgs& a, void* workspace, hipStream_t stream) {
   a.bar = static_cast<int*>(workspace);
   a.hk0 = reinterpret_cast<float*>(static_cast<char*>(workspace) + BAR_BYTES);
   a.hk1 = TWO ? a.hk0 + (int64_t)a.T * a.B * HH : nullptr;
+  a.hk0b = reinterpret_cast<__bf16*>(a.hk0);
+  a.hk1b = TWO ? a.hk0b + (int64_t)a.T * a.B * HH : nullptr;
   a.timeout_ticks = 20000000;   // 200 ms of s_memrealtime (100 MHz) per wait
-  hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO>()), stream, a);
+  hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO, BF>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO, BF>()), stream,
+                     a);
 }
 
 }  // namespace
@@ -478,6 +578,34 @@ extern "C" int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx
   a.h0_ldb = (int64_t)T * H; a.h0_ldt = H;
   AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
   launch_persist<1024, true>(a, workspace, stream);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm2_fwd_persist_bf16(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                                             const uint16_t* W_hh0_b, const float* b_ih1, const float* b_hh1,
+                                             const uint16_t* W_ih1_b, const uint16_t* W_hh1_b, float* h0, float* c0,
+                                             float* gates0, float* h1, float* c1, float* gates1, void* workspace,
+                                             hipStream_t stream) {
+  static const char* fn = "autovc_lstm2_fwd_persist_bf16";
+  AVC_CHECK_ARG(T > 0 && H == 1024 && B == PB && (persist_fits<1024, true, true>()),
+                "%s: unsupported shape B=%d H=%d on this device (needs H=1024, B=%d, one CU per workgroup)", fn,
+                B, H, PB);
+  AVC_CHECK_ARG(gx0 && W_hh0_b && b_ih1 && b_hh1 && W_ih1_b && W_hh1_b && h0 && c0 && h1 && c1 && workspace,
+                "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh0_b) && AVC_ALIGNED16(W_ih1_b) && AVC_ALIGNED16(W_hh1_b) &&
+                AVC_ALIGNED16(workspace), "%s: weights / workspace must be 16-byte aligned", fn);
+  PArgs a = {};
+  a.B = B; a.T = T; a.H = H;
+  a.gx0 = gx0; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt;
+  a.b_ih1 = b_ih1; a.b_hh1 = b_hh1;
+  a.W0b = reinterpret_cast<const __bf16*>(W_hh0_b);
+  a.Wi1b = reinterpret_cast<const __bf16*>(W_ih1_b);
+  a.W1b = reinterpret_cast<const __bf16*>(W_hh1_b);
+  a.h0 = h0; a.c0 = c0; a.g0 = gates0; a.h1 = h1; a.c1 = c1; a.g1 = gates1;
+  a.h0_ldb = (int64_t)T * H; a.h0_ldt = H;
+  AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
+  launch_persist<1024, true, true>(a, workspace, stream);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
 }

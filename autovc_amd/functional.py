@@ -719,10 +719,16 @@ class LSTM2StackFn(torch.autograd.Function):
             # the bf16 weight copies must be alive together (a temporary's block would be
             # reused by the next conversion before the launches read it)
             W0b, Wi1b, W1b = _bf(W_hh0), _bf(W_ih1), _bf(W_hh1)
-            _lib.call("autovc_lstm2_fwd_bf16", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W0b.data_ptr(),
-                      b_ih1.data_ptr(), b_hh1.data_ptr(), Wi1b.data_ptr(), W1b.data_ptr(),
-                      h0.data_ptr(), h0b.data_ptr(), c0.data_ptr(), _p(g0), h1.data_ptr(), h1b.data_ptr(),
-                      c1.data_ptr(), _p(g1), _s())
+            if lstm2_persistent(B, H):
+                ws = _ws(dev, _lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), "lstm2p")
+                _lib.call("autovc_lstm2_fwd_persist_bf16", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H,
+                          W0b.data_ptr(), b_ih1.data_ptr(), b_hh1.data_ptr(), Wi1b.data_ptr(), W1b.data_ptr(),
+                          h0.data_ptr(), c0.data_ptr(), _p(g0), h1.data_ptr(), c1.data_ptr(), _p(g1), ws, _s())
+            else:
+                _lib.call("autovc_lstm2_fwd_bf16", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W0b.data_ptr(),
+                          b_ih1.data_ptr(), b_hh1.data_ptr(), Wi1b.data_ptr(), W1b.data_ptr(),
+                          h0.data_ptr(), h0b.data_ptr(), c0.data_ptr(), _p(g0), h1.data_ptr(), h1b.data_ptr(),
+                          c1.data_ptr(), _p(g1), _s())
         elif lstm2_persistent(B, H):
             ws = _ws(dev, _lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), "lstm2p")
             _lib.call("autovc_lstm2_fwd_persist_f32", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H, W_hh0.data_ptr(),

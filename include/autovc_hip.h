@@ -219,6 +219,14 @@ int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx0, int64_t 
                                  const float* W_hh0, const float* b_ih1, const float* b_hh1,
                                  const float* W_ih1, const float* W_hh1, float* h0, float* c0, float* gates0,
                                  float* h1, float* c1, float* gates1, void* workspace, hipStream_t stream);
+/* autovc_lstm2_fwd_bf16 (precision "bf16") the same way: bf16 weight copies, bf16 hand-off
+ * copies of h inside the workspace (autovc_lstm2_persist_workspace_bytes), fp32 outputs;
+ * H = 1024, B = 64 where autovc_lstm2_persist_supported holds (the bf16 kernel needs less LDS). */
+int autovc_lstm2_fwd_persist_bf16(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
+                                  const uint16_t* W_hh0_b, const float* b_ih1, const float* b_hh1,
+                                  const uint16_t* W_ih1_b, const uint16_t* W_hh1_b, float* h0, float* c0,
+                                  float* gates0, float* h1, float* c1, float* gates1, void* workspace,
+                                  hipStream_t stream);
 /* One large-H layer (decoder lstm1, model_vc_mel.py:90,111) the same way: arguments and
  * outputs of autovc_lstm_fwd_f32 (forward direction) plus a workspace of
  * autovc_lstm_persist_workspace_bytes bytes; H = 512 or 1024, B = 64
