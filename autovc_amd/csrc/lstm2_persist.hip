@@ -541,7 +541,7 @@ void launch_persist(PArgs& a, void* workspace, hipStream_t stream) {
   a.hk1 = TWO ? a.hk0 + (int64_t)a.T * a.B * HH : nullptr;
   a.hk0b = reinterpret_cast<__bf16*>(a.hk0);
   a.hk1b = TWO ? a.hk0b + (int64_t)a.T * a.B * HH : nullptr;
-  a.timeout_ticks = 20000000;   // 200 ms of s_memrealtime (100 MHz) per wait
+  a.timeout_ticks = 100000000;  // 1 s of s_memrealtime (100 MHz) per wait: a safety net, never a schedule
   hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO, BF>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO, BF>()), stream,
                      a);
 }

@@ -106,7 +106,7 @@ def lstm_roofline(solver, B, T, dev):
             xs.append(e0.elapsed_time(e1) * 1e3)
         launch_us = sorted(xs[1:])[1]
         flop_launch, bytes_launch = flop2 * T, 2 * per_layer_step * T
-        kernel = "lstm_persist_kernel<1024, true> (decoder lstm2 forward, both layers, whole sequence per launch, H=1024, B=64)"
+        kernel = "lstm_persist_kernel<1024, true, false> (decoder lstm2 forward, both layers, whole sequence per launch, H=1024, B=64)"
         pmc_file = "lstm2_persist_pmc.json"
     else:
         launch_us, flop_launch, bytes_launch = us2, flop2, 2 * per_layer_step

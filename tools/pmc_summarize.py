@@ -11,7 +11,7 @@ import sys
 
 MODE = sys.argv[3] if len(sys.argv) > 3 else "single"
 KERNEL = {"stack": "lstm2_fwd_step_kernel", "stackbwd": "lstm2_bwd_rec_kernel",
-          "persist": "lstm_persist_kernel<1024, true>"}.get(MODE, "lstm_fwd_step_kernel")
+          "persist": "lstm_persist_kernel<1024, true, false>"}.get(MODE, "lstm_fwd_step_kernel")
 
 
 def per_dispatch(d, counter):
@@ -39,7 +39,7 @@ fa = sum(keep(f)) / max(1, len(keep(f)))
 wa = sum(keep(w)) / max(1, len(keep(w)))
 out = {"kernel": {"stack": "lstm2_fwd_step_kernel (decoder lstm2, both layers, H=1024, B=64)",
                   "stackbwd": "lstm2_bwd_rec_kernel (decoder lstm2 backward, both layers + W_ih1, H=1024, B=64)",
-                  "persist": "lstm_persist_kernel<1024, true> (decoder lstm2 forward, whole sequence, H=1024, B=64, T=128)"}
+                  "persist": "lstm_persist_kernel<1024, true, false> (decoder lstm2 forward, whole sequence, H=1024, B=64, T=128)"}
        .get(MODE, "lstm_fwd_step_kernel (H=1024, B=64)"), "launches": len(f),
        "fetch_size_kib_raw": round(fa, 1), "write_size_kib": round(wa, 1),
        "hbm_bytes_per_launch": int(round((2 * fa + wa) * 1024)),
