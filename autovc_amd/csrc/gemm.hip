@@ -721,7 +721,15 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   }
   if (batch > 1 && !bf16) {   // batched: tile count x batch decides between 128x128 and 64x64
     const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch;
-    cfg = t128 >= 512 ? kCfg[2] : kCfg[8];
+    // the 128-tile batched case (the Winograd GEMMs): 8 waves of 64x32 with pipelined fragment
+    // reads (cfg 9) — isolated 78.6 vs 88.2 us on 8 x 2048x512x512 (tools/gemm_bench.hip wino,
+    // profiles/r02/gemm_wino_sweep.txt), in the step 16.465-16.485 vs 16.491-16.542 ms
+    // alternating; AVC_GEMM_BATCHED_CFG=<id> overrides
+    static const int wino_cfg = [] {
+      const char* e = getenv("AVC_GEMM_BATCHED_CFG");
+      return e ? atoi(e) : 9;
+    }();
+    cfg = g_force_cfg >= 0 ? kCfg[g_force_cfg] : t128 >= 512 ? kCfg[wino_cfg] : kCfg[8];
   }
   const int BKc = cfg.bk;
   int64_t kps = ((int64_t)K + splits - 1) / splits;

@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 struct Case { const char* name; int M, N, K, at, bt, aconv, bconv, C, splits; };
 
@@ -40,6 +41,36 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(A, h, big * 4, hipMemcpyHostToDevice);
     (void)hipMemcpy(B, h, big * 4, hipMemcpyHostToDevice);
     free(h);
+  }
+  if (argc > 1 && std::string(argv[1]) == "wino") {   // the Winograd F(4,5) batched GEMMs (8 per conv)
+    struct W { const char* name; int M, N, K; };
+    const W ws[] = {{"wino 512->512", 2048, 512, 512}, {"wino 336->512", 2048, 512, 336},
+                    {"wino 512->80", 2048, 80, 512}, {"wino dX 512<-512", 2048, 512, 512}};
+    hipEvent_t a0, a1;
+    (void)hipEventCreate(&a0);
+    (void)hipEventCreate(&a1);
+    for (const W& w : ws) {
+      printf("%-18s 8 x M=%5d N=%5d K=%5d :", w.name, w.M, w.N, w.K);
+      for (int cfg = 0; cfg < 12; ++cfg) {
+        g_force_cfg = cfg;
+        auto run = [&]() {
+          return autovc_gemm_batched_f32(8, w.M, w.N, w.K, A, w.K, (int64_t)w.M * w.K, 0, B, w.K, (int64_t)w.N * w.K, 0,
+                                         Cm, w.N, (int64_t)w.M * w.N, 0, 0);
+        };
+        if (run() != 0) { printf(" cfg%d ERR", cfg); continue; }
+        (void)hipDeviceSynchronize();
+        (void)hipEventRecord(a0, 0);
+        for (int i = 0; i < 20; ++i) run();
+        (void)hipEventRecord(a1, 0);
+        (void)hipEventSynchronize(a1);
+        float ms;
+        (void)hipEventElapsedTime(&ms, a0, a1);
+        const double us = ms * 50.0;
+        printf("  cfg%d %6.1fus %5.1fTF", cfg, us, 2.0 * 8 * w.M * w.N * w.K / (us * 1e-6) / 1e12);
+      }
+      printf("\n");
+    }
+    return 0;
   }
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
