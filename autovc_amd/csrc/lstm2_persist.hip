@@ -58,6 +58,13 @@
 #ifndef LP_NW
 #define LP_NW 8
 #endif
+// grid barrier: 0 = XCC counters -> top counter -> generation words (two atomic round trips
+// on the critical path); 1 = XCC counters only, every waiting workgroup polls all of them —
+// measured 24.1 vs 20.2 us per wavefront step (256 pollers x 8 counters contend with the
+// arrivals: profiles/r02/lstm2_persist_ab_8wave.txt), kept as a diagnostic build only
+#ifndef LP_BARRIER
+#define LP_BARRIER 0
+#endif
 
 namespace {
 
@@ -147,10 +154,34 @@ __device__ __noinline__ bool wait_ge(int* p, int target, int* err, int timeout_t
 // workgroup timed out (then every workgroup leaves the kernel).
 // xcc / mine / nx: this workgroup's XCC, the workgroups on it and the XCCs in use (held by
 // thread 0); *status: an LDS word broadcasting the outcome to the workgroup
-__device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int nx, int* status, int gen) {
+// polls every XCC's arrival counter (census[x] = workgroups on XCC x, 0 = unused) until each
+// has reached census[x] * (gen + 1); bounded like wait_ge
+__device__ __noinline__ bool wait_all_xcc(int* bar, const int (&census)[16], int gen, int timeout_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool all = true;
+    for (int x = 0; x < 16; ++x)
+      if (census[x] > 0 && ld_rlx(bar + (BAR_ARRIVE + x) * L) < census[x] * (gen + 1)) all = false;
+    if (all) return true;
+    if (ld_rlx(bar + BAR_ERR * L) != 0) return false;
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)timeout_ticks) {
+      st_rlx(bar + BAR_ERR * L, 1);
+      return false;
+    }
+  }
+}
+
+__device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int nx, const int (&census)[16],
+                                          int* status, int gen) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's stores are in L2
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && LP_BARRIER == 1) {
+    add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
+    const bool ok = wait_all_xcc(a.bar, census, gen, a.timeout_ticks);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)
+    *status = ok ? 0 : 1;
+  } else if (threadIdx.x == 0) {
     bool ok = true;
     const int old = add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
     if (old == mine * (gen + 1) - 1) {                    // last of this XCC
@@ -353,6 +384,7 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
   // broadcast word: the pad column of slot 0's row 0, never written by put_tile / add_tile
   int* status = reinterpret_cast<int*>(red + PC);
   int xcc_id = 0, xcc_wgs = 0, xcc_n = 0;
+  int census[16] = {};                     // workgroups per XCC (thread 0)
   constexpr int H = HH;
   const int B = a.B, T = a.T;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -368,7 +400,10 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
     add_rlx(a.bar + BAR_START * L, 1);
     const bool ok = wait_ge(a.bar + BAR_START * L, gridDim.x, a.bar + BAR_ERR * L, a.timeout_ticks);
     int nx = 0;
-    for (int x = 0; x < 16; ++x) nx += ld_rlx(a.bar + (BAR_CENSUS + x) * L) > 0;
+    for (int x = 0; x < 16; ++x) {
+      census[x] = ld_rlx(a.bar + (BAR_CENSUS + x) * L);
+      nx += census[x] > 0;
+    }
     xcc_id = (int)xcc;
     xcc_wgs = ld_rlx(a.bar + (BAR_CENSUS + xcc) * L);
     xcc_n = nx;
@@ -505,7 +540,7 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
       a.h0[0] = 0.f;                                                  // keep the products live
     }
     if (LP_ABLATE == 1) __syncthreads();
-    else if (t < last && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, status, t)) return;
+    else if (t < last && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, census, status, t)) return;
   }
   store_outputs(last);                                               // the final iteration's outputs
 }
