@@ -94,6 +94,19 @@ class ResidualConv1dGLU(nn.Module):
         self.conv1x1_out = _conv1x1(gate_channels // 2, residual_channels, weight_normalization)
         self.conv1x1_skip = _conv1x1(gate_channels // 2, skip_out_channels, weight_normalization)
 
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        # wavenet_vocoder 0.1.1 (the reference's pin) gives the conditioning 1x1 a bias (its
+        # weight-normalised Conv1d1x1 asserts bias=True); later releases build it with
+        # bias=False.  A checkpoint of either kind loads: a missing
+        # conv1x1c.bias is a zero bias, the same arithmetic.
+        key = prefix + "conv1x1c.bias"
+        if self.conv1x1c is not None and key not in state_dict and any(k.startswith(prefix + "conv1x1c.")
+                                                                       for k in state_dict):
+            state_dict[key] = torch.zeros_like(self.conv1x1c.bias)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+
 
 def receptive_field_size(total_layers, num_cycles, kernel_size, dilation=lambda x: 2 ** x):
     layers_per_cycle = total_layers // num_cycles

@@ -102,6 +102,29 @@ def test_module_keys_match_r9y9_layout():
     assert model.receptive_field == 505  # (k-1) * sum(dilations) + 1, SURVEY a23
 
 
+def test_checkpoint_without_conditioning_bias_loads():
+    """wavenet_vocoder 0.1.1 (the reference's pin) gives conv1x1c a bias; later releases do
+    not (SURVEY a23).  A state_dict without the conv1x1c.bias keys loads strictly, as zeros;
+    one with them round-trips unchanged."""
+    from autovc_amd.synthesis import build_model
+    src = build_model()
+    sd = src.state_dict()
+    for k in sd:
+        if k.endswith("conv1x1c.bias"):
+            sd[k] = torch.randn_like(sd[k])
+    dst = build_model()
+    dst.load_state_dict(sd, strict=True)
+    assert all(torch.equal(dst.state_dict()[k], v) for k, v in sd.items())
+    nobias = {k: v for k, v in sd.items() if not k.endswith("conv1x1c.bias")}
+    assert len(nobias) == len(sd) - 24
+    dst.load_state_dict(nobias, strict=True)
+    for k, v in dst.state_dict().items():
+        if k.endswith("conv1x1c.bias"):
+            assert not bool(v.any()), k
+        else:
+            assert torch.equal(v, sd[k]), k
+
+
 def test_module_rejects_unsupported_configs():
     from autovc_amd.wavenet import WaveNet
     with pytest.raises(NotImplementedError):

@@ -136,3 +136,23 @@ def test_checkpoint_resume_reproduces_uninterrupted_run(cuda, tmp_path, monkeypa
     rel = (psnt.cpu().double() - ref_psnt.double()).abs().max() / ref_psnt.abs().max()
     assert rel.item() < 1e-4
     assert (code.cpu().double() - ref_code.double()).abs().max().item() < 1e-4 * ref_code.abs().max().item()
+
+
+def test_model_ema_matches_reference_formula(cuda, tmp_path, monkeypatch):
+    """solver_encoder.py:168-177: the EMA pass writes ema*p + (1-ema)*p (fp32) over the
+    concatenation of G.parameters() back into every parameter, bit for bit."""
+    import bench
+    x, e = bench.synthetic_batch(4, 128, "cpu", 5)
+    monkeypatch.chdir(tmp_path)
+    from autovc_amd.solver_encoder import Solver
+    s = Solver(_FixedLoader(x, e), _main_config(".", "ema", num_iters=1, log_step=1, ema=0.9999))
+    s.G.load_state_dict(og.make_weights())
+    with torch.no_grad():
+        for p in s.G.parameters():             # non-trivial values everywhere
+            p.mul_(1.37)
+    flat = torch.cat([p.detach().reshape(-1) for p in s.G.parameters()])
+    want = s.ema * flat + (1 - s.ema) * flat
+    s.model_EMA()
+    got = torch.cat([p.detach().reshape(-1) for p in s.G.parameters()])
+    assert torch.equal(got, want)
+    assert (got - flat).abs().max().item() <= 2e-7 * flat.abs().max().item()   # ~p, as in the reference
