@@ -70,6 +70,7 @@ struct OpTile {
   static_assert(PER * NT == F4, "staging map");
   static_assert(RK ? NT % (BK / 4) == 0 : NT % (ROWS / 4) == 0, "slots of a thread share k (RK) / row (CK)");
   f32x4 v[PER];
+  f32x4 v2[PER];            // second staging set (bf16 kernel: two stages in flight)
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t off[PER];        // byte offset of the slot's next float4 (valid when unmasked)
   bool rok[PER];            // RK: row inside the operand
@@ -116,7 +117,9 @@ struct OpTile {
       }
     }
   }
-  __device__ __forceinline__ void load(const Opnd& o, int64_t K) {
+  __device__ __forceinline__ void load(const Opnd& o, int64_t K) { load_to(o, K, v); }
+  // the next stage's loads into `dst` (v or v2); the address state advances by one stage
+  __device__ __forceinline__ void load_to(const Opnd& o, int64_t K, f32x4 (&dst)[PER]) {
     if (RK) {
       const bool kin = kk < K;
       const int tt0 = tap + o.tap0;
@@ -124,7 +127,7 @@ struct OpTile {
       for (int i = 0; i < PER; ++i) {
         bool ok = rok[i] && kin;
         if (o.conv_T > 0) ok = ok && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T;
-        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
+        dst[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
         off[i] += BK * 4;
       }
       kk += BK;
@@ -139,7 +142,7 @@ struct OpTile {
       for (int i = 0; i < PER; ++i) {
         bool ok = rowok && kpos[i] < K;
         if (o.conv_T > 0) ok = ok && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T;
-        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
+        dst[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
         off[i] += (uint32_t)(BK * o.ld * 4);
         kpos[i] += BK;
         if (o.conv_T > 0) {   // (frame + BK) % T with the uniform BK % T
@@ -158,14 +161,15 @@ struct OpTile {
     }
   }
   // bf16 image [row][LDB] (k contiguous) of an RK operand: each slot as one 8-byte write
-  template <int LDB>
+  template <int LDB, int SET = 0>
   __device__ __forceinline__ void store_bf16(__bf16* lds) const {
     static_assert(RK, "CK operands use store_bf16_kr");
+    const f32x4 (&src)[PER] = SET ? v2 : v;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
       coords(i, r, k);
-      const bf16x4 b = {(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
+      const bf16x4 b = {(__bf16)src[i][0], (__bf16)src[i][1], (__bf16)src[i][2], (__bf16)src[i][3]};
       *reinterpret_cast<bf16x4*>(lds + r * LDB + k) = b;
     }
   }
@@ -174,12 +178,14 @@ struct OpTile {
   // ds_read_b64_tr_b16 (frag_tr below).  The 32-element pad makes the k-row stride 16 dwords
   // mod 64, so the 4 k rows one 32-lane half reads sit on disjoint banks.
   static constexpr int LDK = ROWS + 32;
+  template <int SET = 0>
   __device__ __forceinline__ void store_bf16_kr(__bf16* lds) const {
+    const f32x4 (&src)[PER] = SET ? v2 : v;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
       coords(i, r, k);
-      const bf16x4 b = {(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
+      const bf16x4 b = {(__bf16)src[i][0], (__bf16)src[i][1], (__bf16)src[i][2], (__bf16)src[i][3]};
       *reinterpret_cast<bf16x4*>(lds + k * LDK + r) = b;
     }
   }
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
 // v_mfma_f32_32x32x16_bf16 accumulates in fp32 (lane (r = l & 31, h = l >> 5) reads the 8
 // contiguous k = 16 ks + 8h .. +8 of its row with one ds_read_b128, the operand map of
 // the instruction, for A and B alike).
-template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK>
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool DEEP = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
@@ -399,10 +405,20 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     if constexpr (B_RK) sb.template store_bf16<LDB>(img + A_EL);
     else sb.store_bf16_kr(img + A_EL);
   };
+  auto stage2 = [&](__bf16* img) {   // from the second staging set
+    if constexpr (A_RK) sa.template store_bf16<LDB, 1>(img);
+    else sa.template store_bf16_kr<1>(img);
+    if constexpr (B_RK) sb.template store_bf16<LDB, 1>(img + A_EL);
+    else sb.template store_bf16_kr<1>(img + A_EL);
+  };
   if (nk > 0) {
     sa.load(A, kend);
     sb.load(B, kend);
     stage(smem[0]);
+  }
+  if (DEEP) {                        // stages 1 and 2 in flight before the first barrier
+    if (nk > 1) { sa.load(A, kend); sb.load(B, kend); }
+    if (nk > 2) { sa.load_to(A, kend, sa.v2); sb.load_to(B, kend, sb.v2); }
   }
   __syncthreads();
 
@@ -421,14 +437,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     const s16x4 w[2] = {lo, hi};
     return __builtin_bit_cast(bf16x8, w);
   };
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) {
-      sa.load(A, kend);
-      sb.load(B, kend);
-    }
-    const __bf16* As = smem[buf];
-    const __bf16* Bs = smem[buf] + A_EL;
+  auto compute = [&](const __bf16* As) {
+    const __bf16* Bs = As + A_EL;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 fa[TI], fb[TJ];
@@ -446,8 +456,38 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) stage(smem[buf ^ 1]);
-    __syncthreads();
+  };
+  if (DEEP) {
+    // two register stages in flight: at the top of an iteration LDS buffer 0 holds stage kt,
+    // set 1 (v) stage kt + 1 and set 2 (v2) stage kt + 2; each half computes one buffer and
+    // refills the other from the set whose loads are oldest, then reloads that set
+    for (int kt = 0; kt < nk; kt += 2) {
+      compute(smem[0]);
+      if (kt + 1 < nk) {
+        stage(smem[1]);
+        if (kt + 3 < nk) { sa.load(A, kend); sb.load(B, kend); }
+      }
+      __syncthreads();
+      if (kt + 1 < nk) {
+        compute(smem[1]);
+        if (kt + 2 < nk) {
+          stage2(smem[0]);
+          if (kt + 4 < nk) { sa.load_to(A, kend, sa.v2); sb.load_to(B, kend, sb.v2); }
+        }
+        __syncthreads();
+      }
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) {
+        sa.load(A, kend);
+        sb.load(B, kend);
+      }
+      compute(smem[buf]);
+      if (kt + 1 < nk) stage(smem[buf ^ 1]);
+      __syncthreads();
+    }
   }
 
   float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
@@ -653,7 +693,10 @@ template <int BM, int BN, int BK, int WM, int WN>
 void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                          float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR>), grid, dim3(NT), \
+  // two stages in flight only on the 256-row tiles, and not for 256x256 with both operands
+  // K-strided (spills): tools/gemm_bf16_bench.hip, profiles/r02/gemm_bf16_deep.txt
+#define AVC_DEEP(AR, BR) (BM == 256 && !(BN == 256 && !(AR) && !(BR)))
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, AVC_DEEP(AR, BR)>), grid, dim3(NT), \
                                          dyn_lds_for(bf16_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, \
                                          K, oa, ob, C, ldc, b1, b2, acc, kps, slab, g_batch)
   if (!a_trans && !b_trans) AVC_L(true, true);
@@ -661,6 +704,7 @@ void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, in
   else if (a_trans && !b_trans) AVC_L(false, true);
   else AVC_L(false, false);
 #undef AVC_L
+#undef AVC_DEEP
 }
 
 void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa,
