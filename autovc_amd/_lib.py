@@ -97,6 +97,8 @@ sig("autovc_lstm_fwd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_p
     c_int, c_ptr)
 sig("autovc_lstm2_fwd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
+sig("autovc_lstm2_bwd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_lstm_bwd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_int, c_int, c_ptr, c_ptr)
 sig("autovc_blstm_fwd_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,

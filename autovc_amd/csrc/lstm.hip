@@ -466,7 +466,8 @@ __global__ __launch_bounds__(64 * NW_) void lstm_bwd_rec_kernel(int B, int T, in
 // -> P1), [H/32, 2H/32) = dG1_t1 W_ih1 (its input gradient = layer 0's dh at t1, -> the
 // upper S slabs of PQ0), [2H/32, 3H/32) = dG0_t0 W_hh0 (-> the lower S slabs of PQ0).
 // W*T are the (H, 4H) transposes.  Out-of-range steps (t1 < 0, t0 >= T) exit.
-template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF>
+// BF: dG* / W*T are the bf16 copies (autovc_lstm2_bwd_bf16).
+template <int KCH_ = KCH, int NW_ = NWV, int D_ = DPF, bool BF = false>
 __global__ __launch_bounds__(64 * NW_) void lstm2_bwd_rec_kernel(int B, int T, int H, const float* dG1,
                                                                 const float* dG0, int t1, int t0,
                                                                 const float* WT1, const float* WIT1,
@@ -475,11 +476,11 @@ __global__ __launch_bounds__(64 * NW_) void lstm2_bwd_rec_kernel(int B, int T, i
   const int64_t slabs = (int64_t)gridDim.z * B * H;
   if (prod < 2) {
     if (t1 < 0) return;
-    if (prod == 0) bwd_rec_body<KCH_, NW_, D_, false>(B, T, H, dG1, t1, WT1, P1, j0);
-    else bwd_rec_body<KCH_, NW_, D_, false>(B, T, H, dG1, t1, WIT1, PQ0 + slabs, j0);
+    if (prod == 0) bwd_rec_body<KCH_, NW_, D_, BF>(B, T, H, dG1, t1, WT1, P1, j0);
+    else bwd_rec_body<KCH_, NW_, D_, BF>(B, T, H, dG1, t1, WIT1, PQ0 + slabs, j0);
   } else {
     if (t0 >= T) return;
-    bwd_rec_body<KCH_, NW_, D_, false>(B, T, H, dG0, t0, WT0, PQ0, j0);
+    bwd_rec_body<KCH_, NW_, D_, BF>(B, T, H, dG0, t0, WT0, PQ0, j0);
   }
 }
 
@@ -918,6 +919,47 @@ extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, in
                        reinterpret_cast<const float*>(dG_b), t, reinterpret_cast<const float*>(W_hh_T_b), P);
   }
   AVC_CHECK_LAUNCH("autovc_lstm_bwd_bf16");
+  return avc::kOk;
+}
+
+// autovc_lstm2_bwd_f32 with the recurrent products on bf16 copies (precision "bf16"): the
+// pointwise passes also write dG1_b / dG0_b, which the next launch's products read; W*T_b are
+// RNE bf16 copies of the (H, 4H) transposes.  Cell backward, dG, partials fp32.
+extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                     const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                     const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
+                                     float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits,
+                                     float* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(T > 0 && bf16_shape_ok(B, H), "autovc_lstm2_bwd_bf16: bad dims");
+  AVC_CHECK_ARG((splits == 2 || splits == 4) && (2 * H) % (KCH * splits) == 0,
+                "autovc_lstm2_bwd_bf16: splits must be 2 or 4 with 2H a multiple of %d x splits", KCH);
+  AVC_CHECK_ARG(dh1_out && gates1 && c1 && gates0 && c0 && W_hh1_T_b && W_ih1_T_b && W_hh0_T_b && dG1 && dG1_b &&
+                dG0 && dG0_b && workspace, "autovc_lstm2_bwd_bf16: null pointer");
+  AVC_CHECK_ARG(d_ldb % 4 == 0 && d_ldt % 4 == 0 && AVC_ALIGNED16(dh1_out) && AVC_ALIGNED16(W_hh1_T_b) &&
+                AVC_ALIGNED16(W_ih1_T_b) && AVC_ALIGNED16(W_hh0_T_b) && AVC_ALIGNED16(dG1_b) && AVC_ALIGNED16(dG0_b),
+                "autovc_lstm2_bwd_bf16: operands must be 16-byte aligned with strides %% 4 == 0");
+  const int64_t BH = (int64_t)B * H;
+  float* P1 = workspace;
+  float* PQ0 = P1 + splits * BH;
+  float* dcs1 = PQ0 + 2 * splits * BH;
+  float* dcs0 = dcs1 + BH;
+  AVC_HIP(hipMemsetAsync(PQ0, 0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_bf16");
+  AVC_HIP(hipMemsetAsync(dcs0, 0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_bf16");
+  BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits, reinterpret_cast<__bf16*>(dG1_b)};
+  BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits, reinterpret_cast<__bf16*>(dG0_b)};
+  const dim3 pgrid((H / 4 + 63) / 64, B, 2);
+  const dim3 rgrid(3 * H / TN, (B + TB - 1) / TB, splits);
+  for (int s = 0; s <= T; ++s) {
+    const int t1 = T - 1 - s, t0 = T - s;
+    if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    else hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<2>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    if (s == T) break;
+    hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF, true>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
+                       reinterpret_cast<const float*>(dG1_b), reinterpret_cast<const float*>(dG0_b), t1, t0,
+                       reinterpret_cast<const float*>(W_hh1_T_b), reinterpret_cast<const float*>(W_ih1_T_b),
+                       reinterpret_cast<const float*>(W_hh0_T_b), P1, PQ0);
+  }
+  AVC_CHECK_LAUNCH("autovc_lstm2_bwd_bf16");
   return avc::kOk;
 }
 

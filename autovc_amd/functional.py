@@ -749,7 +749,7 @@ class LSTM2StackFn(torch.autograd.Function):
         need0 = (n[0],) + tuple(n[1:5])
         need1 = (any(need0),) + tuple(n[5:9])
         H = W_hh0.shape[1]
-        if (any(need0) and g0 is not None and g1 is not None and not _bf16_rec(H)
+        if (any(need0) and g0 is not None and g1 is not None
                 and os.environ.get("AVC_LSTM2_BWD", "1") != "0" and H % 64 == 0):
             return LSTM2StackFn._backward_stacked(ctx, dh1, need0, need1)
         dh0, *grads1 = _lstm_layer_backward(dh1, h0, W_ih1, W_hh1, h1, c1, g1, ctx.params[1], need1)
@@ -780,9 +780,16 @@ class LSTM2StackFn(torch.autograd.Function):
         dG1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         dG0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         mark = _grad_mark(dev)   # queued weight gradients run beside the recurrences
-        _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                  g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(), dG1.data_ptr(),
-                  dG0.data_ptr(), splits, ws, _s())
+        if _bf16_rec(H):
+            WTb = [_bf(w) for w in (WT1, WIT1, WT0)]   # alive together until the launches are queued
+            dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
+            _lib.call("autovc_lstm2_bwd_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
+                      g0.data_ptr(), c0.data_ptr(), WTb[0].data_ptr(), WTb[1].data_ptr(), WTb[2].data_ptr(),
+                      dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), splits, ws, _s())
+        else:
+            _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
+                      g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(), dG1.data_ptr(),
+                      dG0.data_ptr(), splits, ws, _s())
         _flush_grad_queue(after=mark)
         grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
         grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)

@@ -197,6 +197,15 @@ int autovc_lstm2_fwd_bf16(int B, int T, int H, const float* gx0, int64_t gx_ldb,
 int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
                          const float* gates, const float* c_all, const uint16_t* W_hh_T_b, float* dG,
                          uint16_t* dG_b, int reverse, int splits, float* workspace, hipStream_t stream);
+/* autovc_lstm2_bwd_f32 with the recurrent products on bf16 copies: W*T_b are RNE copies of
+ * the (H, 4H) transposes; the steps also write dG1_b / dG0_b (B,T,4H) bf16 beside the fp32
+ * dG1 / dG0.  H a multiple of 128, splits 2 or 4, workspace of
+ * autovc_lstm2_bwd_workspace_floats floats. */
+int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                          const float* gates1, const float* c1, const float* gates0, const float* c0,
+                          const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
+                          float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits, float* workspace,
+                          hipStream_t stream);
 /* autovc_lstm2_fwd_f32 with every launch timed by its own dispatch events; synchronises;
  * *avg_us (HOST pointer) = mean kernel time of launches 2..T-1 (bench.py roofline). */
 int autovc_lstm2_fwd_timed_f32(int B, int T, int H, const float* gx0, int64_t gx_ldb, int64_t gx_ldt,
