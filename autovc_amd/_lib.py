@@ -27,7 +27,7 @@ _SIGS: dict[str, list] = {}
 _RESTYPES = {"autovc_last_error": ctypes.c_char_p,
              "autovc_gemm_workspace_floats": c_i64, "autovc_bn_workspace_bytes": c_i64,
              "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_lstm2_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
-             "autovc_colsum_workspace_floats": c_i64, "autovc_wavenet_packed_floats": c_i64,
+             "autovc_colsum_workspace_floats": c_i64, "autovc_wavenet_packed_floats": c_i64, "autovc_wavenet_ring_frames": c_i64,
              "autovc_wavenet_workspace_bytes": c_i64, "autovc_lstm2_persist_workspace_bytes": c_i64,
              "autovc_lstm_persist_workspace_bytes": c_i64}
 
@@ -122,6 +122,7 @@ sig("autovc_l2norm_rows_f32", c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr)
 sig("autovc_colsum_workspace_floats", c_int)
 sig("autovc_colsum_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_wavenet_packed_floats", c_int, c_int, c_int, c_int, c_int, c_int)
+sig("autovc_wavenet_ring_frames", c_int, c_int, c_int)
 sig("autovc_wavenet_workspace_bytes", c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int)
 sig("autovc_wavenet_upsample_f32", c_int, c_int, c_int, c_int, ctypes.POINTER(c_int), c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr)

@@ -44,15 +44,20 @@
 
 namespace {
 
-// Diagnostic ablations of the step kernels (tools/wn_ablate.sh builds them into a separate
-// library; the product build is WN_ABLATE 0): 1 = step index a constant (no dependent
-// counter load), 2 = 1 + no activation loads, 3 = 1 + no weight loads, 4 = 1 + no residual
-// wave work, 5 = every step kernel returns at once (launch boundaries only), 6 = 2+3+4,
-// 7 = 1 + no cross-lane reduction, 8 = layer kernels l >= 1 return at once, 9 = every layer
-// kernel returns at once, 10 = tail and head return at once.  Outputs are meaningless
-// unless WN_ABLATE == 0.
-#ifndef WN_ABLATE
-#define WN_ABLATE 0
+// Diagnostic timeline (tools/wn_stamps.sh builds it into a separate library; the product
+// build is WN_STAMP 0): lane 0 of wave 0 (gate) and of wave kGW (residual) of every
+// workgroup records s_memrealtime (100 MHz, one clock for the whole chip) at the phase
+// boundaries of the kernel for ONE chosen sample step; autovc_wavenet_stamps reads them.
+#ifndef WN_STAMP
+#define WN_STAMP 0
+#endif
+#if WN_STAMP
+constexpr int kStampLaunch = 64, kStampWG = 512, kStampN = 8;
+__device__ unsigned long long g_wn_stamp[kStampLaunch * kStampWG * kStampN];
+__device__ int g_wn_stamp_t = -1;
+#define WN_NOW() __builtin_amdgcn_s_memrealtime()
+// the value must have arrived before the clock is read
+#define WN_AFTER(v) asm volatile("" ::"v"(v))
 #endif
 
 constexpr float kSqrtHalf = 0.70710677f;  // float(math.sqrt(0.5))
@@ -61,7 +66,7 @@ constexpr int kMaxNO = 32;                // MoL head width limit (3 x up to 10 
 constexpr int kCtrSlots = 128;
 
 struct WnArgs {
-  int B, T, R, G, S, NO, K, RING, n_layers, lps, Tch, legacy, n_kern;
+  int B, T, R, G, S, NO, K, RING, n_layers, lps, Tch, legacy;
   const float* packed;
   const float* pre;
   float* ring;
@@ -145,6 +150,32 @@ __device__ float mol_sample(const float* y, int nr, int64_t t, int utt, const Wn
   return fminf(fmaxf(x, -1.0f), 1.0f);
 }
 
+// The step-dependent, parameter-independent part of mol_sample for one (utterance, index j)
+// lane: j < nr -> logf(-logf(u_j)) (the Gumbel term), j == 10 -> logf(u) - logf(1 - u) of the
+// logistic draw.  Computed while the MoL parameters are still in flight; mol_pick finishes
+// with the same float operations as mol_sample.
+__device__ inline float mol_noise(int j, int64_t t, int utt, const WnArgs& a) {
+  uint32_t c[4] = {(uint32_t)t, (uint32_t)utt, (uint32_t)(j >> 2), 0u};
+  philox(c, a.seed_lo, a.seed_hi);
+  const int w = j & 3;
+  const float u = uniform_from_word(w == 0 ? c[0] : w == 1 ? c[1] : w == 2 ? c[2] : c[3]);
+  if (j == 10) return logf(u) - logf(1.0f - u);
+  return logf(-logf(u));
+}
+
+__device__ inline float mol_pick(const float* y, int nr, const float* gum, float dlog, float log_scale_min) {
+  int best = 0;
+  float bv = -INFINITY;
+  for (int j = 0; j < nr; ++j) {
+    const float v = y[j] - gum[j];
+    if (v > bv) { bv = v; best = j; }
+  }
+  const float mean = y[nr + best];
+  const float ls = fmaxf(y[2 * nr + best], log_scale_min);
+  const float x = mean + expf(ls) * dlog;
+  return fminf(fmaxf(x, -1.0f), 1.0f);
+}
+
 // Butterfly reduction of NV per-lane partial sums over the 64 lanes of a wave: NV-1
 // shuffles for the halving rounds instead of 6*NV.  On return lane L with
 // (L & (64/NV - 1)) == 0 holds the full sum of value L / (64/NV).  Every array index is a
@@ -189,20 +220,26 @@ __device__ inline float dot4(f32x4 w, f32x4 x, float acc) {
 
 __device__ inline f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-// step index: a kernel argument for direct launches (targ >= 0), else (graph replay) the
-// counter slot the previous kernel wrote
-__device__ inline int read_step(const WnArgs& a, int slot, int next_delta, int targ) {
-  if (WN_ABLATE != 0) return a.T - 1;
-  if (targ >= 0) return targ;
-  const int t = a.ctr[slot];
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[slot + 1 == a.n_kern ? 0 : slot + 1] = t + next_delta;
-  return t;
+// The absolute sample step: a kernel argument for direct launches (targ >= 0), else (graph
+// replay) the counter the previous step's head kernel advanced.  Only layer 0 (sampling draw,
+// recorded outputs, teacher inputs) and the head read it: every load of the step kernels is
+// addressed by the ring slot and the conditioning row, which are kernel arguments in both
+// modes (a captured graph covers one RING-aligned conditioning chunk), so no load waits for
+// a dependent counter read (it cost 0.86 us per launch on the critical path).
+__device__ inline int abs_step(const WnArgs& a, int targ) { return targ >= 0 ? targ : a.ctr[0]; }
+
+// ring row of layer input l (l = 0: x_0 = first_conv(input)) at slot s: (B, R)
+__device__ inline float* ring_row(const WnArgs& a, int l, int s) {
+  return a.ring + ((int64_t)l * a.RING + s) * a.B * a.R;
 }
 
-// All step kernels are latency-bound (a few MB per launch spread over 256 CUs), so each
-// wave issues every load it needs before the first use: batch rows beyond the tile are
-// clamped to a valid row (their sums are computed and dropped) instead of branching, and
-// the K dimension of the gate GEMV is split across the waves of a workgroup.
+// A workgroup barrier that waits for LDS traffic only: __syncthreads' release fence would
+// also drain the wave's outstanding global loads.
+__device__ inline void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // MoL parameters of step tp = tp1 - 1 (from h1) for the batch tile, then the input of
 // step tp1.  Runs on the whole workgroup (NW waves).  Writes s_in[b].
@@ -284,26 +321,24 @@ constexpr int kLayerThreads = 64 * (kGW + kRW);
 constexpr int kTailWaves = 2;             // tail / head: one wave per output row
 
 // MoL head output of the previous step for the utterance tile, in two halves so that its
-// loads (W2 rows, h1) are issued at kernel start: the first reads this wave's W2 rows and
-// h1 chunk (S == 256: one 4-float chunk per lane), the second reduces them into s_mol.
+// loads are issued at kernel start: every wave reads its W2 rows (S == 256: one 4-float
+// chunk per lane); h1 is read ONCE per workgroup, by the last wave, into LDS (nine copies
+// of it in flight were 32 KB of the CU's operand fill); the second half reduces into s_mol.
 constexpr int kMolRows = (kMaxNO + kGW + kRW - 1) / (kGW + kRW);   // W2 rows per wave
 
-__device__ __forceinline__ void mol_load(const WnArgs& a, int wave, int lane, int b0, int nb,
-                                         f32x4 (&mw)[kMolRows], f32x4 (&mh)[kUB]) {
+__device__ __forceinline__ void mol_load(const WnArgs& a, int wave, int lane, f32x4 (&mw)[kMolRows]) {
   const float* W2 = head_base(a) + (int64_t)a.S * a.S + a.S;
 #pragma unroll
   for (int q = 0; q < kMolRows; ++q) {
     const int r = wave + q * (kGW + kRW);
     mw[q] = ld4(W2 + (int64_t)(r < a.NO ? r : 0) * a.S + lane * 4);
   }
-#pragma unroll
-  for (int b = 0; b < kUB; ++b) mh[b] = ld4(a.h1 + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + lane * 4);
 }
 
 // s_mol <- MoL parameters of step tp1 - 1; then s_in <- the input of step tp1 (sampled, or
 // the teacher value); block 0 of the tile records the sample and the input.
 __device__ void mol_finish(const WnArgs& a, int tp1, int wave, int lane, int b0, int nb, const f32x4 (&mw)[kMolRows],
-                           const f32x4 (&mh)[kUB], float* s_mol, float* s_in) {
+                           const f32x4 (*s_h1)[64], float* s_mol, const float* s_gum, float* s_in) {
   const int tp = tp1 - 1;
   if (tp >= 0) {
     const float* b2 = head_base(a) + (int64_t)a.S * a.S + a.S + (int64_t)a.NO * a.S;
@@ -312,41 +347,47 @@ __device__ void mol_finish(const WnArgs& a, int tp1, int wave, int lane, int b0,
       const int r = wave + q * (kGW + kRW);
       float acc[kUB];
 #pragma unroll
-      for (int b = 0; b < kUB; ++b) acc[b] = dot4(mw[q], mh[b], 0.f);
+      for (int b = 0; b < kUB; ++b) acc[b] = dot4(mw[q], s_h1[b][lane], 0.f);
       if (r < a.NO) {  // wave-uniform
         const float v = wave_reduce_multi<kUB>(acc, lane);
         if ((lane & (64 / kUB - 1)) == 0) s_mol[(lane / (64 / kUB)) * kMaxNO + r] = v + b2[r];
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   if ((int)threadIdx.x < nb) {
     const int b = threadIdx.x;
     const int gb = b0 + b;
     float in_v = 0.f;
     float smp = 0.f;
-    if (tp >= 0) smp = mol_sample(s_mol + b * kMaxNO, a.NO / 3, tp, a.utt_base + gb, a);
+    if (tp >= 0) smp = mol_pick(s_mol + b * kMaxNO, a.NO / 3, s_gum + b * 16, s_gum[b * 16 + 10], a.log_scale_min);
     if (a.teacher != nullptr && tp1 < a.teacher_len) in_v = a.teacher[(int64_t)gb * a.teacher_len + tp1];
     else if (tp >= 0) in_v = smp;
     s_in[b] = in_v;
-    if (blockIdx.x == 0) {
-      if (tp1 < a.T) a.yin[(int64_t)gb * a.T + tp1] = in_v;
-      if (tp >= 0) {
-        a.y_out[(int64_t)gb * a.T + tp] = smp;
-        if (a.mol_out)
-          for (int j = 0; j < a.NO; ++j) a.mol_out[((int64_t)gb * a.T + tp) * a.NO + j] = s_mol[b * kMaxNO + j];
-      }
+    if (blockIdx.x == 0 && tp >= 0) {
+      a.y_out[(int64_t)gb * a.T + tp] = smp;
+      if (a.mol_out)
+        for (int j = 0; j < a.NO; ++j) a.mol_out[((int64_t)gb * a.T + tp) * a.NO + j] = s_mol[b * kMaxNO + j];
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 template <bool L0>
-__global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int layer, int slot, int targ) {
+__global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int layer, int slot, int prow, int targ) {
+  // slot: ring slot of this sample step (t & (RING-1)); prow: its row in the conditioning
+  // chunk (t % Tch); targ: t for direct launches, -1 under graph replay (layer 0 then reads
+  // the step counter)
   __shared__ float s_mol[L0 ? kUB * kMaxNO : 1];
+  __shared__ float s_gum[L0 ? kUB * 16 : 1];
   __shared__ float s_in[kUB];
+  __shared__ f32x4 s_h1[L0 ? kUB : 1][64];
   __shared__ float s_red[kGW][2 * kRP * kUB];
-  if (WN_ABLATE == 5 || WN_ABLATE == 9 || (WN_ABLATE == 8 && !L0)) return;
+  __shared__ int s_arrived;
+#if WN_STAMP
+  unsigned long long st[kStampN] = {};
+  st[0] = WN_NOW();
+#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kUB;
   const int nb = min(kUB, a.B - b0);
@@ -354,48 +395,74 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   const int o0 = blockIdx.x * kRP;          // first gate pair of the workgroup
   const int KX = gate_width(a);
   const int KT = (a.K - 1) * a.R;           // end of the ring taps
+  const int d = 1 << (layer % a.lps);
   const float* base = layer_base(a, layer);
   const float* gprev = L0 ? nullptr : gbuf_of(a, layer - 1);
   auto urow = [&](int b) { return (int64_t)(b0 + (b < nb ? b : 0)); };
   auto wrow = [&](int r) { return o0 + (r >> 1) + (r & 1) * H; };   // gate row r of the workgroup
 
-  // ---------------- prologue part 1: every load that does not depend on the step
-  // gate waves: the first chunk's weights (and, for the g_(l-1) chunk, its inputs: gbuf is
-  // addressed by the layer only)
+  // inputs of GEMV chunk kc (k = kc + lane*4) for the kUB utterances; false = the chunk
+  // contributes nothing (layer 0's g_(l-1) block has zero weights; its current tap is the
+  // sampled input, built after the draw)
+  auto load_x = [&](int kc, f32x4 (&x)[kUB]) -> bool {
+    const int k = kc + lane * 4;
+    const float* xr;
+    if (kc < KT) {                          // ring taps 0..K-2 (zero-initialised before t = 0)
+      const int tap = kc / a.R;
+      xr = ring_row(a, layer, (slot - (a.K - 1 - tap) * d) & (a.RING - 1)) + (k - tap * a.R);
+    } else if (kc < KT + H) {               // g_(l-1)
+      if (L0) return false;
+#pragma unroll
+      for (int b = 0; b < kUB; ++b) x[b] = ld4(gprev + urow(b) * H + (k - KT));
+      return true;
+    } else {                                // current tap x_(l-1)(t)
+      if (L0) return false;
+      xr = ring_row(a, layer - 1, slot) + (k - KT - H);
+    }
+#pragma unroll
+    for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
+    return true;
+  };
+
+  // ---------------- prologue: every load of the launch, none waits for another
   const int c0 = wave;
   const bool gate = wave < kGW && c0 * 256 < KX;
   const int kc0 = c0 * 256;
-  const int cat0 = kc0 < KT ? 0 : (kc0 < KT + H ? 1 : 2);    // 0 ring taps, 1 g_(l-1), 2 current tap
+  const bool cur0 = L0 && kc0 >= KT + H;    // layer 0's current-tap chunk: x_0(t) from the draw
   f32x4 w0[2 * kRP], x0[kUB], fw0 = {}, fb0 = {};
+  bool live0 = false;
   if (gate) {
 #pragma unroll
-    for (int r = 0; r < 2 * kRP; ++r) {
-      if ((WN_ABLATE == 3 || WN_ABLATE == 6) && !L0) w0[r] = f32x4{0.01f * lane, 0.f, 0.f, 0.f};
-      else w0[r] = ld4(base + (int64_t)wrow(r) * KX + kc0 + lane * 4);
-    }
-    if (cat0 == 1 && !L0) {
-#pragma unroll
-      for (int b = 0; b < kUB; ++b) x0[b] = ld4(gprev + urow(b) * H + (kc0 - KT) + lane * 4);
-    }
-    if ((L0 && cat0 != 1) || (!L0 && layer == 1 && cat0 == 2)) {     // x_0 = first_conv(input)
-      const int i = (cat0 == 0 ? kc0 % a.R : kc0 - KT - H) + lane * 4;
+    for (int r = 0; r < 2 * kRP; ++r) w0[r] = ld4(base + (int64_t)wrow(r) * KX + kc0 + lane * 4);
+    live0 = load_x(kc0, x0);
+    if (L0) {                               // (unconditional in the wave: no register shuffle
+      const int i = (cur0 ? kc0 - KT - H : 0) + lane * 4;   //  that would drain the loads)
       fw0 = ld4(a.packed + i);
       fb0 = ld4(a.packed + a.R + i);
+      live0 = live0 || cur0;
     }
   }
-  // residual waves (layer l-1's x_l(t) and skip rows): weights, biases, skip accumulator, g
+  // conditioning pre-activations of the epilogue lanes (gate rows 2fp, 2fp+1 x utterance fb)
+  const int fp = (lane / kUB) % kRP, fb = lane % kUB;
+  float pre_a = 0.f, pre_b = 0.f;
+  if (wave < kGW && lane < kRP * kUB) {
+    const float* pr = a.pre + ((int64_t)prow * a.B + urow(fb)) * ((int64_t)a.n_layers * a.G) + (int64_t)layer * a.G;
+    pre_a = pr[wrow(2 * fp)];
+    pre_b = pr[wrow(2 * fp + 1)];
+  }
+  // residual waves (layer l-1's x_l(t) and skip rows): weights, biases, g, skip, residual input
   const int rx = a.R / H, nrp = rx + a.S / H;            // residual rows per gate pair
   const int lp = layer - 1;
   const float* pbase = L0 ? nullptr : layer_base(a, lp) + (int64_t)a.G * KX;
   const float* pbias = L0 ? nullptr : pbase + (int64_t)(a.R + a.S) * H;
   const int rwave = wave - kGW;
-  const bool resid = !L0 && rwave >= 0 && WN_ABLATE != 4 && WN_ABLATE != 6;
+  const bool resid = !L0 && rwave >= 0;
   // after the butterfly, lane L (L % 4 == 0) holds sum index L/4 = q*kUB + b
   const int my_q = (lane >> 2) / kUB, my_b = (lane >> 2) % kUB;
   const int my_gb = b0 + (my_b < nb ? my_b : 0);
   f32x4 rw[kResRows], rg[kUB];
   int myrow = 0;
-  float rbias = 0.f, rskip = 0.f;
+  float rbias = 0.f, rskip = 0.f, rres = 0.f;
   if (resid) {
 #pragma unroll
     for (int q = 0; q < kResRows; ++q) {
@@ -409,76 +476,54 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
 #pragma unroll
     for (int b = 0; b < kUB; ++b) rg[b] = ld4(gbuf_of(a, lp) + urow(b) * H + lane * 4);
     rbias = pbias[myrow];
-    if (myrow >= a.R) rskip = a.skip[(int64_t)my_gb * a.S + (myrow - a.R)];
+    // both loads issued unconditionally (a branch here made the compiler drain the loads
+    // in flight before the barrier below)
+    const bool xrow = myrow < a.R;
+    rskip = a.skip[(int64_t)my_gb * a.S + (xrow ? 0 : myrow - a.R)];
+    rres = ring_row(a, lp, slot)[(int64_t)my_gb * a.R + (xrow ? myrow : 0)];
   }
   // layer 0: the MoL head of the previous step (weights and h1)
-  f32x4 mw[kMolRows], mh[kUB];
-  if (L0) mol_load(a, wave, lane, b0, nb, mw, mh);
-
-  // ---------------- prologue part 2: the step, and every load addressed by it
-  const int t = read_step(a, slot, 0, targ);
-  const int slot_t = t & (a.RING - 1);
-  const int d = 1 << (layer % a.lps);
-  float pre_v = 0.f;            // conditioning pre-activation of (gate row, utterance) threadIdx.x
-  if ((int)threadIdx.x < 2 * kRP * kUB) {
-    const int r = threadIdx.x / kUB, b = threadIdx.x % kUB;
-    pre_v = a.pre[((int64_t)(t % a.Tch) * a.B + urow(b)) * ((int64_t)a.n_layers * a.G) + (int64_t)layer * a.G + wrow(r)];
-  }
-  float rres = 0.f;
-  if (resid && myrow < a.R)
-    rres = lp == 0 ? a.yin[(int64_t)my_gb * a.T + t] * a.packed[myrow] + a.packed[a.R + myrow]
-                   : a.ring[(((int64_t)lp * a.RING + slot_t) * a.B + my_gb) * a.R + myrow];
-  // first chunk's step-addressed inputs; `live0` false = the chunk contributes nothing
-  bool live0 = gate;
-  if (gate) {
-    if ((WN_ABLATE == 2 || WN_ABLATE == 6) && !L0) {
+  f32x4 mw[kMolRows];
+  int t_abs = 0;
+  if (L0) {
+    mol_load(a, wave, lane, mw);
+    if (wave == kGW + kRW - 1) {
+      // the last wave has no residual rows in layer 0: it stages h1 in LDS and, while h1 is
+      // in flight, draws the sampling noise (lane 16 b + j)
+      f32x4 h[kUB];
 #pragma unroll
-      for (int b = 0; b < kUB; ++b) x0[b] = f32x4{0.5f, 0.25f, 0.f, (float)b};
-    } else if (cat0 == 0) {                      // ring taps 0..K-2 of x_l
-      const int tap = kc0 / a.R;
-      const int tau = t - (a.K - 1 - tap) * d;
-      live0 = tau >= 0;                          // zero history before the first sample
-      if (live0) {
-        if (L0) {
+      for (int b = 0; b < kUB; ++b) h[b] = ld4(a.h1 + urow(b) * a.S + lane * 4);
+      t_abs = abs_step(a, targ);
+      static_assert(kUB * 16 <= 64, "one noise lane per (utterance, index)");
+      const int b = lane >> 4, j = lane & 15;
+      if (t_abs >= 1 && b < nb && (j < a.NO / 3 || j == 10)) s_gum[lane] = mol_noise(j, t_abs - 1, a.utt_base + b0 + b, a);
 #pragma unroll
-          for (int b = 0; b < kUB; ++b) {
-            const float in_v = a.yin[urow(b) * a.T + tau];
-            x0[b] = f32x4{in_v * fw0[0] + fb0[0], in_v * fw0[1] + fb0[1], in_v * fw0[2] + fb0[2],
-                          in_v * fw0[3] + fb0[3]};
-          }
-        } else {
-          const float* xr = a.ring + ((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B * a.R +
-                            (kc0 - tap * a.R) + lane * 4;
-#pragma unroll
-          for (int b = 0; b < kUB; ++b) x0[b] = ld4(xr + urow(b) * a.R);
-        }
-      }
-    } else if (cat0 == 1) {
-      live0 = !L0;                               // layer 0: zero weights there, skipped
-    } else if (!L0) {                            // current tap x_(l-1)(t)
-      if (layer == 1) {
-#pragma unroll
-        for (int b = 0; b < kUB; ++b) {
-          const float in_v = a.yin[urow(b) * a.T + t];
-          x0[b] = f32x4{in_v * fw0[0] + fb0[0], in_v * fw0[1] + fb0[1], in_v * fw0[2] + fb0[2],
-                        in_v * fw0[3] + fb0[3]};
-        }
-      } else {
-        const float* xr = a.ring + ((int64_t)(layer - 1) * a.RING + slot_t) * a.B * a.R + (kc0 - KT - H) + lane * 4;
-#pragma unroll
-        for (int b = 0; b < kUB; ++b) x0[b] = ld4(xr + urow(b) * a.R);
-      }
+      for (int q = 0; q < kUB; ++q) s_h1[q][lane] = h[q];
     }
   }
+  if (threadIdx.x == 0) s_arrived = 0;
+  lds_barrier();                            // (layer >= 1: the loads above stay in flight)
+#if WN_STAMP
+  st[1] = WN_NOW();
+  if (gate) { const float xf = x0[0][0] + x0[kUB - 1][3] + w0[0][0] + w0[2 * kRP - 1][3] + pre_a; WN_AFTER(xf); }
+  if (resid) { const float xf = rres + rg[0][0] + rw[0][0] + rskip; WN_AFTER(xf); }
+  st[2] = WN_NOW();
+#endif
 
-  // ---------------- layer 0: sample the previous step's output; its x_0(t) is the current tap
+  // ---------------- layer 0: sample the previous step's output; x_0(t) is its current tap
   if (L0) {
-    mol_finish(a, t, wave, lane, b0, nb, mw, mh, s_mol, s_in);
-    if (gate && cat0 == 2) {
+    const int t = abs_step(a, targ);
+    (void)t_abs;
+    mol_finish(a, t, wave, lane, b0, nb, mw, s_h1, s_mol, s_gum, s_in);
+    if (gate && cur0) {
 #pragma unroll
       for (int b = 0; b < kUB; ++b) {
-        const float in_v = s_in[b];
+        const float in_v = s_in[b < nb ? b : 0];
         x0[b] = f32x4{in_v * fw0[0] + fb0[0], in_v * fw0[1] + fb0[1], in_v * fw0[2] + fb0[2], in_v * fw0[3] + fb0[3]};
+      }
+      if (blockIdx.x == 0) {                // x_0(t) into ring 0: the later taps, layer 1's inputs
+        float* xr = ring_row(a, 0, slot) + (kc0 - KT - H) + lane * 4;
+        for (int b = 0; b < nb; ++b) *reinterpret_cast<f32x4*>(xr + (int64_t)(b0 + b) * a.R) = x0[b];
       }
     }
   }
@@ -496,53 +541,51 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
     }
     for (int c = c0 + kGW; c * 256 < KX; c += kGW) {
       const int kc = c * 256;
-      const int k = kc + lane * 4;
       f32x4 x[kUB];
-      if (kc < KT) {
-        const int tap = kc / a.R;
-        const int tau = t - (a.K - 1 - tap) * d;
-        if (tau < 0) continue;
-        const int i = k - tap * a.R;
-        if (L0) {
-          const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
+      if (L0 && kc >= KT + H) {
+        const int i = kc - KT - H + lane * 4;
+        const f32x4 fw = ld4(a.packed + i), fb4 = ld4(a.packed + a.R + i);
 #pragma unroll
-          for (int b = 0; b < kUB; ++b) {
-            const float in_v = a.yin[urow(b) * a.T + tau];
-            x[b] = f32x4{in_v * fw[0] + fb[0], in_v * fw[1] + fb[1], in_v * fw[2] + fb[2], in_v * fw[3] + fb[3]};
-          }
-        } else {
-          const float* xr = a.ring + ((int64_t)layer * a.RING + (tau & (a.RING - 1))) * a.B * a.R + i;
-#pragma unroll
-          for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
+        for (int b = 0; b < kUB; ++b) {
+          const float in_v = s_in[b < nb ? b : 0];
+          x[b] = f32x4{in_v * fw[0] + fb4[0], in_v * fw[1] + fb4[1], in_v * fw[2] + fb4[2], in_v * fw[3] + fb4[3]};
         }
-      } else if (kc < KT + H) {
-        if (L0) continue;
-#pragma unroll
-        for (int b = 0; b < kUB; ++b) x[b] = ld4(gprev + urow(b) * H + (k - KT));
-      } else {
-        const int i = k - KT - H;
-        if (L0 || layer == 1) {
-          const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + a.R + i);
-#pragma unroll
-          for (int b = 0; b < kUB; ++b) {
-            const float in_v = L0 ? s_in[b] : a.yin[urow(b) * a.T + t];
-            x[b] = f32x4{in_v * fw[0] + fb[0], in_v * fw[1] + fb[1], in_v * fw[2] + fb[2], in_v * fw[3] + fb[3]};
-          }
-        } else {
-          const float* xr = a.ring + ((int64_t)(layer - 1) * a.RING + slot_t) * a.B * a.R + i;
-#pragma unroll
-          for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
+        if (blockIdx.x == 0) {
+          float* xr = ring_row(a, 0, slot) + i;
+          for (int b = 0; b < nb; ++b) *reinterpret_cast<f32x4*>(xr + (int64_t)(b0 + b) * a.R) = x[b];
         }
+      } else if (!load_x(kc, x)) {
+        continue;
       }
 #pragma unroll
       for (int r = 0; r < 2 * kRP; ++r) {
-        const f32x4 w = ld4(base + (int64_t)wrow(r) * KX + k);
+        const f32x4 w = ld4(base + (int64_t)wrow(r) * KX + kc + lane * 4);
 #pragma unroll
         for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w, x[b], acc[r * kUB + b]);
       }
     }
-    const float s = WN_ABLATE == 7 ? acc[lane & 15] : wave_reduce_multi<2 * kRP * kUB>(acc, lane);
+#if WN_STAMP
+    { const float af = acc[0] + acc[2 * kRP * kUB - 1]; WN_AFTER(af); st[3] = WN_NOW(); }
+#endif
+    const float s = wave_reduce_multi<2 * kRP * kUB>(acc, lane);
     if ((lane & (64 / (2 * kRP * kUB) - 1)) == 0) s_red[wave][lane / (64 / (2 * kRP * kUB))] = s;
+    // the last gate wave to arrive finishes the gate (no barrier with the residual waves)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    int prev = 0;
+    if (lane == 0) prev = atomicAdd(&s_arrived, 1);
+    prev = __shfl(prev, 0);
+#if WN_STAMP
+    st[4] = WN_NOW();
+#endif
+    if (prev == kGW - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (lane < kRP * kUB && fb < nb) {
+        float za = pre_a, zb = pre_b;
+#pragma unroll
+        for (int w = 0; w < kGW; ++w) { za += s_red[w][(2 * fp) * kUB + fb]; zb += s_red[w][(2 * fp + 1) * kUB + fb]; }
+        gbuf_of(a, layer)[(int64_t)(b0 + fb) * H + o0 + fp] = tanhf(za) * avc_sigmoid(zb);
+      }
+    }
   } else if (resid) {
     // layer l-1's residual rows: x_l(t) -> ring l, skip rows -> the skip accumulator
     float acc[kResRows * kUB];
@@ -550,39 +593,46 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
     for (int q = 0; q < kResRows; ++q)
 #pragma unroll
       for (int b = 0; b < kUB; ++b) acc[q * kUB + b] = dot4(rw[q], rg[b], 0.f);
+#if WN_STAMP
+    { const float af = acc[0]; WN_AFTER(af); st[3] = WN_NOW(); }
+#endif
     const float v0 = wave_reduce_multi<kResRows * kUB>(acc, lane);
     const int j = rwave + my_q * kRW;
     if ((lane & 3) == 0 && j < kRP * nrp && my_b < nb) {
       const int gb = b0 + my_b;
       const float v = v0 + rbias;
       if (myrow < a.R) {
-        a.ring[(((int64_t)layer * a.RING + slot_t) * a.B + gb) * a.R + myrow] = (v + rres) * kSqrtHalf;
+        ring_row(a, layer, slot)[(int64_t)gb * a.R + myrow] = (v + rres) * kSqrtHalf;
       } else {
         float* sp = a.skip + (int64_t)gb * a.S + (myrow - a.R);
         if (lp == 0) *sp = v;
         else *sp = a.legacy ? (rskip + v) * kSqrtHalf : (rskip + v);
       }
     }
+#if WN_STAMP
+    st[4] = WN_NOW();
+#endif
   }
-  // pre-activations: lane r*kUB + b of wave 0 holds gate row r's; the pair's two rows are
-  // fetched by whole-wave shuffles (every lane active) before the final branch
-  const int fp = (lane / kUB) % kRP, fb = lane % kUB;
-  const float pre_a = __shfl(pre_v, (2 * fp) * kUB + fb);
-  const float pre_b = __shfl(pre_v, (2 * fp + 1) * kUB + fb);
-  __syncthreads();
-  if ((int)threadIdx.x < kRP * kUB && fb < nb) {
-    float za = pre_a, zb = pre_b;
-#pragma unroll
-    for (int w = 0; w < kGW; ++w) { za += s_red[w][(2 * fp) * kUB + fb]; zb += s_red[w][(2 * fp + 1) * kUB + fb]; }
-    gbuf_of(a, layer)[(int64_t)(b0 + fb) * H + o0 + fp] = tanhf(za) * avc_sigmoid(zb);
+#if WN_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  st[6] = WN_NOW();
+  if (lane == 0 && (wave == 0 || wave == kGW)) {
+    if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1))) {
+      const int wg = blockIdx.x + blockIdx.y * gridDim.x;
+      unsigned long long* o = g_wn_stamp + ((int64_t)(layer * 2 + (wave == kGW)) * kStampWG + wg) * kStampN;
+      for (int i = 0; i < kStampN; ++i) o[i] = st[i];
+    }
   }
+#endif
 }
 
 // tail: the last layer's skip rows, one wave per row.  Every operand (weights, g, the skip
 // accumulator) is loaded before the step counter is touched (the tail only forwards it).
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, int targ) {
-  if (WN_ABLATE == 5 || WN_ABLATE == 10) return;
+__global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot) {
+#if WN_STAMP
+  const unsigned long long st0 = WN_NOW();
+#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
@@ -607,8 +657,15 @@ __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, in
 #pragma unroll
     for (int b = 0; b < kBT; ++b) acc[b] = dot4(wv, g[b], acc[b]);
   }
-  read_step(a, slot, 0, targ);
   const float s = wave_reduce_multi<kBT>(acc, lane);
+#if WN_STAMP
+  if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1)) && lane == 0) {
+    WN_AFTER(s);
+    unsigned long long* o = g_wn_stamp + ((int64_t)(2 * a.n_layers) * kStampWG + blockIdx.x + blockIdx.y * gridDim.x) * kStampN;
+    o[0] = st0; o[6] = WN_NOW();
+  }
+#endif
+  (void)slot;
   if ((lane & 7) != 0 || blockIdx.x * NW + wave >= a.S) return;
   const int b = lane >> 3;
   if (b >= nb) return;
@@ -621,7 +678,9 @@ __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot, in
 // head: h1 = relu(W1 relu(skips) + b1); advances the step counter.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, int targ) {
-  if (WN_ABLATE == 5 || WN_ABLATE == 10) return;
+#if WN_STAMP
+  const unsigned long long st0 = WN_NOW();
+#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
@@ -644,8 +703,16 @@ __global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, in
       acc[b] = dot4(wv, x[b], acc[b]);
     }
   }
-  read_step(a, slot, 1, targ);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[0] = abs_step(a, targ) + 1;
   const float s = wave_reduce_multi<kBT>(acc, lane);
+#if WN_STAMP
+  if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1)) && lane == 0) {
+    WN_AFTER(s);
+    unsigned long long* o = g_wn_stamp + ((int64_t)(2 * a.n_layers + 1) * kStampWG + blockIdx.x + blockIdx.y * gridDim.x) * kStampN;
+    o[0] = st0; o[6] = WN_NOW();
+  }
+#endif
+  (void)slot;
   if ((lane & 7) != 0 || blockIdx.x * NW + wave >= a.S) return;
   const int b = lane >> 3;
   if (b >= nb) return;
@@ -714,6 +781,8 @@ __global__ __launch_bounds__(256) void wn_upsample_kernel(UpArgs u, const float*
 struct GraphKey {
   WnArgs a;
   int steps;
+  int slot0;      // ring slot of the graph's first step
+  int prow0;      // conditioning row of the graph's first step
   int device;
   bool operator<(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
@@ -722,29 +791,34 @@ std::map<GraphKey, hipGraphExec_t> g_graphs;
 std::vector<GraphKey> g_order;
 hipStream_t g_capture_stream[64] = {};
 
-int enqueue_step(const WnArgs& a, hipStream_t s, int targ) {
+// one sample step: ring slot, conditioning row, and t (direct launch) or -1 (graph replay)
+int enqueue_step(const WnArgs& a, hipStream_t s, int slot, int prow, int targ) {
   const int H = a.G / 2;
   const int nbt = (a.B + kBT - 1) / kBT;
   const dim3 lgrid(H / kRP, (a.B + kUB - 1) / kUB);
   for (int l = 0; l < a.n_layers; ++l) {
-    if (l == 0) hipLaunchKernelGGL((wn_layer_kernel<true>), lgrid, dim3(kLayerThreads), 0, s, a, 0, 0, targ);
-    else hipLaunchKernelGGL((wn_layer_kernel<false>), lgrid, dim3(kLayerThreads), 0, s, a, l, l, targ);
+    if (l == 0) hipLaunchKernelGGL((wn_layer_kernel<true>), lgrid, dim3(kLayerThreads), 0, s, a, 0, slot, prow, targ);
+    else hipLaunchKernelGGL((wn_layer_kernel<false>), lgrid, dim3(kLayerThreads), 0, s, a, l, slot, prow, targ);
   }
   hipLaunchKernelGGL((wn_tail_kernel<kTailWaves>), dim3((a.S + kTailWaves - 1) / kTailWaves, nbt),
-                     dim3(64 * kTailWaves), 0, s, a, a.n_layers, targ);
+                     dim3(64 * kTailWaves), 0, s, a, slot);
   hipLaunchKernelGGL((wn_head_kernel<kTailWaves>), dim3((a.S + kTailWaves - 1) / kTailWaves, nbt),
-                     dim3(64 * kTailWaves), 0, s, a, a.n_layers + 1, targ);
+                     dim3(64 * kTailWaves), 0, s, a, slot, targ);
   AVC_CHECK_LAUNCH("autovc_wavenet_generate_f32");
   return avc::kOk;
 }
 
-int get_graph(const WnArgs& a, int steps, hipGraphExec_t* out) {
+// a graph of `steps` sample steps starting at ring slot slot0 and conditioning row prow0:
+// every kernel argument is static (slot (slot0 + i) & (RING-1), row prow0 + i)
+int get_graph(const WnArgs& a, int steps, int slot0, int prow0, hipGraphExec_t* out) {
   int dev = 0;
   AVC_HIP(hipGetDevice(&dev), "hipGetDevice");
   GraphKey key;
   memset(&key, 0, sizeof(key));
   key.a = a;
   key.steps = steps;
+  key.slot0 = slot0;
+  key.prow0 = prow0;
   key.device = dev;
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_graphs.find(key);
@@ -754,7 +828,7 @@ int get_graph(const WnArgs& a, int steps, hipGraphExec_t* out) {
   hipStream_t cs = g_capture_stream[dev];
   AVC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
   int rc = avc::kOk;
-  for (int i = 0; i < steps && rc == avc::kOk; ++i) rc = enqueue_step(a, cs, -1);
+  for (int i = 0; i < steps && rc == avc::kOk; ++i) rc = enqueue_step(a, cs, (slot0 + i) & (a.RING - 1), prow0 + i, -1);
   hipGraph_t graph = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &graph);
   if (rc != avc::kOk) { if (graph) (void)hipGraphDestroy(graph); return rc; }
@@ -763,7 +837,7 @@ int get_graph(const WnArgs& a, int steps, hipGraphExec_t* out) {
   const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   AVC_HIP(ei, "hipGraphInstantiate");
-  if (g_order.size() >= 8) {  // bounded cache: drop the oldest graph
+  if (g_order.size() >= 16) {  // bounded cache: drop the oldest graph
     auto old = g_graphs.find(g_order.front());
     if (old != g_graphs.end()) { (void)hipGraphExecDestroy(old->second); g_graphs.erase(old); }
     g_order.erase(g_order.begin());
@@ -785,6 +859,29 @@ int64_t ring_frames(int n_layers, int lps, int K) {
 }  // namespace
 
 extern "C" {
+
+#if WN_STAMP
+// Diagnostic build only: choose the sample step to record (-1 = none) / copy the stamps out
+// ([launch slot = 2 layer + (residual wave), tail 2L, head 2L+1][workgroup][stamp]).
+int autovc_wavenet_stamp_set(int t) {
+  AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wn_stamp_t), &t, sizeof(int)), "hipMemcpyToSymbol");
+  static const unsigned long long zero[1024] = {};
+  for (size_t off = 0; off < sizeof(g_wn_stamp); off += sizeof(zero))
+    AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wn_stamp), zero, std::min(sizeof(zero), sizeof(g_wn_stamp) - off), off),
+            "hipMemcpyToSymbol");
+  return avc::kOk;
+}
+int autovc_wavenet_stamps(unsigned long long* host, int64_t n) {
+  if (n * sizeof(unsigned long long) > sizeof(g_wn_stamp)) return avc::kErrArg;
+  AVC_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wn_stamp), n * sizeof(unsigned long long)), "hipMemcpyFromSymbol");
+  return avc::kOk;
+}
+#endif
+
+int64_t autovc_wavenet_ring_frames(int n_layers, int layers_per_stack, int taps) {
+  if (n_layers <= 0 || layers_per_stack <= 0 || layers_per_stack > 16 || taps <= 0) return -1;
+  return ring_frames(n_layers, layers_per_stack, taps);
+}
 
 int64_t autovc_wavenet_packed_floats(int n_layers, int taps, int R, int G, int S, int n_out) {
   if (n_layers <= 0 || taps <= 0 || R <= 0 || G <= 0 || S <= 0 || n_out <= 0) return -1;
@@ -855,7 +952,6 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   memset(&a, 0, sizeof(a));
   a.B = B; a.T = T; a.R = R; a.G = G; a.S = S; a.NO = n_out; a.K = taps; a.RING = RING;
   a.n_layers = n_layers; a.lps = layers_per_stack; a.Tch = Tch; a.legacy = legacy ? 1 : 0;
-  a.n_kern = n_layers + 2;
   a.packed = packed; a.pre = pre;
   a.ring = ws;                 ws += round64((int64_t)(n_layers + 1) * RING * B * R);
   a.yin = ws;                  ws += round64((int64_t)B * T);
@@ -874,16 +970,22 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   if (t0 == 0) AVC_HIP(hipMemsetAsync(workspace, 0, (size_t)used, stream), "hipMemsetAsync");
   hipLaunchKernelGGL(wn_set_ctr_kernel, dim3(1), dim3(1), 0, stream, a.ctr, t0);
   AVC_CHECK_LAUNCH(fn);
+  // graph replays cover runs of graph_steps steps inside the conditioning chunk (a graph
+  // per (ring slot, chunk row) of its first step: callers keep Tch a small multiple of
+  // graph_steps and of the ring, so a few graphs serve every chunk); the rest launch directly
   int t = t0;
-  if (graph_steps > 0 && t1 - t0 >= graph_steps) {
-    hipGraphExec_t exec = nullptr;
-    const int rc = get_graph(a, graph_steps, &exec);
+  while (t < t1) {
+    if (graph_steps > 0 && t + graph_steps <= t1 && t % Tch + graph_steps <= Tch) {
+      hipGraphExec_t exec = nullptr;
+      const int rc = get_graph(a, graph_steps, t & (RING - 1), t % Tch, &exec);
+      if (rc != avc::kOk) return rc;
+      AVC_HIP(hipGraphLaunch(exec, stream), "hipGraphLaunch");
+      t += graph_steps;
+      continue;
+    }
+    const int rc = enqueue_step(a, stream, t & (RING - 1), t % Tch, t);
     if (rc != avc::kOk) return rc;
-    for (; t + graph_steps <= t1; t += graph_steps) AVC_HIP(hipGraphLaunch(exec, stream), "hipGraphLaunch");
-  }
-  for (; t < t1; ++t) {
-    const int rc = enqueue_step(a, stream, t);
-    if (rc != avc::kOk) return rc;
+    ++t;
   }
   if (t1 == T) {
     hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);

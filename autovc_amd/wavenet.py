@@ -291,10 +291,14 @@ class WaveNet(nn.Module):
                              "(incremental_forward asserts c.size(-1) == T)")
         R, G, S = self.residual_channels, self.gate_channels, self.skip_out_channels
         nG = self.layers * G
+        lib = _lib.load()
+        ring = int(lib.autovc_wavenet_ring_frames(self.layers, self.layers_per_stack, self.kernel_size))
+        # the conditioning chunk is lcm(ring, graph_steps) samples: every captured graph then
+        # starts at one of chunk / graph_steps (ring slot, chunk row) pairs, so a few cached
+        # graphs, whose step kernels get both as static arguments, serve the whole sequence
+        graph_steps = int(graph_steps or 0)
         if chunk is None:
-            chunk = max(1, (1 << 30) // (B * nG * 4))
-            if graph_steps and chunk > graph_steps:
-                chunk -= chunk % graph_steps
+            chunk = math.lcm(ring, graph_steps) if graph_steps else max(1, (1 << 30) // (B * nG * 4))
         chunk = min(chunk, T)
         pre = torch.empty(chunk, B, nG, device=dev, dtype=torch.float32)
         y = torch.empty(B, T, device=dev, dtype=torch.float32)
@@ -302,7 +306,7 @@ class WaveNet(nn.Module):
         tch = None
         if teacher is not None:
             tch = teacher.to(dev, torch.float32).reshape(B, -1).contiguous()
-        ws_bytes = _lib.load().autovc_wavenet_workspace_bytes(B, T, self.layers, self.layers_per_stack,
+        ws_bytes = lib.autovc_wavenet_workspace_bytes(B, T, self.layers, self.layers_per_stack,
                                                               self.kernel_size, R, G, S)
         ws = torch.empty((ws_bytes + 3) // 4, device=dev, dtype=torch.float32)
         stream = _lib.stream_ptr(dev)

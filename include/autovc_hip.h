@@ -347,9 +347,17 @@ int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, 
  *   y_out    (B, T) samples; mol_out optional (B, T, n_out) head outputs
  *   workspace autovc_wavenet_workspace_bytes; zeroed by the call with t0 == 0 and carried
  *            to the following chunks
- *   graph_steps > 0 replays a captured hipGraph of that many steps (cached per argument
- *            set); 0 launches the kernels directly.
+ *   graph_steps > 0: runs of that many steps that stay inside one conditioning chunk replay
+ *            a captured hipGraph, one per (ring slot, chunk row) of the run's first step
+ *            (cached, at most 16): every kernel argument of a step, ring slot and
+ *            conditioning row included, is static in it, so no step kernel waits on a
+ *            counter read.  Keep Tch a small multiple of graph_steps and of the ring
+ *            (autovc_amd/wavenet.py: Tch = lcm(ring, graph_steps)) so a few graphs serve
+ *            every chunk.  The other steps, and graph_steps = 0, launch directly.
+ *   autovc_wavenet_ring_frames: frames of the per-layer input rings (power of two >=
+ *            (taps-1) * max dilation + 1).
  */
+int64_t autovc_wavenet_ring_frames(int n_layers, int layers_per_stack, int taps);
 int64_t autovc_wavenet_packed_floats(int n_layers, int taps, int R, int G, int S, int n_out);
 int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_per_stack, int taps,
                                        int R, int G, int S);
