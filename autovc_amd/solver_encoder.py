@@ -169,7 +169,10 @@ class Solver(object):
         scalars (g_loss, loss_id, loss_id_psnt, loss_cd); nothing synchronises.  With
         `hip_graph` the forward+backward is a graph replay (its outputs are the graph's
         static tensors, overwritten by the next step)."""
-        if self.hip_graph:
+        # the captured step is validated (bit-identical to eager, tests/test_solver_gpu.py)
+        # with the weight-gradient side stream only: with AVC_GRAD_STREAM=0 replays gave
+        # run-to-run different losses on the GPU, so that diagnostic mode runs eagerly
+        if self.hip_graph and AF._GRAD_STREAM_ON:
             if self._graphs is None:
                 from .graph import StepGraphs
                 self._graphs = StepGraphs(self._forward_backward, self.G)

@@ -94,6 +94,12 @@ int autovc_gemm_f32(int M, int N, int K,
  * their workgroups are padded so that no more of them share a CU than fit beside that
  * reserve — a latency-bound kernel on another stream keeps a slot on every CU. */
 int autovc_gemm_set_lds_reserve(int bytes);
+/* A stream whose kernels only run on the CUs set in `mask` (n_words 32-bit words, bit i =
+ * CU i as hipExtStreamCreateWithCUMask numbers them): throughput work (weight-gradient
+ * GEMMs) kept off the CUs a latency-bound recurrence on another stream needs.  No
+ * reference counterpart (torch.cuda streams are unmasked). */
+int autovc_stream_create_cu_mask(int n_words, const uint32_t* mask, hipStream_t* out);
+int autovc_stream_destroy(hipStream_t stream);
 /* Same contract, bf16 compute (BASELINE config 3, "bf16 with fp32 master"): the fp32
  * operands are rounded to bf16 (RNE) as they are staged, v_mfma_f32_32x32x16_bf16
  * accumulates in fp32, C / bias / accumulate stay fp32 — the numerics of a torch.autocast
