@@ -517,8 +517,11 @@ def main():
     args = ap.parse_args()
 
     from autovc_amd import ddp
-    rank, world = ddp.init_from_env()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test hook (tests/test_bench_multirank, 1-GPU boxes): every rank on cuda:0 over gloo, to
+    # exercise the N > 1 flow (sharding, barriers, max-over-ranks timing) without 2 GPUs
+    share = os.environ.get("AVC_BENCH_SHARE_DEVICE") == "1"
+    rank, world = ddp.init_from_env(backend="gloo" if share else None)
+    local = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
