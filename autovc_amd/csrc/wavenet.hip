@@ -74,6 +74,7 @@ struct WnArgs {
   float* skip;
   float* h1;
   float* gbuf;
+  float* ptap;       // past-tap products of the next step: (2, n_layers, B, G), by step parity
   int* ctr;
   const float* teacher;
   int teacher_len;
@@ -314,11 +315,13 @@ __device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_
 // step counter is read.
 constexpr int kRP = 2;                    // gate pairs per workgroup
 constexpr int kUB = 4;                    // utterances per workgroup
-constexpr int kGW = 7;                    // gate waves (KX = 1792 = 7 chunks of 256 for r9y9)
+constexpr int kGW = 3;                    // gate waves: the critical GEMV [g_(l-1) | x_(l-1)(t)] is
+                                          // H + R = 768 = 3 chunks of 256 for r9y9
 constexpr int kRW = 2;                    // residual waves
 constexpr int kResRows = 4;               // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
 constexpr int kLayerThreads = 64 * (kGW + kRW);
-constexpr int kTailWaves = 2;             // tail / head: one wave per output row
+constexpr int kTailWaves = 4;             // tail / head: one wave per output row
+constexpr int kPR = 32;                   // past-tap workgroups: gate rows per workgroup
 
 // MoL head output of the previous step for the utterance tile, in two halves so that its
 // loads are issued at kernel start: every wave reads its W2 rows (S == 256: one 4-float
@@ -395,39 +398,33 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   const int o0 = blockIdx.x * kRP;          // first gate pair of the workgroup
   const int KX = gate_width(a);
   const int KT = (a.K - 1) * a.R;           // end of the ring taps
-  const int d = 1 << (layer % a.lps);
   const float* base = layer_base(a, layer);
   const float* gprev = L0 ? nullptr : gbuf_of(a, layer - 1);
   auto urow = [&](int b) { return (int64_t)(b0 + (b < nb ? b : 0)); };
   auto wrow = [&](int r) { return o0 + (r >> 1) + (r & 1) * H; };   // gate row r of the workgroup
 
-  // inputs of GEMV chunk kc (k = kc + lane*4) for the kUB utterances; false = the chunk
-  // contributes nothing (layer 0's g_(l-1) block has zero weights; its current tap is the
-  // sampled input, built after the draw)
+  // inputs of GEMV chunk kc (k = kc + lane*4, kc >= KT: the ring taps 0..K-2 were
+  // multiplied by the previous step's tail/head launches into ptap) for the kUB utterances;
+  // false = the chunk contributes nothing (layer 0's g_(l-1) block has zero weights; its
+  // current tap is the sampled input, built after the draw)
   auto load_x = [&](int kc, f32x4 (&x)[kUB]) -> bool {
     const int k = kc + lane * 4;
-    const float* xr;
-    if (kc < KT) {                          // ring taps 0..K-2 (zero-initialised before t = 0)
-      const int tap = kc / a.R;
-      xr = ring_row(a, layer, (slot - (a.K - 1 - tap) * d) & (a.RING - 1)) + (k - tap * a.R);
-    } else if (kc < KT + H) {               // g_(l-1)
-      if (L0) return false;
+    if (L0) return false;
+    if (kc < KT + H) {                      // g_(l-1)
 #pragma unroll
       for (int b = 0; b < kUB; ++b) x[b] = ld4(gprev + urow(b) * H + (k - KT));
-      return true;
     } else {                                // current tap x_(l-1)(t)
-      if (L0) return false;
-      xr = ring_row(a, layer - 1, slot) + (k - KT - H);
-    }
+      const float* xr = ring_row(a, layer - 1, slot) + (k - KT - H);
 #pragma unroll
-    for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
+      for (int b = 0; b < kUB; ++b) x[b] = ld4(xr + urow(b) * a.R);
+    }
     return true;
   };
 
   // ---------------- prologue: every load of the launch, none waits for another
   const int c0 = wave;
-  const bool gate = wave < kGW && c0 * 256 < KX;
-  const int kc0 = c0 * 256;
+  const bool gate = wave < kGW && KT + c0 * 256 < KX;
+  const int kc0 = KT + c0 * 256;
   const bool cur0 = L0 && kc0 >= KT + H;    // layer 0's current-tap chunk: x_0(t) from the draw
   f32x4 w0[2 * kRP], x0[kUB], fw0 = {}, fb0 = {};
   bool live0 = false;
@@ -447,8 +444,9 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   float pre_a = 0.f, pre_b = 0.f;
   if (wave < kGW && lane < kRP * kUB) {
     const float* pr = a.pre + ((int64_t)prow * a.B + urow(fb)) * ((int64_t)a.n_layers * a.G) + (int64_t)layer * a.G;
-    pre_a = pr[wrow(2 * fp)];
-    pre_b = pr[wrow(2 * fp + 1)];
+    const float* pt = a.ptap + (((int64_t)(slot & 1) * a.n_layers + layer) * a.B + urow(fb)) * a.G;
+    pre_a = pr[wrow(2 * fp)] + pt[wrow(2 * fp)];
+    pre_b = pr[wrow(2 * fp + 1)] + pt[wrow(2 * fp + 1)];
   }
   // residual waves (layer l-1's x_l(t) and skip rows): weights, biases, g, skip, residual input
   const int rx = a.R / H, nrp = rx + a.S / H;            // residual rows per gate pair
@@ -528,7 +526,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
     }
   }
 
-  // ---------------- gate GEMV (first chunk from the prologue; further chunks only when KX > kGW*256)
+  // ---------------- gate GEMV (first chunk from the prologue; further chunks only when KX - KT > kGW*256)
   if (wave < kGW) {
     float acc[2 * kRP * kUB];
 #pragma unroll
@@ -539,8 +537,8 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
 #pragma unroll
         for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w0[r], x0[b], acc[r * kUB + b]);
     }
-    for (int c = c0 + kGW; c * 256 < KX; c += kGW) {
-      const int kc = c * 256;
+    for (int c = c0 + kGW; KT + c * 256 < KX; c += kGW) {
+      const int kc = KT + c * 256;
       f32x4 x[kUB];
       if (L0 && kc >= KT + H) {
         const int i = kc - KT - H + lane * 4;
@@ -626,10 +624,90 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
 #endif
 }
 
-// tail: the last layer's skip rows, one wave per row.  Every operand (weights, g, the skip
-// accumulator) is loaded before the step counter is touched (the tail only forwards it).
+// Past taps of the NEXT sample step: P_l(t+1) = sum_{j < K-1} W_j x_l(t+1 - (K-1-j) d_l), for
+// kPR gate rows of one layer and the kBT-utterance tile.  Every input is known once the
+// last layer of step t has run (x_l(t) is the newest), so the tail and head launches of
+// step t carry this work in extra workgroups (layers [0, L/2) and [L/2, L)), and the 24
+// chain launches of step t+1 fetch only the current-tap blocks: their per-CU operand fill
+// (the launch's bound) drops from 73 to 41 KB, while these workgroups stream
+// 32 rows x 4 KB of weights in large, latency-tolerant batches.  Each wave takes 256-deep
+// chunks of the (K-1)*R taps on MFMA tiles (a 64-value butterfly per 8 rows took 2.5 us per
+// group); the workgroup sums the waves' partials in LDS.
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot) {
+__device__ void past_taps(const WnArgs& a, int l_lo, int idx, int slot) {
+  // v_mfma_f32_16x16x4_f32 tiles: A = 16 weight rows x 4 k (lane l: row l % 16, k group
+  // l / 16), B = 4 k x 16 utterance columns (8 real, 8 clamped and dropped).  Each lane
+  // loads 4 consecutive k of its row / utterance; element j of those feeds MFMA j, so the
+  // four MFMAs of an iteration cover 16 k (the same k order for A and B).
+  static_assert(kBT == 8 && kPR == 32, "past-tap tiling: 2 x 16 rows, 8 utterances");
+  __shared__ float s_part[NW][kPR][kBT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rblocks = a.G / kPR;
+  const int layer = l_lo + idx / rblocks;
+  const int row0 = (idx % rblocks) * kPR;
+  const int b0 = blockIdx.y * kBT;
+  const int nb = min(kBT, a.B - b0);
+  const int KT = (a.K - 1) * a.R, KX = gate_width(a);
+  const int d = 1 << (layer % a.lps);
+  const int sn = (slot + 1) & (a.RING - 1);           // ring slot of step t+1
+  const float* base = layer_base(a, layer);
+  const int m = lane & 15, q = lane >> 4;
+  const int ub = b0 + ((m & 7) < nb ? (m & 7) : 0);   // utterance of B column m (8..15: dropped)
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int c = wave; c * 256 < KT; c += NW) {
+    const int kc = c * 256, tap = kc / a.R;
+    const float* xr = ring_row(a, layer, (sn - (a.K - 1 - tap) * d) & (a.RING - 1)) + (int64_t)ub * a.R +
+                      (kc - tap * a.R) + 4 * q;
+    const float* w0 = base + (int64_t)(row0 + m) * KX + kc + 4 * q;
+    const float* w1 = w0 + (int64_t)16 * KX;
+    // every load of the chunk in flight before the first MFMA (48 x 16 B per lane): the
+    // workgroup is bound by how many bytes its CU has requested, not by the MFMAs
+    f32x4 xv[16], wa[16], wb[16];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      xv[it] = ld4(xr + it * 16);
+      wa[it] = ld4(w0 + it * 16);
+      wb[it] = ld4(w1 + it * 16);
+    }
+    __builtin_amdgcn_sched_barrier(0);      // keep the scheduler from sinking loads to their uses
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[it][j], xv[it][j], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[it][j], xv[it][j], acc1, 0, 0, 0);
+      }
+    }
+  }
+  // C layout: lane l holds rows 4 (l / 16) + v (v = 0..3) of column l % 16
+  if (m < kBT) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      s_part[wave][4 * q + v][m] = acc0[v];
+      s_part[wave][16 + 4 * q + v][m] = acc1[v];
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < kPR * kBT; j += 64 * NW) {
+    const int r = j >> 3, b = j & 7;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += s_part[w][r][b];
+    if (b < nb) a.ptap[(((int64_t)(sn & 1) * a.n_layers + layer) * a.B + b0 + b) * a.G + row0 + r] = v;
+  }
+}
+
+__host__ __device__ inline int past_tap_blocks(const WnArgs& a, int n_layers_part) { return n_layers_part * (a.G / kPR); }
+
+// tail: the last layer's skip rows, one wave per row (workgroups x < ceil(S/NW)); the
+// workgroups above carry past_taps for layers [0, L/2).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void wn_tail_kernel(WnArgs a, int slot) {
+  const int own = (a.S + NW - 1) / NW;
+  if ((int)blockIdx.x >= own) {
+    past_taps<NW>(a, 0, blockIdx.x - own, slot);
+    return;
+  }
 #if WN_STAMP
   const unsigned long long st0 = WN_NOW();
 #endif
@@ -675,9 +753,15 @@ __global__ __launch_bounds__(64 * NW) void wn_tail_kernel(WnArgs a, int slot) {
   else *sp = a.legacy ? (sk + v) * kSqrtHalf : (sk + v);
 }
 
-// head: h1 = relu(W1 relu(skips) + b1); advances the step counter.
+// head: h1 = relu(W1 relu(skips) + b1); advances the step counter; the workgroups above
+// ceil(S/NW) carry past_taps for layers [L/2, L).
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void wn_head_kernel(WnArgs a, int slot, int targ) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void wn_head_kernel(WnArgs a, int slot, int targ) {
+  const int own = (a.S + NW - 1) / NW;
+  if ((int)blockIdx.x >= own) {
+    past_taps<NW>(a, a.n_layers / 2, blockIdx.x - own, slot);
+    return;
+  }
 #if WN_STAMP
   const unsigned long long st0 = WN_NOW();
 #endif
@@ -800,9 +884,10 @@ int enqueue_step(const WnArgs& a, hipStream_t s, int slot, int prow, int targ) {
     if (l == 0) hipLaunchKernelGGL((wn_layer_kernel<true>), lgrid, dim3(kLayerThreads), 0, s, a, 0, slot, prow, targ);
     else hipLaunchKernelGGL((wn_layer_kernel<false>), lgrid, dim3(kLayerThreads), 0, s, a, l, slot, prow, targ);
   }
-  hipLaunchKernelGGL((wn_tail_kernel<kTailWaves>), dim3((a.S + kTailWaves - 1) / kTailWaves, nbt),
+  const int own = (a.S + kTailWaves - 1) / kTailWaves;
+  hipLaunchKernelGGL((wn_tail_kernel<kTailWaves>), dim3(own + past_tap_blocks(a, a.n_layers / 2), nbt),
                      dim3(64 * kTailWaves), 0, s, a, slot);
-  hipLaunchKernelGGL((wn_head_kernel<kTailWaves>), dim3((a.S + kTailWaves - 1) / kTailWaves, nbt),
+  hipLaunchKernelGGL((wn_head_kernel<kTailWaves>), dim3(own + past_tap_blocks(a, a.n_layers - a.n_layers / 2), nbt),
                      dim3(64 * kTailWaves), 0, s, a, slot, targ);
   AVC_CHECK_LAUNCH("autovc_wavenet_generate_f32");
   return avc::kOk;
@@ -894,7 +979,8 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
                                        int S) {
   if (B <= 0 || T <= 0 || n_layers <= 0 || layers_per_stack <= 0 || taps <= 0) return -1;
   const int64_t ring = (int64_t)(n_layers + 1) * ring_frames(n_layers, layers_per_stack, taps) * B * R;
-  const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + 2 * (int64_t)B * (G / 2) + 5 * 64;
+  const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + 2 * (int64_t)B * (G / 2) +
+                         2 * (int64_t)n_layers * B * G + 6 * 64;
   return floats * 4 + kCtrSlots * 4 + 256;
 }
 
@@ -958,6 +1044,7 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   a.skip = ws;                 ws += round64((int64_t)B * S);
   a.h1 = ws;                   ws += round64((int64_t)B * S);
   a.gbuf = ws;                 ws += round64(2 * (int64_t)B * (G / 2));
+  a.ptap = ws;                 ws += round64(2 * (int64_t)n_layers * B * G);
   a.ctr = reinterpret_cast<int*>(ws);
   a.teacher = teacher; a.teacher_len = teacher ? teacher_len : 0;
   a.y_out = y_out; a.mol_out = mol_out;
