@@ -1,6 +1,6 @@
 """Timeline of one WaveNet sample step from the WN_STAMP diagnostic library (tools/wn_stamps.sh):
 per launch the first/last workgroup start and end, and the median per-workgroup phase
-durations (entry -> step known -> first operands in -> products done -> barrier -> stored).
+durations (entry -> start barrier -> operands in -> products done -> arrived -> stored).
 Not part of the product."""
 import ctypes
 import os
@@ -36,7 +36,7 @@ for rep in range(2):
     t0 = min(a[k][a[k][:, 0] > 0][:, 0].min() for k in range(2 * nl + 2) if (a[k][:, 0] > 0).any())
     us = lambda v: (v - 0) / 100.0  # 100 MHz ticks -> us
     print(f"== sample step {STEP + rep}, B={B}: times in us from the first workgroup start")
-    print("launch            n  start[min,med,max]        end[min,med,max]      | med phases: t-known ops-in prod-done bar-in bar-out stored")
+    print("launch            n  start[min,med,max]        end[min,med,max]      | med phases: barrier ops-in prod-done arrived end")
     prev_end = None
     for k in list(range(2 * nl)) + [2 * nl, 2 * nl + 1]:
         r = a[k]
@@ -47,9 +47,11 @@ for rep in range(2):
         s0, s6 = r[:, 0] - t0, r[:, 6] - t0
         ph = ""
         if k < 2 * nl:
-            d = np.diff(r[:, :7], axis=1)
-            d[d < -1e12] = 0
-            ph = " ".join(f"{us(np.median(d[:, i])):6.2f}" for i in range(6))
+            # stamps: 0 entry, 1 after the start barrier, 2 operands in, 3 products done,
+            # 4 arrived / residual rows stored, 6 stores drained (5 unused)
+            cols = [0, 1, 2, 3, 4, 6]
+            d = np.diff(r[:, cols], axis=1)
+            ph = " ".join(f"{us(np.median(d[:, i])):6.2f}" for i in range(len(cols) - 1))
         gap = "" if prev_end is None or k % 2 else f" gap {us(s0.min() - prev_end):5.2f}"
         print(f"{name}  {len(r):4d}  {us(s0.min()):7.2f} {us(np.median(s0)):7.2f} {us(s0.max()):7.2f}   "
               f"{us(s6.min()):7.2f} {us(np.median(s6)):7.2f} {us(s6.max()):7.2f} | {ph}{gap}")
