@@ -153,7 +153,7 @@ __device__ float mol_sample(const float* y, int nr, int64_t t, int utt, const Wn
 
 // The step-dependent, parameter-independent part of mol_sample for one (utterance, index j)
 // lane: j < nr -> logf(-logf(u_j)) (the Gumbel term), j == 10 -> logf(u) - logf(1 - u) of the
-// logistic draw.  Computed while the MoL parameters are still in flight; mol_pick finishes
+// logistic draw.  Computed while the MoL parameters are still in flight; mol_finish finishes
 // with the same float operations as mol_sample.
 __device__ inline float mol_noise(int j, int64_t t, int utt, const WnArgs& a) {
   uint32_t c[4] = {(uint32_t)t, (uint32_t)utt, (uint32_t)(j >> 2), 0u};
@@ -162,19 +162,6 @@ __device__ inline float mol_noise(int j, int64_t t, int utt, const WnArgs& a) {
   const float u = uniform_from_word(w == 0 ? c[0] : w == 1 ? c[1] : w == 2 ? c[2] : c[3]);
   if (j == 10) return logf(u) - logf(1.0f - u);
   return logf(-logf(u));
-}
-
-__device__ inline float mol_pick(const float* y, int nr, const float* gum, float dlog, float log_scale_min) {
-  int best = 0;
-  float bv = -INFINITY;
-  for (int j = 0; j < nr; ++j) {
-    const float v = y[j] - gum[j];
-    if (v > bv) { bv = v; best = j; }
-  }
-  const float mean = y[nr + best];
-  const float ls = fmaxf(y[2 * nr + best], log_scale_min);
-  const float x = mean + expf(ls) * dlog;
-  return fminf(fmaxf(x, -1.0f), 1.0f);
 }
 
 // Butterfly reduction of NV per-lane partial sums over the 64 lanes of a wave: NV-1
@@ -358,19 +345,41 @@ __device__ void mol_finish(const WnArgs& a, int tp1, int wave, int lane, int b0,
     }
   }
   lds_barrier();
-  if ((int)threadIdx.x < nb) {
-    const int b = threadIdx.x;
-    const int gb = b0 + b;
-    float in_v = 0.f;
-    float smp = 0.f;
-    if (tp >= 0) smp = mol_pick(s_mol + b * kMaxNO, a.NO / 3, s_gum + b * 16, s_gum[b * 16 + 10], a.log_scale_min);
-    if (a.teacher != nullptr && tp1 < a.teacher_len) in_v = a.teacher[(int64_t)gb * a.teacher_len + tp1];
-    else if (tp >= 0) in_v = smp;
-    s_in[b] = in_v;
-    if (blockIdx.x == 0 && tp >= 0) {
-      a.y_out[(int64_t)gb * a.T + tp] = smp;
-      if (a.mol_out)
-        for (int j = 0; j < a.NO; ++j) a.mol_out[((int64_t)gb * a.T + tp) * a.NO + j] = s_mol[b * kMaxNO + j];
+  if (wave == 0) {
+    // the mixture pick on 16 lanes per utterance (lane 16 b + j): the argmax of
+    // y_j - logf(-logf(u_j)) over j < nr in four shuffle rounds, ties to the lowest j (the
+    // serial loop's strict '>'; NaN never wins), then lane j = 0 finishes as mol_sample does
+    const int b = lane >> 4, j = lane & 15, nr = a.NO / 3;
+    float v = -INFINITY;
+    if (tp >= 0 && b < nb && j < nr) {
+      v = s_mol[b * kMaxNO + j] - s_gum[b * 16 + j];
+      if (!(v == v)) v = -INFINITY;
+    }
+    int bi = j;
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) {
+      const float ov = __shfl_xor(v, m);
+      const int oi = __shfl_xor(bi, m);
+      if (ov > v || (ov == v && oi < bi)) { v = ov; bi = oi; }
+    }
+    if (j == 0 && b < nb) {
+      const int gb = b0 + b;
+      float in_v = 0.f;
+      float smp = 0.f;
+      if (tp >= 0) {
+        const float mean = s_mol[b * kMaxNO + nr + bi];
+        const float ls = fmaxf(s_mol[b * kMaxNO + 2 * nr + bi], a.log_scale_min);
+        const float x = mean + expf(ls) * s_gum[b * 16 + 10];
+        smp = fminf(fmaxf(x, -1.0f), 1.0f);
+      }
+      if (a.teacher != nullptr && tp1 < a.teacher_len) in_v = a.teacher[(int64_t)gb * a.teacher_len + tp1];
+      else if (tp >= 0) in_v = smp;
+      s_in[b] = in_v;
+      if (blockIdx.x == 0 && tp >= 0) {
+        a.y_out[(int64_t)gb * a.T + tp] = smp;
+        if (a.mol_out)
+          for (int q = 0; q < a.NO; ++q) a.mol_out[((int64_t)gb * a.T + tp) * a.NO + q] = s_mol[b * kMaxNO + q];
+      }
     }
   }
   lds_barrier();

@@ -218,6 +218,9 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
               C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, _s())
 
 
+_DW_MIN_BLOCKS = int(os.environ.get("AVC_DW_MIN_BLOCKS", "1024"))
+
+
 def _splits_for(M, N, K):
     """Split-K factor for the long-K weight-gradient GEMMs: >= 1024 blocks of 64x64 output
     tiles (4 per CU) while each split keeps >= 1024 k (tools/gemm_bench.hip sweep: conv dW
@@ -226,7 +229,7 @@ def _splits_for(M, N, K):
     ways with >= 256 k each — so the serial k loop stops dominating (42 us -> a few us)."""
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     s = 1
-    while tiles * s < 1024 and K // (s + 1) >= 1024 and s < 8:
+    while tiles * s < _DW_MIN_BLOCKS and K // (s + 1) >= 1024 and s < 8:
         s += 1
     if tiles < 64:
         s = max(s, min(64, K // 256, max(1, 1024 // tiles)))
