@@ -308,7 +308,11 @@ constexpr int kRW = 2;                    // residual waves
 constexpr int kResRows = 4;               // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
 constexpr int kLayerThreads = 64 * (kGW + kRW);
 constexpr int kTailWaves = 4;             // tail / head: one wave per output row
-constexpr int kPR = 32;                   // past-tap workgroups: gate rows per workgroup
+#ifndef WN_PR
+#define WN_PR 32
+#endif
+constexpr int kPR = WN_PR;                // past-tap workgroups: gate rows per workgroup (16, 32 or 64)
+constexpr int kPRT = kPR / 16;            // 16-row MFMA tiles per workgroup
 
 // MoL head output of the previous step for the utterance tile, in two halves so that its
 // loads are issued at kernel start: every wave reads its W2 rows (S == 256: one 4-float
@@ -648,7 +652,7 @@ __device__ void past_taps(const WnArgs& a, int l_lo, int idx, int slot) {
   // l / 16), B = 4 k x 16 utterance columns (8 real, 8 clamped and dropped).  Each lane
   // loads 4 consecutive k of its row / utterance; element j of those feeds MFMA j, so the
   // four MFMAs of an iteration cover 16 k (the same k order for A and B).
-  static_assert(kBT == 8 && kPR == 32, "past-tap tiling: 2 x 16 rows, 8 utterances");
+  static_assert(kBT == 8 && (kPR == 16 || kPR == 32 || kPR == 64), "past-tap tiling: 1-4 x 16 rows, 8 utterances");
   __shared__ float s_part[NW][kPR][kBT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rblocks = a.G / kPR;
@@ -662,39 +666,38 @@ __device__ void past_taps(const WnArgs& a, int l_lo, int idx, int slot) {
   const float* base = layer_base(a, layer);
   const int m = lane & 15, q = lane >> 4;
   const int ub = b0 + ((m & 7) < nb ? (m & 7) : 0);   // utterance of B column m (8..15: dropped)
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[kPRT];
+#pragma unroll
+  for (int r = 0; r < kPRT; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int c = wave; c * 256 < KT; c += NW) {
     const int kc = c * 256, tap = kc / a.R;
     const float* xr = ring_row(a, layer, (sn - (a.K - 1 - tap) * d) & (a.RING - 1)) + (int64_t)ub * a.R +
                       (kc - tap * a.R) + 4 * q;
     const float* w0 = base + (int64_t)(row0 + m) * KX + kc + 4 * q;
-    const float* w1 = w0 + (int64_t)16 * KX;
-    // every load of the chunk in flight before the first MFMA (48 x 16 B per lane): the
-    // workgroup is bound by how many bytes its CU has requested, not by the MFMAs
-    f32x4 xv[16], wa[16], wb[16];
+    // every load of the chunk in flight before the first MFMA: the workgroup is bound by
+    // how many bytes its CU has requested, not by the MFMAs
+    f32x4 xv[16], wv[kPRT][16];
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       xv[it] = ld4(xr + it * 16);
-      wa[it] = ld4(w0 + it * 16);
-      wb[it] = ld4(w1 + it * 16);
+#pragma unroll
+      for (int r = 0; r < kPRT; ++r) wv[r][it] = ld4(w0 + (int64_t)(16 * r) * KX + it * 16);
     }
     __builtin_amdgcn_sched_barrier(0);      // keep the scheduler from sinking loads to their uses
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[it][j], xv[it][j], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[it][j], xv[it][j], acc1, 0, 0, 0);
-      }
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < kPRT; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[r][it][j], xv[it][j], acc[r], 0, 0, 0);
     }
   }
   // C layout: lane l holds rows 4 (l / 16) + v (v = 0..3) of column l % 16
   if (m < kBT) {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      s_part[wave][4 * q + v][m] = acc0[v];
-      s_part[wave][16 + 4 * q + v][m] = acc1[v];
-    }
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int r = 0; r < kPRT; ++r) s_part[wave][16 * r + 4 * q + v][m] = acc[r][v];
   }
   __syncthreads();
   for (int j = threadIdx.x; j < kPR * kBT; j += 64 * NW) {
