@@ -302,8 +302,15 @@ __device__ void sample_stage(const WnArgs& a, int tp1, int b0, int nb, float* s_
 // step counter is read.
 constexpr int kRP = 2;                    // gate pairs per workgroup
 constexpr int kUB = 4;                    // utterances per workgroup
-constexpr int kGW = 3;                    // gate waves: the critical GEMV [g_(l-1) | x_(l-1)(t)] is
-                                          // H + R = 768 = 3 chunks of 256 for r9y9
+constexpr int kGC = 3;                    // chunks of the critical GEMV [g_(l-1) | x_(l-1)(t)]:
+                                          // H + R = 768 = 3 x 256 for r9y9
+#ifndef WN_GSPLIT
+#define WN_GSPLIT 2
+#endif
+constexpr int kGS = WN_GSPLIT;            // gate-row groups: 1 = a wave takes all 4 rows of its
+                                          // chunk, 2 = two waves per chunk, 2 rows each
+constexpr int kGW = kGC * kGS;            // gate waves
+constexpr int kWR = 2 * kRP / kGS;        // gate rows per gate wave
 constexpr int kRW = 2;                    // residual waves
 constexpr int kResRows = 4;               // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
 constexpr int kLayerThreads = 64 * (kGW + kRW);
@@ -398,7 +405,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   __shared__ float s_gum[L0 ? kUB * 16 : 1];
   __shared__ float s_in[kUB];
   __shared__ f32x4 s_h1[L0 ? kUB : 1][64];
-  __shared__ float s_red[kGW][2 * kRP * kUB];
+  __shared__ float s_red[kGW][kWR * kUB];
   __shared__ int s_arrived;
 #if WN_STAMP
   unsigned long long st[kStampN] = {};
@@ -435,15 +442,15 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   };
 
   // ---------------- prologue: every load of the launch, none waits for another
-  const int c0 = wave;
+  const int c0 = wave % kGC, grp = wave / kGC;  // chunk and row group of a gate wave
   const bool gate = wave < kGW && KT + c0 * 256 < KX;
   const int kc0 = KT + c0 * 256;
   const bool cur0 = L0 && kc0 >= KT + H;    // layer 0's current-tap chunk: x_0(t) from the draw
-  f32x4 w0[2 * kRP], x0[kUB], fw0 = {}, fb0 = {};
+  f32x4 w0[kWR], x0[kUB], fw0 = {}, fb0 = {};
   bool live0 = false;
   if (gate) {
 #pragma unroll
-    for (int r = 0; r < 2 * kRP; ++r) w0[r] = ld4(base + (int64_t)wrow(r) * KX + kc0 + lane * 4);
+    for (int r = 0; r < kWR; ++r) w0[r] = ld4(base + (int64_t)wrow(grp * kWR + r) * KX + kc0 + lane * 4);
     live0 = load_x(kc0, x0);
     if (L0) {                               // (unconditional in the wave: no register shuffle
       const int i = (cur0 ? kc0 - KT - H : 0) + lane * 4;   //  that would drain the loads)
@@ -516,7 +523,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   lds_barrier();                            // (layer >= 1: the loads above stay in flight)
 #if WN_STAMP
   st[1] = WN_NOW();
-  if (gate) { const float xf = x0[0][0] + x0[kUB - 1][3] + w0[0][0] + w0[2 * kRP - 1][3] + pre_a; WN_AFTER(xf); }
+  if (gate) { const float xf = x0[0][0] + x0[kUB - 1][3] + w0[0][0] + w0[kWR - 1][3] + pre_a; WN_AFTER(xf); }
   if (resid) { const float xf = rres + rg[0][0] + rw[0][0] + rskip; WN_AFTER(xf); }
   st[2] = WN_NOW();
 #endif
@@ -541,16 +548,16 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
 
   // ---------------- gate GEMV (first chunk from the prologue; further chunks only when KX - KT > kGW*256)
   if (wave < kGW) {
-    float acc[2 * kRP * kUB];
+    float acc[kWR * kUB];
 #pragma unroll
-    for (int j = 0; j < 2 * kRP * kUB; ++j) acc[j] = 0.f;
+    for (int j = 0; j < kWR * kUB; ++j) acc[j] = 0.f;
     if (live0) {
 #pragma unroll
-      for (int r = 0; r < 2 * kRP; ++r)
+      for (int r = 0; r < kWR; ++r)
 #pragma unroll
         for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w0[r], x0[b], acc[r * kUB + b]);
     }
-    for (int c = c0 + kGW; KT + c * 256 < KX; c += kGW) {
+    for (int c = c0 + kGC; KT + c * 256 < KX; c += kGC) {
       const int kc = KT + c * 256;
       f32x4 x[kUB];
       if (L0 && kc >= KT + H) {
@@ -569,17 +576,17 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
         continue;
       }
 #pragma unroll
-      for (int r = 0; r < 2 * kRP; ++r) {
-        const f32x4 w = ld4(base + (int64_t)wrow(r) * KX + kc + lane * 4);
+      for (int r = 0; r < kWR; ++r) {
+        const f32x4 w = ld4(base + (int64_t)wrow(grp * kWR + r) * KX + kc + lane * 4);
 #pragma unroll
         for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w, x[b], acc[r * kUB + b]);
       }
     }
 #if WN_STAMP
-    { const float af = acc[0] + acc[2 * kRP * kUB - 1]; WN_AFTER(af); st[3] = WN_NOW(); }
+    { const float af = acc[0] + acc[kWR * kUB - 1]; WN_AFTER(af); st[3] = WN_NOW(); }
 #endif
-    const float s = wave_reduce_multi<2 * kRP * kUB>(acc, lane);
-    if ((lane & (64 / (2 * kRP * kUB) - 1)) == 0) s_red[wave][lane / (64 / (2 * kRP * kUB))] = s;
+    const float s = wave_reduce_multi<kWR * kUB>(acc, lane);
+    if ((lane & (64 / (kWR * kUB) - 1)) == 0) s_red[wave][lane / (64 / (kWR * kUB))] = s;
     // the last gate wave to arrive finishes the gate (no barrier with the residual waves)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     int prev = 0;
@@ -592,8 +599,13 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       if (lane < kRP * kUB && fb < nb) {
         float za = pre_a, zb = pre_b;
+        // gate row r = 2 fp (+1) lives in row group r / kWR at position r % kWR
+        const int ga = 2 * fp, gbr = 2 * fp + 1;
 #pragma unroll
-        for (int w = 0; w < kGW; ++w) { za += s_red[w][(2 * fp) * kUB + fb]; zb += s_red[w][(2 * fp + 1) * kUB + fb]; }
+        for (int c = 0; c < kGC; ++c) {
+          za += s_red[(ga / kWR) * kGC + c][(ga % kWR) * kUB + fb];
+          zb += s_red[(gbr / kWR) * kGC + c][(gbr % kWR) * kUB + fb];
+        }
         gbuf_of(a, layer)[(int64_t)(b0 + fb) * H + o0 + fp] = tanhf(za) * avc_sigmoid(zb);
       }
     }
