@@ -311,8 +311,11 @@ constexpr int kGS = WN_GSPLIT;            // gate-row groups: 1 = a wave takes a
                                           // chunk, 2 = two waves per chunk, 2 rows each
 constexpr int kGW = kGC * kGS;            // gate waves
 constexpr int kWR = 2 * kRP / kGS;        // gate rows per gate wave
-constexpr int kRW = 2;                    // residual waves
-constexpr int kResRows = 4;               // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
+#ifndef WN_RW
+#define WN_RW 2
+#endif
+constexpr int kRW = WN_RW;                // residual waves
+constexpr int kResRows = 8 / kRW;         // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
 constexpr int kLayerThreads = 64 * (kGW + kRW);
 constexpr int kTailWaves = 4;             // tail / head: one wave per output row
 #ifndef WN_PR
@@ -475,8 +478,9 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   const float* pbias = L0 ? nullptr : pbase + (int64_t)(a.R + a.S) * H;
   const int rwave = wave - kGW;
   const bool resid = !L0 && rwave >= 0;
-  // after the butterfly, lane L (L % 4 == 0) holds sum index L/4 = q*kUB + b
-  const int my_q = (lane >> 2) / kUB, my_b = (lane >> 2) % kUB;
+  // after the butterfly, lane L (L % kRStep == 0) holds sum index L/kRStep = q*kUB + b
+  constexpr int kRStep = 64 / (kResRows * kUB);        // lanes per reduced residual value
+  const int my_q = (lane / kRStep) / kUB, my_b = (lane / kRStep) % kUB;
   const int my_gb = b0 + (my_b < nb ? my_b : 0);
   f32x4 rw[kResRows], rg[kUB];
   int myrow = 0;
@@ -621,7 +625,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
 #endif
     const float v0 = wave_reduce_multi<kResRows * kUB>(acc, lane);
     const int j = rwave + my_q * kRW;
-    if ((lane & 3) == 0 && j < kRP * nrp && my_b < nb) {
+    if (lane % kRStep == 0 && j < kRP * nrp && my_b < nb) {
       const int gb = b0 + my_b;
       const float v = v0 + rbias;
       if (myrow < a.R) {
