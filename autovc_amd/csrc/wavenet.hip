@@ -317,7 +317,10 @@ constexpr int kWR = 2 * kRP / kGS;        // gate rows per gate wave
 constexpr int kRW = WN_RW;                // residual waves
 constexpr int kResRows = 8 / kRW;         // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
 constexpr int kLayerThreads = 64 * (kGW + kRW);
-constexpr int kTailWaves = 4;             // tail / head: one wave per output row
+#ifndef WN_TW
+#define WN_TW 4
+#endif
+constexpr int kTailWaves = WN_TW;         // tail / head: one wave per output row
 #ifndef WN_PR
 #define WN_PR 32
 #endif
@@ -659,7 +662,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
 // step t carry this work in extra workgroups (layers [0, L/2) and [L/2, L)), and the 24
 // chain launches of step t+1 fetch only the current-tap blocks: their per-CU operand fill
 // (the launch's bound) drops from 73 to 41 KB, while these workgroups stream
-// 32 rows x 4 KB of weights in large, latency-tolerant batches.  Each wave takes 256-deep
+// 32 rows x 4 KB of weights in large, latency-tolerant batches.  Each wave takes 128-deep
 // chunks of the (K-1)*R taps on MFMA tiles (a 64-value butterfly per 8 rows took 2.5 us per
 // group); the workgroup sums the waves' partials in LDS.
 template <int NW>
@@ -685,23 +688,24 @@ __device__ void past_taps(const WnArgs& a, int l_lo, int idx, int slot) {
   f32x4 acc[kPRT];
 #pragma unroll
   for (int r = 0; r < kPRT; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c = wave; c * 256 < KT; c += NW) {
-    const int kc = c * 256, tap = kc / a.R;
+  constexpr int KC = 128;                // k per wave-chunk (8 MFMA iterations of 16 k)
+  for (int c = wave; c * KC < KT; c += NW) {
+    const int kc = c * KC, tap = kc / a.R;
     const float* xr = ring_row(a, layer, (sn - (a.K - 1 - tap) * d) & (a.RING - 1)) + (int64_t)ub * a.R +
                       (kc - tap * a.R) + 4 * q;
     const float* w0 = base + (int64_t)(row0 + m) * KX + kc + 4 * q;
     // every load of the chunk in flight before the first MFMA: the workgroup is bound by
     // how many bytes its CU has requested, not by the MFMAs
-    f32x4 xv[16], wv[kPRT][16];
+    f32x4 xv[KC / 16], wv[kPRT][KC / 16];
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
+    for (int it = 0; it < KC / 16; ++it) {
       xv[it] = ld4(xr + it * 16);
 #pragma unroll
       for (int r = 0; r < kPRT; ++r) wv[r][it] = ld4(w0 + (int64_t)(16 * r) * KX + it * 16);
     }
     __builtin_amdgcn_sched_barrier(0);      // keep the scheduler from sinking loads to their uses
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
+    for (int it = 0; it < KC / 16; ++it) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
