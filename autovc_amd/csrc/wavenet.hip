@@ -75,6 +75,7 @@ struct WnArgs {
   float* h1;
   float* gbuf;
   float* ptap;       // past-tap products of the next step: (2, n_layers, B, G), by step parity
+  float* molp;       // MoL head partials of the head kernel's row blocks: (S / kHR, B, kMaxNO)
   int* ctr;
   const float* teacher;
   int teacher_len;
@@ -327,40 +328,18 @@ constexpr int kTailWaves = WN_TW;         // tail / head: one wave per output ro
 constexpr int kPR = WN_PR;                // past-tap workgroups: gate rows per workgroup (16, 32 or 64)
 constexpr int kPRT = kPR / 16;            // 16-row MFMA tiles per workgroup
 
-// MoL head output of the previous step for the utterance tile, in two halves so that its
-// loads are issued at kernel start: every wave reads its W2 rows (S == 256: one 4-float
-// chunk per lane); h1 is read ONCE per workgroup, by the last wave, into LDS (nine copies
-// of it in flight were 32 KB of the CU's operand fill); the second half reduces into s_mol.
-constexpr int kMolRows = (kMaxNO + kGW + kRW - 1) / (kGW + kRW);   // W2 rows per wave
-
-__device__ __forceinline__ void mol_load(const WnArgs& a, int wave, int lane, f32x4 (&mw)[kMolRows]) {
-  const float* W2 = head_base(a) + (int64_t)a.S * a.S + a.S;
-#pragma unroll
-  for (int q = 0; q < kMolRows; ++q) {
-    const int r = wave + q * (kGW + kRW);
-    mw[q] = ld4(W2 + (int64_t)(r < a.NO ? r : 0) * a.S + lane * 4);
-  }
-}
+// MoL head output of the previous step: the head kernel's row-block workgroups (kHR rows
+// of h1 each) also multiply their rows into W2 and leave (S / kHR) partial sums per (utterance,
+// output); layer 0 adds them in fixed order — 16 loads per output issued at kernel start
+// instead of W2 (30 KB) and h1 per workgroup and a GEMV on the chain.
+constexpr int kHR = 16;                   // head rows per head workgroup (4 waves x 4 rows)
 
 // s_mol <- MoL parameters of step tp1 - 1; then s_in <- the input of step tp1 (sampled, or
 // the teacher value); block 0 of the tile records the sample and the input.
-__device__ void mol_finish(const WnArgs& a, int tp1, int wave, int lane, int b0, int nb, const f32x4 (&mw)[kMolRows],
-                           const f32x4 (*s_h1)[64], float* s_mol, const float* s_gum, float* s_in) {
+__device__ void mol_finish(const WnArgs& a, int tp1, int wave, int lane, int b0, int nb, float mol_v, float* s_mol,
+                           const float* s_gum, float* s_in) {
   const int tp = tp1 - 1;
-  if (tp >= 0) {
-    const float* b2 = head_base(a) + (int64_t)a.S * a.S + a.S + (int64_t)a.NO * a.S;
-#pragma unroll
-    for (int q = 0; q < kMolRows; ++q) {
-      const int r = wave + q * (kGW + kRW);
-      float acc[kUB];
-#pragma unroll
-      for (int b = 0; b < kUB; ++b) acc[b] = dot4(mw[q], s_h1[b][lane], 0.f);
-      if (r < a.NO) {  // wave-uniform
-        const float v = wave_reduce_multi<kUB>(acc, lane);
-        if ((lane & (64 / kUB - 1)) == 0) s_mol[(lane / (64 / kUB)) * kMaxNO + r] = v + b2[r];
-      }
-    }
-  }
+  if (tp >= 0 && (int)threadIdx.x < kUB * kMaxNO) s_mol[threadIdx.x] = mol_v;   // [b][j], b = tid / kMaxNO
   lds_barrier();
   if (wave == 0) {
     // the mixture pick on 16 lanes per utterance (lane 16 b + j): the argmax of
@@ -410,7 +389,6 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   __shared__ float s_mol[L0 ? kUB * kMaxNO : 1];
   __shared__ float s_gum[L0 ? kUB * 16 : 1];
   __shared__ float s_in[kUB];
-  __shared__ f32x4 s_h1[L0 ? kUB : 1][64];
   __shared__ float s_red[kGW][kWR * kUB];
   __shared__ int s_arrived;
 #if WN_STAMP
@@ -507,23 +485,27 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
     rskip = a.skip[(int64_t)my_gb * a.S + (xrow ? 0 : myrow - a.R)];
     rres = ring_row(a, lp, slot)[(int64_t)my_gb * a.R + (xrow ? myrow : 0)];
   }
-  // layer 0: the MoL head of the previous step (weights and h1)
-  f32x4 mw[kMolRows];
-  int t_abs = 0;
+  // layer 0: the MoL head of the previous step, from the head kernel's partial sums
+  // (thread b * kMaxNO + j: utterance b, output j), and the sampling noise
+  float mol_v = 0.f;
   if (L0) {
-    mol_load(a, wave, lane, mw);
-    if (wave == kGW + kRW - 1) {
-      // the last wave has no residual rows in layer 0: it stages h1 in LDS and, while h1 is
-      // in flight, draws the sampling noise (lane 16 b + j)
-      f32x4 h[kUB];
+    if ((int)threadIdx.x < kUB * kMaxNO) {
+      const int b = threadIdx.x / kMaxNO, j = threadIdx.x % kMaxNO;
+      const int jj = j < a.NO ? j : 0;
+      const float* mp = a.molp + urow(b) * kMaxNO + jj;
+      float part[256 / kHR];
 #pragma unroll
-      for (int b = 0; b < kUB; ++b) h[b] = ld4(a.h1 + urow(b) * a.S + lane * 4);
-      t_abs = abs_step(a, targ);
+      for (int w = 0; w < 256 / kHR; ++w) part[w] = mp[(int64_t)w * a.B * kMaxNO];
+      mol_v = head_base(a)[(int64_t)a.S * a.S + a.S + (int64_t)a.NO * a.S + jj];   // b2
+#pragma unroll
+      for (int w = 0; w < 256 / kHR; ++w) mol_v += part[w];
+    }
+    if (wave == kGW + kRW - 1) {
+      // the last wave has no residual rows in layer 0: it draws the noise (lane 16 b + j)
+      const int t_abs = abs_step(a, targ);
       static_assert(kUB * 16 <= 64, "one noise lane per (utterance, index)");
       const int b = lane >> 4, j = lane & 15;
       if (t_abs >= 1 && b < nb && (j < a.NO / 3 || j == 10)) s_gum[lane] = mol_noise(j, t_abs - 1, a.utt_base + b0 + b, a);
-#pragma unroll
-      for (int q = 0; q < kUB; ++q) s_h1[q][lane] = h[q];
     }
   }
   if (threadIdx.x == 0) s_arrived = 0;
@@ -538,8 +520,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   // ---------------- layer 0: sample the previous step's output; x_0(t) is its current tap
   if (L0) {
     const int t = abs_step(a, targ);
-    (void)t_abs;
-    mol_finish(a, t, wave, lane, b0, nb, mw, s_h1, s_mol, s_gum, s_in);
+    mol_finish(a, t, wave, lane, b0, nb, mol_v, s_mol, s_gum, s_in);
     if (gate && cur0) {
 #pragma unroll
       for (int b = 0; b < kUB; ++b) {
@@ -785,11 +766,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1)))
   else *sp = a.legacy ? (sk + v) * kSqrtHalf : (sk + v);
 }
 
-// head: h1 = relu(W1 relu(skips) + b1); advances the step counter; the workgroups above
-// ceil(S/NW) carry past_taps for layers [L/2, L).
+// head: h1 = relu(W1 relu(skips) + b1), kHR rows per workgroup (kHR / NW per wave), and the
+// MoL partials of those rows (layer 0 of the next step adds the S / kHR partials);
+// advances the step counter; the workgroups above S / kHR carry past_taps for layers
+// [L/2, L).
 template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void wn_head_kernel(WnArgs a, int slot, int targ) {
-  const int own = (a.S + NW - 1) / NW;
+  static_assert(kHR % NW == 0, "head rows per wave");
+  constexpr int RPW = kHR / NW;
+  __shared__ float s_h1[kHR][kBT];
+  const int own = a.S / kHR;
   if ((int)blockIdx.x >= own) {
     past_taps<NW>(a, a.n_layers / 2, blockIdx.x - own, slot);
     return;
@@ -800,39 +786,59 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1)))
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
-  const int row = min(blockIdx.x * NW + wave, a.S - 1);
+  const int row0 = blockIdx.x * kHR;
   const float* W1 = head_base(a);
   const float* b1 = W1 + (int64_t)a.S * a.S;
-  const float bv = b1[row];
-  float acc[kBT];
+  const float* W2 = b1 + a.S;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[0] = abs_step(a, targ) + 1;
+  // relu(skip) of the utterance tile, one 4-float chunk per lane (S == 256)
+  f32x4 x[kBT];
 #pragma unroll
-  for (int b = 0; b < kBT; ++b) acc[b] = 0.f;
-  for (int k = lane * 4; k < a.S; k += 256) {
-    const f32x4 wv = ld4(W1 + (int64_t)row * a.S + k);
-    f32x4 x[kBT];
+  for (int b = 0; b < kBT; ++b) {
+    x[b] = ld4(a.skip + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + lane * 4);
+    x[b][0] = fmaxf(x[b][0], 0.f); x[b][1] = fmaxf(x[b][1], 0.f);
+    x[b][2] = fmaxf(x[b][2], 0.f); x[b][3] = fmaxf(x[b][3], 0.f);
+  }
+  f32x4 wv[RPW];
+  float bv[RPW];
 #pragma unroll
-    for (int b = 0; b < kBT; ++b) x[b] = ld4(a.skip + (int64_t)(b0 + (b < nb ? b : 0)) * a.S + k);
+  for (int q = 0; q < RPW; ++q) {
+    const int row = row0 + wave * RPW + q;
+    wv[q] = ld4(W1 + (int64_t)row * a.S + lane * 4);
+    bv[q] = b1[row];
+  }
+  // the MoL partial operands: thread t < NO * kBT takes output j = t / kBT, utterance t % kBT
+  const int mj = min((int)threadIdx.x / kBT, a.NO - 1), mb = threadIdx.x % kBT;
+  float w2[kHR];
 #pragma unroll
-    for (int b = 0; b < kBT; ++b) {
-      x[b][0] = fmaxf(x[b][0], 0.f); x[b][1] = fmaxf(x[b][1], 0.f);
-      x[b][2] = fmaxf(x[b][2], 0.f); x[b][3] = fmaxf(x[b][3], 0.f);
-      acc[b] = dot4(wv, x[b], acc[b]);
+  for (int r = 0; r < kHR; ++r) w2[r] = W2[(int64_t)mj * a.S + row0 + r];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    float acc[kBT];
+#pragma unroll
+    for (int b = 0; b < kBT; ++b) acc[b] = dot4(wv[q], x[b], 0.f);
+    const float s = wave_reduce_multi<kBT>(acc, lane);
+    if ((lane & 7) == 0) {
+      const int b = lane >> 3;
+      const float h = fmaxf(s + bv[q], 0.f);
+      s_h1[wave * RPW + q][b] = h;
+      if (b < nb) a.h1[(int64_t)(b0 + b) * a.S + row0 + wave * RPW + q] = h;
     }
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.ctr[0] = abs_step(a, targ) + 1;
-  const float s = wave_reduce_multi<kBT>(acc, lane);
+  __syncthreads();
+  if ((int)threadIdx.x < a.NO * kBT && mb < nb) {
+    float p = 0.f;
+#pragma unroll
+    for (int r = 0; r < kHR; ++r) p += w2[r] * s_h1[r][mb];
+    a.molp[((int64_t)blockIdx.x * a.B + b0 + mb) * kMaxNO + mj] = p;
+  }
 #if WN_STAMP
-  if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1)) && lane == 0) {
-    WN_AFTER(s);
+  if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1)) && lane == 0 && wave == 0) {
     unsigned long long* o = g_wn_stamp + ((int64_t)(2 * a.n_layers + 1) * kStampWG + blockIdx.x + blockIdx.y * gridDim.x) * kStampN;
     o[0] = st0; o[6] = WN_NOW();
   }
 #endif
   (void)slot;
-  if ((lane & 7) != 0 || blockIdx.x * NW + wave >= a.S) return;
-  const int b = lane >> 3;
-  if (b >= nb) return;
-  a.h1[(int64_t)(b0 + b) * a.S + row] = fmaxf(s + bv, 0.f);
 }
 
 // Sample the last output (step T-1) after the final head.
@@ -919,7 +925,7 @@ int enqueue_step(const WnArgs& a, hipStream_t s, int slot, int prow, int targ) {
   const int own = (a.S + kTailWaves - 1) / kTailWaves;
   hipLaunchKernelGGL((wn_tail_kernel<kTailWaves>), dim3(own + past_tap_blocks(a, a.n_layers / 2), nbt),
                      dim3(64 * kTailWaves), 0, s, a, slot);
-  hipLaunchKernelGGL((wn_head_kernel<kTailWaves>), dim3(own + past_tap_blocks(a, a.n_layers - a.n_layers / 2), nbt),
+  hipLaunchKernelGGL((wn_head_kernel<kTailWaves>), dim3(a.S / kHR + past_tap_blocks(a, a.n_layers - a.n_layers / 2), nbt),
                      dim3(64 * kTailWaves), 0, s, a, slot, targ);
   AVC_CHECK_LAUNCH("autovc_wavenet_generate_f32");
   return avc::kOk;
@@ -1012,7 +1018,7 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
   if (B <= 0 || T <= 0 || n_layers <= 0 || layers_per_stack <= 0 || taps <= 0) return -1;
   const int64_t ring = (int64_t)(n_layers + 1) * ring_frames(n_layers, layers_per_stack, taps) * B * R;
   const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + 2 * (int64_t)B * (G / 2) +
-                         2 * (int64_t)n_layers * B * G + 6 * 64;
+                         2 * (int64_t)n_layers * B * G + (int64_t)(S / kHR) * B * kMaxNO + 7 * 64;
   return floats * 4 + kCtrSlots * 4 + 256;
 }
 
@@ -1077,6 +1083,7 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   a.h1 = ws;                   ws += round64((int64_t)B * S);
   a.gbuf = ws;                 ws += round64(2 * (int64_t)B * (G / 2));
   a.ptap = ws;                 ws += round64(2 * (int64_t)n_layers * B * G);
+  a.molp = ws;                 ws += round64((int64_t)(S / kHR) * B * kMaxNO);
   a.ctr = reinterpret_cast<int*>(ws);
   a.teacher = teacher; a.teacher_len = teacher ? teacher_len : 0;
   a.y_out = y_out; a.mol_out = mol_out;
