@@ -12,26 +12,29 @@
 //                x_l(t) = sqrt(.5) (W_out(l-1) g_(l-1) + b_out(l-1) + x_(l-1)(t))
 //                W_2 x_l(t) = [sqrt(.5) W_2 W_out(l-1)] g_(l-1) + [sqrt(.5) W_2] x_(l-1)(t)
 //                             + sqrt(.5) W_2 b_out(l-1)  (the last term folded into pre)
-//              so the layer's GEMV reads [x_l(t-2d); x_l(t-d); g_(l-1); x_(l-1)(t)] (1792
-//              inputs) and needs nothing produced in this launch.  The same kernel does
-//              layer l-1's residual work: its slice of x_l(t) (written to ring l for the
-//              later taps) and of the skip accumulation.
-//              layer(0) first samples the previous output (MoL head tail + Philox draw)
-//              and builds x_0 = first_conv(input) on the fly.
-//   tail     : the last layer's skip rows
-//   head     : h1 = relu(W1 relu(skips) + b1)
+//              so the layer's GEMV on the chain reads only [g_(l-1); x_(l-1)(t)] (768
+//              inputs): the past taps W_0 x_l(t-2d) + W_1 x_l(t-d) were multiplied by the
+//              previous step's tail and head launches (past_taps) and arrive with pre.
+//              The same kernel does layer l-1's residual work: its slice of x_l(t)
+//              (written to ring l for the later taps) and of the skip accumulation.
+//              layer(0) first samples the previous output (the MoL head from the head
+//              kernel's partial sums + Philox draw) and builds x_0 = first_conv(input).
+//   tail     : the last layer's skip rows (+ past taps of half the layers for step t+1)
+//   head     : h1 = relu(W1 relu(skips) + b1) and its MoL partials (+ the other half)
 // 26 launches per sample step instead of 49 for the two-kernel-per-layer form.
 //
 // pre(l, t) = W_cond(l) c_up(t) + b_cond(l) + b_conv(l) for every layer and sample comes
-// from ONE MFMA GEMM per time chunk (autovc_gemm_f32) — the conditioning 1x1 convs are
-// sample-independent, so they leave the sequential chain.
+// from ONE MFMA GEMM per conditioning chunk (autovc_gemm_f32) — the conditioning 1x1 convs
+// are sample-independent, so they leave the sequential chain.
 //
-// Layer inputs live in per-layer rings of RING (power of two >= 2*d_max + 1) frames: the
-// dilated taps read ring slots (t - j*d) & (RING-1); slots before t = 0 are zero, as the
-// reference's zero-initialised conv input buffers.
+// Layer inputs (x_0 included) live in per-layer rings of RING (power of two >= 2*d_max + 1,
+// at least 4) frames: the dilated taps read ring slots (t - j*d) & (RING-1); slots before
+// t = 0 are zero, as the reference's zero-initialised conv input buffers.
 //
-// Every kernel reads the current step t from a device counter slot and forwards it to the
-// next slot, so a captured hipGraph of S steps replays for any t (graph mode).
+// The ring slot and the conditioning row of a step are kernel arguments (static in a
+// captured hipGraph: one graph per (slot, row) of its first step), so no step kernel waits
+// for a dependent counter read; only layer 0 (sampling draw, recorded outputs) reads the
+// step counter, which the head advances.
 #include "common.h"
 #include "../../include/autovc_hip.h"
 
