@@ -27,8 +27,8 @@
 // from ONE MFMA GEMM per conditioning chunk (autovc_gemm_f32) — the conditioning 1x1 convs
 // are sample-independent, so they leave the sequential chain.
 //
-// Layer inputs (x_0 included) live in per-layer rings of RING (power of two >= 2*d_max + 1,
-// at least 4) frames: the dilated taps read ring slots (t - j*d) & (RING-1); slots before
+// Layer inputs (x_0 included) live in per-layer rings of RING (power of two >= 2*d_max + 1)
+// frames: the dilated taps read ring slots (t - j*d) & (RING-1); slots before
 // t = 0 are zero, as the reference's zero-initialised conv input buffers.
 //
 // The ring slot and the conditioning row of a step are kernel arguments (static in a
