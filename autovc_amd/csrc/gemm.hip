@@ -152,12 +152,14 @@ struct OpTile {
       }
     }
   }
+  template <int SET = 0>
   __device__ __forceinline__ void store(float* lds) const {
+    const f32x4 (&src)[PER] = SET ? v2 : v;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
       coords(i, r, k);
-      *reinterpret_cast<f32x4*>(lds + (RK ? r * LD + k : k * LD + r)) = v[i];
+      *reinterpret_cast<f32x4*>(lds + (RK ? r * LD + k : k * LD + r)) = src[i];
     }
   }
   // bf16 image [row][LDB] (k contiguous) of an RK operand: each slot as one 8-byte write
@@ -213,7 +215,9 @@ struct OpTile {
 };
 
 // Block tile BM x BN, k-stage BK, waves of WM x WN (each (WM/32) x (WN/32) MFMA 32x32x2).
-template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool PIPE = false>
+// DEEP: two k-stages of global loads in flight (register sets v / v2 alternate), so a
+// stage's load latency hides behind two stages of MFMAs instead of one.
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool PIPE = false, bool DEEP = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
@@ -261,13 +265,23 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
     sb.load(B, kend);
     sa.store(smem[0]);
     sb.store(smem[0] + TA::FLOATS);
+    if (DEEP && nk > 1) {
+      sa.load_to(A, kend, sa.v2);
+      sb.load_to(B, kend, sb.v2);
+    }
   }
   __syncthreads();
 
   const int h = lane >> 5, li = lane & 31;
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) {
+    if (DEEP) {
+      // stage kt + 2 into the register set stage kt used (already in LDS)
+      if (kt + 2 < nk) {
+        if (kt & 1) { sa.load_to(A, kend, sa.v2); sb.load_to(B, kend, sb.v2); }
+        else        { sa.load_to(A, kend, sa.v);  sb.load_to(B, kend, sb.v); }
+      }
+    } else if (kt + 1 < nk) {
       sa.load(A, kend);
       sb.load(B, kend);
     }
@@ -314,8 +328,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][p], bf[j][p], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < nk) {
-      sa.store(smem[buf ^ 1]);
-      sb.store(smem[buf ^ 1] + TA::FLOATS);
+      if (DEEP && ((kt + 1) & 1)) {
+        sa.template store<1>(smem[buf ^ 1]);
+        sb.template store<1>(smem[buf ^ 1] + TA::FLOATS);
+      } else {
+        sa.store(smem[buf ^ 1]);
+        sb.store(smem[buf ^ 1] + TA::FLOATS);
+      }
     }
     __syncthreads();
   }
@@ -557,6 +576,9 @@ constexpr GemmShape kCfg[] = {
     {9, 128, 128, 32},   // 8 waves of 64x32, pipelined (sweep candidate)
     {10, 64, 64, 64},    // BK 64, pipelined (sweep candidate)
     {11, 128, 64, 32},   // 8 waves of 32x32, pipelined (sweep candidate)
+    {12, 128, 128, 32},  // cfg 2 with two k-stages of loads in flight
+    {13, 64, 64, 32},    // cfg 8 with two k-stages of loads in flight
+    {14, 128, 128, 32},  // cfg 9 with two k-stages of loads in flight
 };
 
 #ifndef AVC_GEMM_FORCE_CFG
@@ -594,8 +616,11 @@ GemmShape pick_config(int M, int N, int K, int splits) {
   // reads (conv fwd/dX 105-109 TF); split-K weight gradients on 64x64/BK16 (92-99 TF).
   // (8-wave tiles, cfg 9/11, won 5-7 % in the isolated sweep but nothing inside the step:
   // 21.62 vs 21.52 ms, same box, alternating)
+  constexpr int NCFG = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
+  static const int big = [] { const char* e = getenv("AVC_GEMM_BIG"); return e ? atoi(e) : 2; }();
+  static const int small = [] { const char* e = getenv("AVC_GEMM_SMALL"); return e ? atoi(e) : 8; }();
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
-  if (t128 >= 512) return kCfg[2];
+  if (t128 >= 512) return kCfg[big >= 0 && big < NCFG ? big : 2];
   // deep-K outputs that fill the chip once with 128-tiles (the LSTM weight gradients,
   // 4096 x 1024 over K = B*T = 8192, on the gradient side stream): 128x128/BK32 measured
   // 17.86 vs 17.98 ms/step against 64x64 (tools/ab_gemm_bigk.sh; AVC_GEMM_BIGK=<cfg id>
@@ -604,16 +629,16 @@ GemmShape pick_config(int M, int N, int K, int splits) {
     const char* e = getenv("AVC_GEMM_BIGK");
     return e ? atoi(e) : 2;
   }();
-  if (bigk >= 0 && bigk < (int)(sizeof(kCfg) / sizeof(kCfg[0])) && t128 >= 256 && K >= 4096) return kCfg[bigk];
+  if (bigk >= 0 && bigk < NCFG && t128 >= 256 && K >= 4096) return kCfg[bigk];
   if (splits > 1) return kCfg[3];
-  return kCfg[8];
+  return kCfg[small >= 0 && small < NCFG ? small : 8];
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool PIPE = false>
+template <int BM, int BN, int BK, int WM, int WN, bool PIPE = false, bool DEEP = false>
 void launch_layouts(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                     float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE>), grid, dim3(NT), \
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AR, BR, PIPE, DEEP>), grid, dim3(NT), \
                                          dyn_lds_for(f32_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, K, \
                                          oa, ob, C, ldc, b1, b2, acc, kps, slab, g_batch)
   if (!a_trans && !b_trans) AVC_L(true, true);
@@ -637,6 +662,9 @@ void launch_gemm(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, in
     case 9: launch_layouts<128, 128, 32, 64, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     case 10: launch_layouts<64, 64, 64, 32, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     case 11: launch_layouts<128, 64, 32, 32, 32, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 12: launch_layouts<128, 128, 32, 64, 64, false, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 13: launch_layouts<64, 64, 32, 32, 32, true, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 14: launch_layouts<128, 128, 32, 64, 32, true, true>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
     default: launch_layouts<64, 64, 16, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
   }
 }
