@@ -281,11 +281,14 @@ def _padded_weight(W, Cop, Cip):
 
 
 _WINOGRAD = os.environ.get("AVC_WINOGRAD", "1") != "0"
+_WINO_KEEP_XT = os.environ.get("AVC_WINO_KEEP_XT", "1") != "0"
 
 
-def _wino_conv(x, Wp, bias, T, flip):
+def _wino_conv(x, Wp, bias, T, flip, keep_xt=False):
     """Winograd F(4,5) conv (csrc/winograd.hip): flip=0 -> conv(x, W) + bias (B,T,Cop);
-    flip=1 -> the input-gradient correlation of x = dy (B,T,Cop) with W: (B,T,Cip)."""
+    flip=1 -> the input-gradient correlation of x = dy (B,T,Cop) with W: (B,T,Cip).
+    keep_xt: also return the input transform X~ (8, B*T/4, Cin), which the weight gradient
+    of the same conv reuses instead of transforming x again."""
     B, _, Cin = x.shape
     Cop, Cip, _ = Wp.shape
     Cout = Cip if flip else Cop
@@ -300,20 +303,22 @@ def _wino_conv(x, Wp, bias, T, flip):
               Cout * Cin, 0, Yt.data_ptr(), Cout, nt * Cout, 0, _s())
     y = torch.empty((B, T, Cout), device=dev, dtype=torch.float32)
     _lib.call("autovc_wino5_output_f32", B, T, Cout, Yt.data_ptr(), _p(bias), y.data_ptr(), Cout, _s())
-    return y
+    return (y, Xt) if keep_xt else y
 
 
-def _wino_wgrad(x, dy, T, dW, acc):
+def _wino_wgrad(x, dy, T, dW, acc, Xt=None):
     """dW (Co,Ci,5) (+)= Winograd F(4,5) weight gradient of conv(x) against dy (B,T,Co):
-    dY~ and X~ transforms, 8 GEMMs over the B*T/4 tiles (M_i = dY~_i^T X~_i), G^T combine."""
+    dY~ and X~ transforms, 8 GEMMs over the B*T/4 tiles (M_i = dY~_i^T X~_i), G^T combine.
+    Xt: X~ kept from the forward (the same transform of the same x), else computed here."""
     B, _, Cin = x.shape
     Cout = dy.shape[2]
     nt = B * T // 4
     dev = x.device
-    Xt = torch.empty((8, nt, Cin), device=dev, dtype=torch.float32)
     Dt = torch.empty((8, nt, Cout), device=dev, dtype=torch.float32)
     Mt = torch.empty((8, Cout, Cin), device=dev, dtype=torch.float32)
-    _lib.call("autovc_wino5_input_f32", B, T, Cin, x.data_ptr(), x.stride(1), Xt.data_ptr(), _s())
+    if Xt is None:
+        Xt = torch.empty((8, nt, Cin), device=dev, dtype=torch.float32)
+        _lib.call("autovc_wino5_input_f32", B, T, Cin, x.data_ptr(), x.stride(1), Xt.data_ptr(), _s())
     _lib.call("autovc_wino5_dy_f32", B, T, Cout, dy.data_ptr(), dy.stride(1), Dt.data_ptr(), _s())
     _lib.call("autovc_gemm_batched_f32", 8, Cout, Cin, nt, Dt.data_ptr(), Cout, nt * Cout, 1, Xt.data_ptr(), Cin,
               nt * Cin, 1, Mt.data_ptr(), Cin, Cout * Cin, 0, _s())
@@ -327,24 +332,25 @@ def _wino_ok(T, *channels):
     return _WINOGRAD and _PRECISION[0] == "fp32" and T % 4 == 0 and all(c % 4 == 0 for c in channels)
 
 
-def _conv_fwd(x, Wp, bp, T):
+def _conv_fwd(x, Wp, bp, T, keep_xt=False):
     """y (B,T,Cop) = conv1d_k5p2(x (B,T,Cip)) + b: Winograd F(4,5) (8 batched GEMMs) when T
-    is a multiple of 4, else one implicit-im2col GEMM."""
+    is a multiple of 4, else one implicit-im2col GEMM.  keep_xt: return (y, X~ or None)."""
     B, _, Cip = x.shape
     Cop = Wp.shape[0]
     if _wino_ok(T, Cip, Cop) and x.is_contiguous():
-        return _wino_conv(x, Wp, bp, T, 0)
+        return _wino_conv(x, Wp, bp, T, 0, keep_xt)
     Wf = torch.empty((Cop, KS * Cip), device=x.device, dtype=torch.float32)
     _lib.call("autovc_conv_pack_f32", Cop, Cip, KS, Wp.data_ptr(), Wf.data_ptr(), 0, _s())
     y = torch.empty((B, T, Cop), device=x.device, dtype=torch.float32)
     gemm(B * T, Cop, KS * Cip, x, Cip, 0, Wf, KS * Cip, 0, y, Cop, a_conv=(T, Cip, -PAD), bias1=bp)
-    return y
+    return (y, None) if keep_xt else y
 
 
-def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None):
+def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None, Xt=None):
     """Backward of _conv_fwd given dy (B,T,Cop): (dx (B,T,Cip), dW, db).  W / b are the
     parameters: when their gradients live in a flat buffer (and no channel padding is in
-    play) dW / db are accumulated there and returned as None."""
+    play) dW / db are accumulated there and returned as None.  Xt: the forward's Winograd
+    input transform of x (_conv_fwd keep_xt), reused by the weight gradient."""
     B, T, Cip = x.shape
     Cop = Wp.shape[0]
     M = B * T
@@ -360,14 +366,14 @@ def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None):
 
         def dw(go=go):
             if _wino_ok(T, Cip, Cop) and dy.is_contiguous() and x.is_contiguous():
-                _wino_wgrad(x, dy, T, go.buf, go.acc)
+                _wino_wgrad(x, dy, T, go.buf, go.acc, Xt)
                 return
             dWf = torch.empty((Cop, KS * Cip), device=dev, dtype=torch.float32)
             gemm(Cop, KS * Cip, M, dy, Cop, 1, x, Cip, 1, dWf, KS * Cip, b_conv=(T, Cip, -PAD),
                  splits=_splits_for(Cop, KS * Cip, M))
             _lib.call("autovc_conv_unpack_grad_f32", Cop, Cip, KS, dWf.data_ptr(), go.buf.data_ptr(), int(go.acc),
                       _s())
-        _grad_launch(dev, go.acc, dw, dy, x)
+        _grad_launch(dev, go.acc, dw, dy, x, *(() if Xt is None else (Xt,)))
         dW = go.result()
     if need_x:
         if _wino_ok(T, Cip, Cop) and dy.is_contiguous():
@@ -399,7 +405,10 @@ class ConvBNActFn(torch.autograd.Function):
         xp = _pad_last(x, Cip)
         Wp = _padded_weight(W, Cop, Cip)
         bp = b if (b is None or Cop == Co) else _pad_last(b, Cop)
-        y = _conv_fwd(xp, Wp, bp, T)
+        # the weight gradient reuses the forward's Winograd input transform (AVC_WINO_KEEP_XT=0:
+        # recompute it in backward)
+        keep = bool(training and _WINO_KEEP_XT and ctx.needs_input_grad[1])
+        y, ctx.xt = _conv_fwd(xp, Wp, bp, T, keep_xt=True) if keep else (_conv_fwd(xp, Wp, bp, T), None)
         if training:
             mean = torch.empty(Co, device=dev, dtype=torch.float32)
             var = torch.empty(Co, device=dev, dtype=torch.float32)
@@ -447,7 +456,8 @@ class ConvBNActFn(torch.autograd.Function):
         dgamma = gg.result() if gg else None
         dbeta = gb.result() if gb else None
         dx, dW, db = _conv_bwd(dy, xp, Wp, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               ctx.needs_input_grad[2], W_param, b_param)
+                               ctx.needs_input_grad[2], W_param, b_param, ctx.xt)
+        ctx.xt = None
         if dx is not None and Cip != Ci:
             dx = dx[..., :Ci].contiguous()
         if dW is not None and (Cop, Cip) != (Co, Ci):
