@@ -137,6 +137,24 @@ def test_conv_bn_act_train_fwd_bwd(cuda, act):
     assert int(bn_d.num_batches_tracked) == 1
 
 
+def test_wino_weight_grad_reuses_forward_transform_bit_exact(cuda, monkeypatch):
+    """The conv weight gradient fed with the forward's Winograd input transform (default)
+    equals the one that transforms x again (AVC_WINO_KEEP_XT=0) bit for bit."""
+    from autovc_amd import functional as AF
+    torch.manual_seed(5)
+    x = torch.randn(4, 64, 512).to(cuda)
+    gz = torch.randn(4, 64, 512).to(cuda)
+    grads = []
+    for keep in (True, False):
+        monkeypatch.setattr(AF, "_WINO_KEEP_XT", keep)
+        torch.manual_seed(6)
+        conv, bn = torch.nn.Conv1d(512, 512, 5, padding=2).to(cuda), torch.nn.BatchNorm1d(512).to(cuda)
+        xd = x.clone().requires_grad_()
+        AF.conv_bn_act(xd, conv, bn, "relu").backward(gz)
+        grads.append((conv.weight.grad.clone(), xd.grad.clone()))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
 # ------------------------------------------------------------------ LSTM unit tests
 @pytest.mark.parametrize("B,T,I,H", [(64, 16, 512, 1024), (3, 9, 320, 512), (17, 5, 64, 64)])
 def test_lstm_layer_fwd_bwd(cuda, B, T, I, H):
