@@ -89,6 +89,8 @@ sig("autovc_lstm2_persist_supported", c_int, c_int)
 sig("autovc_lstm2_fwd_persist_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_lstm2_persist_status", c_ptr, c_ptr)
+sig("autovc_fault_status", c_ptr, c_int, c_ptr)
+sig("autovc_lstm_persist_set_timeout_ticks", c_int)
 sig("autovc_lstm2_fwd_persist_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_lstm_persist_workspace_bytes", c_int, c_int, c_int)

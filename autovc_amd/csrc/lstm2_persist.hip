@@ -197,6 +197,15 @@ __device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int
   return *status == 0;
 }
 
+// Sticky per-device fault word: a launch whose grid barrier timed out (its workgroups were
+// not all resident at once — e.g. another process's kernels held part of the chip) ORs
+// kFaultPersistBarrier into it, after writing NaN over every h and c it owns, so the
+// failure reaches the loss.  The host reads and clears it at its sync points
+// (autovc_fault_status: Solver log steps, bench.py) and raises.
+__device__ int g_avc_fault = 0;
+constexpr int kFaultPersistBarrier = 1;
+int g_timeout_ticks = 0;             // 0 = the default 1 s; tests force a timeout with a tiny value
+
 // per-step cell update of one (batch row b, unit j) from its 4 gate pre-activations
 // Only the k-blocked h copy is handed to other workgroups, so only it is stored before the
 // grid barrier (sc1, write-through); h, c and the gates are kept in registers and stored
@@ -390,6 +399,24 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j0 = blockIdx.x * PU;
   auto grow = [&](int col) { return (col >> 2) * H + j0 + (col & 3); };   // tile column -> gate row
+  // epilogue ownership: thread e owns (batch row e / 4, unit j0 + e % 4) of both layers
+  const int eb = tid >> 2, ej = j0 + (tid & 3), eu = tid & 3;
+  const bool eown = eb < B;
+  // a timed-out barrier: NaN over everything this workgroup owns (its h / c of every step
+  // and layer), the device fault word set once per workgroup, then the workgroup exits
+  auto fail = [&]() {
+    const float nan = __builtin_nanf("");
+    if (eown)
+      for (int t = 0; t < T; ++t) {
+        a.h0[(int64_t)eb * a.h0_ldb + (int64_t)t * a.h0_ldt + ej] = nan;
+        a.c0[((int64_t)eb * T + t) * H + ej] = nan;
+        if (TWO) {
+          a.h1[((int64_t)eb * T + t) * H + ej] = nan;
+          a.c1[((int64_t)eb * T + t) * H + ej] = nan;
+        }
+      }
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
 
   // ---- start: census of workgroups per XCC (the barrier's groups)
   if (tid == 0) {
@@ -444,11 +471,11 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
     }
   }
   __syncthreads();
-  if (*status != 0) return;
+  if (*status != 0) {
+    fail();
+    return;
+  }
 
-  // epilogue ownership: thread e owns (batch row e / 4, unit j0 + e % 4) of both layers
-  const int eb = tid >> 2, ej = j0 + (tid & 3), eu = tid & 3;
-  const bool eown = eb < B;
   float bias1[4] = {0.f, 0.f, 0.f, 0.f};
   if (TWO && eown)
 #pragma unroll
@@ -540,7 +567,10 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
       a.h0[0] = 0.f;                                                  // keep the products live
     }
     if (LP_ABLATE == 1) __syncthreads();
-    else if (t < last && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, census, status, t)) return;
+    else if (t < last && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, census, status, t)) {
+      fail();
+      return;
+    }
   }
   store_outputs(last);                                               // the final iteration's outputs
 }
@@ -576,7 +606,8 @@ void launch_persist(PArgs& a, void* workspace, hipStream_t stream) {
   a.hk1 = TWO ? a.hk0 + (int64_t)a.T * a.B * HH : nullptr;
   a.hk0b = reinterpret_cast<__bf16*>(a.hk0);
   a.hk1b = TWO ? a.hk0b + (int64_t)a.T * a.B * HH : nullptr;
-  a.timeout_ticks = 100000000;  // 1 s of s_memrealtime (100 MHz) per wait: a safety net, never a schedule
+  // 1 s of s_memrealtime (100 MHz) per wait: a safety net, never a schedule
+  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
   hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO, BF>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO, BF>()), stream,
                      a);
 }
@@ -687,4 +718,29 @@ extern "C" int autovc_lstm2_persist_status(const void* workspace, hipStream_t st
                          stream), "autovc_lstm2_persist_status");
   AVC_HIP(hipStreamSynchronize(stream), "autovc_lstm2_persist_status");
   return err;
+}
+
+// test hook: the spin budget of the persistent launches in s_memrealtime ticks (0 = 1 s)
+extern "C" int autovc_lstm_persist_set_timeout_ticks(int ticks) {
+  AVC_CHECK_ARG(ticks >= 0, "autovc_lstm_persist_set_timeout_ticks: ticks must be >= 0");
+  g_timeout_ticks = ticks;
+  return avc::kOk;
+}
+
+// The device fault word (bit 0: a persistent LSTM launch's grid barrier timed out) after
+// everything queued on `stream`; synchronises the stream.  clear != 0 resets it.
+extern "C" int autovc_fault_status(hipStream_t stream, int clear, int* out) {
+  AVC_CHECK_ARG(out != nullptr, "autovc_fault_status: null out");
+  int v = 0;
+  AVC_HIP(hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_avc_fault), sizeof(int), 0, hipMemcpyDeviceToHost, stream),
+          "autovc_fault_status");
+  AVC_HIP(hipStreamSynchronize(stream), "autovc_fault_status");
+  if (clear && v) {
+    const int zero = 0;
+    AVC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_avc_fault), &zero, sizeof(int), 0, hipMemcpyHostToDevice, stream),
+            "autovc_fault_status");
+    AVC_HIP(hipStreamSynchronize(stream), "autovc_fault_status");
+  }
+  *out = v;
+  return avc::kOk;
 }

@@ -14,9 +14,15 @@ one captured HIP graph (autovc_amd.graph): collectives are kept OUT of that grap
 under stream capture is not exercised on the single-GPU boxes this build is tested on),
 which is why the exchange cannot start inside the backward in graph mode.
 
-Exchange precision: fp32 (113.7 MB per step) by default; `grad_dtype=torch.bfloat16`
-halves the bytes (56.8 MB) for BASELINE config 3 — the rank sum is then
-rounded to bf16 (the mean gradient loses the low 16 bits of its mantissa).
+Exchange precision: fp32 (113.7 MB per step, one ring all-reduce per bucket) or bf16
+(BASELINE config 3) with fp32 accumulation: each rank rounds its bucket to
+bf16 once, an all-to-all hands rank r the r-th shard of every rank's bucket, rank r sums
+those N shards in fp32 in rank order (deterministic, identical on every rank) and scales
+by 1/N, and an all-gather returns the mean rounded to bf16 once.  Two roundings whatever
+N is (a bf16 ring all-reduce would round at every one of its N-1 hops), and
+(N-1)/N x 56.8 MB x 2 on the wire per rank instead of (N-1)/N x 113.7 MB x 2.
+`make_data_parallel(grad_dtype="auto")` (the default) picks bf16 while the Solver runs
+under precision "bf16" and fp32 otherwise.
 """
 from __future__ import annotations
 
@@ -63,16 +69,71 @@ def _buckets(n, bucket_bytes):
     return [(s, min(nb, n - s)) for s in range(0, n, nb)]
 
 
-def _issue(chunk, grad_dtype):
-    buf = chunk if grad_dtype is None or grad_dtype == chunk.dtype else chunk.to(grad_dtype)
-    return buf, dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True)
+class _Bf16Mean:
+    """Mean of one fp32 bucket over the ranks, exchanged as bf16 and accumulated in fp32
+    (module docstring).  issue() starts the all-to-all, reduce() sums this rank's shard and
+    starts the all-gather, finish() writes the mean back into the fp32 bucket."""
+
+    def __init__(self, chunk, world):
+        self.chunk, self.world = chunk, world
+        n = chunk.numel()
+        self.shard = (n + world - 1) // world
+        self.shard = (self.shard + 7) // 8 * 8          # 16-byte aligned bf16 shards
+        padded = self.shard * world
+        self.send = torch.zeros(padded, dtype=torch.bfloat16, device=chunk.device)
+        self.send[:n].copy_(chunk)
+        self.recv = torch.empty_like(self.send)
+        self.work = dist.all_to_all_single(self.recv, self.send, async_op=True)
+
+    def reduce(self):
+        self.work.wait()
+        parts = self.recv.view(self.world, self.shard)
+        acc = parts[0].float()
+        for r in range(1, self.world):                  # fixed rank order
+            acc.add_(parts[r].float())
+        mine = acc.mul_(1.0 / self.world).to(torch.bfloat16)
+        self.gathered = torch.empty_like(self.send)
+        self.work = dist.all_gather_into_tensor(self.gathered, mine, async_op=True)
+
+    def finish(self):
+        self.work.wait()
+        self.chunk.copy_(self.gathered[:self.chunk.numel()])
 
 
-def _finish(chunk, buf, work, world):
-    work.wait()
-    if buf is not chunk:
-        chunk.copy_(buf)
-    chunk.mul_(1.0 / world)
+class _Fp32Mean:
+    """Mean of one fp32 bucket: one all-reduce (sum) in place, then x 1/N."""
+
+    def __init__(self, chunk, world):
+        self.chunk, self.world = chunk, world
+        self.work = dist.all_reduce(chunk, op=dist.ReduceOp.SUM, async_op=True)
+
+    def reduce(self):
+        pass
+
+    def finish(self):
+        self.work.wait()
+        self.chunk.mul_(1.0 / self.world)
+
+
+def _exchange(grad_dtype):
+    if grad_dtype is None or grad_dtype == torch.float32:
+        return _Fp32Mean
+    if grad_dtype == torch.bfloat16:
+        return _Bf16Mean
+    raise ValueError(f"gradient exchange dtype must be float32 or bfloat16, got {grad_dtype}")
+
+
+def _run_exchange(items, grad_dtype, world, after=None):
+    """items: (key, fp32 chunk) pairs.  Every bucket's first collective is issued before
+    any is waited on; `after(key)` runs as each bucket's mean lands (the Adam slice)."""
+    cls = _exchange(grad_dtype)
+    ex = [(k, cls(chunk, world)) for k, chunk in items]
+    for _, e in ex:
+        e.reduce()
+    for k, e in ex:
+        e.finish()
+        if after is not None:
+            after(k)
 
 
 def allreduce_gradients(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None):
@@ -83,13 +144,8 @@ def allreduce_gradients(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype
         return
     from .functional import join_grad_stream   # weight gradients may still be in flight
     join_grad_stream()
-    pending = []
-    for flat in optimizer.flat_grads():
-        for s, c in _buckets(flat.numel(), bucket_bytes):
-            chunk = flat[s:s + c]
-            pending.append((chunk, *_issue(chunk, grad_dtype)))
-    for chunk, buf, work in pending:
-        _finish(chunk, buf, work, world)
+    items = [(None, flat[s:s + c]) for flat in optimizer.flat_grads() for s, c in _buckets(flat.numel(), bucket_bytes)]
+    _run_exchange(items, grad_dtype, world)
 
 
 def reduce_and_step(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None):
@@ -104,26 +160,27 @@ def reduce_and_step(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=Non
             if f is not None:
                 optimizer.update_range(gi, 0, f["p"].numel())
         return
-    pending = []
-    for gi, f in enumerate(optimizer._flat):
-        if f is None:
-            continue
-        flat = f["g"]
-        for s, c in _buckets(flat.numel(), bucket_bytes):
-            chunk = flat[s:s + c]
-            pending.append((gi, s, c, chunk, *_issue(chunk, grad_dtype)))
-    for gi, s, c, chunk, buf, work in pending:
-        _finish(chunk, buf, work, world)
-        optimizer.update_range(gi, s, c)
+    items = [((gi, s, c), f["g"][s:s + c]) for gi, f in enumerate(optimizer._flat) if f is not None
+             for s, c in _buckets(f["g"].numel(), bucket_bytes)]
+    _run_exchange(items, grad_dtype, world, after=lambda k: optimizer.update_range(*k))
 
 
-def make_data_parallel(solver, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None, overlap=True):
+def make_data_parallel(solver, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype="auto", overlap=True):
     """Attach the gradient exchange to an autovc_amd Solver and sync its initial weights.
-    overlap=True: reduce_and_step (bucketed all-reduce interleaved with the Adam update);
-    overlap=False: allreduce_gradients after backward, then one Adam launch."""
+    overlap=True: reduce_and_step (bucketed exchange interleaved with the Adam update);
+    overlap=False: allreduce_gradients after backward, then one Adam launch.
+    grad_dtype "auto": bf16 while solver.precision is "bf16" (BASELINE config 3), else fp32;
+    or torch.float32 / torch.bfloat16 for a fixed exchange precision."""
     broadcast_parameters(solver.g_optimizer)
+
+    def dtype():
+        if grad_dtype == "auto":
+            return torch.bfloat16 if getattr(solver, "precision", "fp32") == "bf16" else torch.float32
+        return grad_dtype
+
     if overlap:
-        solver._optimizer_step = lambda: reduce_and_step(solver.g_optimizer, bucket_bytes, grad_dtype)
+        solver._optimizer_step = lambda: reduce_and_step(solver.g_optimizer, bucket_bytes, dtype())
     else:
-        solver._after_backward = lambda: allreduce_gradients(solver.g_optimizer, bucket_bytes, grad_dtype)
+        solver._after_backward = lambda: allreduce_gradients(solver.g_optimizer, bucket_bytes, dtype())
+    solver._ddp_grad_dtype = dtype
     return solver

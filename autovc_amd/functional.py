@@ -697,6 +697,26 @@ def lstm2_persistent(B, H):
     return _PERSIST_ON and bool(_lib.load().autovc_lstm2_persist_supported(B, H))
 
 
+class DeviceFault(RuntimeError):
+    """A kernel reported a failure through the device fault word (autovc_fault_status)."""
+
+
+def check_device_faults(device=None):
+    """Raise DeviceFault if a persistent LSTM launch's grid barrier timed out since the
+    last check (the launch then wrote NaN over its h / c, so the losses are NaN too).
+    Synchronises the current stream: called at the Solver's log steps and by bench.py,
+    never per iteration."""
+    import ctypes
+    v = ctypes.c_int(0)
+    _lib.call("autovc_fault_status", _lib.stream_ptr(device), 1, ctypes.byref(v))
+    if v.value & 1:
+        raise DeviceFault(
+            "lstm_persist_kernel (decoder lstm2 forward): a grid barrier timed out — its 256 workgroups were "
+            "not all resident at once (another process's kernels held part of the GPU?); the forward's h/c were "
+            "overwritten with NaN.  Run one training process per GPU (INTEGRATION.md, Co-residency) or set "
+            "AVC_LSTM2_PERSIST=0.")
+
+
 # the single-layer recurrence (decoder lstm1, H = 512) the same way — opt-in
 # (AVC_LSTM_PERSIST=1): at H = 512 the grid barrier costs what the launch boundary did
 # (6.58 vs 6.75 us per step, profiles/r02/lstm_persist_ab.txt; 16.47-16.50 vs 16.49-16.55 ms

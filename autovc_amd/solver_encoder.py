@@ -169,10 +169,9 @@ class Solver(object):
         scalars (g_loss, loss_id, loss_id_psnt, loss_cd); nothing synchronises.  With
         `hip_graph` the forward+backward is a graph replay (its outputs are the graph's
         static tensors, overwritten by the next step)."""
-        # the captured step is validated (bit-identical to eager, tests/test_solver_gpu.py)
-        # with the weight-gradient side stream only: with AVC_GRAD_STREAM=0 replays gave
-        # run-to-run different losses on the GPU, so that diagnostic mode runs eagerly
-        if self.hip_graph and AF._GRAD_STREAM_ON:
+        # the captured step is bit-identical to eager with the weight-gradient side stream on
+        # and off (tests/test_solver_gpu.py::test_hip_graph_step_bit_identical)
+        if self.hip_graph:
             if self._graphs is None:
                 from .graph import StepGraphs
                 self._graphs = StepGraphs(self._forward_backward, self.G)
@@ -235,6 +234,7 @@ class Solver(object):
                 print("The current convtas learning rate:", lr)
 
             if (i + 1) % self.log_step == 0:
+                AF.check_device_faults(self.device)   # raises if a persistent launch failed
                 loss = {"G/loss_id": g_loss_id.item(), "G/loss_id_psnt": g_loss_id_psnt.item(),
                         "G/loss_cd": g_loss_cd.item()}
                 self.loss = loss
@@ -259,4 +259,5 @@ class Solver(object):
                                      "g_loss_id_psnt": loss["G/loss_id_psnt"], "g_loss_cd": loss["G/loss_cd"],
                                      "g_loss_SISNR": float("nan")})
                 _barrier()
+        AF.check_device_faults(self.device)
         return self

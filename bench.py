@@ -498,6 +498,23 @@ def _cpu_step(B, T, threads, seconds):
                       f"{s:.2f} s/step), torch {torch.__version__} CPU, {threads} threads"}
 
 
+def spawn_ranks(n):
+    """Run this script as n ranks of one node (torch.distributed.run, one process per GPU,
+    rendezvous on 127.0.0.1) and return the worst exit status.  Called before anything
+    initialises HIP in this process (importing torch does not)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -515,12 +532,26 @@ def main():
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
                     help="precision of the headline measurement (default fp32 = BASELINE config 2)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` outside torchrun: start the N ranks here, before this
+        # process touches the GPU, and exit with their status (rank 0 prints the line)
+        sys.exit(spawn_ranks(args.gpus))
 
-    from autovc_amd import ddp
     # test hook (tests/test_bench_multirank, 1-GPU boxes): every rank on cuda:0 over gloo, to
-    # exercise the N > 1 flow (sharding, barriers, max-over-ranks timing) without 2 GPUs
+    # exercise the N > 1 flow (sharding, barriers, max-over-ranks timing) without 2 GPUs.
+    # The persistent lstm2 forward needs every CU to itself (all 256 workgroups co-resident,
+    # INTEGRATION.md "Co-residency"): two processes' grids on one device could each hold
+    # part of the chip, so ranks sharing a device use the per-step launches.
     share = os.environ.get("AVC_BENCH_SHARE_DEVICE") == "1"
+    if share:
+        os.environ["AVC_LSTM2_PERSIST"] = "0"
+    from autovc_amd import ddp
     rank, world = ddp.init_from_env(backend="gloo" if share else None)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s)", file=sys.stderr)
+        sys.exit(3)
     local = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -529,7 +560,9 @@ def main():
 
     solver = make_solver(dev, B)
     if world > 1:
-        ddp.make_data_parallel(solver)
+        # fp32 exchange for the fp32 headline (config 2 numerics), bf16 with fp32
+        # accumulation while the bf16 object runs (config 3): grad_dtype "auto"
+        ddp.make_data_parallel(solver, grad_dtype="auto")
     solver.G.train()
     solver.precision = args.precision
     solver.hip_graph = not args.no_graph
@@ -547,6 +580,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
+    from autovc_amd import functional as AF
+    AF.check_device_faults(dev)      # a co-residency failure of a persistent launch raises here
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -577,10 +612,12 @@ def main():
         solver.precision = "bf16"
         timed_steps(max(2, args.warmup // 2))
         dtb, lb = timed_steps(args.steps)
+        AF.check_device_faults(dev)
         solver.precision = args.precision
         bf = {"value": round(world * B * T * args.steps / dtb, 1), "unit": "mel-frames/s",
               "ms_per_step": round(dtb / args.steps * 1000, 3), "dtype": "bf16 MFMA operands, fp32 accumulate",
               "final_loss": round(float(lb[0].item()), 6),
+              "grad_exchange": None if world == 1 else "bf16 all-to-all + fp32 shard sums + bf16 all-gather",
               "note": "BASELINE config 3 precision; the headline value above is config 2 (fp32)"}
 
     roof = blstm = None

@@ -252,6 +252,16 @@ int autovc_lstm_fwd_persist_f32(int B, int T, int H, const float* gx, int64_t gx
                                 const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                                 float* gates, void* workspace, hipStream_t stream);
 int autovc_lstm2_persist_status(const void* workspace, hipStream_t stream);
+/* Co-residency failures reach the caller without a per-call sync: a persistent launch
+ * whose grid barrier timed out writes NaN over the h / c it owns (so the loss turns NaN)
+ * and sets bit 0 of a sticky per-device fault word.  autovc_fault_status (synchronises
+ * `stream`) returns the word in *out and resets it when clear != 0; the Solver and
+ * bench.py check it at their sync points and raise.  No reference counterpart (the
+ * reference's nn.LSTM has no grid barrier). */
+int autovc_fault_status(hipStream_t stream, int clear, int* out);
+/* Test hook: the persistent launches' spin budget in s_memrealtime ticks (100 MHz); 0
+ * restores the default of 1 s.  A tiny value forces the timeout path. */
+int autovc_lstm_persist_set_timeout_ticks(int ticks);
 /* autovc_lstm_fwd_f32 with every step launch timed by its own dispatch events;
  * synchronises; *avg_us (HOST pointer) = mean kernel time of steps 1..T-1 (bench.py). */
 int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_ldb,

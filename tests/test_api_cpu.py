@@ -94,3 +94,15 @@ def test_solver_refuses_cpu():
                                 num_iters=1, ema=0.9999, run_name="x", model_type="spmel", log_step=1)
     with pytest.raises(RuntimeError, match="MI355X"):
         Solver(None, cfg)
+
+
+def test_bench_rank_count_mismatch_exits_nonzero():
+    """bench.py under a launcher that started fewer ranks than --gpus asks for refuses to
+    report (exit 3) instead of labelling a 1-rank number as N GPUs."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1")     # a launcher's env: no self-spawn
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 3, out.stderr[-2000:]
+    assert "process group has 1 rank" in out.stderr
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

@@ -25,3 +25,23 @@ def test_bench_two_ranks_one_json_line():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 128
     assert d["value"] > 0 and d["steps"] == 2 and d["scaling"] == "weak"
+
+
+def test_plain_bench_gpus2_spawns_two_ranks():
+    """`python bench.py --gpus 2` (no torchrun around it, the driver's command shape) starts
+    its two ranks itself and reports them; the bf16 object runs with the bf16 gradient
+    exchange (all-to-all + fp32 shard sums + all-gather)."""
+    env = dict(os.environ, AVC_BENCH_SHARE_DEVICE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "2", "--no-wavenet", "--no-e2e",
+           "--no-cpu-baseline", "--no-roofline"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 128
+    assert d["value"] > 0 and d["bf16"]["value"] > 0
+    assert d["bf16"]["grad_exchange"].startswith("bf16")
+    assert d["final_loss"] == d["final_loss"] and d["bf16"]["final_loss"] == d["bf16"]["final_loss"]   # not NaN

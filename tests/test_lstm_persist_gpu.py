@@ -145,3 +145,36 @@ def test_bf16_persistent_matches_bf16_per_step_launches(cuda, T):
         # summation order moves a bf16 rounding of h now and then: bounded, and rare
         assert d.max().item() < 2e-2 * max(r.abs().max().item(), 1e-30), (name, d.max().item())
         assert d.mean().item() < 1e-4 * max(r.abs().max().item(), 1e-30), (name, d.mean().item())
+
+
+def test_barrier_timeout_surfaces_as_error(cuda):
+    """A persistent launch whose grid barrier times out (forced with a 1-tick spin budget)
+    must not let training continue on garbage: its h / c become NaN (so the losses do) and
+    check_device_faults raises DeviceFault naming the kernel; the fault word is then clear
+    and the next step with the normal budget is finite again."""
+    import bench
+    from autovc_amd import _lib, functional as AF
+    B, H = 64, 1024
+    if not _supported(B, H):
+        pytest.skip("persistent lstm2 needs one CU per workgroup on this device")
+    AF.check_device_faults(cuda)                 # nothing pending from earlier tests
+    torch.manual_seed(0)
+    solver = bench.make_solver(cuda, B)
+    solver.G.train()
+    x, e = bench.synthetic_batch(B, 32, cuda, 5)
+    _lib.call("autovc_lstm_persist_set_timeout_ticks", 1)
+    try:
+        losses = solver.train_step(x, e)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("autovc_lstm_persist_set_timeout_ticks", 0)
+    assert not bool(torch.isfinite(losses[1]).item())          # loss_id went through the NaN h
+    with pytest.raises(AF.DeviceFault, match="lstm_persist_kernel"):
+        AF.check_device_faults(cuda)
+    AF.check_device_faults(cuda)                 # cleared by the raising check
+    torch.manual_seed(0)
+    solver = bench.make_solver(cuda, B)
+    solver.G.train()
+    losses = solver.train_step(x, e)
+    assert bool(torch.isfinite(torch.stack([v.reshape(()) for v in losses])).all())
+    AF.check_device_faults(cuda)

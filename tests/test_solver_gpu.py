@@ -96,28 +96,39 @@ def test_grad_side_stream_bit_identical(cuda):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B", [8, 64])
+@pytest.mark.parametrize("grad_stream", [True, False])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_hip_graph_step_bit_identical(cuda, precision):
+def test_hip_graph_step_bit_identical(cuda, precision, grad_stream, B):
     """Solver(hip_graph=True) replays the captured forward+backward: three steps (the first
     captures) give bit-identical losses, parameters and BatchNorm running stats to eager,
-    and a second input batch of the same shape is picked up by the replay."""
+    and a second input batch of the same shape is picked up by the replay — with the
+    weight-gradient side stream on and off (AVC_GRAD_STREAM), and at B=64, where the
+    persistent lstm2 forward is in the graph."""
     import bench
+    from autovc_amd import functional as AF
     res = []
-    for graph in (False, True):
-        torch.manual_seed(0)
-        solver = bench.make_solver(cuda, 8)
-        solver.G.train()
-        solver.precision = precision
-        solver.hip_graph = graph
-        xa, ea = bench.synthetic_batch(8, 128, cuda, 99)
-        xb, eb = bench.synthetic_batch(8, 128, cuda, 100)
-        losses = []
-        for x, e in ((xa, ea), (xb, eb), (xa, ea)):
-            out = solver.train_step(x, e)
-            losses.append(torch.stack([o.detach().reshape(()) for o in out]).clone())
-        torch.cuda.synchronize()
-        res.append((losses, [f.clone() for f in solver.g_optimizer.flat_params()],
-                    [b.clone() for b in solver.G.buffers()]))
+    prev = AF._GRAD_STREAM_ON
+    try:
+        AF._GRAD_STREAM_ON = grad_stream
+        for graph in (False, True):
+            torch.manual_seed(0)
+            solver = bench.make_solver(cuda, B)
+            solver.G.train()
+            solver.precision = precision
+            solver.hip_graph = graph
+            xa, ea = bench.synthetic_batch(B, 128, cuda, 99)
+            xb, eb = bench.synthetic_batch(B, 128, cuda, 100)
+            losses = []
+            for x, e in ((xa, ea), (xb, eb), (xa, ea)):
+                out = solver.train_step(x, e)
+                losses.append(torch.stack([o.detach().reshape(()) for o in out]).clone())
+            torch.cuda.synchronize()
+            res.append((losses, [f.clone() for f in solver.g_optimizer.flat_params()],
+                        [b.clone() for b in solver.G.buffers()]))
+            del solver
+    finally:
+        AF._GRAD_STREAM_ON = prev
     (la, pa, ba), (lb, pb, bb) = res
     for a, b in zip(la, lb):
         assert torch.equal(a, b)
