@@ -87,7 +87,13 @@ class SpeakerCropSampler(data.Sampler):
 def get_loader(root_dir, batch_size=16, len_crop=128, model_type="spmel", num_workers=0, rank=None, world=None,
                seed=0):
     """data_loader.py:90-102 (shuffle, drop_last, seeded workers).  With rank/world (and
-    world > 1) the batches come from a per-rank `SpeakerCropSampler` instead."""
+    world > 1) the batches come from a per-rank `SpeakerCropSampler` instead.  rank/world
+    not given: taken from a launcher's environment (torchrun's RANK / WORLD_SIZE), so
+    main.py's unchanged call `get_loader(main_dir, batch_size, len_crop, model_type)`
+    (main.py:36) shards under torchrun."""
+    if world is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
     dataset = Utterances(root_dir, len_crop, model_type)
     sampler = None
     if world is not None and world > 1:

@@ -42,7 +42,8 @@ def init_from_env(backend=None):
     if world <= 1:
         return 0, 1
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # AVC_DIST_BACKEND: test hook (gloo ranks sharing one GPU of a 1-GPU box)
+        backend = os.environ.get("AVC_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend == "nccl":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))

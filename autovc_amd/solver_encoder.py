@@ -101,13 +101,21 @@ class Solver(object):
 
         self.path = "chkpnt_" + self.model_type + "_" + self.run_name + ".ckpt"
         self.file_exists = os.path.exists(self.path)
-        self.logger = _make_logger(config, self.file_exists) if _rank() == 0 else _NoLogger()
 
         if not torch.cuda.is_available():
             raise RuntimeError("autovc_amd.Solver trains on the MI355X only (no CPU fallback)")
+        # data parallel under a launcher (torchrun: WORLD_SIZE > 1): one process per GPU, the
+        # process group is created here (RCCL, device = LOCAL_RANK) so that main.py's
+        # unchanged `Solver(vcc_loader, config).train()` (main.py:39-40) trains on every rank
+        # with the gradient exchange of autovc_amd.ddp; get_loader shards from the same env
+        from . import ddp
+        self.world = ddp.init_from_env()[1]
+        self.logger = _make_logger(config, self.file_exists) if _rank() == 0 else _NoLogger()
         self.device = torch.device("cuda", torch.cuda.current_device())
         print("Training on GPU.")
         self.build_model()
+        if self.world > 1:
+            ddp.make_data_parallel(self)      # rank 0's weights everywhere, then bucketed exchange
 
     def build_model(self):
         if self.model_type == "spmel":

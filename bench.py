@@ -558,11 +558,11 @@ def main():
     torch.manual_seed(0)
     B, T = args.batch, args.frames
 
+    # world > 1: the Solver joins the process group and attaches the gradient exchange
+    # itself (ddp.make_data_parallel, grad_dtype "auto": fp32 for the fp32 headline = config 2
+    # numerics, bf16 with fp32 accumulation while the bf16 object runs = config 3)
     solver = make_solver(dev, B)
-    if world > 1:
-        # fp32 exchange for the fp32 headline (config 2 numerics), bf16 with fp32
-        # accumulation while the bf16 object runs (config 3): grad_dtype "auto"
-        ddp.make_data_parallel(solver, grad_dtype="auto")
+    assert world == 1 or solver.world == world
     solver.G.train()
     solver.precision = args.precision
     solver.hip_graph = not args.no_graph

@@ -156,3 +156,39 @@ def test_model_ema_matches_reference_formula(cuda, tmp_path, monkeypatch):
     got = torch.cat([p.detach().reshape(-1) for p in s.G.parameters()])
     assert torch.equal(got, want)
     assert (got - flat).abs().max().item() <= 2e-7 * flat.abs().max().item()   # ~p, as in the reference
+
+
+def test_main_py_under_torchrun_trains_data_parallel(cuda, tmp_path):
+    """main.py unchanged under torchrun: two ranks sharing cuda:0 over
+    gloo (AVC_DIST_BACKEND=gloo; the driver's nodes use RCCL, one GPU per rank) run
+    main.py's get_loader + Solver(...).train() with no data-parallel code of their own.
+    get_loader shards from RANK/WORLD_SIZE (each rank draws different crops), the Solver
+    joins the process group and exchanges gradients, so the ranks' parameters stay
+    bit-identical; only rank 0 writes the checkpoint."""
+    import json
+    import socket
+    import subprocess
+    main_dir = str(tmp_path / "corpus")
+    _corpus(main_dir)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, AVC_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tests", "ddp_main_worker.py"), main_dir,
+           str(tmp_path)]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-3000:]
+    p = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2)]
+    info = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    for r in range(2):
+        assert info[r]["sampler"] == "SpeakerCropSampler" and info[r]["rank"] == r and info[r]["world"] == 2
+        assert info[r]["solver_world"] == 2
+    assert info[0]["saves"] == ["chkpnt_spmel_ddpmain.ckpt"] * 2 and info[1]["saves"] == []
+    for a, b in zip(*p):
+        assert torch.equal(a, b)
+    ck = torch.load(tmp_path / "chkpnt_spmel_ddpmain.ckpt", map_location="cpu", weights_only=True)
+    assert ck["epoch"] == 4 and all(np.isfinite(v) for v in ck["loss"].values())
