@@ -799,7 +799,8 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
     // alternating; AVC_GEMM_BATCHED_CFG=<id> overrides
     static const int wino_cfg = [] {
       const char* e = getenv("AVC_GEMM_BATCHED_CFG");
-      return e ? atoi(e) : 9;
+      const int v = e ? atoi(e) : 9;
+      return (v >= 0 && v < (int)(sizeof(kCfg) / sizeof(kCfg[0]))) ? v : 9;   // out of range: the default
     }();
     cfg = g_force_cfg >= 0 ? kCfg[g_force_cfg] : t128 >= 512 ? kCfg[wino_cfg] : kCfg[8];
   }

@@ -297,8 +297,18 @@ class WaveNet(nn.Module):
         # starts at one of chunk / graph_steps (ring slot, chunk row) pairs, so a few cached
         # graphs, whose step kernels get both as static arguments, serve the whole sequence
         graph_steps = int(graph_steps or 0)
-        if chunk is None:
-            chunk = math.lcm(ring, graph_steps) if graph_steps else max(1, (1 << 30) // (B * nG * 4))
+        cap = max(1, (1 << 30) // (B * nG * 4))          # <= 1 GiB of conditioning per chunk
+        if graph_steps:
+            # a multiple of lcm(ring, graph_steps): a graph-step count sharing few factors
+            # with the ring makes that lcm large, so it is capped (graphs then recapture
+            # at the chunk seams instead of holding a multi-GiB chunk)
+            unit = math.lcm(ring, graph_steps)
+            want = unit if chunk is None else max(unit, (int(chunk) + unit - 1) // unit * unit)
+            if want > cap:
+                want = max(graph_steps, cap // graph_steps * graph_steps)
+            chunk = want
+        elif chunk is None:
+            chunk = cap
         chunk = min(chunk, T)
         pre = torch.empty(chunk, B, nG, device=dev, dtype=torch.float32)
         y = torch.empty(B, T, device=dev, dtype=torch.float32)
