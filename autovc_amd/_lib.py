@@ -29,7 +29,7 @@ _RESTYPES = {"autovc_last_error": ctypes.c_char_p,
              "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_lstm2_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
              "autovc_colsum_workspace_floats": c_i64, "autovc_wavenet_packed_floats": c_i64, "autovc_wavenet_ring_frames": c_i64,
              "autovc_wavenet_workspace_bytes": c_i64, "autovc_lstm2_persist_workspace_bytes": c_i64,
-             "autovc_lstm_persist_workspace_bytes": c_i64}
+             "autovc_lstm_persist_workspace_bytes": c_i64, "autovc_wino5_rows": c_i64}
 
 
 def sig(name: str, *argtypes):
@@ -55,6 +55,20 @@ sig("autovc_wino5_input_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr)
 sig("autovc_wino5_output_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_i64, c_ptr)
 sig("autovc_wino5_dy_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr)
 sig("autovc_wino5_wgrad_f32", c_int, c_int, c_ptr, c_ptr, c_int, c_ptr)
+sig("autovc_wino5_rows", c_int, c_int)
+sig("autovc_wino5_input_bn_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_ptr)
+sig("autovc_wino5_output_stats_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr)
+sig("autovc_wino5_output_bnbwd_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_i64, c_ptr,
+    c_ptr)
+sig("autovc_wino5_bnbwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
+    c_ptr, c_ptr)
+sig("autovc_bn_finalize_f32", c_int, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_f32, c_ptr, c_ptr)
+sig("autovc_bn_coef_f32", c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_ptr, c_ptr)
+sig("autovc_bn_partial_rows", c_i64)
+sig("autovc_bn_bwd_partial_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_ptr)
+sig("autovc_bn_bwd_finalize_f32", c_int, c_int, c_ptr, c_ptr, c_f32, c_ptr, c_ptr, c_ptr, c_int, c_ptr)
+sig("autovc_colsum_f64_finalize_f32", c_int, c_int, c_ptr, c_ptr, c_int, c_ptr)
 sig("autovc_gemm_f32", c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,

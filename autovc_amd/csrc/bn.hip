@@ -195,6 +195,71 @@ __global__ __launch_bounds__(256) void bwd_apply_kernel(int64_t M, int C, const 
   }
 }
 
+// ---- fused Conv-BN chain (winograd.hip's wino_output_stats_kernel partials) ----------
+// raw fp64 sums (sum y, sum y^2) of RS row blocks -> mean, biased var, running stats, and
+// the coefficients the consumers apply on load: coef = [alpha | shift | mean | invstd],
+// alpha = gamma invstd, shift = beta - mean alpha (apply_kernel's arithmetic)
+__global__ __launch_bounds__(256) void stats_finalize_raw_kernel(int64_t M, int C, const double* __restrict__ part,
+                                                                int RS, const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps,
+                                                                float* __restrict__ mean, float* __restrict__ var,
+                                                                float* __restrict__ coef, float* __restrict__ run_mean,
+                                                                float* __restrict__ run_var, float momentum,
+                                                                int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double a, b;
+  sum_partials(part, RS, C, c, a, b);
+  if (threadIdx.x >= 64) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  const double n = (double)M;
+  const double mu = a / n;
+  double v = b / n - mu * mu;
+  if (v < 0.0) v = 0.0;
+  const float muf = (float)mu, vf = (float)v;
+  mean[c] = muf;
+  var[c] = vf;
+  const float invstd = 1.0f / sqrtf(vf + eps);
+  const float alpha = invstd * (gamma ? gamma[c] : 1.f);
+  coef[c] = alpha;
+  coef[C + c] = (beta ? beta[c] : 0.f) - muf * alpha;
+  coef[2 * C + c] = muf;
+  coef[3 * C + c] = invstd;
+  if (run_mean) run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mu);
+  if (run_var) run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * v * n / (n > 1.0 ? n - 1.0 : 1.0));
+}
+
+// eval mode: the same coefficients from the running statistics
+__global__ void coef_kernel(int C, const float* __restrict__ mean, const float* __restrict__ var,
+                            const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                            float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.0f / sqrtf(var[c] + eps);
+  const float alpha = invstd * (gamma ? gamma[c] : 1.f);
+  coef[c] = alpha;
+  coef[C + c] = (beta ? beta[c] : 0.f) - mean[c] * alpha;
+  coef[2 * C + c] = mean[c];
+  coef[3 * C + c] = invstd;
+}
+
+// column sums of RS fp64 partial rows (the fused conv bias gradient), fixed order
+__global__ __launch_bounds__(256) void colsum_f64_finalize_kernel(int C, int RS, const double* __restrict__ part,
+                                                                 float* __restrict__ out, int accumulate) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (c < C)
+#pragma unroll 8
+    for (int rs = w; rs < RS; rs += 4) s += part[(int64_t)rs * C + c];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+  const float v = (float)(((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+  out[c] = accumulate ? out[c] + v : v;
+}
+
 // 2-D grid of the apply kernels: 64-channel column tiles x row groups (~8 rows per thread)
 dim3 grid2d(int64_t M, int C) {
   const int64_t ry = std::max<int64_t>(1, std::min<int64_t>((M + 31) / 32, 4096));
@@ -249,5 +314,56 @@ extern "C" int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t 
   hipLaunchKernelGGL(bwd_apply_kernel, grid2d(M, C), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y, ldy,
                      mean, var, gamma, eps, act, (const float*)sums, dy, lddy);
   AVC_CHECK_LAUNCH("autovc_bn_act_bwd_f32");
+  return avc::kOk;
+}
+
+// ------------------------------------------------------------------ fused Conv-BN chain
+extern "C" int autovc_bn_finalize_f32(int RS, int64_t M, int C, const double* part, const float* gamma,
+                                      const float* beta, float eps, float* mean, float* var, float* coef,
+                                      float* running_mean, float* running_var, float momentum, int64_t* num_batches,
+                                      hipStream_t stream) {
+  AVC_CHECK_ARG(RS > 0 && M > 0 && C > 0 && part && mean && var && coef, "autovc_bn_finalize_f32: bad args");
+  hipLaunchKernelGGL(stats_finalize_raw_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, M, C, part, RS, gamma,
+                     beta, eps, mean, var, coef, running_mean, running_var, momentum, num_batches);
+  AVC_CHECK_LAUNCH("autovc_bn_finalize_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_coef_f32(int C, const float* mean, const float* var, const float* gamma, const float* beta,
+                                  float eps, float* coef, hipStream_t stream) {
+  AVC_CHECK_ARG(C > 0 && mean && var && coef, "autovc_bn_coef_f32: bad args");
+  hipLaunchKernelGGL(coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, mean, var, gamma, beta, eps, coef);
+  AVC_CHECK_LAUNCH("autovc_bn_coef_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_partial_rows(int64_t M) { return (int)std::min<int64_t>(kRowSplits, M); }
+
+extern "C" int autovc_bn_bwd_partial_f32(int64_t M, int C, const float* dz, int64_t lddz, const float* z, int64_t ldz,
+                                         const float* y, int64_t ldy, const float* mean, int act, double* part,
+                                         hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && C > 0 && dz && y && mean && part, "autovc_bn_bwd_partial_f32: bad args");
+  AVC_CHECK_ARG(act == kNone || z, "autovc_bn_bwd_partial_f32: activation backward needs the output z");
+  hipLaunchKernelGGL(bwd_partial_kernel, dim3((C + 63) / 64, autovc_bn_partial_rows(M)), dim3(256), 0, stream, M, C,
+                     dz, lddz, z, ldz, y, ldy, mean, act, part);
+  AVC_CHECK_LAUNCH("autovc_bn_bwd_partial_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_bwd_finalize_f32(int RS, int C, const double* part, const float* var, float eps, float* sums,
+                                          float* dgamma, float* dbeta, int accumulate, hipStream_t stream) {
+  AVC_CHECK_ARG(RS > 0 && C > 0 && part && var && sums, "autovc_bn_bwd_finalize_f32: bad args");
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, C, part, RS, var, eps, sums,
+                     dgamma, dbeta, accumulate);
+  AVC_CHECK_LAUNCH("autovc_bn_bwd_finalize_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_colsum_f64_finalize_f32(int RS, int C, const double* part, float* out, int accumulate,
+                                              hipStream_t stream) {
+  AVC_CHECK_ARG(RS > 0 && C > 0 && part && out, "autovc_colsum_f64_finalize_f32: bad args");
+  hipLaunchKernelGGL(colsum_f64_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, C, RS, part, out,
+                     accumulate);
+  AVC_CHECK_LAUNCH("autovc_colsum_f64_finalize_f32");
   return avc::kOk;
 }

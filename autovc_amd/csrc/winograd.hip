@@ -66,19 +66,65 @@ __global__ void wino_weight_kernel(int Co, int Ci, const float* __restrict__ W, 
   }
 }
 
-// thread = (tile, 4 channels); grid (ceil(C/4 / 64), B * T / 4), block 64
+enum Act { kNone = 0, kRelu = 1, kTanh = 2 };
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// BatchNorm + activation of the previous layer applied to its pre-BN output y on load:
+// z = act(y * alpha + shift), coef = [alpha | shift | mean | invstd] (4 x C floats, from
+// autovc_bn_finalize_f32 / autovc_bn_coef_f32) — the same fmaf as bn.hip's apply_kernel
+__device__ __forceinline__ f32x4 bn_act(f32x4 y, f32x4 al, f32x4 sh, int act) {
+  f32x4 z;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float v = fmaf(y[e], al[e], sh[e]);
+    z[e] = act == kRelu ? fmaxf(v, 0.f) : (act == kTanh ? tanhf(v) : v);
+  }
+  return z;
+}
+
+// g = d act / d pre * dz at pre = y * alpha + shift (bn.hip's act_grad through the output:
+// relu z > 0 <=> pre > 0, tanh 1 - z^2 with z = tanhf(pre) recomputed bit for bit)
+__device__ __forceinline__ f32x4 act_back(f32x4 dz, f32x4 y, f32x4 al, f32x4 sh, int act) {
+  if (act == kNone) return dz;
+  f32x4 g;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float v = fmaf(y[e], al[e], sh[e]);
+    if (act == kRelu) {
+      g[e] = v > 0.f ? dz[e] : 0.f;
+    } else {
+      const float z = tanhf(v);
+      g[e] = dz[e] * (1.f - z * z);
+    }
+  }
+  return g;
+}
+
+// thread = (tile, 4 channels); grid (ceil(C/4 / 64), B * T / 4), block 64.  BN: the input
+// is the previous layer's pre-BN output and its BatchNorm + activation are applied on load
+// (the padding frames stay zero: the reference pads the activation, model_vc_mel.py:33)
+template <bool BN>
 __global__ __launch_bounds__(64) void wino_input_kernel(int T, int C, const float* __restrict__ x, int64_t ldx,
-                                                        float* __restrict__ out, int64_t ntiles) {
+                                                        float* __restrict__ out, int64_t ntiles,
+                                                        const float* __restrict__ coef, int act) {
   const int c = 4 * (blockIdx.x * 64 + threadIdx.x);
   if (c >= C) return;
   const int64_t tile = blockIdx.y;
   const int64_t b = tile / (T / 4);
   const int q = (int)(tile % (T / 4));
+  f32x4 al = {}, sh = {};
+  if (BN) {
+    al = ld4(coef + c);
+    sh = ld4(coef + C + c);
+  }
   f32x4 d[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int t = 4 * q - 2 + j;
     d[j] = (t >= 0 && t < T) ? *reinterpret_cast<const f32x4*>(x + (b * T + t) * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BN && t >= 0 && t < T) d[j] = bn_act(d[j], al, sh, act);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -153,7 +199,212 @@ __global__ void wino_wgrad_kernel(int64_t n, const float* __restrict__ Mt, float
   }
 }
 
+// ---------------------------------------------------------------- fused Conv-BN chain
+// (autovc_amd.functional.ConvBNChainFn: the encoder / decoder / postnet stacks,
+// model_vc_mel.py:49-59,68-69,92-102,113-115,132-169).  Row-reducing kernels share one
+// geometry: block = 4 waves x 64 lanes, lane = 4 channels, wave = kTPW consecutive tiles
+// (4 frames each), so a block covers kTPB tiles and writes ONE partial row per channel;
+// the finalize kernels sum the rows in fixed order (deterministic, no atomics).
+constexpr int kTPW = 4;
+constexpr int kTPB = 4 * kTPW;
+
+// y = A^T Y~ + bias (the output transform) and the per-block BatchNorm statistics of y:
+// part[rs][c] = (sum y, sum y^2) in double (raw sums: fp64 keeps the cancellation of
+// E[y^2] - E[y]^2 far below fp32 resolution for activations of this scale)
+__global__ __launch_bounds__(256) void wino_output_stats_kernel(int T, int C, const float* __restrict__ Yt,
+                                                                const float* __restrict__ bias, float* __restrict__ y,
+                                                                int64_t ldy, int64_t ntiles,
+                                                                double* __restrict__ part) {
+  __shared__ double red[4][64][8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = 4 * (blockIdx.x * 64 + lane);
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C) {
+    const f32x4 bv = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < kTPW; ++i) {
+      const int64_t tile = (int64_t)blockIdx.y * kTPB + w * kTPW + i;
+      if (tile >= ntiles) break;
+      const int64_t b = tile / (T / 4);
+      const int q = (int)(tile % (T / 4));
+      f32x4 m[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[k] = ld4(Yt + ((int64_t)k * ntiles + tile) * C + c);
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        f32x4 v = bv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (kAT[o][k] != 0.f) v += kAT[o][k] * m[k];
+        st4(y + (b * T + 4 * q + o) * ldy + c, v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[e] += (double)v[e];
+          s2[e] += (double)v[e] * (double)v[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[w][lane][2 * e] = s1[e];
+    red[w][lane][2 * e + 1] = s2[e];
+  }
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const double a = ((red[0][lane][2 * e] + red[1][lane][2 * e]) + red[2][lane][2 * e]) + red[3][lane][2 * e];
+    const double q = ((red[0][lane][2 * e + 1] + red[1][lane][2 * e + 1]) + red[2][lane][2 * e + 1]) +
+                     red[3][lane][2 * e + 1];
+    part[((int64_t)blockIdx.y * C + c + e) * 2 + 0] = a;
+    part[((int64_t)blockIdx.y * C + c + e) * 2 + 1] = q;
+  }
+}
+
+// Input gradient of a conv whose input is the previous layer's BN + activation output:
+// dz = A^T Yd~ (the output transform of the flipped correlation) and, for that layer's
+// BatchNorm backward, part[rs][c] = (sum g, sum g (y - mean)) with g = act'(pre) dz
+// (bn.hip's bwd_partial_kernel sums, here produced where dz is)
+__global__ __launch_bounds__(256) void wino_output_bnbwd_kernel(int T, int C, const float* __restrict__ Yt,
+                                                                const float* __restrict__ yprev, int64_t ldy,
+                                                                const float* __restrict__ coef, int act,
+                                                                float* __restrict__ dz, int64_t lddz, int64_t ntiles,
+                                                                double* __restrict__ part) {
+  __shared__ double red[4][64][8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = 4 * (blockIdx.x * 64 + lane);
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C) {
+    const f32x4 al = ld4(coef + c), sh = ld4(coef + C + c), mu = ld4(coef + 2 * C + c);
+    for (int i = 0; i < kTPW; ++i) {
+      const int64_t tile = (int64_t)blockIdx.y * kTPB + w * kTPW + i;
+      if (tile >= ntiles) break;
+      const int64_t b = tile / (T / 4);
+      const int q = (int)(tile % (T / 4));
+      f32x4 m[8], yv[4];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) yv[o] = ld4(yprev + (b * T + 4 * q + o) * ldy + c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[k] = ld4(Yt + ((int64_t)k * ntiles + tile) * C + c);
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (kAT[o][k] != 0.f) v += kAT[o][k] * m[k];
+        st4(dz + (b * T + 4 * q + o) * lddz + c, v);
+        const f32x4 g = act_back(v, yv[o], al, sh, act);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[e] += (double)g[e];
+          s2[e] += (double)g[e] * (double)(yv[o][e] - mu[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[w][lane][2 * e] = s1[e];
+    red[w][lane][2 * e + 1] = s2[e];
+  }
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const double a = ((red[0][lane][2 * e] + red[1][lane][2 * e]) + red[2][lane][2 * e]) + red[3][lane][2 * e];
+    const double q = ((red[0][lane][2 * e + 1] + red[1][lane][2 * e + 1]) + red[2][lane][2 * e + 1]) +
+                     red[3][lane][2 * e + 1];
+    part[((int64_t)blockIdx.y * C + c + e) * 2 + 0] = a;
+    part[((int64_t)blockIdx.y * C + c + e) * 2 + 1] = q;
+  }
+}
+
+// BatchNorm + activation backward of one layer fused with every consumer of its dy:
+//   dy = (g - sum_g / M - xhat sum_gxhat / M) * alpha,  g = act'(pre) dz,  xhat = (y - mean) invstd
+// (bn.hip's bwd_apply_kernel arithmetic) computed per frame from dz and y, then
+//   Dt  = the weight gradient's dY~ transform of the tile's 4 frames (wino_dy_kernel),
+//   Xt  = the input gradient's input transform of frames 4q-2 .. 4q+5 (wino_input_kernel),
+//   bpart[rs][c] = sum over the block's frames of dy (the conv bias gradient, double).
+// Each may be null.  sums = [C][2] from autovc_bn_bwd_finalize_f32.  dy itself is never stored.
+__global__ __launch_bounds__(256) void wino_bnbwd_kernel(int T, int C, const float* __restrict__ dz, int64_t lddz,
+                                                         const float* __restrict__ y, int64_t ldy,
+                                                         const float* __restrict__ coef, int act,
+                                                         const float* __restrict__ sums, float inv_m,
+                                                         float* __restrict__ Dt, float* __restrict__ Xt,
+                                                         double* __restrict__ bpart, int64_t ntiles) {
+  __shared__ double red[4][64][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = 4 * (blockIdx.x * 64 + lane);
+  double sb[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C) {
+    const f32x4 al = ld4(coef + c), sh = ld4(coef + C + c), mu = ld4(coef + 2 * C + c), is = ld4(coef + 3 * C + c);
+    f32x4 s0, s1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s0[e] = sums[2 * (c + e)] * inv_m;
+      s1[e] = sums[2 * (c + e) + 1] * inv_m;
+    }
+    auto dy_at = [&](int64_t row) {
+      const f32x4 yv = ld4(y + row * ldy + c);
+      const f32x4 g = act_back(ld4(dz + row * lddz + c), yv, al, sh, act);
+      f32x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = (g[e] - s0[e] - (yv[e] - mu[e]) * is[e] * s1[e]) * al[e];
+      return r;
+    };
+    for (int i = 0; i < kTPW; ++i) {
+      const int64_t tile = (int64_t)blockIdx.y * kTPB + w * kTPW + i;
+      if (tile >= ntiles) break;
+      const int64_t b = tile / (T / 4);
+      const int q = (int)(tile % (T / 4));
+      f32x4 d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = 4 * q - 2 + j;
+        const bool own = j >= 2 && j < 6;
+        d[j] = (own || (Xt && t >= 0 && t < T)) ? dy_at(b * T + t) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 2; j < 6; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sb[e] += (double)d[j][e];
+      if (Dt)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int o = 0; o < 4; ++o)
+            if (kAT[o][k] != 0.f) v += kAT[o][k] * d[2 + o];
+          st4(Dt + ((int64_t)k * ntiles + tile) * C + c, v);
+        }
+      if (Xt)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (kBT[k][j] != 0.f) v += kBT[k][j] * d[j];
+          st4(Xt + ((int64_t)k * ntiles + tile) * C + c, v);
+        }
+    }
+  }
+  if (!bpart) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[w][lane][e] = sb[e];
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    bpart[(int64_t)blockIdx.y * C + c + e] =
+        ((red[0][lane][e] + red[1][lane][e]) + red[2][lane][e]) + red[3][lane][e];
+}
+
 }  // namespace
+
+extern "C" int64_t autovc_wino5_rows(int B, int T) {
+  if (B <= 0 || T <= 0 || T % 4) return -1;
+  return ((int64_t)B * T / 4 + kTPB - 1) / kTPB;
+}
 
 extern "C" int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip, float* out, hipStream_t stream) {
   AVC_CHECK_ARG(Co > 0 && Ci > 0 && W && out && (flip == 0 || flip == 1), "autovc_wino5_weights_f32: bad args");
@@ -170,9 +421,66 @@ extern "C" int autovc_wino5_input_f32(int B, int T, int C, const float* x, int64
                 "autovc_wino5_input_f32: bad args (T and C multiples of 4)");
   AVC_CHECK_ARG(AVC_ALIGNED16(x) && AVC_ALIGNED16(out), "autovc_wino5_input_f32: alignment");
   const int64_t ntiles = (int64_t)B * T / 4;
-  hipLaunchKernelGGL(wino_input_kernel, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C, x, ldx,
-                     out, ntiles);
+  hipLaunchKernelGGL(wino_input_kernel<false>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C,
+                     x, ldx, out, ntiles, (const float*)nullptr, 0);
   AVC_CHECK_LAUNCH("autovc_wino5_input_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_wino5_input_bn_f32(int B, int T, int C, const float* y, int64_t ldy, const float* coef, int act,
+                                         float* out, hipStream_t stream) {
+  AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && ldy % 4 == 0 && y && coef && out,
+                "autovc_wino5_input_bn_f32: bad args (T and C multiples of 4)");
+  AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_wino5_input_bn_f32: unknown activation %d", act);
+  AVC_CHECK_ARG(AVC_ALIGNED16(y) && AVC_ALIGNED16(out) && AVC_ALIGNED16(coef), "autovc_wino5_input_bn_f32: alignment");
+  const int64_t ntiles = (int64_t)B * T / 4;
+  hipLaunchKernelGGL(wino_input_kernel<true>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C, y,
+                     ldy, out, ntiles, coef, act);
+  AVC_CHECK_LAUNCH("autovc_wino5_input_bn_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
+                                             int64_t ldy, double* part, hipStream_t stream) {
+  AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && ldy % 4 == 0 && Yt && y && part,
+                "autovc_wino5_output_stats_f32: bad args (T and C multiples of 4)");
+  AVC_CHECK_ARG(AVC_ALIGNED16(Yt) && AVC_ALIGNED16(y) && (!bias || AVC_ALIGNED16(bias)),
+                "autovc_wino5_output_stats_f32: alignment");
+  const int64_t ntiles = (int64_t)B * T / 4;
+  hipLaunchKernelGGL(wino_output_stats_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(256),
+                     0, stream, T, C, Yt, bias, y, ldy, ntiles, part);
+  AVC_CHECK_LAUNCH("autovc_wino5_output_stats_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_wino5_output_bnbwd_f32(int B, int T, int C, const float* Yt, const float* yprev, int64_t ldy,
+                                             const float* coef, int act, float* dz, int64_t lddz, double* part,
+                                             hipStream_t stream) {
+  AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && ldy % 4 == 0 && lddz % 4 == 0 && Yt && yprev &&
+                coef && dz && part, "autovc_wino5_output_bnbwd_f32: bad args (T and C multiples of 4)");
+  AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_wino5_output_bnbwd_f32: unknown activation %d", act);
+  AVC_CHECK_ARG(AVC_ALIGNED16(Yt) && AVC_ALIGNED16(yprev) && AVC_ALIGNED16(dz) && AVC_ALIGNED16(coef),
+                "autovc_wino5_output_bnbwd_f32: alignment");
+  const int64_t ntiles = (int64_t)B * T / 4;
+  hipLaunchKernelGGL(wino_output_bnbwd_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(256),
+                     0, stream, T, C, Yt, yprev, ldy, coef, act, dz, lddz, ntiles, part);
+  AVC_CHECK_LAUNCH("autovc_wino5_output_bnbwd_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_wino5_bnbwd_f32(int B, int T, int C, const float* dz, int64_t lddz, const float* y, int64_t ldy,
+                                      const float* coef, int act, const float* sums, float* Dt, float* Xt,
+                                      double* bias_part, hipStream_t stream) {
+  AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && lddz % 4 == 0 && ldy % 4 == 0 && dz && y &&
+                coef && sums && (Dt || Xt || bias_part), "autovc_wino5_bnbwd_f32: bad args (T and C multiples of 4)");
+  AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_wino5_bnbwd_f32: unknown activation %d", act);
+  AVC_CHECK_ARG(AVC_ALIGNED16(dz) && AVC_ALIGNED16(y) && AVC_ALIGNED16(coef) && (!Dt || AVC_ALIGNED16(Dt)) &&
+                (!Xt || AVC_ALIGNED16(Xt)), "autovc_wino5_bnbwd_f32: alignment");
+  const int64_t ntiles = (int64_t)B * T / 4;
+  hipLaunchKernelGGL(wino_bnbwd_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(256), 0,
+                     stream, T, C, dz, lddz, y, ldy, coef, act, sums, 1.0f / (float)((int64_t)B * T), Dt, Xt,
+                     bias_part, ntiles);
+  AVC_CHECK_LAUNCH("autovc_wino5_bnbwd_f32");
   return avc::kOk;
 }
 

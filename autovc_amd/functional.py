@@ -481,6 +481,211 @@ def conv_bn_act(x, conv, bn, act, residual=None):
                              momentum, bn.eps, residual)
 
 
+# ---------------------------------------------------------------- fused Conv-BN stacks
+# A whole ConvNorm -> BatchNorm1d -> act stack (encoder 3 x relu, decoder 3 x relu, postnet
+# 4 x tanh + 1 x none with the residual, model_vc_mel.py:49-59,68-69,92-102,113-115,132-169)
+# as one autograd op whose BatchNorm passes live inside the Winograd transforms
+# (csrc/winograd.hip "fused Conv-BN chain"): every pre-BN activation y_l is written once and
+# read by the next layer's input transform, which applies BN_l + act on load; only the
+# stack's output is materialised.  AVC_CONV_CHAIN=0 selects the per-layer ConvBNActFn path.
+_CHAIN_ON = os.environ.get("AVC_CONV_CHAIN", "1") != "0"
+
+
+def _chain_ok(x, layers, training):
+    if not (_CHAIN_ON and _WINOGRAD and _PRECISION[0] == "fp32" and x.is_cuda and x.dim() == 3
+            and x.dtype == torch.float32):
+        return False
+    T = x.shape[1]
+    if T % 4 or x.shape[2] % 4:
+        return False
+    for conv, bn, _ in layers:
+        if (conv.kernel_size[0] != KS or conv.padding[0] != PAD or conv.stride[0] != 1 or conv.dilation[0] != 1
+                or conv.groups != 1 or conv.out_channels % 4 or conv.in_channels % 4):
+            return False
+        if bn.training != training or not bn.track_running_stats or bn.running_mean is None or not bn.affine:
+            return False
+    return True
+
+
+class ConvBNChainFn(torch.autograd.Function):
+    """Forward / backward of a Conv-BN-act stack (see above).  apply(spec, x, residual,
+    *per-layer (W, b, gamma, beta, running_mean, running_var, num_batches_tracked));
+    spec = (training, acts, momenta, epss)."""
+
+    @staticmethod
+    def forward(ctx, spec, x, residual, *tensors):
+        training, acts, moms, epss = spec
+        L = len(acts)
+        x = x.contiguous()
+        B, T, _ = x.shape
+        M, nt = B * T, B * T // 4
+        dev = x.device
+        lib = _lib.load()
+        RS = int(lib.autovc_wino5_rows(B, T))
+        ys, coefs, means, varis, xts = [], [], [], [], []
+        for l in range(L):
+            W, b, g, be, rm, rv, nbt = tensors[7 * l:7 * l + 7]
+            Co, Ci = W.shape[0], W.shape[1]
+            Wt = torch.empty((8, Co, Ci), device=dev, dtype=torch.float32)
+            _lib.call("autovc_wino5_weights_f32", Co, Ci, W.data_ptr(), 0, Wt.data_ptr(), _s())
+            Xt = torch.empty((8, nt, Ci), device=dev, dtype=torch.float32)
+            if l == 0:
+                _lib.call("autovc_wino5_input_f32", B, T, Ci, x.data_ptr(), Ci, Xt.data_ptr(), _s())
+            else:
+                _lib.call("autovc_wino5_input_bn_f32", B, T, Ci, ys[-1].data_ptr(), Ci, coefs[-1].data_ptr(),
+                          ACT[acts[l - 1]], Xt.data_ptr(), _s())
+            Yt = torch.empty((8, nt, Co), device=dev, dtype=torch.float32)
+            _lib.call("autovc_gemm_batched_f32", 8, nt, Co, Ci, Xt.data_ptr(), Ci, nt * Ci, 0, Wt.data_ptr(), Ci,
+                      Co * Ci, 0, Yt.data_ptr(), Co, nt * Co, 0, _s())
+            del Wt
+            y = torch.empty((B, T, Co), device=dev, dtype=torch.float32)
+            coef = torch.empty((4, Co), device=dev, dtype=torch.float32)
+            if training:
+                part = _ws(dev, RS * Co * 16, "chain_fwd")
+                _lib.call("autovc_wino5_output_stats_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, part, _s())
+                mean = torch.empty(Co, device=dev, dtype=torch.float32)
+                var = torch.empty(Co, device=dev, dtype=torch.float32)
+                _lib.call("autovc_bn_finalize_f32", RS, M, Co, part, _p(g), _p(be), float(epss[l]), mean.data_ptr(),
+                          var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt), _s())
+            else:
+                _lib.call("autovc_wino5_output_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, _s())
+                mean, var = rm, rv
+                _lib.call("autovc_bn_coef_f32", Co, rm.data_ptr(), rv.data_ptr(), _p(g), _p(be), float(epss[l]),
+                          coef.data_ptr(), _s())
+            del Yt
+            ys.append(y)
+            coefs.append(coef)
+            means.append(mean)
+            varis.append(var)
+            xts.append(Xt if training else None)
+            del Xt
+        C = ys[-1].shape[2]
+        g, be = tensors[7 * (L - 1) + 2], tensors[7 * (L - 1) + 3]
+        z = torch.empty((B, T, C), device=dev, dtype=torch.float32)
+        res = residual.contiguous() if residual is not None else None
+        _lib.call("autovc_bn_act_fwd_f32", M, C, ys[-1].data_ptr(), C, means[-1].data_ptr(), varis[-1].data_ptr(),
+                  _p(g), _p(be), float(epss[-1]), ACT[acts[-1]], _p(res), C, z.data_ptr(), C, _s())
+        if training:
+            ctx.spec = spec
+            ctx.ys, ctx.coefs, ctx.means, ctx.varis, ctx.xts = ys, coefs, means, varis, xts
+            ctx.x = x
+            ctx.z = z if acts[-1] != "none" else None
+            ctx.has_res = residual is not None
+            ctx.params = tensors
+        else:
+            ctx.spec = None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        if ctx.spec is None:
+            raise NotImplementedError("autovc_amd: backward through eval-mode BatchNorm is not supported")
+        training, acts, moms, epss = ctx.spec
+        L = len(acts)
+        needs = ctx.needs_input_grad
+        x, ys, coefs, means, varis, xts = ctx.x, ctx.ys, ctx.coefs, ctx.means, ctx.varis, ctx.xts
+        tensors = ctx.params
+        B, T, _ = x.shape
+        M, nt = B * T, B * T // 4
+        dev = x.device
+        lib = _lib.load()
+        RS = int(lib.autovc_wino5_rows(B, T))
+        dres = dz.contiguous() if ctx.has_res else None
+        dz = dz.contiguous()
+        grads = [None] * len(tensors)
+        dx = None
+        part, rows = None, 0
+        for l in range(L - 1, -1, -1):
+            W, b, g, be = tensors[7 * l:7 * l + 4]
+            Co, Ci = W.shape[0], W.shape[1]
+            act = ACT[acts[l]]
+            y = ys[l]
+            # BatchNorm backward sums of layer l (the stack's last layer reduces its dz here;
+            # the others got them from the output transform that produced dz)
+            if l == L - 1:
+                rows = int(lib.autovc_bn_partial_rows(M))
+                part = _ws(dev, rows * Co * 16, "chain_bwd")
+                _lib.call("autovc_bn_bwd_partial_f32", M, Co, dz.data_ptr(), Co, _p(ctx.z), Co, y.data_ptr(), Co,
+                          means[l].data_ptr(), act, part, _s())
+            ng, nb = needs[3 + 7 * l + 2], needs[3 + 7 * l + 3]
+            gg = _GradOut(g, (Co,), dev) if ng else None
+            gb = _GradOut(be, (Co,), dev) if nb else None
+            acc = bool(gg is not None and gb is not None and gg.acc and gb.acc)
+            if not acc:
+                gg = _GradOut(None, (Co,), dev) if ng else None
+                gb = _GradOut(None, (Co,), dev) if nb else None
+            sums = _ws(dev, 8 * Co, "chain_sums")
+            _lib.call("autovc_bn_bwd_finalize_f32", rows, Co, part, varis[l].data_ptr(), float(epss[l]), sums,
+                      _p(gg.buf if gg else None), _p(gb.buf if gb else None), int(acc), _s())
+            if gg is not None:
+                grads[7 * l + 2] = gg.result()
+            if gb is not None:
+                grads[7 * l + 3] = gb.result()
+            need_w, need_b = needs[3 + 7 * l], b is not None and needs[3 + 7 * l + 1]
+            need_dx = l > 0 or needs[1]
+            Dt = torch.empty((8, nt, Co), device=dev, dtype=torch.float32) if need_w else None
+            Xd = torch.empty((8, nt, Co), device=dev, dtype=torch.float32) if need_dx else None
+            bpart = _ws(dev, RS * Co * 8, "chain_bias") if need_b else 0
+            if Dt is not None or Xd is not None or need_b:
+                _lib.call("autovc_wino5_bnbwd_f32", B, T, Co, dz.data_ptr(), Co, y.data_ptr(), Co,
+                          coefs[l].data_ptr(), act, sums, _p(Dt), _p(Xd), bpart, _s())
+            if need_b:
+                go = _GradOut(b, (Co,), dev)
+                _lib.call("autovc_colsum_f64_finalize_f32", RS, Co, bpart, go.buf.data_ptr(), int(go.acc), _s())
+                grads[7 * l + 1] = go.result()
+            if need_w:
+                go = _GradOut(W, (Co, Ci, KS), dev)
+                Xt = xts[l]
+
+                def dw(go=go, Dt=Dt, Xt=Xt, Co=Co, Ci=Ci):
+                    Mt = torch.empty((8, Co, Ci), device=dev, dtype=torch.float32)
+                    _lib.call("autovc_gemm_batched_f32", 8, Co, Ci, nt, Dt.data_ptr(), Co, nt * Co, 1, Xt.data_ptr(),
+                              Ci, nt * Ci, 1, Mt.data_ptr(), Ci, Co * Ci, 0, _s())
+                    _lib.call("autovc_wino5_wgrad_f32", Co, Ci, Mt.data_ptr(), go.buf.data_ptr(), int(go.acc), _s())
+                _grad_launch(dev, go.acc, dw, Dt, Xt)
+                grads[7 * l] = go.result()
+            xts[l] = None
+            if need_dx:
+                Wd = torch.empty((8, Ci, Co), device=dev, dtype=torch.float32)
+                _lib.call("autovc_wino5_weights_f32", Co, Ci, W.data_ptr(), 1, Wd.data_ptr(), _s())
+                Yd = torch.empty((8, nt, Ci), device=dev, dtype=torch.float32)
+                _lib.call("autovc_gemm_batched_f32", 8, nt, Ci, Co, Xd.data_ptr(), Co, nt * Co, 0, Wd.data_ptr(), Co,
+                          Ci * Co, 0, Yd.data_ptr(), Ci, nt * Ci, 0, _s())
+                del Wd, Xd
+                dzp = torch.empty((B, T, Ci), device=dev, dtype=torch.float32)
+                if l > 0:
+                    rows = RS
+                    part = _ws(dev, RS * Ci * 16, "chain_bwd")
+                    _lib.call("autovc_wino5_output_bnbwd_f32", B, T, Ci, Yd.data_ptr(), ys[l - 1].data_ptr(), Ci,
+                              coefs[l - 1].data_ptr(), ACT[acts[l - 1]], dzp.data_ptr(), Ci, part, _s())
+                    dz = dzp
+                else:
+                    _lib.call("autovc_wino5_output_f32", B, T, Ci, Yd.data_ptr(), 0, dzp.data_ptr(), Ci, _s())
+                    dx = dzp
+                del Yd
+        ctx.ys = ctx.xts = ctx.coefs = None
+        return (None, dx, dres, *grads)
+
+
+def conv_bn_chain(x, layers, residual=None):
+    """x (B,T,C) -> a Conv-BN-act stack; layers = [(nn.Conv1d, nn.BatchNorm1d, act), ...],
+    residual (optional) is added to the last layer's output.  The fused ConvBNChainFn where
+    it applies (fp32, Winograd shapes), else one ConvBNActFn per layer."""
+    training = layers[0][1].training
+    if not _chain_ok(x, layers, training):
+        for i, (conv, bn, act) in enumerate(layers):
+            x = conv_bn_act(x, conv, bn, act, residual=residual if i == len(layers) - 1 else None)
+        return x
+    tensors = []
+    for conv, bn, _ in layers:
+        nbt = bn.num_batches_tracked if training else None
+        tensors += [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt]
+    spec = (training, tuple(a for _, _, a in layers),
+            tuple((bn.momentum if bn.momentum is not None else 0.0) for _, bn, _ in layers),
+            tuple(bn.eps for _, bn, _ in layers))
+    return ConvBNChainFn.apply(spec, x, residual, *tensors)
+
+
 class ConvFn(torch.autograd.Function):
     """Plain ConvNorm (k=5, p=2) on NTC activations (ConvNorm.forward API path)."""
 

@@ -132,8 +132,7 @@ class Encoder(nn.Module):
             x = x.squeeze(1)
         B, T, F_in = x.shape
         h = AF.FrameConcatFn.apply(x, c_org, T, 1)            # :64-66
-        for conv in self.convolutions:                         # :68-69
-            h = AF.conv_bn_act(h, conv[0].conv, conv[1], "relu")
+        h = AF.conv_bn_chain(h, [(conv[0].conv, conv[1], "relu") for conv in self.convolutions])   # :68-69
         out, _ = self.lstm(h)                                  # :72-73
         return AF.CodeGatherFn.apply(out, self.freq)           # :74-79
 
@@ -160,8 +159,7 @@ class Decoder(nn.Module):
 
     def forward(self, x):
         x, _ = self.lstm1(x)
-        for conv in self.convolutions:
-            x = AF.conv_bn_act(x, conv[0].conv, conv[1], "relu")
+        x = AF.conv_bn_chain(x, [(conv[0].conv, conv[1], "relu") for conv in self.convolutions])
         outputs, _ = self.lstm2(x)
         return self.linear_projection(outputs)
 
@@ -186,10 +184,9 @@ class Postnet(nn.Module):
     def forward_ntc(self, x, residual=None):
         """x (B,T,C) -> postnet(x) (+ residual), NTC; the residual add of
         model_vc_mel.py:197 is fused into the last BN pass."""
-        for i in range(len(self.convolutions) - 1):
-            x = AF.conv_bn_act(x, self.convolutions[i][0].conv, self.convolutions[i][1], "tanh")
-        last = self.convolutions[-1]
-        return AF.conv_bn_act(x, last[0].conv, last[1], "none", residual=residual)
+        n = len(self.convolutions)
+        return AF.conv_bn_chain(x, [(c[0].conv, c[1], "tanh" if i < n - 1 else "none")
+                                    for i, c in enumerate(self.convolutions)], residual=residual)
 
     def forward(self, x):
         return self.forward_ntc(x.transpose(1, 2)).transpose(1, 2)

@@ -164,6 +164,48 @@ int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t lddz, const
                           int64_t lddy, float* dgamma, float* dbeta, int accumulate,
                           void* workspace, hipStream_t stream);
 
+/* ---------------------------------------------------------------- fused Conv-BN stacks
+ * The encoder / decoder / postnet stacks (ConvNorm -> BatchNorm1d -> act, x3 / x3 / x5,
+ * model_vc_mel.py:49-59,68-69,92-102,113-115,132-169) with every BatchNorm pass folded
+ * into the Winograd transforms around it.  Each layer's pre-BN output y is written once;
+ * its BatchNorm + activation are applied by the next layer's input transform
+ * (input_bn), and its statistics come from the output transform that writes y
+ * (output_stats).  Backward: the input-gradient output transform also reduces the
+ * previous layer's BatchNorm-backward sums (output_bnbwd), and ONE kernel turns (dz, y)
+ * into every consumer of dy — the weight-gradient dY~ transform, the input-gradient input
+ * transform and the conv bias sums — without storing dy (bnbwd).
+ * Row-block partials: autovc_wino5_rows(B, T) rows x C (x 2) doubles.
+ * coef (4 x C floats) = [alpha | shift | mean | invstd], alpha = gamma / sqrt(var + eps),
+ * shift = beta - mean alpha: written by autovc_bn_finalize_f32 (train: batch statistics,
+ * running stats updated as autovc_bn_stats_f32 does) or autovc_bn_coef_f32 (eval: from
+ * running stats).  sums ([C][2]) from autovc_bn_bwd_finalize_f32.  B*T/4 tiles, T, C % 4 == 0. */
+int64_t autovc_wino5_rows(int B, int T);
+int autovc_wino5_input_bn_f32(int B, int T, int C, const float* y, int64_t ldy, const float* coef, int act,
+                              float* out, hipStream_t stream);
+int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
+                                  int64_t ldy, double* part, hipStream_t stream);
+int autovc_wino5_output_bnbwd_f32(int B, int T, int C, const float* Yt, const float* yprev, int64_t ldy,
+                                  const float* coef, int act, float* dz, int64_t lddz, double* part,
+                                  hipStream_t stream);
+int autovc_wino5_bnbwd_f32(int B, int T, int C, const float* dz, int64_t lddz, const float* y, int64_t ldy,
+                           const float* coef, int act, const float* sums, float* Dt, float* Xt,
+                           double* bias_part, hipStream_t stream);
+int autovc_bn_finalize_f32(int RS, int64_t M, int C, const double* part, const float* gamma, const float* beta,
+                           float eps, float* mean, float* var, float* coef, float* running_mean,
+                           float* running_var, float momentum, int64_t* num_batches, hipStream_t stream);
+int autovc_bn_coef_f32(int C, const float* mean, const float* var, const float* gamma, const float* beta,
+                       float eps, float* coef, hipStream_t stream);
+/* The BatchNorm-backward sums of a stack's LAST layer, whose dz comes from outside the
+ * stack: kRowSplits-row partials (autovc_bn_partial_rows(M) rows) over dz and z. */
+int autovc_bn_partial_rows(int64_t M);
+int autovc_bn_bwd_partial_f32(int64_t M, int C, const float* dz, int64_t lddz, const float* z, int64_t ldz,
+                              const float* y, int64_t ldy, const float* mean, int act, double* part,
+                              hipStream_t stream);
+int autovc_bn_bwd_finalize_f32(int RS, int C, const double* part, const float* var, float eps, float* sums,
+                               float* dgamma, float* dbeta, int accumulate, hipStream_t stream);
+int autovc_colsum_f64_finalize_f32(int RS, int C, const double* part, float* out, int accumulate,
+                                   hipStream_t stream);
+
 /* ---------------------------------------------------------------- LSTM recurrences
  * Replaces the cuDNN/mkldnn recurrence of nn.LSTM (model_vc_mel.py:61,90,104).
  * gx = x W_ih^T + b_ih + b_hh precomputed (autovc_gemm_f32).  Large H (multiple of 16):
