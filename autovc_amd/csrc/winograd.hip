@@ -201,49 +201,37 @@ __global__ void wino_wgrad_kernel(int64_t n, const float* __restrict__ Mt, float
 
 // ---------------------------------------------------------------- fused Conv-BN chain
 // (autovc_amd.functional.ConvBNChainFn: the encoder / decoder / postnet stacks,
-// model_vc_mel.py:49-59,68-69,92-102,113-115,132-169).  Row-reducing kernels share one
-// geometry: block = 4 waves x 64 lanes, lane = 4 channels, wave = kTPW consecutive tiles
-// (4 frames each), so a block covers kTPB tiles and writes ONE partial row per channel;
-// the finalize kernels sum the rows in fixed order (deterministic, no atomics).
+// model_vc_mel.py:49-59,68-69,92-102,113-115,132-169).  These kernels share one geometry:
+// block = 4 waves x 64 lanes, lane = 4 channels, wave = kTPW consecutive tiles of ONE
+// sequence (T % (4 kTPW) == 0), so a block covers kTPB tiles and writes one partial row
+// per channel (the finalize kernels sum the rows in fixed order: deterministic, no
+// atomics), every load of a wave is issued before its first use, and the input-type
+// transforms read each frame of the wave's window (4 kTPW + 4 frames) once instead of
+// twice (neighbouring tiles share their 4 halo frames).
 constexpr int kTPW = 4;
 constexpr int kTPB = 4 * kTPW;
+constexpr int kWin = 4 * kTPW + 4;       // frames of a wave's window: 4q0 - 2 .. 4(q0 + kTPW) + 1
 
-// y = A^T Y~ + bias (the output transform) and the per-block BatchNorm statistics of y:
-// part[rs][c] = (sum y, sum y^2) in double (raw sums: fp64 keeps the cancellation of
-// E[y^2] - E[y]^2 far below fp32 resolution for activations of this scale)
-__global__ __launch_bounds__(256) void wino_output_stats_kernel(int T, int C, const float* __restrict__ Yt,
-                                                                const float* __restrict__ bias, float* __restrict__ y,
-                                                                int64_t ldy, int64_t ntiles,
-                                                                double* __restrict__ part) {
+struct WaveTiles {
+  int64_t tile0, b;
+  int q0;
+  bool live;
+};
+
+__device__ __forceinline__ WaveTiles wave_tiles(int T, int64_t ntiles) {
+  WaveTiles w;
+  w.tile0 = (int64_t)blockIdx.y * kTPB + (threadIdx.x >> 6) * kTPW;
+  w.live = w.tile0 < ntiles;                 // ntiles % kTPW == 0: a live wave has all kTPW tiles
+  w.b = w.tile0 / (T / 4);
+  w.q0 = (int)(w.tile0 % (T / 4));
+  return w;
+}
+
+// the 4 waves' per-channel double pairs (s1, s2) summed in fixed order into partial row
+// blockIdx.y (w == 0 lanes write)
+__device__ __forceinline__ void block_pairs(double (&s1)[4], double (&s2)[4], int C, int c, double* __restrict__ part) {
   __shared__ double red[4][64][8];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = 4 * (blockIdx.x * 64 + lane);
-  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  if (c < C) {
-    const f32x4 bv = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < kTPW; ++i) {
-      const int64_t tile = (int64_t)blockIdx.y * kTPB + w * kTPW + i;
-      if (tile >= ntiles) break;
-      const int64_t b = tile / (T / 4);
-      const int q = (int)(tile % (T / 4));
-      f32x4 m[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) m[k] = ld4(Yt + ((int64_t)k * ntiles + tile) * C + c);
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        f32x4 v = bv;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (kAT[o][k] != 0.f) v += kAT[o][k] * m[k];
-        st4(y + (b * T + 4 * q + o) * ldy + c, v);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s1[e] += (double)v[e];
-          s2[e] += (double)v[e] * (double)v[e];
-        }
-      }
-    }
-  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     red[w][lane][2 * e] = s1[e];
@@ -259,6 +247,80 @@ __global__ __launch_bounds__(256) void wino_output_stats_kernel(int T, int C, co
     part[((int64_t)blockIdx.y * C + c + e) * 2 + 0] = a;
     part[((int64_t)blockIdx.y * C + c + e) * 2 + 1] = q;
   }
+}
+
+// Input transform over a wave's window (T % 16 == 0): X~ of kTPW tiles from 4 kTPW + 4
+// frames; BN: the previous layer's BatchNorm + activation applied on load (pads stay zero)
+template <bool BN>
+__global__ __launch_bounds__(256) void wino_input_win_kernel(int T, int C, const float* __restrict__ x, int64_t ldx,
+                                                             float* __restrict__ out, int64_t ntiles,
+                                                             const float* __restrict__ coef, int act) {
+  const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
+  const WaveTiles wt = wave_tiles(T, ntiles);
+  if (c >= C || !wt.live) return;
+  f32x4 al = {}, sh = {};
+  if (BN) {
+    al = ld4(coef + c);
+    sh = ld4(coef + C + c);
+  }
+  f32x4 d[kWin];
+#pragma unroll
+  for (int s = 0; s < kWin; ++s) {
+    const int t = 4 * wt.q0 - 2 + s;
+    d[s] = (t >= 0 && t < T) ? ld4(x + (wt.b * T + t) * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (BN)
+#pragma unroll
+    for (int s = 0; s < kWin; ++s) {
+      const int t = 4 * wt.q0 - 2 + s;
+      if (t >= 0 && t < T) d[s] = bn_act(d[s], al, sh, act);
+    }
+#pragma unroll
+  for (int i = 0; i < kTPW; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (kBT[k][j] != 0.f) v += kBT[k][j] * d[4 * i + j];
+      st4(out + ((int64_t)k * ntiles + wt.tile0 + i) * C + c, v);
+    }
+}
+
+// y = A^T Y~ + bias (the output transform) and the per-block BatchNorm statistics of y:
+// part[rs][c] = (sum y, sum y^2) in double (raw sums: fp64 keeps the cancellation of
+// E[y^2] - E[y]^2 far below fp32 resolution for activations of this scale)
+__global__ __launch_bounds__(256) void wino_output_stats_kernel(int T, int C, const float* __restrict__ Yt,
+                                                                const float* __restrict__ bias, float* __restrict__ y,
+                                                                int64_t ldy, int64_t ntiles,
+                                                                double* __restrict__ part) {
+  const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
+  const WaveTiles wt = wave_tiles(T, ntiles);
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C && wt.live) {
+    f32x4 m[kTPW][8];
+#pragma unroll
+    for (int i = 0; i < kTPW; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[i][k] = ld4(Yt + ((int64_t)k * ntiles + wt.tile0 + i) * C + c);
+    const f32x4 bv = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < kTPW; ++i)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        f32x4 v = bv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (kAT[o][k] != 0.f) v += kAT[o][k] * m[i][k];
+        st4(y + (wt.b * T + 4 * (wt.q0 + i) + o) * ldy + c, v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[e] += (double)v[e];
+          s2[e] += (double)v[e] * (double)v[e];
+        }
+      }
+  }
+  block_pairs(s1, s2, C, c, part);
 }
 
 // Input gradient of a conv whose input is the previous layer's BN + activation output:
@@ -270,73 +332,68 @@ __global__ __launch_bounds__(256) void wino_output_bnbwd_kernel(int T, int C, co
                                                                 const float* __restrict__ coef, int act,
                                                                 float* __restrict__ dz, int64_t lddz, int64_t ntiles,
                                                                 double* __restrict__ part) {
-  __shared__ double red[4][64][8];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = 4 * (blockIdx.x * 64 + lane);
+  const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
+  const WaveTiles wt = wave_tiles(T, ntiles);
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  if (c < C) {
+  if (c < C && wt.live) {
+    f32x4 m[kTPW][8], yv[kTPW][4];
+#pragma unroll
+    for (int i = 0; i < kTPW; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[i][k] = ld4(Yt + ((int64_t)k * ntiles + wt.tile0 + i) * C + c);
+#pragma unroll
+    for (int i = 0; i < kTPW; ++i)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) yv[i][o] = ld4(yprev + (wt.b * T + 4 * (wt.q0 + i) + o) * ldy + c);
     const f32x4 al = ld4(coef + c), sh = ld4(coef + C + c), mu = ld4(coef + 2 * C + c);
-    for (int i = 0; i < kTPW; ++i) {
-      const int64_t tile = (int64_t)blockIdx.y * kTPB + w * kTPW + i;
-      if (tile >= ntiles) break;
-      const int64_t b = tile / (T / 4);
-      const int q = (int)(tile % (T / 4));
-      f32x4 m[8], yv[4];
 #pragma unroll
-      for (int o = 0; o < 4; ++o) yv[o] = ld4(yprev + (b * T + 4 * q + o) * ldy + c);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) m[k] = ld4(Yt + ((int64_t)k * ntiles + tile) * C + c);
+    for (int i = 0; i < kTPW; ++i)
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          if (kAT[o][k] != 0.f) v += kAT[o][k] * m[k];
-        st4(dz + (b * T + 4 * q + o) * lddz + c, v);
-        const f32x4 g = act_back(v, yv[o], al, sh, act);
+          if (kAT[o][k] != 0.f) v += kAT[o][k] * m[i][k];
+        st4(dz + (wt.b * T + 4 * (wt.q0 + i) + o) * lddz + c, v);
+        const f32x4 g = act_back(v, yv[i][o], al, sh, act);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           s1[e] += (double)g[e];
-          s2[e] += (double)g[e] * (double)(yv[o][e] - mu[e]);
+          s2[e] += (double)g[e] * (double)(yv[i][o][e] - mu[e]);
         }
       }
-    }
   }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    red[w][lane][2 * e] = s1[e];
-    red[w][lane][2 * e + 1] = s2[e];
-  }
-  __syncthreads();
-  if (w != 0 || c >= C) return;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const double a = ((red[0][lane][2 * e] + red[1][lane][2 * e]) + red[2][lane][2 * e]) + red[3][lane][2 * e];
-    const double q = ((red[0][lane][2 * e + 1] + red[1][lane][2 * e + 1]) + red[2][lane][2 * e + 1]) +
-                     red[3][lane][2 * e + 1];
-    part[((int64_t)blockIdx.y * C + c + e) * 2 + 0] = a;
-    part[((int64_t)blockIdx.y * C + c + e) * 2 + 1] = q;
-  }
+  block_pairs(s1, s2, C, c, part);
 }
 
 // BatchNorm + activation backward of one layer fused with every consumer of its dy:
 //   dy = (g - sum_g / M - xhat sum_gxhat / M) * alpha,  g = act'(pre) dz,  xhat = (y - mean) invstd
-// (bn.hip's bwd_apply_kernel arithmetic) computed per frame from dz and y, then
+// (bn.hip's bwd_apply_kernel arithmetic) computed once per frame of the wave's window from
+// dz and y, then per tile
 //   Dt  = the weight gradient's dY~ transform of the tile's 4 frames (wino_dy_kernel),
 //   Xt  = the input gradient's input transform of frames 4q-2 .. 4q+5 (wino_input_kernel),
 //   bpart[rs][c] = sum over the block's frames of dy (the conv bias gradient, double).
-// Each may be null.  sums = [C][2] from autovc_bn_bwd_finalize_f32.  dy itself is never stored.
+// Dt / Xt / bpart may be null.  sums = [C][2] from autovc_bn_bwd_finalize_f32.  dy itself
+// is never stored.
 __global__ __launch_bounds__(256) void wino_bnbwd_kernel(int T, int C, const float* __restrict__ dz, int64_t lddz,
                                                          const float* __restrict__ y, int64_t ldy,
                                                          const float* __restrict__ coef, int act,
                                                          const float* __restrict__ sums, float inv_m,
                                                          float* __restrict__ Dt, float* __restrict__ Xt,
                                                          double* __restrict__ bpart, int64_t ntiles) {
-  __shared__ double red[4][64][4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = 4 * (blockIdx.x * 64 + lane);
+  const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
+  const WaveTiles wt = wave_tiles(T, ntiles);
   double sb[4] = {0.0, 0.0, 0.0, 0.0};
-  if (c < C) {
+  if (c < C && wt.live) {
+    // the window: own frames (slots 2 .. 4 kTPW + 1) always, halo slots only for the input transform
+    f32x4 g[kWin], yv[kWin];
+#pragma unroll
+    for (int s = 0; s < kWin; ++s) {
+      const int t = 4 * wt.q0 - 2 + s;
+      const bool in = (s >= 2 && s < kWin - 2) || (Xt && t >= 0 && t < T);
+      g[s] = in ? ld4(dz + (wt.b * T + t) * lddz + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      yv[s] = in ? ld4(y + (wt.b * T + t) * ldy + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     const f32x4 al = ld4(coef + c), sh = ld4(coef + C + c), mu = ld4(coef + 2 * C + c), is = ld4(coef + 3 * C + c);
     f32x4 s0, s1;
 #pragma unroll
@@ -344,38 +401,30 @@ __global__ __launch_bounds__(256) void wino_bnbwd_kernel(int T, int C, const flo
       s0[e] = sums[2 * (c + e)] * inv_m;
       s1[e] = sums[2 * (c + e) + 1] * inv_m;
     }
-    auto dy_at = [&](int64_t row) {
-      const f32x4 yv = ld4(y + row * ldy + c);
-      const f32x4 g = act_back(ld4(dz + row * lddz + c), yv, al, sh, act);
+#pragma unroll
+    for (int s = 0; s < kWin; ++s) {
+      const int t = 4 * wt.q0 - 2 + s;
+      const bool in = (s >= 2 && s < kWin - 2) || (Xt && t >= 0 && t < T);
+      const f32x4 gg = act_back(g[s], yv[s], al, sh, act);
       f32x4 r;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) r[e] = (g[e] - s0[e] - (yv[e] - mu[e]) * is[e] * s1[e]) * al[e];
-      return r;
-    };
+      for (int e = 0; e < 4; ++e) r[e] = (gg[e] - s0[e] - (yv[s][e] - mu[e]) * is[e] * s1[e]) * al[e];
+      g[s] = in ? r : f32x4{0.f, 0.f, 0.f, 0.f};     // g now holds dy (zero outside the sequence)
+    }
+#pragma unroll
+    for (int s = 2; s < kWin - 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sb[e] += (double)g[s][e];
+#pragma unroll
     for (int i = 0; i < kTPW; ++i) {
-      const int64_t tile = (int64_t)blockIdx.y * kTPB + w * kTPW + i;
-      if (tile >= ntiles) break;
-      const int64_t b = tile / (T / 4);
-      const int q = (int)(tile % (T / 4));
-      f32x4 d[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int t = 4 * q - 2 + j;
-        const bool own = j >= 2 && j < 6;
-        d[j] = (own || (Xt && t >= 0 && t < T)) ? dy_at(b * T + t) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int j = 2; j < 6; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sb[e] += (double)d[j][e];
       if (Dt)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int o = 0; o < 4; ++o)
-            if (kAT[o][k] != 0.f) v += kAT[o][k] * d[2 + o];
-          st4(Dt + ((int64_t)k * ntiles + tile) * C + c, v);
+            if (kAT[o][k] != 0.f) v += kAT[o][k] * g[4 * i + 2 + o];
+          st4(Dt + ((int64_t)k * ntiles + wt.tile0 + i) * C + c, v);
         }
       if (Xt)
 #pragma unroll
@@ -383,12 +432,14 @@ __global__ __launch_bounds__(256) void wino_bnbwd_kernel(int T, int C, const flo
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (kBT[k][j] != 0.f) v += kBT[k][j] * d[j];
-          st4(Xt + ((int64_t)k * ntiles + tile) * C + c, v);
+            if (kBT[k][j] != 0.f) v += kBT[k][j] * g[4 * i + j];
+          st4(Xt + ((int64_t)k * ntiles + wt.tile0 + i) * C + c, v);
         }
     }
   }
   if (!bpart) return;
+  __shared__ double red[4][64][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int e = 0; e < 4; ++e) red[w][lane][e] = sb[e];
   __syncthreads();
@@ -402,7 +453,7 @@ __global__ __launch_bounds__(256) void wino_bnbwd_kernel(int T, int C, const flo
 }  // namespace
 
 extern "C" int64_t autovc_wino5_rows(int B, int T) {
-  if (B <= 0 || T <= 0 || T % 4) return -1;
+  if (B <= 0 || T <= 0 || T % (4 * kTPW)) return -1;
   return ((int64_t)B * T / 4 + kTPB - 1) / kTPB;
 }
 
@@ -421,8 +472,12 @@ extern "C" int autovc_wino5_input_f32(int B, int T, int C, const float* x, int64
                 "autovc_wino5_input_f32: bad args (T and C multiples of 4)");
   AVC_CHECK_ARG(AVC_ALIGNED16(x) && AVC_ALIGNED16(out), "autovc_wino5_input_f32: alignment");
   const int64_t ntiles = (int64_t)B * T / 4;
-  hipLaunchKernelGGL(wino_input_kernel<false>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C,
-                     x, ldx, out, ntiles, (const float*)nullptr, 0);
+  if (T % (4 * kTPW) == 0)
+    hipLaunchKernelGGL(wino_input_win_kernel<false>, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)),
+                       dim3(256), 0, stream, T, C, x, ldx, out, ntiles, (const float*)nullptr, 0);
+  else
+    hipLaunchKernelGGL(wino_input_kernel<false>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C,
+                       x, ldx, out, ntiles, (const float*)nullptr, 0);
   AVC_CHECK_LAUNCH("autovc_wino5_input_f32");
   return avc::kOk;
 }
@@ -434,14 +489,19 @@ extern "C" int autovc_wino5_input_bn_f32(int B, int T, int C, const float* y, in
   AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_wino5_input_bn_f32: unknown activation %d", act);
   AVC_CHECK_ARG(AVC_ALIGNED16(y) && AVC_ALIGNED16(out) && AVC_ALIGNED16(coef), "autovc_wino5_input_bn_f32: alignment");
   const int64_t ntiles = (int64_t)B * T / 4;
-  hipLaunchKernelGGL(wino_input_kernel<true>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C, y,
-                     ldy, out, ntiles, coef, act);
+  if (T % (4 * kTPW) == 0)
+    hipLaunchKernelGGL(wino_input_win_kernel<true>, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)),
+                       dim3(256), 0, stream, T, C, y, ldy, out, ntiles, coef, act);
+  else
+    hipLaunchKernelGGL(wino_input_kernel<true>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C,
+                       y, ldy, out, ntiles, coef, act);
   AVC_CHECK_LAUNCH("autovc_wino5_input_bn_f32");
   return avc::kOk;
 }
 
 extern "C" int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
                                              int64_t ldy, double* part, hipStream_t stream) {
+  AVC_CHECK_ARG(T % (4 * kTPW) == 0, "%s: T must be a multiple of %d", "autovc_wino5_output_stats_f32", 4 * kTPW);
   AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && ldy % 4 == 0 && Yt && y && part,
                 "autovc_wino5_output_stats_f32: bad args (T and C multiples of 4)");
   AVC_CHECK_ARG(AVC_ALIGNED16(Yt) && AVC_ALIGNED16(y) && (!bias || AVC_ALIGNED16(bias)),
@@ -456,6 +516,7 @@ extern "C" int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Y
 extern "C" int autovc_wino5_output_bnbwd_f32(int B, int T, int C, const float* Yt, const float* yprev, int64_t ldy,
                                              const float* coef, int act, float* dz, int64_t lddz, double* part,
                                              hipStream_t stream) {
+  AVC_CHECK_ARG(T % (4 * kTPW) == 0, "%s: T must be a multiple of %d", "autovc_wino5_output_bnbwd_f32", 4 * kTPW);
   AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && ldy % 4 == 0 && lddz % 4 == 0 && Yt && yprev &&
                 coef && dz && part, "autovc_wino5_output_bnbwd_f32: bad args (T and C multiples of 4)");
   AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_wino5_output_bnbwd_f32: unknown activation %d", act);
@@ -471,6 +532,7 @@ extern "C" int autovc_wino5_output_bnbwd_f32(int B, int T, int C, const float* Y
 extern "C" int autovc_wino5_bnbwd_f32(int B, int T, int C, const float* dz, int64_t lddz, const float* y, int64_t ldy,
                                       const float* coef, int act, const float* sums, float* Dt, float* Xt,
                                       double* bias_part, hipStream_t stream) {
+  AVC_CHECK_ARG(T % (4 * kTPW) == 0, "%s: T must be a multiple of %d", "autovc_wino5_bnbwd_f32", 4 * kTPW);
   AVC_CHECK_ARG(B > 0 && T > 0 && T % 4 == 0 && C > 0 && C % 4 == 0 && lddz % 4 == 0 && ldy % 4 == 0 && dz && y &&
                 coef && sums && (Dt || Xt || bias_part), "autovc_wino5_bnbwd_f32: bad args (T and C multiples of 4)");
   AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_wino5_bnbwd_f32: unknown activation %d", act);

@@ -269,6 +269,20 @@ def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=
                         "note": "weight-streaming convention: packed per-step weights once per sample step; "
                                 "traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per sample step summed over its "
                                 "launches (profiles/wavenet_pmc.json)"}}
+    # the reference's own call shape: wavegen synthesises ONE utterance at a time
+    # (synthesis.py:58-69); 32 conditioning frames = 8,192 samples of one stream
+    c1 = c[:1, :, :32].contiguous()
+    model.generate(c1[:, :, :1], seed=1, log_scale_min=hparams.log_scale_min)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    y1 = model.generate(c1, seed=5, log_scale_min=hparams.log_scale_min)
+    torch.cuda.synchronize()
+    d1 = time.perf_counter() - t0
+    n1 = c1.shape[2] * hparams.hop_size
+    assert y1.shape == (1, n1) and bool(torch.isfinite(y1).all())
+    out["b1"] = {"workload": f"1 utterance x {n1} samples (wavegen's batch of one)",
+                 "us_per_sample_step": round(d1 / n1 * 1e6, 2), "samples_per_s": round(n1 / d1, 1),
+                 "rtf": round(n1 / 16000.0 / d1, 3)}
     if cpu:
         out["cpu_baseline"] = wavenet_cpu_baseline(n_utt, seconds_cpu)
         out["vs_cpu_baseline"] = round(out["samples_per_s"] / out["cpu_baseline"]["value"], 1)

@@ -11,7 +11,7 @@ for STEP in ${1//,/ }; do
     tests) timeout -k 10 ${T_TESTS:-1500} python -u -m pytest ${PYTEST_FILES:-tests} -m gpu ${PYTEST_X--x} -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/tests.log 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) timeout -k 10 900 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err ;;
-    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-wavenet --no-e2e > gpurun_out/prof.log 2>&1 ;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof${PROF_TAG} -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-wavenet --no-e2e --no-roofline ${PROF_ARGS} > gpurun_out/prof${PROF_TAG}.log 2>&1 ;;
     wnprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wnprof -o run --output-format csv -- python tools/wn_pmc.py 4 > gpurun_out/wnprof.log 2>&1 ;;
     wnpmc) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/wnpmc_f -o run --output-format csv -- python tools/wn_pmc.py 1 > gpurun_out/wnpmc_f.log 2>&1 && \
            timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/wnpmc_w -o run --output-format csv -- python tools/wn_pmc.py 1 > gpurun_out/wnpmc_w.log 2>&1 && \
@@ -23,6 +23,8 @@ for STEP in ${1//,/ }; do
     wnsweep) timeout -k 10 600 python tools/wavenet_bench.py 16 8 > gpurun_out/wnsweep.log 2>&1 ;;
     det) timeout -k 10 ${T_DET:-600} python -u tools/det_probe.py ${DET_B:-64} ${DET_STEPS:-6} ${DET_VARIANTS:-graph=1,stream=0 graph=1,stream=1} > gpurun_out/det.log 2> gpurun_out/det.err ;;
     bench2) timeout -k 10 900 python bench.py --gpus 2 ${BENCH_ARGS} > gpurun_out/bench2.json 2> gpurun_out/bench2.err ;;
+    wnpersist) timeout -k 10 120 tools/ubin/wn_persist_ubench > gpurun_out/wn_persist_ubench.txt 2>&1 && \
+               timeout -k 10 300 tools/ubin/chain_ubench > gpurun_out/chain_ubench.txt 2>&1 ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
   rc=$?

@@ -51,6 +51,15 @@ def main(path):
         print(f"  queue {q}: {d / 1e6:.2f} ms busy")
     for c, d in cat.most_common():
         print(f"  {c:24s} {d / 1e6:7.3f} ms  {100 * d / tot:5.1f} %  {calls[c]:5d} launches")
+    if "--kernels" in sys.argv:
+        per, n = collections.Counter(), collections.Counter()
+        for r in seg:
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "")[:60]
+            per[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            n[k] += 1
+        print("per kernel:")
+        for k, d in per.most_common(40):
+            print(f"  {k:60s} {d / 1e6:7.3f} ms {n[k]:5d} x {d / n[k] / 1e3:7.2f} us")
 
 
 if __name__ == "__main__":
