@@ -208,8 +208,18 @@ __global__ void wino_wgrad_kernel(int64_t n, const float* __restrict__ Mt, float
 // atomics), every load of a wave is issued before its first use, and the input-type
 // transforms read each frame of the wave's window (4 kTPW + 4 frames) once instead of
 // twice (neighbouring tiles share their 4 halo frames).
-constexpr int kTPW = 4;
-constexpr int kTPB = 4 * kTPW;
+#ifndef WINO_TPW
+#define WINO_TPW 1
+#endif
+#ifndef WINO_WAVES
+#define WINO_WAVES 8
+#endif
+constexpr int kTPW = WINO_TPW;           // tiles per wave: 4 (1024 waves, halo frames shared)
+                                         // measured 16.11-16.21 vs 16.00 ms/step for 1 (4096 waves),
+                                         // profiles/r03/ab_conv_chain.txt
+constexpr int kWaves = WINO_WAVES;       // waves per block
+constexpr int kThreads = 64 * kWaves;
+constexpr int kTPB = kWaves * kTPW;
 constexpr int kWin = 4 * kTPW + 4;       // frames of a wave's window: 4q0 - 2 .. 4(q0 + kTPW) + 1
 
 struct WaveTiles {
@@ -229,30 +239,37 @@ __device__ __forceinline__ WaveTiles wave_tiles(int T, int64_t ntiles) {
 
 // the 4 waves' per-channel double pairs (s1, s2) summed in fixed order into partial row
 // blockIdx.y (w == 0 lanes write)
-__device__ __forceinline__ void block_pairs(double (&s1)[4], double (&s2)[4], int C, int c, double* __restrict__ part) {
-  __shared__ double red[4][64][8];
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], int C, int c, double* __restrict__ out, int stride) {
+  __shared__ double red[kWaves][64][NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    red[w][lane][2 * e] = s1[e];
-    red[w][lane][2 * e + 1] = s2[e];
-  }
+  for (int e = 0; e < NV; ++e) red[w][lane][e] = v[e];
   __syncthreads();
   if (w != 0 || c >= C) return;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const double a = ((red[0][lane][2 * e] + red[1][lane][2 * e]) + red[2][lane][2 * e]) + red[3][lane][2 * e];
-    const double q = ((red[0][lane][2 * e + 1] + red[1][lane][2 * e + 1]) + red[2][lane][2 * e + 1]) +
-                     red[3][lane][2 * e + 1];
-    part[((int64_t)blockIdx.y * C + c + e) * 2 + 0] = a;
-    part[((int64_t)blockIdx.y * C + c + e) * 2 + 1] = q;
+  for (int e = 0; e < NV; ++e) {
+    double a = red[0][lane][e];
+#pragma unroll
+    for (int q = 1; q < kWaves; ++q) a += red[q][lane][e];      // fixed order
+    out[(int64_t)blockIdx.y * C * stride + (c + e / stride) * stride + e % stride] = a;
   }
+}
+
+__device__ __forceinline__ void block_pairs(double (&s1)[4], double (&s2)[4], int C, int c, double* __restrict__ part) {
+  double v[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = s1[e];
+    v[2 * e + 1] = s2[e];
+  }
+  block_sum<8>(v, C, c, part, 2);
 }
 
 // Input transform over a wave's window (T % 16 == 0): X~ of kTPW tiles from 4 kTPW + 4
 // frames; BN: the previous layer's BatchNorm + activation applied on load (pads stay zero)
 template <bool BN>
-__global__ __launch_bounds__(256) void wino_input_win_kernel(int T, int C, const float* __restrict__ x, int64_t ldx,
+__global__ __launch_bounds__(kThreads) void wino_input_win_kernel(int T, int C, const float* __restrict__ x, int64_t ldx,
                                                              float* __restrict__ out, int64_t ntiles,
                                                              const float* __restrict__ coef, int act) {
   const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
@@ -290,7 +307,7 @@ __global__ __launch_bounds__(256) void wino_input_win_kernel(int T, int C, const
 // y = A^T Y~ + bias (the output transform) and the per-block BatchNorm statistics of y:
 // part[rs][c] = (sum y, sum y^2) in double (raw sums: fp64 keeps the cancellation of
 // E[y^2] - E[y]^2 far below fp32 resolution for activations of this scale)
-__global__ __launch_bounds__(256) void wino_output_stats_kernel(int T, int C, const float* __restrict__ Yt,
+__global__ __launch_bounds__(kThreads) void wino_output_stats_kernel(int T, int C, const float* __restrict__ Yt,
                                                                 const float* __restrict__ bias, float* __restrict__ y,
                                                                 int64_t ldy, int64_t ntiles,
                                                                 double* __restrict__ part) {
@@ -327,7 +344,7 @@ __global__ __launch_bounds__(256) void wino_output_stats_kernel(int T, int C, co
 // dz = A^T Yd~ (the output transform of the flipped correlation) and, for that layer's
 // BatchNorm backward, part[rs][c] = (sum g, sum g (y - mean)) with g = act'(pre) dz
 // (bn.hip's bwd_partial_kernel sums, here produced where dz is)
-__global__ __launch_bounds__(256) void wino_output_bnbwd_kernel(int T, int C, const float* __restrict__ Yt,
+__global__ __launch_bounds__(kThreads) void wino_output_bnbwd_kernel(int T, int C, const float* __restrict__ Yt,
                                                                 const float* __restrict__ yprev, int64_t ldy,
                                                                 const float* __restrict__ coef, int act,
                                                                 float* __restrict__ dz, int64_t lddz, int64_t ntiles,
@@ -375,7 +392,7 @@ __global__ __launch_bounds__(256) void wino_output_bnbwd_kernel(int T, int C, co
 //   bpart[rs][c] = sum over the block's frames of dy (the conv bias gradient, double).
 // Dt / Xt / bpart may be null.  sums = [C][2] from autovc_bn_bwd_finalize_f32.  dy itself
 // is never stored.
-__global__ __launch_bounds__(256) void wino_bnbwd_kernel(int T, int C, const float* __restrict__ dz, int64_t lddz,
+__global__ __launch_bounds__(kThreads) void wino_bnbwd_kernel(int T, int C, const float* __restrict__ dz, int64_t lddz,
                                                          const float* __restrict__ y, int64_t ldy,
                                                          const float* __restrict__ coef, int act,
                                                          const float* __restrict__ sums, float inv_m,
@@ -437,17 +454,7 @@ __global__ __launch_bounds__(256) void wino_bnbwd_kernel(int T, int C, const flo
         }
     }
   }
-  if (!bpart) return;
-  __shared__ double red[4][64][4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) red[w][lane][e] = sb[e];
-  __syncthreads();
-  if (w != 0 || c >= C) return;
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-    bpart[(int64_t)blockIdx.y * C + c + e] =
-        ((red[0][lane][e] + red[1][lane][e]) + red[2][lane][e]) + red[3][lane][e];
+  if (bpart) block_sum<4>(sb, C, c, bpart, 1);
 }
 
 }  // namespace
@@ -474,7 +481,7 @@ extern "C" int autovc_wino5_input_f32(int B, int T, int C, const float* x, int64
   const int64_t ntiles = (int64_t)B * T / 4;
   if (T % (4 * kTPW) == 0)
     hipLaunchKernelGGL(wino_input_win_kernel<false>, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)),
-                       dim3(256), 0, stream, T, C, x, ldx, out, ntiles, (const float*)nullptr, 0);
+                       dim3(kThreads), 0, stream, T, C, x, ldx, out, ntiles, (const float*)nullptr, 0);
   else
     hipLaunchKernelGGL(wino_input_kernel<false>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C,
                        x, ldx, out, ntiles, (const float*)nullptr, 0);
@@ -491,7 +498,7 @@ extern "C" int autovc_wino5_input_bn_f32(int B, int T, int C, const float* y, in
   const int64_t ntiles = (int64_t)B * T / 4;
   if (T % (4 * kTPW) == 0)
     hipLaunchKernelGGL(wino_input_win_kernel<true>, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)),
-                       dim3(256), 0, stream, T, C, y, ldy, out, ntiles, coef, act);
+                       dim3(kThreads), 0, stream, T, C, y, ldy, out, ntiles, coef, act);
   else
     hipLaunchKernelGGL(wino_input_kernel<true>, dim3((C / 4 + 63) / 64, (unsigned)ntiles), dim3(64), 0, stream, T, C,
                        y, ldy, out, ntiles, coef, act);
@@ -507,7 +514,7 @@ extern "C" int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Y
   AVC_CHECK_ARG(AVC_ALIGNED16(Yt) && AVC_ALIGNED16(y) && (!bias || AVC_ALIGNED16(bias)),
                 "autovc_wino5_output_stats_f32: alignment");
   const int64_t ntiles = (int64_t)B * T / 4;
-  hipLaunchKernelGGL(wino_output_stats_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(256),
+  hipLaunchKernelGGL(wino_output_stats_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(kThreads),
                      0, stream, T, C, Yt, bias, y, ldy, ntiles, part);
   AVC_CHECK_LAUNCH("autovc_wino5_output_stats_f32");
   return avc::kOk;
@@ -523,7 +530,7 @@ extern "C" int autovc_wino5_output_bnbwd_f32(int B, int T, int C, const float* Y
   AVC_CHECK_ARG(AVC_ALIGNED16(Yt) && AVC_ALIGNED16(yprev) && AVC_ALIGNED16(dz) && AVC_ALIGNED16(coef),
                 "autovc_wino5_output_bnbwd_f32: alignment");
   const int64_t ntiles = (int64_t)B * T / 4;
-  hipLaunchKernelGGL(wino_output_bnbwd_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(256),
+  hipLaunchKernelGGL(wino_output_bnbwd_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(kThreads),
                      0, stream, T, C, Yt, yprev, ldy, coef, act, dz, lddz, ntiles, part);
   AVC_CHECK_LAUNCH("autovc_wino5_output_bnbwd_f32");
   return avc::kOk;
@@ -539,7 +546,7 @@ extern "C" int autovc_wino5_bnbwd_f32(int B, int T, int C, const float* dz, int6
   AVC_CHECK_ARG(AVC_ALIGNED16(dz) && AVC_ALIGNED16(y) && AVC_ALIGNED16(coef) && (!Dt || AVC_ALIGNED16(Dt)) &&
                 (!Xt || AVC_ALIGNED16(Xt)), "autovc_wino5_bnbwd_f32: alignment");
   const int64_t ntiles = (int64_t)B * T / 4;
-  hipLaunchKernelGGL(wino_bnbwd_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(256), 0,
+  hipLaunchKernelGGL(wino_bnbwd_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(kThreads), 0,
                      stream, T, C, dz, lddz, y, ldy, coef, act, sums, 1.0f / (float)((int64_t)B * T), Dt, Xt,
                      bias_part, ntiles);
   AVC_CHECK_LAUNCH("autovc_wino5_bnbwd_f32");

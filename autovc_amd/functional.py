@@ -496,7 +496,7 @@ def _chain_ok(x, layers, training):
             and x.dtype == torch.float32):
         return False
     T = x.shape[1]
-    if T % 16 or x.shape[2] % 4:   # the fused transforms take 4-tile windows of one sequence
+    if T % 4 or x.shape[2] % 4 or _lib.load().autovc_wino5_rows(x.shape[0], T) <= 0:
         return False
     for conv, bn, _ in layers:
         if (conv.kernel_size[0] != KS or conv.padding[0] != PAD or conv.stride[0] != 1 or conv.dilation[0] != 1

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build a variant of libautovc_hip.so with extra -D flags for A/B runs (tools only):
+#   tools/build_variant.sh NAME "-DWINO_TPW=4 -DWINO_WAVES=4"  ->  tools/ubin/libautovc_NAME.so
+# then AUTOVC_HIP_LIB=tools/ubin/libautovc_NAME.so selects it (autovc_amd/_lib.py).
+set -e
+cd "$(dirname "$0")/.."
+name=$1; shift
+mkdir -p tools/ubin/obj_$name
+for f in autovc_amd/csrc/capi.cpp autovc_amd/csrc/*.hip; do
+  b=$(basename "${f%.*}")
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -munsafe-fp-atomics \
+    -Iinclude $* -x hip -c "$f" -o tools/ubin/obj_$name/$b.o &
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/ubin/libautovc_$name.so tools/ubin/obj_$name/*.o
+rm -rf tools/ubin/obj_$name
+echo tools/ubin/libautovc_$name.so
