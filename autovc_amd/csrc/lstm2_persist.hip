@@ -612,7 +612,229 @@ void launch_persist(PArgs& a, void* workspace, hipStream_t stream) {
                      a);
 }
 
+// ================================================================ XCD-local recurrences
+// Decoder lstm1 (nn.LSTM(2*dim_neck + dim_emb, 512), model_vc_mel.py:90,111) as ONE
+// persistent launch whose synchronisation never leaves an XCD.  The batch rows of a step are
+// independent sequences, so XCD x (its 32 CUs, its own L2) owns batch rows 8x .. 8x+7 for the
+// whole sequence: its 32 workgroups (slot s = 0..31, one per CU) hold a replica of W_hh's
+// columns for units 16s .. 16s+15 (4 gates x 16 units x H = 128 KB fp32, in VGPRs as MFMA A
+// fragments), and per step only the 8 rows of h_{t-1} (16 KB) move, written and read inside
+// the XCD's L2: plain stores (kept in L2), sc1 loads (L1 bypassed, L2-served), and a per-XCD
+// step counter advanced by workgroup-scope atomics — executed in that L2, the coherence point
+// of every CU of the XCD — instead of a chip-wide barrier (lstm2_persist's costs ~2.8 us, a
+// launch boundary ~1.5 us).  Workgroups learn their XCD from HW_REG_XCC_ID and take slots
+// from a per-XCD counter, so any dispatch order works; a group that does not get exactly 32
+// workgroups (another partition mode, a second process's kernels) times out into the fault
+// path below (NaN over the outputs, device fault word, autovc_fault_status).
+// Products: v_mfma_f32_16x16x4_f32 with A = 16 gate columns x 4 k (W, registers) and B = 4 k
+// x 16 batch lanes, of which the group's 8 rows are real (the other 8 read a zero row):
+// 128 MFMAs per wave per step (wave w = gate w), k split as 4 lane groups x 128 consecutive k.
+constexpr int XRB = 8;                 // batch rows per XCD group
+constexpr int XNX = 8;                 // groups = XCDs
+constexpr int XSL = 32;                // workgroups (slots) per group
+constexpr int XNT = 256;               // 4 waves
+// barrier block (ints, one 128-B line per word): census and step counters per XCD, error word
+constexpr int XC_CENSUS = 0, XC_STEP = 16, XC_ERR = 32, XC_LINES = 33;
+constexpr int64_t XC_BYTES = XC_LINES * L * 4;
+constexpr int XC_PAD_LDS = 96 * 1024;  // dynamic LDS that keeps one workgroup per CU
+
+struct XArgs {
+  int B, T;
+  const float* gx;
+  int64_t gx_ldb, gx_ldt;
+  const float* W;            // W_hh (4H, H)
+  float *h, *c, *g;          // h (b*h_ldb + t*h_ldt), c (B,T,H), gates (B,T,4H) or null
+  int64_t h_ldb, h_ldt;
+  int* bar;
+  int timeout_ticks;
+};
+
+__device__ __forceinline__ int add_l2(int* p, int v) {
+  // every adder and poller of this word runs on ONE XCD: the add is performed in its L2
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int HH>
+__global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
+  constexpr int U = HH / XSL;            // units per slot
+  constexpr int KG = HH / 4;             // k per MFMA lane group
+  constexpr int HS = HH + 4;             // LDS row stride of the staged h rows (bank spread)
+  static_assert(U == 16, "one 16-column MFMA tile per gate");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* hs = lds;                        // [XRB + 1][HS], row XRB = zeros
+  float* pre = lds + (XRB + 1) * HS;      // [4 gates][U][XRB + 1]
+  __shared__ int s_info[3];               // xcc, slot, status
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T;
+  if (tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    const int xcc = (int)(x & 15);
+    const int slot = add_rlx(a.bar + (XC_CENSUS + xcc) * L, 1);
+    s_info[0] = xcc;
+    s_info[1] = slot;
+    s_info[2] = (xcc < XNX && slot < XSL) ? 0 : 1;
+    if (s_info[2]) st_rlx(a.bar + XC_ERR * L, 1);
+  }
+  for (int i = tid; i < HS; i += XNT) hs[XRB * HS + i] = 0.f;
+  __syncthreads();
+  const int xcc = s_info[0] < XNX ? s_info[0] : 0, slot = s_info[1] < XSL ? s_info[1] : 0;
+  const int r0 = XRB * xcc, u0 = U * slot;
+  // cell ownership: threads 0..127 own (row tid / 16, unit tid % 16) for the whole sequence
+  const int cb = tid >> 4, cu = tid & 15;
+  const bool cown = tid < XRB * U;
+  auto fail = [&]() {
+    const float nan = __builtin_nanf("");
+    if (cown)
+      for (int t = 0; t < T; ++t) {
+        a.h[(int64_t)(r0 + cb) * a.h_ldb + (int64_t)t * a.h_ldt + u0 + cu] = nan;
+        a.c[((int64_t)(r0 + cb) * T + t) * HH + u0 + cu] = nan;
+      }
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (s_info[2]) {
+    if (s_info[0] < XNX && s_info[1] < XSL) fail();   // an in-range slot of a failed group
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // W fragments: wave = gate, lane -> column u0 + lane % 16, k = 128 (lane / 16) + q
+  float wf[KG];
+  {
+    const float* src = a.W + (int64_t)(wave * HH + u0 + (lane & 15)) * HH + KG * (lane >> 4);
+#pragma unroll
+    for (int q = 0; q < KG; q += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + q);
+      wf[q] = v[0]; wf[q + 1] = v[1]; wf[q + 2] = v[2]; wf[q + 3] = v[3];
+    }
+  }
+  // B rows of this lane: its batch row of the staged h, or the zero row
+  const float* hrow = hs + (((lane & 15) < XRB) ? (lane & 15) : XRB) * HS + KG * (lane >> 4);
+  float cst = 0.f;                        // cell state (cown)
+  float gxv[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load_gx = [&](int t) {
+    const float* g = a.gx + (int64_t)(r0 + cb) * a.gx_ldb + (int64_t)t * a.gx_ldt + u0 + cu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gxv[q] = g[q * HH];
+  };
+  if (cown) load_gx(0);
+  int* step_ctr = a.bar + (XC_STEP + xcc) * L;
+  for (int t = 0; t < T; ++t) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (t > 0) {
+      // ---- XCD barrier: all 32 slots stored h_{t-1}
+      if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        while (ld_rlx(step_ctr) < XSL * t) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout_ticks || ld_rlx(a.bar + XC_ERR * L)) {
+            st_rlx(a.bar + XC_ERR * L, 1);
+            ok = 0;
+            break;
+          }
+        }
+        s_info[2] = ok ? 0 : 1;
+      }
+      __syncthreads();
+      if (s_info[2]) {
+        fail();
+        return;
+      }
+      // ---- stage h_{t-1} of the group's 8 rows (sc1 loads: L1 bypassed, L2-served)
+      {
+        const int row = tid >> 5, k = (tid & 31) * (HH / 32);
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            a.h + (int64_t)(r0 + row) * a.h_ldb + (int64_t)(t - 1) * a.h_ldt, (short)0, 0x7fffffff, 0x00020000);
+        f32x4 v[HH / 128];
+#pragma unroll
+        for (int i = 0; i < HH / 128; ++i)
+          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (k + 4 * i) * 4, 0, 16));
+#pragma unroll
+        for (int i = 0; i < HH / 128; ++i) *reinterpret_cast<f32x4*>(hs + row * HS + k + 4 * i) = v[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < KG; q += 4) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(hrow + q);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q], bv[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 1], bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 2], bv[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 3], bv[3], acc, 0, 0, 0);
+      }
+    }
+    // C[unit 4 (lane / 16) + r][batch lane % 16] of gate `wave`
+    if ((lane & 15) < XRB)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pre[(wave * U + 4 * (lane >> 4) + r) * (XRB + 1) + (lane & 15)] = acc[r];
+    __syncthreads();
+    if (cown) {
+      float p[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p[q] = pre[(q * U + cu) * (XRB + 1) + cb] + gxv[q];
+      if (t + 1 < T) load_gx(t + 1);
+      const float i_ = avc_sigmoid(p[0]), f_ = avc_sigmoid(p[1]), g_ = tanhf(p[2]), o_ = avc_sigmoid(p[3]);
+      cst = f_ * cst + i_ * g_;
+      const float hn = o_ * tanhf(cst);
+      const int64_t bt = (int64_t)(r0 + cb) * T + t;
+      a.h[(int64_t)(r0 + cb) * a.h_ldb + (int64_t)t * a.h_ldt + u0 + cu] = hn;
+      a.c[bt * HH + u0 + cu] = cst;
+      if (a.g) {
+        float* gs = a.g + bt * 4 * HH + u0 + cu;
+        gs[0] = i_; gs[HH] = f_; gs[2 * HH] = g_; gs[3 * HH] = o_;
+      }
+    }
+    // ---- arrive: this workgroup's h_t is in the XCD's L2
+    if (t + 1 < T) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) add_l2(step_ctr, 1);
+    }
+  }
+}
+
+int g_xcd_ok = -1;
+
+bool xcd_fits() {
+  if (g_xcd_ok < 0) {
+    int dev = 0, per = 0;
+    hipDeviceProp_t p;
+    const void* k = reinterpret_cast<const void*>(lstm_xcd_fwd_kernel<512>);
+    const int lb = XC_PAD_LDS;
+    g_xcd_ok = hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess &&
+               p.multiProcessorCount == XNX * XSL &&
+               hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
+               hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_fwd_kernel<512>, XNT, lb) == hipSuccess &&
+               per >= 1;
+  }
+  return g_xcd_ok == 1;
+}
+
 }  // namespace
+
+extern "C" int autovc_lstm_xcd_supported(int B, int H) {
+  return (B == XRB * XNX && H == 512 && xcd_fits()) ? 1 : 0;
+}
+
+extern "C" int64_t autovc_lstm_xcd_workspace_bytes(void) { return XC_BYTES; }
+
+extern "C" int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                                       const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                                       float* gates, void* workspace, hipStream_t stream) {
+  static const char* fn = "autovc_lstm_fwd_xcd_f32";
+  AVC_CHECK_ARG(T > 0 && autovc_lstm_xcd_supported(B, H),
+                "%s: unsupported shape B=%d H=%d on this device (needs B=64, H=512, 8 XCDs x 32 CUs)", fn, B, H);
+  AVC_CHECK_ARG(gx && W_hh && h && c_all && workspace, "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh) && AVC_ALIGNED16(workspace), "%s: W_hh / workspace must be 16-byte aligned", fn);
+  XArgs a;
+  a.B = B; a.T = T; a.gx = gx; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt; a.W = W_hh;
+  a.h = h; a.c = c_all; a.g = gates; a.h_ldb = h_ldb; a.h_ldt = h_ldt;
+  a.bar = static_cast<int*>(workspace);
+  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
+  AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
+  hipLaunchKernelGGL(lstm_xcd_fwd_kernel<512>, dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
 
 extern "C" int64_t autovc_lstm2_persist_workspace_bytes(int B, int T, int H) {
   if (B <= 0 || T <= 0 || H != 1024) return -1;

@@ -796,6 +796,10 @@ class LSTMLayerFn(torch.autograd.Function):
             Wb = _bf(W_hh)   # held until the launches are enqueued (stream-ordered reuse after)
             _lib.call("autovc_lstm_fwd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),
                       h.data_ptr(), hb.data_ptr(), c.data_ptr(), _p(gates), 0, _s())
+        elif lstm_xcd(B, H):
+            ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmx")
+            _lib.call("autovc_lstm_fwd_xcd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
+                      h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), ws, _s())
         elif lstm_persistent(B, H):
             ws = _ws(dev, _lib.load().autovc_lstm_persist_workspace_bytes(B, T, H), "lstmp")
             _lib.call("autovc_lstm_fwd_persist_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W_hh.data_ptr(),
@@ -931,6 +935,16 @@ _PERSIST1_ON = os.environ.get("AVC_LSTM_PERSIST", "0") != "0"
 
 def lstm_persistent(B, H):
     return _PERSIST1_ON and bool(_lib.load().autovc_lstm_persist_supported(B, H))
+
+
+# decoder lstm1 forward (fp32, B = 64, H = 512) as one persistent launch whose batch rows are
+# split over the 8 XCDs, every synchronisation inside one XCD's L2 (csrc/lstm2_persist.hip
+# "XCD-local recurrences"); AVC_LSTM_XCD=0 selects the per-step launches
+_XCD_ON = os.environ.get("AVC_LSTM_XCD", "1") != "0"
+
+
+def lstm_xcd(B, H):
+    return _XCD_ON and bool(_lib.load().autovc_lstm_xcd_supported(B, H))
 
 
 class LSTM2StackFn(torch.autograd.Function):

@@ -294,6 +294,20 @@ int autovc_lstm_fwd_persist_f32(int B, int T, int H, const float* gx, int64_t gx
                                 const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                                 float* gates, void* workspace, hipStream_t stream);
 int autovc_lstm2_persist_status(const void* workspace, hipStream_t stream);
+/* One large-H layer (decoder lstm1, model_vc_mel.py:90,111) as ONE persistent launch whose
+ * synchronisation stays inside each XCD: XCD x owns batch rows 8x .. 8x+7 (independent
+ * sequences), its 32 workgroups each hold W_hh's 4 x 16 columns for 16 units in registers,
+ * and per step only those rows' h_{t-1} moves, through the XCD's L2, behind a per-XCD step
+ * counter.  Arguments and outputs of autovc_lstm_fwd_f32 (forward direction) plus a
+ * workspace of autovc_lstm_xcd_workspace_bytes() bytes (barrier words, re-initialised by
+ * every call).  Only where autovc_lstm_xcd_supported(B, H): B = 64, H = 512 on 8 XCDs x 32
+ * CUs.  A group that cannot run its 32 workgroups together times out into the fault path
+ * of autovc_fault_status. */
+int autovc_lstm_xcd_supported(int B, int H);
+int64_t autovc_lstm_xcd_workspace_bytes(void);
+int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                            const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                            float* gates, void* workspace, hipStream_t stream);
 /* Co-residency failures reach the caller without a per-call sync: a persistent launch
  * whose grid barrier timed out writes NaN over the h / c it owns (so the loss turns NaN)
  * and sets bit 0 of a sticky per-device fault word.  autovc_fault_status (synchronises

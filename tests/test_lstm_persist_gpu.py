@@ -178,3 +178,65 @@ def test_barrier_timeout_surfaces_as_error(cuda):
     losses = solver.train_step(x, e)
     assert bool(torch.isfinite(torch.stack([v.reshape(()) for v in losses])).all())
     AF.check_device_faults(cuda)
+
+
+def _xcd_supported():
+    from autovc_amd import _lib
+    return bool(_lib.load().autovc_lstm_xcd_supported(64, 512))
+
+
+def _run1(name, B, T, H, gx, W, dev, ws=None):
+    from autovc_amd import _lib
+    h, c = (torch.full((B, T, H), float("nan"), device=dev) for _ in range(2))
+    g = torch.full((B, T, 4 * H), float("nan"), device=dev)
+    args = [B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(), h.data_ptr(), T * H, H, c.data_ptr(), g.data_ptr()]
+    if ws is not None:
+        args.append(ws.data_ptr())
+    else:
+        args.append(0)   # autovc_lstm_fwd_f32's `reverse`
+    _lib.call(name, *args, _lib.stream_ptr(dev))
+    torch.cuda.synchronize()
+    return h, c, g
+
+
+@pytest.mark.parametrize("T", [1, 2, 128])
+def test_xcd_local_lstm_matches_per_step_launches(cuda, T):
+    """Decoder lstm1 forward as one XCD-local persistent launch (autovc_lstm_fwd_xcd_f32:
+    batch rows split over the 8 XCDs, every hand-off inside one XCD's L2) against the
+    per-step launches: h, c, gates within fp32 summation-order noise; a second call is
+    bit-identical; no fault recorded."""
+    from autovc_amd import _lib, functional as AF
+    if not _xcd_supported():
+        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
+    B, H = 64, 512
+    AF.check_device_faults(cuda)
+    gx, W, _, _ = _inputs(B, T, H, cuda, seed=9)
+    ref = _run1("autovc_lstm_fwd_f32", B, T, H, gx, W[0], cuda)
+    ws = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
+    got = _run1("autovc_lstm_fwd_xcd_f32", B, T, H, gx, W[0], cuda, ws)
+    AF.check_device_faults(cuda)
+    for name, a, r in zip(["h", "c", "gates"], got, ref):
+        assert bool(torch.isfinite(a).all()), name
+        err = (a.double() - r.double()).abs().max().item() / max(r.abs().max().item(), 1e-30)
+        assert err < 2e-5, (name, err)
+    again = _run1("autovc_lstm_fwd_xcd_f32", B, T, H, gx, W[0], cuda, ws)
+    for a, b in zip(got, again):
+        assert torch.equal(a, b)
+
+
+def test_xcd_local_lstm_timeout_surfaces(cuda):
+    from autovc_amd import _lib, functional as AF
+    if not _xcd_supported():
+        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
+    B, H, T = 64, 512, 16
+    AF.check_device_faults(cuda)
+    gx, W, _, _ = _inputs(B, T, H, cuda, seed=9)
+    ws = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
+    _lib.call("autovc_lstm_persist_set_timeout_ticks", 1)
+    try:
+        h, _, _ = _run1("autovc_lstm_fwd_xcd_f32", B, T, H, gx, W[0], cuda, ws)
+    finally:
+        _lib.call("autovc_lstm_persist_set_timeout_ticks", 0)
+    assert bool(torch.isnan(h[:, -1]).any())
+    with pytest.raises(AF.DeviceFault):
+        AF.check_device_faults(cuda)
