@@ -710,6 +710,7 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
   // B rows of this lane: its batch row of the staged h, or the zero row
   const float* hrow = hs + (((lane & 15) < XRB) ? (lane & 15) : XRB) * HS + KG * (lane >> 4);
   float cst = 0.f;                        // cell state (cown)
+  float cell_out[5];
   float gxv[4] = {0.f, 0.f, 0.f, 0.f};
   auto load_gx = [&](int t) {
     const float* g = a.gx + (int64_t)(r0 + cb) * a.gx_ldb + (int64_t)t * a.gx_ldt + u0 + cu;
@@ -771,23 +772,186 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
       float p[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) p[q] = pre[(q * U + cu) * (XRB + 1) + cb] + gxv[q];
-      if (t + 1 < T) load_gx(t + 1);
-      const float i_ = avc_sigmoid(p[0]), f_ = avc_sigmoid(p[1]), g_ = tanhf(p[2]), o_ = avc_sigmoid(p[3]);
+      const float i_ = avc_sigmoid_fast(p[0]), f_ = avc_sigmoid_fast(p[1]), g_ = avc_tanh_fast(p[2]);
+      const float o_ = avc_sigmoid_fast(p[3]);
       cst = f_ * cst + i_ * g_;
-      const float hn = o_ * tanhf(cst);
-      const int64_t bt = (int64_t)(r0 + cb) * T + t;
+      const float hn = o_ * avc_tanh_fast(cst);
       a.h[(int64_t)(r0 + cb) * a.h_ldb + (int64_t)t * a.h_ldt + u0 + cu] = hn;
-      a.c[bt * HH + u0 + cu] = cst;
-      if (a.g) {
-        float* gs = a.g + bt * 4 * HH + u0 + cu;
-        gs[0] = i_; gs[HH] = f_; gs[2 * HH] = g_; gs[3 * HH] = o_;
-      }
+      cell_out[0] = cst; cell_out[1] = i_; cell_out[2] = f_; cell_out[3] = g_; cell_out[4] = o_;
     }
-    // ---- arrive: this workgroup's h_t is in the XCD's L2
+    // ---- arrive once h_t (only it) is in the XCD's L2; c / gates and the next gx loads
+    // go out after the arrive, under the next step's wait
     if (t + 1 < T) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) add_l2(step_ctr, 1);
+    }
+    if (cown) {
+      const int64_t bt = (int64_t)(r0 + cb) * T + t;
+      a.c[bt * HH + u0 + cu] = cell_out[0];
+      if (a.g) {
+        float* gs = a.g + bt * 4 * HH + u0 + cu;
+        gs[0] = cell_out[1]; gs[HH] = cell_out[2]; gs[2 * HH] = cell_out[3]; gs[3 * HH] = cell_out[4];
+      }
+      if (t + 1 < T) load_gx(t + 1);
+    }
+  }
+}
+
+// Backward of the same layer (BPTT, reverse time), same XCD split: slot s owns units
+// 16s .. 16s+15 of the group's 8 rows — the cells whose dG it writes and the columns of the
+// recurrent product dh_rec(t) = dG_{t+1} W_hh (K = 4H = 2048) it reduces.  W_hh's 16 columns
+// stay in registers (A fragments: 16 units x 4 k); each wave takes a quarter of K and streams
+// its B fragments (dG_{t+1} rows of the group, written by the 32 slots of the XCD) straight
+// from L2 with sc1 loads, one chunk ahead of its MFMAs; the 4 partial tiles are summed in LDS
+// in fixed order, then the pointwise pass (lstm.hip bwd_pointwise_body's arithmetic).
+struct XBArgs {
+  int B, T;
+  const float* dh;           // dh_out (b*d_ldb + t*d_ldt), may be null
+  int64_t d_ldb, d_ldt;
+  const float* gates;        // (B,T,4H) i, f, g, o
+  const float* c;            // (B,T,H)
+  const float* W;            // W_hh (4H, H)
+  float* dG;                 // (B,T,4H)
+  int* bar;
+  int timeout_ticks;
+};
+
+template <int HH>
+__global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
+  constexpr int U = HH / XSL;            // units per slot (16)
+  constexpr int K4 = 4 * HH;             // recurrent K
+  constexpr int KW = K4 / 4;             // k per wave
+  constexpr int KG = KW / 4;             // k per MFMA lane group (consecutive)
+  constexpr int CH = 16;                 // k per load chunk (4 b128 per lane)
+  static_assert(U == 16 && KG % CH == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* part = lds;                      // [4 waves][U][XRB + 1]
+  __shared__ int s_info[3];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T;
+  if (tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    const int xcc = (int)(x & 15);
+    const int slot = add_rlx(a.bar + (XC_CENSUS + xcc) * L, 1);
+    s_info[0] = xcc;
+    s_info[1] = slot;
+    s_info[2] = (xcc < XNX && slot < XSL) ? 0 : 1;
+    if (s_info[2]) st_rlx(a.bar + XC_ERR * L, 1);
+  }
+  __syncthreads();
+  const int xcc = s_info[0] < XNX ? s_info[0] : 0, slot = s_info[1] < XSL ? s_info[1] : 0;
+  const int r0 = XRB * xcc, u0 = U * slot;
+  const int cb = tid >> 4, cu = tid & 15;
+  const bool cown = tid < XRB * U;
+  const int64_t cell0 = (int64_t)(r0 + cb) * T;     // (b, t) row base of this cell's batch row
+  auto fail = [&]() {
+    const float nan = __builtin_nanf("");
+    if (cown)
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a.dG[(cell0 + t) * K4 + q * HH + u0 + cu] = nan;
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (s_info[2]) {
+    if (s_info[0] < XNX && s_info[1] < XSL) fail();
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // A fragments: lane -> unit u0 + lane % 16, k = KW wave + KG (lane / 16) + q: W_hh[k][unit]
+  const int kbase = KW * wave + KG * (lane >> 4);
+  float wf[KG];
+#pragma unroll
+  for (int q = 0; q < KG; ++q) wf[q] = a.W[(int64_t)(kbase + q) * HH + u0 + (lane & 15)];
+  const bool bvalid = (lane & 15) < XRB;
+  const int brow = r0 + ((lane & 15) < XRB ? (lane & 15) : 0);
+  // pointwise operands of step t (prefetched one step ahead)
+  f32x4 gt = {0.f, 0.f, 0.f, 0.f};
+  float cc = 0.f, cpv = 0.f, dho = 0.f, dcs = 0.f;
+  auto load_pw = [&](int t) {
+    const float* g = a.gates + (cell0 + t) * K4 + u0 + cu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gt[q] = g[q * HH];
+    cc = a.c[(cell0 + t) * HH + u0 + cu];
+    cpv = t > 0 ? a.c[(cell0 + t - 1) * HH + u0 + cu] : 0.f;
+    dho = a.dh ? a.dh[(int64_t)(r0 + cb) * a.d_ldb + (int64_t)t * a.d_ldt + u0 + cu] : 0.f;
+  };
+  if (cown) load_pw(T - 1);
+  int* step_ctr = a.bar + (XC_STEP + xcc) * L;
+  for (int s = 0; s < T; ++s) {
+    const int t = T - 1 - s;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      // ---- XCD barrier: all 32 slots stored dG_{t+1}
+      if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        while (ld_rlx(step_ctr) < XSL * s) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout_ticks || ld_rlx(a.bar + XC_ERR * L)) {
+            st_rlx(a.bar + XC_ERR * L, 1);
+            ok = 0;
+            break;
+          }
+        }
+        s_info[2] = ok ? 0 : 1;
+      }
+      __syncthreads();
+      if (s_info[2]) {
+        fail();
+        return;
+      }
+      // ---- dh_rec = dG_{t+1} W_hh over this wave's K quarter; B from L2 (sc1), a chunk ahead
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          a.dG + ((int64_t)brow * T + t + 1) * K4 + kbase, (short)0, 0x7fffffff, 0x00020000);
+      f32x4 nb[CH / 4];
+      auto ld_chunk = [&](int c0) {
+#pragma unroll
+        for (int i = 0; i < CH / 4; ++i)
+          nb[i] = bvalid ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (c0 + 4 * i) * 4, 0, 16))
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+      };
+      ld_chunk(0);
+#pragma unroll
+      for (int c0 = 0; c0 < KG; c0 += CH) {
+        f32x4 cur[CH / 4];
+#pragma unroll
+        for (int i = 0; i < CH / 4; ++i) cur[i] = nb[i];
+        if (c0 + CH < KG) ld_chunk(c0 + CH);
+#pragma unroll
+        for (int i = 0; i < CH / 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c0 + 4 * i + e], cur[i][e], acc, 0, 0, 0);
+      }
+    }
+    // C[unit 4 (lane / 16) + r][batch lane % 16]: the 4 waves' K quarters, summed in order
+    if (bvalid)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[(wave * U + 4 * (lane >> 4) + r) * (XRB + 1) + (lane & 15)] = acc[r];
+    __syncthreads();
+    float dgo[4];
+    if (cown) {
+      const float dh = dho + (((part[(0 * U + cu) * (XRB + 1) + cb] + part[(1 * U + cu) * (XRB + 1) + cb]) +
+                               part[(2 * U + cu) * (XRB + 1) + cb]) + part[(3 * U + cu) * (XRB + 1) + cb]);
+      const float i_ = gt[0], f_ = gt[1], g_ = gt[2], o_ = gt[3];
+      const float tc = tanhf(cc);
+      const float dc = dcs + dh * o_ * (1.f - tc * tc);
+      dgo[0] = dc * g_ * i_ * (1.f - i_);
+      dgo[1] = dc * cpv * f_ * (1.f - f_);
+      dgo[2] = dc * i_ * (1.f - g_ * g_);
+      dgo[3] = dh * tc * o_ * (1.f - o_);
+      dcs = dc * f_;
+      float* d = a.dG + (cell0 + t) * K4 + u0 + cu;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q * HH] = dgo[q];
+    }
+    if (s + 1 < T) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) add_l2(step_ctr, 1);
+      if (cown) load_pw(t - 1);
     }
   }
 }
@@ -804,6 +968,10 @@ bool xcd_fits() {
                p.multiProcessorCount == XNX * XSL &&
                hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_fwd_kernel<512>, XNT, lb) == hipSuccess &&
+               per >= 1 &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_bwd_kernel<512>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
+               hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_bwd_kernel<512>, XNT, lb) == hipSuccess &&
                per >= 1;
   }
   return g_xcd_ok == 1;
@@ -832,6 +1000,25 @@ extern "C" int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
   AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
   hipLaunchKernelGGL(lstm_xcd_fwd_kernel<512>, dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm_bwd_xcd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                                       const float* gates, const float* c_all, const float* W_hh, float* dG,
+                                       void* workspace, hipStream_t stream) {
+  static const char* fn = "autovc_lstm_bwd_xcd_f32";
+  AVC_CHECK_ARG(T > 0 && autovc_lstm_xcd_supported(B, H),
+                "%s: unsupported shape B=%d H=%d on this device (needs B=64, H=512, 8 XCDs x 32 CUs)", fn, B, H);
+  AVC_CHECK_ARG(gates && c_all && W_hh && dG && workspace, "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(dG) && AVC_ALIGNED16(workspace), "%s: dG / workspace must be 16-byte aligned", fn);
+  XBArgs a;
+  a.B = B; a.T = T; a.dh = dh_out; a.d_ldb = d_ldb; a.d_ldt = d_ldt; a.gates = gates; a.c = c_all; a.W = W_hh;
+  a.dG = dG;
+  a.bar = static_cast<int*>(workspace);
+  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
+  AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
+  hipLaunchKernelGGL(lstm_xcd_bwd_kernel<512>, dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
 }

@@ -838,6 +838,15 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     B, T, I = x.shape
     H = W_hh.shape[1]
     dev = x.device
+    if not _bf16_rec(H) and lstm_xcd(B, H):
+        # one XCD-local persistent launch (the recurrent product reads W_hh untransposed)
+        dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+        ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmx")
+        mark = _grad_mark(dev)
+        _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
+                  W_hh.data_ptr(), dG.data_ptr(), ws, _s())
+        _flush_grad_queue(after=mark)
+        return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs)
     WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
     _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
     # split-K of the recurrent product (same box, alternating): fp32 4 ways at H=1024 (256

@@ -308,6 +308,14 @@ int64_t autovc_lstm_xcd_workspace_bytes(void);
 int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                             const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                             float* gates, void* workspace, hipStream_t stream);
+/* Its backward (BPTT of autovc_lstm_bwd_f32 with reverse = 0) the same way: slot s of XCD x
+ * reduces dh_rec for units 16s .. 16s+15 of rows 8x .. 8x+7 over K = 4H with W_hh's columns
+ * in registers (W_hh as stored, (4H, H): no transpose) and writes those cells' dG; the dG
+ * rows of the group are the per-step hand-off (L2, per-XCD step counter).  dh_out may be
+ * null.  Same workspace and support rule as autovc_lstm_fwd_xcd_f32. */
+int autovc_lstm_bwd_xcd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                            const float* gates, const float* c_all, const float* W_hh, float* dG,
+                            void* workspace, hipStream_t stream);
 /* Co-residency failures reach the caller without a per-call sync: a persistent launch
  * whose grid barrier timed out writes NaN over the h / c it owns (so the loss turns NaN)
  * and sets bit 0 of a sticky per-device fault word.  autovc_fault_status (synchronises

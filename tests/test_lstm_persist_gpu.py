@@ -240,3 +240,36 @@ def test_xcd_local_lstm_timeout_surfaces(cuda):
     assert bool(torch.isnan(h[:, -1]).any())
     with pytest.raises(AF.DeviceFault):
         AF.check_device_faults(cuda)
+
+
+@pytest.mark.parametrize("T", [1, 2, 128])
+def test_xcd_local_lstm_backward_matches_split_k_launches(cuda, T):
+    """The lstm1 backward as one XCD-local persistent launch (autovc_lstm_bwd_xcd_f32) against
+    the per-step split-K launches (autovc_lstm_bwd_f32 on W_hh^T): dG within fp32
+    summation-order noise (relative to its max), repeat calls bit-identical."""
+    from autovc_amd import _lib, functional as AF
+    if not _xcd_supported():
+        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
+    B, H = 64, 512
+    AF.check_device_faults(cuda)
+    gx, W, _, _ = _inputs(B, T, H, cuda, seed=11)
+    _, c, g = _run1("autovc_lstm_fwd_f32", B, T, H, gx, W[0], cuda)
+    dh = (torch.randn(B, T, H, generator=torch.Generator().manual_seed(3)) * 0.1).to(cuda)
+    WT = W[0].t().contiguous()
+    ref = torch.empty(B, T, 4 * H, device=cuda)
+    ws = torch.empty(4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, 8), dtype=torch.uint8, device=cuda)
+    _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(), WT.data_ptr(),
+              ref.data_ptr(), 0, 8, ws.data_ptr(), _lib.stream_ptr(cuda))
+    wx = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
+    outs = []
+    for _ in range(2):
+        got = torch.full((B, T, 4 * H), float("nan"), device=cuda)
+        _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(),
+                  W[0].data_ptr(), got.data_ptr(), wx.data_ptr(), _lib.stream_ptr(cuda))
+        torch.cuda.synchronize()
+        outs.append(got)
+    AF.check_device_faults(cuda)
+    assert bool(torch.isfinite(outs[0]).all())
+    err = (outs[0].double() - ref.double()).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-5, err
+    assert torch.equal(outs[0], outs[1])

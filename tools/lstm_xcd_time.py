@@ -28,6 +28,16 @@ def main():
     runs = {"per-step launches": lambda: _lib.call("autovc_lstm_fwd_f32", *base, 0, st),
             "persistent (chip-wide barrier)": lambda: _lib.call("autovc_lstm_fwd_persist_f32", *base, wsp.data_ptr(), st),
             "persistent (XCD-local)": lambda: _lib.call("autovc_lstm_fwd_xcd_f32", *base, wsx.data_ptr(), st)}
+    WT = W.t().contiguous()
+    dh = torch.randn(B, T, H, generator=g).to(dev) * 0.1
+    dG = torch.empty(B, T, 4 * H, device=dev)
+    wsb = torch.empty(4 * lib.autovc_lstm_bwd_workspace_floats(B, H, 8), dtype=torch.uint8, device=dev)
+    runs["backward: split-K launches"] = lambda: _lib.call(
+        "autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gt.data_ptr(), c.data_ptr(), WT.data_ptr(),
+        dG.data_ptr(), 0, 8, wsb.data_ptr(), st)
+    runs["backward: persistent (XCD-local)"] = lambda: _lib.call(
+        "autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, gt.data_ptr(), c.data_ptr(), W.data_ptr(),
+        dG.data_ptr(), wsx.data_ptr(), st)
     ts = {k: [] for k in runs}
     for _ in range(7):
         for k, fn in runs.items():
