@@ -823,12 +823,14 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
   constexpr int K4 = 4 * HH;             // recurrent K
   constexpr int KW = K4 / 4;             // k per wave
   constexpr int KG = KW / 4;             // k per MFMA lane group (consecutive)
-  constexpr int CH = 16;                 // k per load chunk (4 b128 per lane)
-  static_assert(U == 16 && KG % CH == 0, "tile shape");
+  static_assert(U == 16, "tile shape");
+  static_assert(4 * U * (XRB + 1) * 4 + 4 * (XRB + 1) * (KW + 4) * 4 <= XC_PAD_LDS, "LDS budget");
+  constexpr int SS = KW + 4;             // LDS row stride of a wave's slab (bank spread)
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* part = lds;                      // [4 waves][U][XRB + 1]
-  __shared__ int s_info[3];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* slab = lds + 4 * U * (XRB + 1) + wave * (XRB + 1) * SS;   // this wave's [XRB + 1][SS], row XRB = 0
+  __shared__ int s_info[3];
   const int T = a.T;
   if (tid == 0) {
     unsigned x;
@@ -840,6 +842,7 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
     s_info[2] = (xcc < XNX && slot < XSL) ? 0 : 1;
     if (s_info[2]) st_rlx(a.bar + XC_ERR * L, 1);
   }
+  for (int i = lane; i < SS; i += 64) slab[XRB * SS + i] = 0.f;
   __syncthreads();
   const int xcc = s_info[0] < XNX ? s_info[0] : 0, slot = s_info[1] < XSL ? s_info[1] : 0;
   const int r0 = XRB * xcc, u0 = U * slot;
@@ -865,7 +868,7 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
 #pragma unroll
   for (int q = 0; q < KG; ++q) wf[q] = a.W[(int64_t)(kbase + q) * HH + u0 + (lane & 15)];
   const bool bvalid = (lane & 15) < XRB;
-  const int brow = r0 + ((lane & 15) < XRB ? (lane & 15) : 0);
+  const float* brow_lds = slab + (bvalid ? (lane & 15) : XRB) * SS + KG * (lane >> 4);
   // pointwise operands of step t (prefetched one step ahead)
   f32x4 gt = {0.f, 0.f, 0.f, 0.f};
   float cc = 0.f, cpv = 0.f, dho = 0.f, dcs = 0.f;
@@ -902,28 +905,35 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
         fail();
         return;
       }
-      // ---- dh_rec = dG_{t+1} W_hh over this wave's K quarter; B from L2 (sc1), a chunk ahead
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-          a.dG + ((int64_t)brow * T + t + 1) * K4 + kbase, (short)0, 0x7fffffff, 0x00020000);
-      f32x4 nb[CH / 4];
-      auto ld_chunk = [&](int c0) {
+      // ---- this wave's K quarter of the group's dG_{t+1} rows -> its LDS slab: coalesced sc1
+      // loads (whole lines: L1 is bypassed, so scattered 16-B B-fragment loads would re-fetch
+      // every line 4-8 times), then the products dh_rec = dG_{t+1} W_hh from LDS
+      {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            a.dG + ((int64_t)r0 * T + t + 1) * K4 + KW * wave, (short)0, 0x7fffffff, 0x00020000);
+        constexpr int NL = XRB * KW / 4 / 64;            // b128 loads per lane (16)
+        f32x4 v[NL];
 #pragma unroll
-        for (int i = 0; i < CH / 4; ++i)
-          nb[i] = bvalid ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (c0 + 4 * i) * 4, 0, 16))
-                         : f32x4{0.f, 0.f, 0.f, 0.f};
-      };
-      ld_chunk(0);
+        for (int i = 0; i < NL; ++i) {
+          const int ci = i * 64 + lane, row = ci / (KW / 4), k4 = ci % (KW / 4);
+          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               r, (uint32_t)(((int64_t)row * T * K4 + 4 * k4) * 4), 0, 16));
+        }
 #pragma unroll
-      for (int c0 = 0; c0 < KG; c0 += CH) {
-        f32x4 cur[CH / 4];
+        for (int i = 0; i < NL; ++i) {
+          const int ci = i * 64 + lane, row = ci / (KW / 4), k4 = ci % (KW / 4);
+          *reinterpret_cast<f32x4*>(slab + row * SS + 4 * k4) = v[i];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+      }
 #pragma unroll
-        for (int i = 0; i < CH / 4; ++i) cur[i] = nb[i];
-        if (c0 + CH < KG) ld_chunk(c0 + CH);
-#pragma unroll
-        for (int i = 0; i < CH / 4; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c0 + 4 * i + e], cur[i][e], acc, 0, 0, 0);
+      for (int q = 0; q < KG; q += 4) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(brow_lds + q);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q], bv[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 1], bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 2], bv[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 3], bv[3], acc, 0, 0, 0);
       }
     }
     // C[unit 4 (lane / 16) + r][batch lane % 16]: the 4 waves' K quarters, summed in order

@@ -838,14 +838,17 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     B, T, I = x.shape
     H = W_hh.shape[1]
     dev = x.device
-    if not _bf16_rec(H) and lstm_xcd(B, H):
+    if not _bf16_rec(H) and lstm_xcd(B, H) and _XCD_BWD_ON:
         # one XCD-local persistent launch (the recurrent product reads W_hh untransposed)
         dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmx")
         mark = _grad_mark(dev)
         _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
                   W_hh.data_ptr(), dG.data_ptr(), ws, _s())
-        _flush_grad_queue(after=mark)
+        if _XCD_FLUSH == "before":
+            _flush_grad_queue(after=mark)
+        elif _XCD_FLUSH == "after":
+            _flush_grad_queue()
         return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs)
     WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
     _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
@@ -950,6 +953,15 @@ def lstm_persistent(B, H):
 # split over the 8 XCDs, every synchronisation inside one XCD's L2 (csrc/lstm2_persist.hip
 # "XCD-local recurrences"); AVC_LSTM_XCD=0 selects the per-step launches
 _XCD_ON = os.environ.get("AVC_LSTM_XCD", "1") != "0"
+
+
+# the backward the same way is opt-in (AVC_LSTM_XCD_BWD=1): alone 4.2 vs 9.3 us per step, but
+# in the training step the split-K launches' idle CUs host ~1 ms of queued weight-gradient
+# GEMMs that the all-CU persistent kernel cannot, so the step measured 15.91 (released beside
+# it) / 16.93 (after it) / 15.99-16.03 (deferred) vs 15.65-15.67 ms with the split-K backward
+# (profiles/r03/ab_lstm_xcd.txt).  AVC_XCD_FLUSH picks where the queued gradients go.
+_XCD_BWD_ON = os.environ.get("AVC_LSTM_XCD_BWD", "0") != "0"
+_XCD_FLUSH = os.environ.get("AVC_XCD_FLUSH", "before")
 
 
 def lstm_xcd(B, H):
