@@ -643,6 +643,7 @@ struct XArgs {
   const float* gx;
   int64_t gx_ldb, gx_ldt;
   const float* W;            // W_hh (4H, H)
+  const __bf16* Wb;          // its RNE bf16 copy (BF)
   float *h, *c, *g;          // h (b*h_ldb + t*h_ldt), c (B,T,H), gates (B,T,4H) or null
   int64_t h_ldb, h_ldt;
   int* bar;
@@ -654,14 +655,19 @@ __device__ __forceinline__ int add_l2(int* p, int v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int HH>
+// BF: the recurrent product on bf16 copies (autovc_lstm_fwd_bf16's numerics: RNE W_hh and h,
+// fp32 accumulation, fp32 cell math and outputs) with v_mfma_f32_16x16x32_bf16: 16 MFMAs per
+// wave per step instead of 128.
+template <int HH, bool BF>
 __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
   constexpr int U = HH / XSL;            // units per slot
   constexpr int KG = HH / 4;             // k per MFMA lane group
   constexpr int HS = HH + 4;             // LDS row stride of the staged h rows (bank spread)
   static_assert(U == 16, "one 16-column MFMA tile per gate");
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int HSB = HH + 8;            // bf16 row stride
   float* hs = lds;                        // [XRB + 1][HS], row XRB = zeros
+  __bf16* hsb = reinterpret_cast<__bf16*>(lds);   // BF: [XRB + 1][HSB]
   float* pre = lds + (XRB + 1) * HS;      // [4 gates][U][XRB + 1]
   __shared__ int s_info[3];               // xcc, slot, status
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -677,6 +683,8 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
     if (s_info[2]) st_rlx(a.bar + XC_ERR * L, 1);
   }
   for (int i = tid; i < HS; i += XNT) hs[XRB * HS + i] = 0.f;
+  if (BF)
+    for (int i = tid; i < HSB; i += XNT) hsb[XRB * HSB + i] = (__bf16)0.f;
   __syncthreads();
   const int xcc = s_info[0] < XNX ? s_info[0] : 0, slot = s_info[1] < XSL ? s_info[1] : 0;
   const int r0 = XRB * xcc, u0 = U * slot;
@@ -698,8 +706,14 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
     return;
   }
   // W fragments: wave = gate, lane -> column u0 + lane % 16, k = 128 (lane / 16) + q
-  float wf[KG];
-  {
+  float wf[BF ? 1 : KG];
+  bf16x8 wb[BF ? KG / 8 : 1];
+  if constexpr (BF) {
+    // k of MFMA q, lane group g, element e: KG g + 8 q + e (A and B alike)
+    const __bf16* src = a.Wb + (int64_t)(wave * HH + u0 + (lane & 15)) * HH + KG * (lane >> 4);
+#pragma unroll
+    for (int q = 0; q < KG / 8; ++q) wb[q] = *reinterpret_cast<const bf16x8*>(src + 8 * q);
+  } else {
     const float* src = a.W + (int64_t)(wave * HH + u0 + (lane & 15)) * HH + KG * (lane >> 4);
 #pragma unroll
     for (int q = 0; q < KG; q += 4) {
@@ -708,7 +722,9 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
     }
   }
   // B rows of this lane: its batch row of the staged h, or the zero row
-  const float* hrow = hs + (((lane & 15) < XRB) ? (lane & 15) : XRB) * HS + KG * (lane >> 4);
+  const int hsel = ((lane & 15) < XRB) ? (lane & 15) : XRB;
+  const float* hrow = hs + hsel * HS + KG * (lane >> 4);
+  const __bf16* hrowb = hsb + hsel * HSB + KG * (lane >> 4);
   float cst = 0.f;                        // cell state (cown)
   float cell_out[5];
   float gxv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -750,17 +766,31 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
 #pragma unroll
         for (int i = 0; i < HH / 128; ++i)
           v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (k + 4 * i) * 4, 0, 16));
+        if constexpr (BF) {
 #pragma unroll
-        for (int i = 0; i < HH / 128; ++i) *reinterpret_cast<f32x4*>(hs + row * HS + k + 4 * i) = v[i];
+          for (int i = 0; i < HH / 128; ++i)
+            *reinterpret_cast<bf16x4*>(hsb + row * HSB + k + 4 * i) =
+                bf16x4{(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
+        } else {
+#pragma unroll
+          for (int i = 0; i < HH / 128; ++i) *reinterpret_cast<f32x4*>(hs + row * HS + k + 4 * i) = v[i];
+        }
       }
       __syncthreads();
+      if constexpr (BF) {
 #pragma unroll
-      for (int q = 0; q < KG; q += 4) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(hrow + q);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q], bv[0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 1], bv[1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 2], bv[2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 3], bv[3], acc, 0, 0, 0);
+        for (int q = 0; q < KG / 8; ++q)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[q], *reinterpret_cast<const bf16x8*>(hrowb + 8 * q), acc,
+                                                        0, 0, 0);
+      } else {
+#pragma unroll
+        for (int q = 0; q < KG; q += 4) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(hrow + q);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q], bv[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 1], bv[1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 2], bv[2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 3], bv[3], acc, 0, 0, 0);
+        }
       }
     }
     // C[unit 4 (lane / 16) + r][batch lane % 16] of gate `wave`
@@ -972,13 +1002,15 @@ bool xcd_fits() {
   if (g_xcd_ok < 0) {
     int dev = 0, per = 0;
     hipDeviceProp_t p;
-    const void* k = reinterpret_cast<const void*>(lstm_xcd_fwd_kernel<512>);
+    const void* k = reinterpret_cast<const void*>(lstm_xcd_fwd_kernel<512, false>);
     const int lb = XC_PAD_LDS;
     g_xcd_ok = hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess &&
                p.multiProcessorCount == XNX * XSL &&
                hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
-               hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_fwd_kernel<512>, XNT, lb) == hipSuccess &&
+               hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_fwd_kernel<512, false>, XNT, lb) == hipSuccess &&
                per >= 1 &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_fwd_kernel<512, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
                hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_bwd_kernel<512>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_bwd_kernel<512>, XNT, lb) == hipSuccess &&
@@ -1004,12 +1036,33 @@ extern "C" int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int
   AVC_CHECK_ARG(gx && W_hh && h && c_all && workspace, "%s: null pointer", fn);
   AVC_CHECK_ARG(AVC_ALIGNED16(W_hh) && AVC_ALIGNED16(workspace), "%s: W_hh / workspace must be 16-byte aligned", fn);
   XArgs a;
-  a.B = B; a.T = T; a.gx = gx; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt; a.W = W_hh;
+  a.B = B; a.T = T; a.gx = gx; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt; a.W = W_hh; a.Wb = nullptr;
   a.h = h; a.c = c_all; a.g = gates; a.h_ldb = h_ldb; a.h_ldt = h_ldt;
   a.bar = static_cast<int*>(workspace);
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
   AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
-  hipLaunchKernelGGL(lstm_xcd_fwd_kernel<512>, dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
+  hipLaunchKernelGGL((lstm_xcd_fwd_kernel<512, false>), dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm_fwd_xcd_bf16(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                                        const uint16_t* W_hh_b, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                                        float* gates, void* workspace, hipStream_t stream) {
+  static const char* fn = "autovc_lstm_fwd_xcd_bf16";
+  AVC_CHECK_ARG(T > 0 && autovc_lstm_xcd_supported(B, H),
+                "%s: unsupported shape B=%d H=%d on this device (needs B=64, H=512, 8 XCDs x 32 CUs)", fn, B, H);
+  AVC_CHECK_ARG(gx && W_hh_b && h && c_all && workspace, "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(W_hh_b) && AVC_ALIGNED16(workspace), "%s: W_hh_b / workspace must be 16-byte aligned",
+                fn);
+  XArgs a;
+  a.B = B; a.T = T; a.gx = gx; a.gx_ldb = gx_ldb; a.gx_ldt = gx_ldt; a.W = nullptr;
+  a.Wb = reinterpret_cast<const __bf16*>(W_hh_b);
+  a.h = h; a.c = c_all; a.g = gates; a.h_ldb = h_ldb; a.h_ldt = h_ldt;
+  a.bar = static_cast<int*>(workspace);
+  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
+  AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
+  hipLaunchKernelGGL((lstm_xcd_fwd_kernel<512, true>), dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
 }

@@ -791,7 +791,12 @@ class LSTMLayerFn(torch.autograd.Function):
         h = torch.empty((B, T, H), device=dev, dtype=torch.float32)
         c = torch.empty((B, T, H), device=dev, dtype=torch.float32)
         gates = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
-        if _bf16_rec(H):
+        if _bf16_rec(H) and lstm_xcd(B, H):
+            Wb = _bf(W_hh)
+            ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmx")
+            _lib.call("autovc_lstm_fwd_xcd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),
+                      h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), ws, _s())
+        elif _bf16_rec(H):
             hb = torch.empty((B, T, H), device=dev, dtype=torch.bfloat16)
             Wb = _bf(W_hh)   # held until the launches are enqueued (stream-ordered reuse after)
             _lib.call("autovc_lstm_fwd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),

@@ -308,6 +308,12 @@ int64_t autovc_lstm_xcd_workspace_bytes(void);
 int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                             const float* W_hh, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                             float* gates, void* workspace, hipStream_t stream);
+/* precision "bf16": the same launch on the RNE bf16 copy of W_hh and bf16-rounded h in the
+ * recurrent product (autovc_lstm_fwd_bf16's numerics; fp32 accumulation, cell math and
+ * outputs). */
+int autovc_lstm_fwd_xcd_bf16(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
+                             const uint16_t* W_hh_b, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
+                             float* gates, void* workspace, hipStream_t stream);
 /* Its backward (BPTT of autovc_lstm_bwd_f32 with reverse = 0) the same way: slot s of XCD x
  * reduces dh_rec for units 16s .. 16s+15 of rows 8x .. 8x+7 over K = 4H with W_hh's columns
  * in registers (W_hh as stored, (4H, H): no transpose) and writes those cells' dG; the dG

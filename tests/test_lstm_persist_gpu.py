@@ -273,3 +273,35 @@ def test_xcd_local_lstm_backward_matches_split_k_launches(cuda, T):
     err = (outs[0].double() - ref.double()).abs().max().item() / ref.abs().max().item()
     assert err < 2e-5, err
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("T", [3, 128])
+def test_xcd_local_lstm_bf16_matches_bf16_per_step_launches(cuda, T):
+    """autovc_lstm_fwd_xcd_bf16 against the per-step bf16 launches (autovc_lstm_fwd_bf16): the
+    same RNE-rounded W_hh and h copies, fp32 accumulation in a different order."""
+    from autovc_amd import _lib
+    if not _xcd_supported():
+        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
+    B, H = 64, 512
+    gx, W, _, _ = _inputs(B, T, H, cuda, seed=13)
+    Wb = W[0].bfloat16().contiguous()
+    st = _lib.stream_ptr(cuda)
+    outs = []
+    for xcd in (False, True):
+        h, c = (torch.full((B, T, H), float("nan"), device=cuda) for _ in range(2))
+        g = torch.full((B, T, 4 * H), float("nan"), device=cuda)
+        if xcd:
+            ws = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
+            _lib.call("autovc_lstm_fwd_xcd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),
+                      h.data_ptr(), T * H, H, c.data_ptr(), g.data_ptr(), ws.data_ptr(), st)
+        else:
+            hb = torch.empty((B, T, H), device=cuda, dtype=torch.bfloat16)
+            _lib.call("autovc_lstm_fwd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(), h.data_ptr(),
+                      hb.data_ptr(), c.data_ptr(), g.data_ptr(), 0, st)
+        torch.cuda.synchronize()
+        outs.append((h, c, g))
+    for name, a, r in zip(["h", "c", "gates"], outs[1], outs[0]):
+        assert bool(torch.isfinite(a).all()), name
+        d = (a.double() - r.double()).abs()
+        assert d.max().item() < 2e-2 * max(r.abs().max().item(), 1e-30), (name, d.max().item())
+        assert d.mean().item() < 1e-4 * max(r.abs().max().item(), 1e-30), (name, d.mean().item())

@@ -38,6 +38,14 @@ def main():
     runs["backward: persistent (XCD-local)"] = lambda: _lib.call(
         "autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, gt.data_ptr(), c.data_ptr(), W.data_ptr(),
         dG.data_ptr(), wsx.data_ptr(), st)
+    Wb = W.bfloat16().contiguous()
+    hb = torch.empty(B, T, H, device=dev, dtype=torch.bfloat16)
+    runs["bf16: per-step launches"] = lambda: _lib.call(
+        "autovc_lstm_fwd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(), h.data_ptr(), hb.data_ptr(),
+        c.data_ptr(), gt.data_ptr(), 0, st)
+    runs["bf16: persistent (XCD-local)"] = lambda: _lib.call(
+        "autovc_lstm_fwd_xcd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(), h.data_ptr(), T * H, H,
+        c.data_ptr(), gt.data_ptr(), wsx.data_ptr(), st)
     ts = {k: [] for k in runs}
     for _ in range(7):
         for k, fn in runs.items():
