@@ -637,6 +637,29 @@ constexpr int XNT = 256;               // 4 waves
 constexpr int XC_CENSUS = 0, XC_STEP = 16, XC_ERR = 32, XC_LINES = 33;
 constexpr int64_t XC_BYTES = XC_LINES * L * 4;
 constexpr int XC_PAD_LDS = 96 * 1024;  // dynamic LDS that keeps one workgroup per CU
+// Diagnostic timeline (tools only: tools/build_variant.sh xstamp -DXCD_STAMP=1, then
+// tools/xcd_stamps.py): thread 0 of every workgroup records s_memrealtime at the phase
+// boundaries of steps 1..kXS of the forward kernel; the product build is XCD_STAMP 0.
+#ifndef XCD_STAMP
+#define XCD_STAMP 0
+#endif
+// 1: B fragments loaded per wave straight from global memory (plain loads, no LDS staging):
+// measured 5.05 / 3.96 us per step (fp32 / bf16) against 3.86 / 1.98 for the coalesced LDS
+// staging (profiles/r03/lstm_xcd_time.txt) — diagnostic build only
+#ifndef XCD_DIRECT
+#define XCD_DIRECT 0
+#endif
+#if XCD_STAMP
+constexpr int kXS = 16, kXP = 8;
+__device__ unsigned long long g_xcd_stamp[XNX * XSL * kXS * kXP];
+#define XSTAMP(t, ph)                                                                                \
+  do {                                                                                              \
+    if (tid == 0 && (t) >= 1 && (t) <= kXS)                                                         \
+      g_xcd_stamp[((xcc * XSL + slot) * kXS + (t) - 1) * kXP + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define XSTAMP(t, ph) do { } while (0)
+#endif
 
 struct XArgs {
   int B, T;
@@ -723,8 +746,8 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
   }
   // B rows of this lane: its batch row of the staged h, or the zero row
   const int hsel = ((lane & 15) < XRB) ? (lane & 15) : XRB;
-  const float* hrow = hs + hsel * HS + KG * (lane >> 4);
-  const __bf16* hrowb = hsb + hsel * HSB + KG * (lane >> 4);
+  [[maybe_unused]] const float* hrow = hs + hsel * HS + KG * (lane >> 4);
+  [[maybe_unused]] const __bf16* hrowb = hsb + hsel * HSB + KG * (lane >> 4);
   float cst = 0.f;                        // cell state (cown)
   float cell_out[5];
   float gxv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -737,6 +760,7 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
   int* step_ctr = a.bar + (XC_STEP + xcc) * L;
   for (int t = 0; t < T; ++t) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    XSTAMP(t, 0);
     if (t > 0) {
       // ---- XCD barrier: all 32 slots stored h_{t-1}
       if (tid == 0) {
@@ -753,30 +777,83 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
         s_info[2] = ok ? 0 : 1;
       }
       __syncthreads();
+      XSTAMP(t, 1);
       if (s_info[2]) {
         fail();
         return;
       }
+#if XCD_DIRECT
+      // ---- every wave loads its own B fragments straight from global memory, a chunk
+      // ahead of its MFMAs: lane (batch l % 16, k group l / 16) reads h_{t-1}[row][KG g ..
+      // KG g + KG) — PLAIN loads: every h_{t-1} address is read once per launch, after the
+      // barrier, by a CU that never loaded it before in this launch (and a kernel start
+      // invalidates L1), so no L1 line can be stale; the line then serves the wave's next
+      // 16-B pieces from L1 and the other 3 waves of the CU
+      {
+        const bool bval = (lane & 15) < XRB;
+        const float* src = a.h + (int64_t)(r0 + (bval ? (lane & 15) : 0)) * a.h_ldb + (int64_t)(t - 1) * a.h_ldt +
+                           KG * (lane >> 4);
+        constexpr int CH = BF ? 16 : 8;            // floats per chunk
+        constexpr int NC = KG / CH;
+        f32x4 nb[CH / 4];
+        auto ld = [&](int c) {
+#pragma unroll
+          for (int i = 0; i < CH / 4; ++i)
+            nb[i] = bval ? *reinterpret_cast<const f32x4*>(src + c * CH + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+        };
+        ld(0);
+        XSTAMP(t, 2);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          f32x4 cur[CH / 4];
+#pragma unroll
+          for (int i = 0; i < CH / 4; ++i) cur[i] = nb[i];
+          if (c + 1 < NC) ld(c + 1);
+          if constexpr (BF) {
+#pragma unroll
+            for (int j = 0; j < CH / 8; ++j) {
+              const f32x4 lo = cur[2 * j], hi = cur[2 * j + 1];
+              const bf16x8 bv = {(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
+                                 (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[c * (CH / 8) + j], bv, acc, 0, 0, 0);
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < CH / 4; ++i)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c * CH + 4 * i + e], cur[i][e], acc, 0, 0, 0);
+          }
+        }
+      }
+    }
+#else
       // ---- stage h_{t-1} of the group's 8 rows (sc1 loads: L1 bypassed, L2-served)
       {
-        const int row = tid >> 5, k = (tid & 31) * (HH / 32);
+        // wave-instruction i of wave w moves 1 KB chunk 4w + i of the 8 rows (whole lines per
+        // instruction): row (4w + i) / (HH / 256), floats 256 ((4w + i) % (HH / 256)) + 4 lane
+        constexpr int NI = XRB * HH / 256 / 4;     // b128 loads per lane
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            a.h + (int64_t)(r0 + row) * a.h_ldb + (int64_t)(t - 1) * a.h_ldt, (short)0, 0x7fffffff, 0x00020000);
-        f32x4 v[HH / 128];
+            a.h + (int64_t)r0 * a.h_ldb + (int64_t)(t - 1) * a.h_ldt, (short)0, 0x7fffffff, 0x00020000);
+        f32x4 v[NI];
 #pragma unroll
-        for (int i = 0; i < HH / 128; ++i)
-          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (k + 4 * i) * 4, 0, 16));
-        if constexpr (BF) {
+        for (int i = 0; i < NI; ++i) {
+          const int ch = NI * wave + i, row = ch / (HH / 256), k = 256 * (ch % (HH / 256)) + 4 * lane;
+          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               r, (uint32_t)(((int64_t)row * a.h_ldb + k) * 4), 0, 16));
+        }
 #pragma unroll
-          for (int i = 0; i < HH / 128; ++i)
-            *reinterpret_cast<bf16x4*>(hsb + row * HSB + k + 4 * i) =
+        for (int i = 0; i < NI; ++i) {
+          const int ch = NI * wave + i, row = ch / (HH / 256), k = 256 * (ch % (HH / 256)) + 4 * lane;
+          if constexpr (BF)
+            *reinterpret_cast<bf16x4*>(hsb + row * HSB + k) =
                 bf16x4{(__bf16)v[i][0], (__bf16)v[i][1], (__bf16)v[i][2], (__bf16)v[i][3]};
-        } else {
-#pragma unroll
-          for (int i = 0; i < HH / 128; ++i) *reinterpret_cast<f32x4*>(hs + row * HS + k + 4 * i) = v[i];
+          else
+            *reinterpret_cast<f32x4*>(hs + row * HS + k) = v[i];
         }
       }
       __syncthreads();
+      XSTAMP(t, 2);
       if constexpr (BF) {
 #pragma unroll
         for (int q = 0; q < KG / 8; ++q)
@@ -793,11 +870,14 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
         }
       }
     }
+#endif
+    XSTAMP(t, 3);
     // C[unit 4 (lane / 16) + r][batch lane % 16] of gate `wave`
     if ((lane & 15) < XRB)
 #pragma unroll
       for (int r = 0; r < 4; ++r) pre[(wave * U + 4 * (lane >> 4) + r) * (XRB + 1) + (lane & 15)] = acc[r];
     __syncthreads();
+    XSTAMP(t, 4);
     if (cown) {
       float p[4];
 #pragma unroll
@@ -812,8 +892,10 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
     // ---- arrive once h_t (only it) is in the XCD's L2; c / gates and the next gx loads
     // go out after the arrive, under the next step's wait
     if (t + 1 < T) {
+      XSTAMP(t, 5);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      XSTAMP(t, 6);
       if (tid == 0) add_l2(step_ctr, 1);
     }
     if (cown) {
@@ -1216,3 +1298,10 @@ extern "C" int autovc_fault_status(hipStream_t stream, int clear, int* out) {
   *out = v;
   return avc::kOk;
 }
+
+#if XCD_STAMP
+extern "C" int autovc_xcd_stamps(unsigned long long* out) {
+  AVC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xcd_stamp), sizeof(g_xcd_stamp)), "autovc_xcd_stamps");
+  return avc::kOk;
+}
+#endif

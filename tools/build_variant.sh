@@ -5,13 +5,15 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-mkdir -p tools/ubin/obj_$name
+rm -rf tools/ubin/obj_$name; mkdir -p tools/ubin/obj_$name
+pids=()
 for f in autovc_amd/csrc/capi.cpp autovc_amd/csrc/*.hip; do
   b=$(basename "${f%.*}")
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -munsafe-fp-atomics \
     -Iinclude $* -x hip -c "$f" -o tools/ubin/obj_$name/$b.o &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait $p || { echo "build of variant $name failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/ubin/libautovc_$name.so tools/ubin/obj_$name/*.o
 rm -rf tools/ubin/obj_$name
 echo tools/ubin/libautovc_$name.so
