@@ -59,7 +59,10 @@
 #define LP_NW 8
 #endif
 // grid barrier: 0 = XCC counters -> top counter -> generation words (two atomic round trips
-// on the critical path); 1 = XCC counters only, every waiting workgroup polls all of them —
+// on the critical path); 2 = one counter replicated on 16 lines: every workgroup adds to
+// all 16 with one wave instruction (16 lanes) and polls its own XCC's replica (one atomic
+// round trip: MI355X_MICROARCH.md's replicated-counter hand-off); 1 = XCC counters only,
+// every waiting workgroup polls all of them —
 // measured 24.1 vs 20.2 us per wavefront step (256 pollers x 8 counters contend with the
 // arrivals: profiles/r02/lstm2_persist_ab_8wave.txt), kept as a diagnostic build only
 #ifndef LP_BARRIER
@@ -105,7 +108,8 @@ constexpr int BAR_ARRIVE = 17;     // 16 lines: per-XCC arrivals (cumulative)
 constexpr int BAR_TOP = 33;        // 1 line: XCC leaders arrived (cumulative)
 constexpr int BAR_GEN = 34;        // 16 lines: per-XCC generation released
 constexpr int BAR_ERR = 50;        // 1 line: timeout / error code
-constexpr int BAR_LINES = 52;
+constexpr int BAR_REP = 52;        // 16 lines: replicated arrival counters (LP_BARRIER 2)
+constexpr int BAR_LINES = 68;
 constexpr int64_t BAR_BYTES = BAR_LINES * L * 4;
 
 struct PArgs {
@@ -176,7 +180,15 @@ __device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int
                                           int* status, int gen) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's stores are in L2
   __syncthreads();
-  if (threadIdx.x == 0 && LP_BARRIER == 1) {
+  if (LP_BARRIER == 2) {
+    if (threadIdx.x < 16) add_rlx(a.bar + (BAR_REP + threadIdx.x) * L, 1);   // one wave instruction, 16 replicas
+    if (threadIdx.x == 0) {
+      const bool ok = wait_ge(a.bar + (BAR_REP + xcc) * L, (int)gridDim.x * (gen + 1), a.bar + BAR_ERR * L,
+                              a.timeout_ticks);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)
+      *status = ok ? 0 : 1;
+    }
+  } else if (threadIdx.x == 0 && LP_BARRIER == 1) {
     add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
     const bool ok = wait_all_xcc(a.bar, census, gen, a.timeout_ticks);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)

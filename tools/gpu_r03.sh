@@ -23,6 +23,13 @@ for STEP in ${1//,/ }; do
     wnsweep) timeout -k 10 600 python tools/wavenet_bench.py 16 8 > gpurun_out/wnsweep.log 2>&1 ;;
     det) timeout -k 10 ${T_DET:-600} python -u tools/det_probe.py ${DET_B:-64} ${DET_STEPS:-6} ${DET_VARIANTS:-graph=1,stream=0 graph=1,stream=1} > gpurun_out/det.log 2> gpurun_out/det.err ;;
     bench2) timeout -k 10 900 python bench.py --gpus 2 ${BENCH_ARGS} > gpurun_out/bench2.json 2> gpurun_out/bench2.err ;;
+    blpmc) timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/blpmc_f -o run --output-format csv -- python tools/lstm_pmc.py blstm > gpurun_out/blpmc_f.log 2>&1 && \
+           timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/blpmc_w -o run --output-format csv -- python tools/lstm_pmc.py blstm > gpurun_out/blpmc_w.log 2>&1 && \
+           python tools/pmc_summarize.py gpurun_out/blpmc_f gpurun_out/blpmc_w blstm_fwd > gpurun_out/blstm_fwd_pmc.json && \
+           python tools/pmc_summarize.py gpurun_out/blpmc_f gpurun_out/blpmc_w blstm_bwd > gpurun_out/blstm_bwd_pmc.json && \
+           timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/xpmc_f -o run --output-format csv -- python tools/lstm_pmc.py xcd > gpurun_out/xpmc_f.log 2>&1 && \
+           timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/xpmc_w -o run --output-format csv -- python tools/lstm_pmc.py xcd > gpurun_out/xpmc_w.log 2>&1 && \
+           python tools/pmc_summarize.py gpurun_out/xpmc_f gpurun_out/xpmc_w xcd > gpurun_out/lstm_xcd_pmc.json ;;
     wnpersist) timeout -k 10 120 tools/ubin/wn_persist_ubench > gpurun_out/wn_persist_ubench.txt 2>&1 && \
                timeout -k 10 300 tools/ubin/chain_ubench > gpurun_out/chain_ubench.txt 2>&1 ;;
     *) echo "unknown step $STEP"; exit 2 ;;

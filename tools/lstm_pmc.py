@@ -3,7 +3,10 @@
 `stack`: decoder lstm2's two-layer wavefront (lstm2_fwd_step_kernel), as bench.py times it;
 `stackbwd`: its backward wavefront (lstm2_bwd_rec_kernel, autovc_lstm2_bwd_f32, split-K 4);
 `persist`: the persistent weight-stationary lstm2 forward (lstm2_persist_kernel, one launch
-  per sequence, what the Generator runs at B=64).
+  per sequence, what the Generator runs at B=64);
+`blstm`: the encoder BLSTM layer (H=32, both directions per launch), forward and backward
+  kernels, as bench.py's blstm_roofline times them;
+`xcd`: decoder lstm1's XCD-local persistent forward (H=512, B=64).
   rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_f -o run --output-format csv -- python tools/lstm_pmc.py stack
   rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_w -o run --output-format csv -- python tools/lstm_pmc.py stack
   python tools/pmc_summarize.py gpurun_out/pmc_f gpurun_out/pmc_w stack > profiles/lstm2_step_pmc.json"""
@@ -36,8 +39,31 @@ if MODE == "stackbwd":
     WT1, WIT1, WT0 = ((torch.rand(H, 4 * H, generator=g) * 2 - 1).div_(H ** 0.5).to(dev) for _ in range(3))
     dG1, dG0 = torch.empty(B, T, 4 * H, device=dev), torch.empty(B, T, 4 * H, device=dev)
     ws = torch.empty(_lib.load().autovc_lstm2_bwd_workspace_floats(B, H, 4), device=dev)
+if MODE == "blstm":
+    Hs = 32
+    bgx = (torch.randn(B, T, 8 * Hs, generator=g) * 0.5).to(dev)
+    Wf, Wb = ((torch.rand(4 * Hs, Hs, generator=g) * 2 - 1).div_(Hs ** 0.5).to(dev) for _ in range(2))
+    bh, bc = torch.empty(B, T, 2 * Hs, device=dev), torch.empty(B, T, 2 * Hs, device=dev)
+    bgates = torch.empty(B, T, 8 * Hs, device=dev)
+    bdh = torch.randn(B, T, 2 * Hs, generator=g).to(dev)
+    bdG = torch.empty(B, T, 8 * Hs, device=dev)
+if MODE == "xcd":
+    H = 512
+    W = (torch.rand(4 * H, H, generator=g) * 2 - 1).div_(H ** 0.5).to(dev)
+    gx = (torch.randn(B, T, 4 * H, generator=g) * 0.5).to(dev)
+    h, c, gates = torch.empty(B, T, H, device=dev), torch.empty(B, T, H, device=dev), torch.empty(B, T, 4 * H, device=dev)
+    ws = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=dev)
 for _ in range(2):
-    if MODE == "stackbwd":
+    if MODE == "blstm":
+        st = _lib.stream_ptr(dev)
+        _lib.call("autovc_blstm_fwd_f32", B, T, 32, 2, bgx.data_ptr(), Wf.data_ptr(), Wb.data_ptr(), bh.data_ptr(),
+                  bc.data_ptr(), bgates.data_ptr(), st)
+        _lib.call("autovc_blstm_bwd_f32", B, T, 32, 2, bdh.data_ptr(), bgates.data_ptr(), bc.data_ptr(),
+                  Wf.data_ptr(), Wb.data_ptr(), bdG.data_ptr(), st)
+    elif MODE == "xcd":
+        _lib.call("autovc_lstm_fwd_xcd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(), h.data_ptr(),
+                  T * H, H, c.data_ptr(), gates.data_ptr(), ws.data_ptr(), _lib.stream_ptr(dev))
+    elif MODE == "stackbwd":
         _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
                   g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(), dG1.data_ptr(),
                   dG0.data_ptr(), 4, ws.data_ptr(), _lib.stream_ptr(dev))
@@ -55,4 +81,5 @@ for _ in range(2):
         _lib.call("autovc_lstm_fwd_f32", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, W.data_ptr(), h.data_ptr(),
                   T * H, H, c.data_ptr(), gates.data_ptr(), 0, _lib.stream_ptr(dev))
 torch.cuda.synchronize()
-print("ok", float(dG0.abs().mean()) if MODE == "stackbwd" else float(h[:, -1].abs().mean()))
+print("ok", float(dG0.abs().mean()) if MODE == "stackbwd" else
+      float(bdG.abs().mean()) if MODE == "blstm" else float(h[:, -1].abs().mean()))

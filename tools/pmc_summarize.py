@@ -11,7 +11,8 @@ import sys
 
 MODE = sys.argv[3] if len(sys.argv) > 3 else "single"
 KERNEL = {"stack": "lstm2_fwd_step_kernel", "stackbwd": "lstm2_bwd_rec_kernel",
-          "persist": "lstm_persist_kernel<1024, true, false>"}.get(MODE, "lstm_fwd_step_kernel")
+          "persist": "lstm_persist_kernel<1024, true, false>", "blstm_fwd": "blstm_fwd_kernel",
+          "blstm_bwd": "blstm_bwd_kernel", "xcd": "lstm_xcd_fwd_kernel"}.get(MODE, "lstm_fwd_step_kernel")
 
 
 def per_dispatch(d, counter):
@@ -29,7 +30,7 @@ w = per_dispatch(sys.argv[2], "WRITE_SIZE")
 T = 128
 if MODE == "stackbwd":   # T launches per sequence; 1..T-2 carry all three K segments
     keep = lambda xs: [x for i, x in enumerate(xs) if 1 <= i % T <= T - 2]  # noqa: E731
-elif MODE == "persist":   # one launch per sequence
+elif MODE in ("persist", "blstm_fwd", "blstm_bwd", "xcd"):   # one launch per sequence / layer
     keep = lambda xs: list(xs)  # noqa: E731
 elif MODE == "stack":   # T + 1 launches per sequence; 2..T-1 carry both layers' recurrent products
     keep = lambda xs: [x for i, x in enumerate(xs) if 2 <= i % (T + 1) <= T - 1]  # noqa: E731
@@ -39,10 +40,13 @@ fa = sum(keep(f)) / max(1, len(keep(f)))
 wa = sum(keep(w)) / max(1, len(keep(w)))
 out = {"kernel": {"stack": "lstm2_fwd_step_kernel (decoder lstm2, both layers, H=1024, B=64)",
                   "stackbwd": "lstm2_bwd_rec_kernel (decoder lstm2 backward, both layers + W_ih1, H=1024, B=64)",
-                  "persist": "lstm_persist_kernel<1024, true, false> (decoder lstm2 forward, whole sequence, H=1024, B=64, T=128)"}
+                  "persist": "lstm_persist_kernel<1024, true, false> (decoder lstm2 forward, whole sequence, H=1024, B=64, T=128)",
+                  "blstm_fwd": "blstm_fwd_kernel (encoder BLSTM layer, H=32, B=64, T=128, both directions)",
+                  "blstm_bwd": "blstm_bwd_kernel (encoder BLSTM layer backward, H=32, B=64, T=128)",
+                  "xcd": "lstm_xcd_fwd_kernel<512, false> (decoder lstm1 forward, XCD-local, H=512, B=64, T=128)"}
        .get(MODE, "lstm_fwd_step_kernel (H=1024, B=64)"), "launches": len(f),
        "fetch_size_kib_raw": round(fa, 1), "write_size_kib": round(wa, 1),
        "hbm_bytes_per_launch": int(round((2 * fa + wa) * 1024)),
        "correction": "FETCH_SIZE doubled (gfx950 reports half of wide streaming reads); WRITE_SIZE as is",
-       "source": f"tools/lstm_pmc.py {MODE} under rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)"}
+       "source": f"tools/lstm_pmc.py {MODE.split('_')[0]} under rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)"}
 print(json.dumps(out, indent=1))
