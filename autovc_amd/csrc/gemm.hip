@@ -44,7 +44,70 @@ struct Opnd {
 // start z * (a, b, c) floats further (no split-K then).
 struct Batch {
   int64_t a, b, c;
+  int* tk;          // split-K tile tickets (in-kernel fixup), null: slabs + splitk_reduce_kernel
 };
+
+// Split-K without a second launch: every split of a tile writes its partial accumulators
+// to its slab in the lanes' own layout (16 floats per lane per 32x32 block, 16-B sc1 stores:
+// written through, so another XCD's sc1 loads see them), waits for the stores, and one
+// lane takes a ticket on the tile's counter (agent-scope atomic).  The split that takes
+// the last ticket reads the others' partials (sc1 loads) and sums all splits in split order
+// — the order of splitk_reduce_kernel, so the result is bit-identical to the two-launch
+// form — then writes C through the normal epilogue and returns the counter to zero (the
+// counters start zeroed and every call leaves them zero).
+template <int TI, int TJ>
+__device__ __forceinline__ bool splitk_fixup(f32x16 (&acc)[TI][TJ], float* slab, int* tk, int tile, int ntiles) {
+  constexpr int TF = TI * TJ * 1024;                         // floats of one wave's blocks
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int z = blockIdx.z, S = gridDim.z;
+  const int64_t tile_f = (int64_t)nw * TF;
+  auto blk = [&](int s, int i, int j) {
+    return ((int64_t)s * ntiles + tile) * tile_f + (int64_t)wave * TF + (i * TJ + j) * 1024 + lane * 16;
+  };
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)0x80000000u, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
+                                               (uint32_t)((blk(z, i, j) + 4 * q) * 4), 0, 16);
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(tk + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == S - 1;
+    if (s_last) __hip_atomic_store(tk + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return false;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      f32x16 tot;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tot[e] = 0.f;
+      for (int sp = 0; sp < S; ++sp) {
+        if (sp == z) {
+          tot += acc[i][j];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                           r, (uint32_t)((blk(sp, i, j) + 4 * q) * 4), 0, 16));
+            tot[4 * q] += v[0]; tot[4 * q + 1] += v[1]; tot[4 * q + 2] += v[2]; tot[4 * q + 3] += v[3];
+          }
+        }
+      }
+      acc[i][j] = tot;
+    }
+  return true;
+}
 
 // One operand tile (ROWS x BK) of a stage: staging map, LDS image and fragment reads.
 //   RK: LDS [ROWS][BK+4], staged as float4 along k, fragments read with ds_read_b128.
@@ -340,6 +403,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
   }
 
   // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  if (slab && bat.tk) {
+    if (!splitk_fixup<TI, TJ>(acc, slab, bat.tk, logical, nwg)) return;
+    slab = nullptr;                    // the last split writes C with the full sum
+  }
   float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
   const int64_t ld = slab ? N : ldc;
 #pragma unroll
@@ -509,6 +576,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     }
   }
 
+  if (slab && bat.tk) {
+    if (!splitk_fixup<TI, TJ>(acc, slab, bat.tk, logical, nwg)) return;
+    slab = nullptr;                    // the last split writes C with the full sum
+  }
   float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
   const int64_t ld = slab ? N : ldc;
 #pragma unroll
@@ -589,7 +660,13 @@ int g_force_cfg = AVC_GEMM_FORCE_CFG;  // tools/gemm_bench.hip overrides this
 // stream (autovc_gemm_set_lds_reserve): each workgroup is padded with unused dynamic LDS
 // so that the largest count that still fits in 160 KiB - reserve is also the most that fit.
 unsigned g_lds_reserve = 0;
-Batch g_batch = {0, 0, 0};   // set by gemm_impl for every launch (batched calls only non-zero)
+Batch g_batch = {0, 0, 0, nullptr};   // set by gemm_impl for every launch
+// split-K in one launch (splitk_fixup) only with AVC_GEMM_FIXUP=1: the partials' write-through
+// stores and the serial last-split tail measured slower than slabs + splitk_reduce_kernel
+// (fp32 15.91-15.92 vs 15.61-15.65 ms/step, bf16 11.24-11.30 vs 9.99-10.00;
+// profiles/r03/ab_gemm_fixup.txt; identical losses)
+const bool g_fixup = [] { const char* e = getenv("AVC_GEMM_FIXUP"); return e && e[0] == '1'; }();
+constexpr int kTickets = 16384;          // tile counters at the head of a split-K workspace (64 KiB)
 constexpr unsigned kLdsPerCU = 160 * 1024;
 
 unsigned dyn_lds_for(unsigned static_bytes) {
@@ -749,8 +826,10 @@ void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t s
 
 }  // namespace
 
+// split-K workspace: kTickets tile counters (zero before the first call, left zero by every
+// call) followed by the partial slabs (tiles rounded up to 256 x 256)
 extern "C" int64_t autovc_gemm_workspace_floats(int M, int N, int splits) {
-  return splits > 1 ? (int64_t)splits * M * N : 0;
+  return splits > 1 ? kTickets + (int64_t)splits * ((M + 255) / 256 * 256) * ((N + 255) / 256 * 256) : 0;
 }
 
 static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c_bs, int M, int N, int K,
@@ -812,9 +891,11 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   AVC_CHECK_ARG(splits == 1 || workspace, "autovc_gemm_f32: split-K needs a workspace");
   Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0};
   Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0};
-  float* slab = splits > 1 ? workspace : nullptr;
   const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, batch > 1 ? batch : splits);
-  g_batch = batch > 1 ? Batch{a_bs, b_bs, c_bs} : Batch{0, 0, 0};
+  const bool fixup = splits > 1 && g_fixup && (int64_t)grid.x * grid.y <= kTickets;
+  float* slab = splits > 1 ? workspace + kTickets : nullptr;
+  g_batch = batch > 1 ? Batch{a_bs, b_bs, c_bs, nullptr}
+                      : Batch{0, 0, 0, fixup ? reinterpret_cast<int*>(workspace) : nullptr};
   if (bf16)
     launch_gemm_bf16(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate,
                      (int)kps, slab);
@@ -822,7 +903,7 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
     launch_gemm(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
                 slab);
   AVC_CHECK_LAUNCH("autovc_gemm");
-  if (splits > 1) {
+  if (splits > 1 && !fixup) {
     const int gx = (N + 255) / 256;
     const int gy = (int)std::max<int64_t>(1, std::min<int64_t>(M, 4096 / gx + 1));
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, gy), dim3(256), 0, stream, (int64_t)M, (int64_t)N,

@@ -56,7 +56,9 @@ class _Workspace:
             if buf is not None:
                 cls._retired.append(buf)
                 size = max(size, 2 * buf.numel())
-            buf = torch.empty(size, dtype=torch.uint8, device=device)
+            # zeroed: a split-K GEMM workspace starts with tile counters that must be zero
+            # (every call leaves them zero again, csrc/gemm.hip splitk_fixup)
+            buf = torch.zeros(size, dtype=torch.uint8, device=device)
             cls._bufs[key] = buf
         return buf
 

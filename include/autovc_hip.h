@@ -82,7 +82,10 @@ int autovc_preprocess_f64(const void* x, int x_is_f64, const int64_t* wav_off, i
  * accumulate).  a_trans=0: A[m*lda+k], 1: A[k*lda+m].  b_trans=0: B[n*ldb+k], 1: B[k*ldb+n].
  * *_conv_T > 0 turns the operand into the im2col view of an NTC activation with T frames
  * per sequence, C channels and first tap offset tap0 (-2 for k=5/pad=2; -1 = "previous
- * frame").  splits > 1 = split-K with a workspace of autovc_gemm_workspace_floats floats.
+ * frame").  splits > 1 = split-K with a workspace of autovc_gemm_workspace_floats floats
+ * whose first 64 KiB (tile counters) must be zero before its first use; every call leaves
+ * them zero (AVC_GEMM_FIXUP=1: the splits of a tile finish in one launch, the last to arrive
+ * summing the partials in split order; by default slabs + a reduce launch, measured faster).
  */
 int64_t autovc_gemm_workspace_floats(int M, int N, int splits);
 int autovc_gemm_f32(int M, int N, int K,

@@ -13,8 +13,8 @@ CATS = [
     ("lstm2 fwd (per step)", r"lstm2_fwd_step"),
     ("lstm2 bwd products", r"lstm2_bwd_rec"),
     ("lstm2 bwd pointwise", r"lstm2_bwd_pointwise"),
-    ("lstm1 fwd", r"lstm_fwd_step|lstm_persist_kernel<512"),
-    ("lstm1 bwd", r"lstm_bwd_(rec|pointwise)"),
+    ("lstm1 fwd", r"lstm_fwd_step|lstm_persist_kernel<512|lstm_xcd_fwd"),
+    ("lstm1 bwd", r"lstm_bwd_(rec|pointwise)|lstm_xcd_bwd"),
     ("encoder BLSTM", r"blstm_"),
     ("GEMM fp32", r"gemm_kernel<"),
     ("GEMM bf16", r"gemm_bf16_kernel<"),
@@ -54,7 +54,7 @@ def main(path):
     if "--kernels" in sys.argv:
         per, n = collections.Counter(), collections.Counter()
         for r in seg:
-            k = r["Kernel_Name"].replace("(anonymous namespace)::", "")[:60]
+            k = "q" + r["Queue_Id"] + " " + r["Kernel_Name"].replace("(anonymous namespace)::", "")[:57]
             per[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             n[k] += 1
         print("per kernel:")
