@@ -59,37 +59,52 @@ __global__ __launch_bounds__(256) void stats_partial_kernel(int64_t M, int C, co
   }
 }
 
-// sum of partials [RS][C][2] for this block's 64 columns: 4 waves x RS/4 partials each
-__device__ __forceinline__ void sum_partials(const double* __restrict__ part, int RS, int C, int c, double& a,
+// The finalize kernels sum RS partial rows per channel.  Block = 16 row groups x 16
+// channels (lanes t & 15 of a group read one 256 B row segment of (s1, s2) pairs as
+// double2), each group sums every 16th row, then lanes t < 16 add the 16 group sums in
+// group order: fixed order (deterministic), RS/16 loads in flight per thread instead of a
+// serial RS/4-long chain, and C/16 blocks instead of C/64.
+constexpr int kFinCh = 16;
+
+// returns true on the lanes that own a finished channel sum (threadIdx.x < 16, c < C)
+__device__ __forceinline__ bool sum_partials(const double* __restrict__ part, int RS, int C, int c, double& a,
                                              double& b) {
-  __shared__ double red[4][64][2];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ double red[16][kFinCh][2];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   double s1 = 0.0, s2 = 0.0;
   if (c < C)
-#pragma unroll 8
-    for (int rs = w; rs < RS; rs += 4) {
-      s1 += part[((int64_t)rs * C + c) * 2 + 0];
-      s2 += part[((int64_t)rs * C + c) * 2 + 1];
+#pragma unroll 4
+    for (int rs = g; rs < RS; rs += 16) {
+      const double2 v = *reinterpret_cast<const double2*>(part + ((int64_t)rs * C + c) * 2);
+      s1 += v.x;
+      s2 += v.y;
     }
-  red[w][lane][0] = s1;
-  red[w][lane][1] = s2;
+  red[g][cl][0] = s1;
+  red[g][cl][1] = s2;
   __syncthreads();
-  a = red[0][lane][0] + red[1][lane][0] + red[2][lane][0] + red[3][lane][0];
-  b = red[0][lane][1] + red[1][lane][1] + red[2][lane][1] + red[3][lane][1];
+  a = 0.0;
+  b = 0.0;
+  if (threadIdx.x >= 16) return false;
+  for (int q = 0; q < 16; ++q) {
+    a += red[q][cl][0];
+    b += red[q][cl][1];
+  }
+  return c < C;
 }
 
-// grid = ceil(C/64), block 256
+__device__ __forceinline__ int fin_channel() { return blockIdx.x * kFinCh + (threadIdx.x & 15); }
+
+// grid = ceil(C/16), block 256
 __global__ __launch_bounds__(256) void stats_finalize_kernel(int64_t M, int C, const float* __restrict__ y,
                                                             const double* __restrict__ part, int RS,
                                                             float* __restrict__ mean, float* __restrict__ var,
                                                             float* __restrict__ run_mean, float* __restrict__ run_var,
                                                             float momentum, int64_t* __restrict__ nbt) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = fin_channel();
   double a, b;
-  sum_partials(part, RS, C, c, a, b);
-  if (threadIdx.x >= 64) return;
+  const bool own = sum_partials(part, RS, C, c, a, b);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
-  if (c >= C) return;
+  if (!own) return;
   const double n = (double)M;
   const double mu_s = a / n;
   double v = b / n - mu_s * mu_s;
@@ -160,10 +175,9 @@ __global__ __launch_bounds__(256) void bwd_finalize_kernel(int C, const double* 
                                                           const float* __restrict__ var, float eps,
                                                           float* __restrict__ sums, float* __restrict__ dgamma,
                                                           float* __restrict__ dbeta, int accumulate) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = fin_channel();
   double a, b;
-  sum_partials(part, RS, C, c, a, b);
-  if (threadIdx.x >= 64 || c >= C) return;
+  if (!sum_partials(part, RS, C, c, a, b)) return;
   const float invstd = 1.0f / sqrtf(var[c] + eps);
   const float sdy = (float)a, sdyx = (float)(b * (double)invstd);
   sums[2 * c] = sdy;
@@ -206,12 +220,11 @@ __global__ __launch_bounds__(256) void stats_finalize_raw_kernel(int64_t M, int 
                                                                 float* __restrict__ coef, float* __restrict__ run_mean,
                                                                 float* __restrict__ run_var, float momentum,
                                                                 int64_t* __restrict__ nbt) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = fin_channel();
   double a, b;
-  sum_partials(part, RS, C, c, a, b);
-  if (threadIdx.x >= 64) return;
+  const bool own = sum_partials(part, RS, C, c, a, b);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
-  if (c >= C) return;
+  if (!own) return;
   const double n = (double)M;
   const double mu = a / n;
   double v = b / n - mu * mu;
@@ -246,18 +259,59 @@ __global__ void coef_kernel(int C, const float* __restrict__ mean, const float* 
 // column sums of RS fp64 partial rows (the fused conv bias gradient), fixed order
 __global__ __launch_bounds__(256) void colsum_f64_finalize_kernel(int C, int RS, const double* __restrict__ part,
                                                                  float* __restrict__ out, int accumulate) {
-  __shared__ double red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  __shared__ double red[16][kFinCh];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = fin_channel();
   double s = 0.0;
   if (c < C)
 #pragma unroll 8
-    for (int rs = w; rs < RS; rs += 4) s += part[(int64_t)rs * C + c];
-  red[w][lane] = s;
+    for (int rs = g; rs < RS; rs += 16) s += part[(int64_t)rs * C + c];
+  red[g][cl] = s;
   __syncthreads();
-  if (w != 0 || c >= C) return;
-  const float v = (float)(((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+  if (threadIdx.x >= 16 || c >= C) return;
+  double t = 0.0;
+  for (int q = 0; q < 16; ++q) t += red[q][cl];
+  const float v = (float)t;
   out[c] = accumulate ? out[c] + v : v;
+}
+
+// ---- fused Conv-BN stacks under bf16 (gemm.hip autovc_bnconv_*): the BatchNorm +
+// activation backward of one layer and its conv bias sums in one pass:
+//   g = act'(pre) dz, pre = alpha y + shift (relu' from pre > 0, tanh' = 1 - tanhf(pre)^2 as
+//   the forward computed it), dy = (g - sums0 / M - xhat sums1 / M) alpha,
+//   xhat = (y - mean) invstd (bwd_apply_kernel's arithmetic; coef = [alpha|shift|mean|invstd]),
+//   bpart[rs][c] = sum of dy over row block rs (double, fixed order) for the conv bias.
+// grid (ceil(C/64), RS): 4 waves stride the rows of block rs.
+__global__ __launch_bounds__(256) void bn_dy_kernel(int64_t M, int C, const float* __restrict__ dz,
+                                                   const float* __restrict__ y, const float* __restrict__ coef,
+                                                   int act, const float* __restrict__ sums, float* __restrict__ dy,
+                                                   double* __restrict__ bpart) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int rs = blockIdx.y, RS = gridDim.y;
+  const int64_t r0 = M * rs / RS, r1 = M * (rs + 1) / RS;
+  double sb = 0.0;
+  if (c < C) {
+    const float inv_m = 1.0f / (float)M;
+    const float a = coef[c], sh = coef[C + c], mu = coef[2 * C + c], invstd = coef[3 * C + c];
+    const float s0 = sums[2 * c] * inv_m, s1 = sums[2 * c + 1] * inv_m;
+#pragma unroll 4
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      const float yv = y[r * C + c], d = dz[r * C + c];
+      const float pre = fmaf(yv, a, sh);
+      float g = d;
+      if (act == kRelu) g = pre > 0.f ? d : 0.f;
+      else if (act == kTanh) { const float z = tanhf(pre); g = d * (1.f - z * z); }
+      const float xhat = (yv - mu) * invstd;
+      const float v = (g - s0 - xhat * s1) * a;
+      dy[r * C + c] = v;
+      sb += (double)v;
+    }
+  }
+  red[w][lane] = sb;
+  __syncthreads();
+  if (w == 0 && c < C) bpart[(int64_t)rs * C + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // 2-D grid of the apply kernels: 64-channel column tiles x row groups (~8 rows per thread)
@@ -280,7 +334,7 @@ extern "C" int autovc_bn_stats_f32(int64_t M, int C, const float* y, int64_t ldy
   double* part = reinterpret_cast<double*>(workspace);
   const int RS = (int)std::min<int64_t>(kRowSplits, M);
   hipLaunchKernelGGL(stats_partial_kernel, dim3((C + 63) / 64, RS), dim3(256), 0, stream, M, C, y, ldy, part);
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, M, C, y,
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, stream, M, C, y,
                      (const double*)part, RS, mean, var, running_mean, running_var, momentum, num_batches);
   AVC_CHECK_LAUNCH("autovc_bn_stats_f32");
   return avc::kOk;
@@ -309,7 +363,7 @@ extern "C" int autovc_bn_act_bwd_f32(int64_t M, int C, const float* dz, int64_t 
   const int RS = (int)std::min<int64_t>(kRowSplits, M);
   hipLaunchKernelGGL(bwd_partial_kernel, dim3((C + 63) / 64, RS), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y,
                      ldy, mean, act, part);
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, C, (const double*)part, RS,
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, stream, C, (const double*)part, RS,
                      var, eps, sums, dgamma, dbeta, accumulate);
   hipLaunchKernelGGL(bwd_apply_kernel, grid2d(M, C), dim3(256), 0, stream, M, C, dz, lddz, z, ldz, y, ldy,
                      mean, var, gamma, eps, act, (const float*)sums, dy, lddy);
@@ -323,7 +377,7 @@ extern "C" int autovc_bn_finalize_f32(int RS, int64_t M, int C, const double* pa
                                       float* running_mean, float* running_var, float momentum, int64_t* num_batches,
                                       hipStream_t stream) {
   AVC_CHECK_ARG(RS > 0 && M > 0 && C > 0 && part && mean && var && coef, "autovc_bn_finalize_f32: bad args");
-  hipLaunchKernelGGL(stats_finalize_raw_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, M, C, part, RS, gamma,
+  hipLaunchKernelGGL(stats_finalize_raw_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, stream, M, C, part, RS, gamma,
                      beta, eps, mean, var, coef, running_mean, running_var, momentum, num_batches);
   AVC_CHECK_LAUNCH("autovc_bn_finalize_f32");
   return avc::kOk;
@@ -353,7 +407,7 @@ extern "C" int autovc_bn_bwd_partial_f32(int64_t M, int C, const float* dz, int6
 extern "C" int autovc_bn_bwd_finalize_f32(int RS, int C, const double* part, const float* var, float eps, float* sums,
                                           float* dgamma, float* dbeta, int accumulate, hipStream_t stream) {
   AVC_CHECK_ARG(RS > 0 && C > 0 && part && var && sums, "autovc_bn_bwd_finalize_f32: bad args");
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, C, part, RS, var, eps, sums,
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, stream, C, part, RS, var, eps, sums,
                      dgamma, dbeta, accumulate);
   AVC_CHECK_LAUNCH("autovc_bn_bwd_finalize_f32");
   return avc::kOk;
@@ -362,8 +416,18 @@ extern "C" int autovc_bn_bwd_finalize_f32(int RS, int C, const double* part, con
 extern "C" int autovc_colsum_f64_finalize_f32(int RS, int C, const double* part, float* out, int accumulate,
                                               hipStream_t stream) {
   AVC_CHECK_ARG(RS > 0 && C > 0 && part && out, "autovc_colsum_f64_finalize_f32: bad args");
-  hipLaunchKernelGGL(colsum_f64_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, C, RS, part, out,
+  hipLaunchKernelGGL(colsum_f64_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, stream, C, RS, part, out,
                      accumulate);
   AVC_CHECK_LAUNCH("autovc_colsum_f64_finalize_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_dy_f32(int64_t M, int C, const float* dz, const float* y, const float* coef, int act,
+                                const float* sums, float* dy, double* bias_part, hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && C > 0 && dz && y && coef && sums && dy && bias_part, "autovc_bn_dy_f32: bad args");
+  AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_bn_dy_f32: unknown activation %d", act);
+  hipLaunchKernelGGL(bn_dy_kernel, dim3((C + 63) / 64, autovc_bn_partial_rows(M)), dim3(256), 0, stream, M, C, dz, y,
+                     coef, act, sums, dy, bias_part);
+  AVC_CHECK_LAUNCH("autovc_bn_dy_f32");
   return avc::kOk;
 }

@@ -257,20 +257,23 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t M, int N, c
   if (w == 0 && c < N) part[(int64_t)rs * N + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
+// 16 row groups x 16 columns per block (as bn.hip's finalize kernels): RS/16 loads in
+// flight per thread, the 16 group sums added in group order (deterministic)
 __global__ __launch_bounds__(256) void colsum_finalize_kernel(int N, int RS, const float* __restrict__ part,
                                                               float* __restrict__ out, float* __restrict__ out2,
                                                               int accumulate) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  __shared__ float red[16][16];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float s = 0.f;
   if (c < N)
 #pragma unroll 8
-    for (int rs = w; rs < RS; rs += 4) s += part[(int64_t)rs * N + c];
-  red[w][lane] = s;
+    for (int rs = g; rs < RS; rs += 16) s += part[(int64_t)rs * N + c];
+  red[g][cl] = s;
   __syncthreads();
-  if (w != 0 || c >= N) return;
-  s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  if (threadIdx.x >= 16 || c >= N) return;
+  s = 0.f;
+  for (int q = 0; q < 16; ++q) s += red[q][cl];
   out[c] = accumulate ? out[c] + s : s;
   if (out2) out2[c] = accumulate ? out2[c] + s : s;
 }
@@ -401,7 +404,7 @@ extern "C" int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, f
   AVC_CHECK_ARG(M > 0 && N > 0 && X && out && workspace, "autovc_colsum_f32: bad args");
   const int RS = (int)std::min<int64_t>(kColSplits, M);
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 63) / 64, RS), dim3(256), 0, stream, M, N, X, ld, workspace);
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, N, RS,
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((N + 15) / 16), dim3(256), 0, stream, N, RS,
                      (const float*)workspace, out, out2, accumulate);
   AVC_CHECK_LAUNCH("autovc_colsum_f32");
   return avc::kOk;

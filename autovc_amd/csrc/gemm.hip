@@ -38,7 +38,17 @@ struct Opnd {
   const float* p;
   int64_t ld;
   int conv_T, conv_C, tap0;  // conv_T == 0: plain matrix
+  // BatchNorm + activation on load (bf16 kernel, BN instantiations only; conv operands):
+  // element = act(coef[c] x + coef[C + c]) for a frame inside its sequence, else 0
+  const float* coef;
+  int act;
 };
+
+// the fused Conv-BN stacks' transform of a stored pre-BN value (bn.hip apply_kernel's fmaf)
+__device__ __forceinline__ float bn_act(float x, float a, float s, int act) {
+  const float p = fmaf(x, a, s);
+  return act == 1 ? fmaxf(p, 0.f) : (act == 2 ? tanhf(p) : p);
+}
 
 // Batched launch (c != 0): blockIdx.z is the batch index, the operands and C of batch z
 // start z * (a, b, c) floats further (no split-K then).
@@ -143,6 +153,8 @@ struct OpTile {
   int tap, kmod;            // conv: RK: k / C, k % C (advancing); CK: q / C (fixed)
   int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
   bool rowok;               // CK: the thread's row inside the operand
+  f32x4 al[2], sh[2];       // BN on load: the staged set's 4 channels' (alpha, shift) (CK: set 0, fixed)
+  uint32_t okm[2];          // BN on load: slots of the staged set inside their sequence
   // slot i of this thread -> (row r, k)
   __device__ __forceinline__ static void coords(int i, int& r, int& k) {
     const int e = threadIdx.x + i * NT;
@@ -176,11 +188,42 @@ struct OpTile {
         if (i == 0) {
           rowok = r < R;
           if (o.conv_T > 0) tap = (int)(r / o.conv_C);
+          if (o.coef && o.conv_T > 0 && rowok) {   // the thread's 4 rows = channels c .. c+3
+            const int c = (int)(r % o.conv_C);
+            al[0] = *reinterpret_cast<const f32x4*>(o.coef + c);
+            sh[0] = *reinterpret_cast<const f32x4*>(o.coef + o.conv_C + c);
+          }
         }
       }
     }
   }
   __device__ __forceinline__ void load(const Opnd& o, int64_t K) { load_to(o, K, v); }
+  // load into set SET; BN: also record which slots are inside their sequence and (RK) the
+  // stage's channel coefficients, for the transform applied when the set is stored
+  template <bool BN, int SET>
+  __device__ __forceinline__ void load_s(const Opnd& o, int64_t K) {
+    if constexpr (BN) {
+      uint32_t m = 0;
+      if (RK) {
+        const bool kin = kk < K;
+        const int tt0 = tap + o.tap0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+          if (rok[i] && kin && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T) m |= 1u << i;
+        if (kin) {
+          al[SET] = *reinterpret_cast<const f32x4*>(o.coef + kmod);
+          sh[SET] = *reinterpret_cast<const f32x4*>(o.coef + o.conv_C + kmod);
+        }
+      } else {
+        const int tt0 = tap + o.tap0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+          if (rowok && kpos[i] < K && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T) m |= 1u << i;
+      }
+      okm[SET] = m;
+    }
+    load_to(o, K, SET ? v2 : v);
+  }
   // the next stage's loads into `dst` (v or v2); the address state advances by one stage
   __device__ __forceinline__ void load_to(const Opnd& o, int64_t K, f32x4 (&dst)[PER]) {
     if (RK) {
@@ -226,15 +269,25 @@ struct OpTile {
     }
   }
   // bf16 image [row][LDB] (k contiguous) of an RK operand: each slot as one 8-byte write
-  template <int LDB, int SET = 0>
-  __device__ __forceinline__ void store_bf16(__bf16* lds) const {
+  // BN: slot values become bn_act(value) (inside the sequence) or 0 before the rounding
+  template <bool BN, int SET>
+  __device__ __forceinline__ f32x4 staged(int i, int act) const {
+    const f32x4 x = SET ? v2[i] : v[i];
+    if constexpr (!BN) return x;
+    const int cs = RK ? SET : 0;
+    if (!((okm[SET] >> i) & 1u)) return f32x4{0.f, 0.f, 0.f, 0.f};
+    return f32x4{bn_act(x[0], al[cs][0], sh[cs][0], act), bn_act(x[1], al[cs][1], sh[cs][1], act),
+                 bn_act(x[2], al[cs][2], sh[cs][2], act), bn_act(x[3], al[cs][3], sh[cs][3], act)};
+  }
+  template <int LDB, int SET = 0, bool BN = false>
+  __device__ __forceinline__ void store_bf16(__bf16* lds, int act = 0) const {
     static_assert(RK, "CK operands use store_bf16_kr");
-    const f32x4 (&src)[PER] = SET ? v2 : v;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
       coords(i, r, k);
-      const bf16x4 b = {(__bf16)src[i][0], (__bf16)src[i][1], (__bf16)src[i][2], (__bf16)src[i][3]};
+      const f32x4 x = staged<BN, SET>(i, act);
+      const bf16x4 b = {(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
       *reinterpret_cast<bf16x4*>(lds + r * LDB + k) = b;
     }
   }
@@ -243,14 +296,14 @@ struct OpTile {
   // ds_read_b64_tr_b16 (frag_tr below).  The 32-element pad makes the k-row stride 16 dwords
   // mod 64, so the 4 k rows one 32-lane half reads sit on disjoint banks.
   static constexpr int LDK = ROWS + 32;
-  template <int SET = 0>
-  __device__ __forceinline__ void store_bf16_kr(__bf16* lds) const {
-    const f32x4 (&src)[PER] = SET ? v2 : v;
+  template <int SET = 0, bool BN = false>
+  __device__ __forceinline__ void store_bf16_kr(__bf16* lds, int act = 0) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
       coords(i, r, k);
-      const bf16x4 b = {(__bf16)src[i][0], (__bf16)src[i][1], (__bf16)src[i][2], (__bf16)src[i][3]};
+      const f32x4 x = staged<BN, SET>(i, act);
+      const bf16x4 b = {(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
       *reinterpret_cast<bf16x4*>(lds + k * LDK + r) = b;
     }
   }
@@ -440,11 +493,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
 // v_mfma_f32_32x32x16_bf16 accumulates in fp32 (lane (r = l & 31, h = l >> 5) reads the 8
 // contiguous k = 16 ks + 8h .. +8 of its row with one ds_read_b128, the operand map of
 // the instruction, for A and B alike).
-template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool DEEP = false>
+// BNOP (fused Conv-BN stacks): 1 = A, 2 = B is a conv operand with BatchNorm + activation
+// applied on load (Opnd::coef / act).
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool DEEP = false, int BNOP = 0>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
     int k_per_split, float* __restrict__ slab, Batch bat) {
+  constexpr bool ABN = BNOP == 1, BBN = BNOP == 2;
   constexpr int NWN = BN / WN;
   constexpr int NT = 64 * (BM / WM) * NWN;
   constexpr int TI = WM / 32, TJ = WN / 32;
@@ -486,25 +542,26 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   sa.init(A, m0, kbeg, M);
   sb.init(B, n0, kbeg, N);
   auto stage = [&](__bf16* img) {
-    if constexpr (A_RK) sa.template store_bf16<LDB>(img);
-    else sa.store_bf16_kr(img);
-    if constexpr (B_RK) sb.template store_bf16<LDB>(img + A_EL);
-    else sb.store_bf16_kr(img + A_EL);
+    if constexpr (A_RK) sa.template store_bf16<LDB, 0, ABN>(img, A.act);
+    else sa.template store_bf16_kr<0, ABN>(img, A.act);
+    if constexpr (B_RK) sb.template store_bf16<LDB, 0, BBN>(img + A_EL, B.act);
+    else sb.template store_bf16_kr<0, BBN>(img + A_EL, B.act);
   };
   auto stage2 = [&](__bf16* img) {   // from the second staging set
-    if constexpr (A_RK) sa.template store_bf16<LDB, 1>(img);
-    else sa.template store_bf16_kr<1>(img);
-    if constexpr (B_RK) sb.template store_bf16<LDB, 1>(img + A_EL);
-    else sb.template store_bf16_kr<1>(img + A_EL);
+    if constexpr (A_RK) sa.template store_bf16<LDB, 1, ABN>(img, A.act);
+    else sa.template store_bf16_kr<1, ABN>(img, A.act);
+    if constexpr (B_RK) sb.template store_bf16<LDB, 1, BBN>(img + A_EL, B.act);
+    else sb.template store_bf16_kr<1, BBN>(img + A_EL, B.act);
   };
+  auto load1 = [&]() { sa.template load_s<ABN, 0>(A, kend); sb.template load_s<BBN, 0>(B, kend); };
+  auto load2 = [&]() { sa.template load_s<ABN, 1>(A, kend); sb.template load_s<BBN, 1>(B, kend); };
   if (nk > 0) {
-    sa.load(A, kend);
-    sb.load(B, kend);
+    load1();
     stage(smem[0]);
   }
   if (DEEP) {                        // stages 1 and 2 in flight before the first barrier
-    if (nk > 1) { sa.load(A, kend); sb.load(B, kend); }
-    if (nk > 2) { sa.load_to(A, kend, sa.v2); sb.load_to(B, kend, sb.v2); }
+    if (nk > 1) load1();
+    if (nk > 2) load2();
   }
   __syncthreads();
 
@@ -551,14 +608,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
       compute(smem[0]);
       if (kt + 1 < nk) {
         stage(smem[1]);
-        if (kt + 3 < nk) { sa.load(A, kend); sb.load(B, kend); }
+        if (kt + 3 < nk) load1();
       }
       __syncthreads();
       if (kt + 1 < nk) {
         compute(smem[1]);
         if (kt + 2 < nk) {
           stage2(smem[0]);
-          if (kt + 4 < nk) { sa.load_to(A, kend, sa.v2); sb.load_to(B, kend, sb.v2); }
+          if (kt + 4 < nk) load2();
         }
         __syncthreads();
       }
@@ -566,10 +623,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   } else {
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nk) {
-        sa.load(A, kend);
-        sb.load(B, kend);
-      }
+      if (kt + 1 < nk) load1();
       compute(smem[buf]);
       if (kt + 1 < nk) stage(smem[buf ^ 1]);
       __syncthreads();
@@ -627,6 +681,64 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int64_t M, int64_t N
     float* dst = C + m * ldc + n;
     if (accumulate) v += *dst;
     *dst = v;
+  }
+}
+
+// The fused Conv-BN stacks' split-K reduce (bf16 conv GEMMs always end in one): C = the
+// split sum (+ bias), and per row block blockIdx.y (a contiguous range of M / gridDim.y
+// rows) and column n the fp64 partials part[y][n][2] of
+//   MODE 1: (sum v, sum v^2) — the BatchNorm statistics of the conv output v (bn.hip
+//           stats_finalize_raw_kernel sums them);
+//   MODE 2: (sum g, sum g (yp - mean)), g = act'(pre) v, pre = alpha yp + shift — the
+//           BatchNorm backward sums of the layer whose pre-BN output yp (M x N) this input
+//           gradient v belongs to (bn.hip bwd_partial_kernel's sums; relu' from pre > 0,
+//           tanh' = 1 - tanhf(pre)^2 recomputed as the forward computed it).
+// Block = 64 columns x 4 waves; wave w takes rows r0 + w, r0 + w + 4, ... of the block's
+// range (the loads of 4 rows in flight per thread), the 4 waves' sums are added in wave
+// order through LDS (deterministic).
+template <int MODE>
+__global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N, int splits,
+                                                          const float* __restrict__ slab, float* __restrict__ C,
+                                                          int64_t ldc, const float* __restrict__ bias,
+                                                          const float* __restrict__ yp, const float* __restrict__ coefp,
+                                                          int actp, double* __restrict__ part) {
+  __shared__ double red[4][64][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t total = M * N;
+  const int64_t r0 = M * blockIdx.y / gridDim.y, r1 = M * (blockIdx.y + 1) / gridDim.y;
+  double s1 = 0.0, s2 = 0.0;
+  if (n < N) {
+    const float bsum = bias ? bias[n] : 0.f;
+    float a = 0.f, sh = 0.f, mu = 0.f;
+    if (MODE == 2) { a = coefp[n]; sh = coefp[N + n]; mu = coefp[2 * N + n]; }
+#pragma unroll 4
+    for (int64_t m = r0 + w; m < r1; m += 4) {
+      const int64_t i = m * N + n;
+      float v = 0.f;
+      for (int s = 0; s < splits; ++s) v += slab[s * total + i];
+      v += bsum;
+      C[m * ldc + n] = v;
+      if (MODE == 1) {
+        s1 += (double)v;
+        s2 += (double)v * (double)v;
+      } else {
+        const float y = yp[i];
+        const float pre = fmaf(y, a, sh);
+        float g = v;
+        if (actp == 1) g = pre > 0.f ? v : 0.f;
+        else if (actp == 2) { const float z = tanhf(pre); g = v * (1.f - z * z); }
+        s1 += (double)g;
+        s2 += (double)g * (double)(y - mu);
+      }
+    }
+  }
+  red[w][lane][0] = s1;
+  red[w][lane][1] = s2;
+  __syncthreads();
+  if (w == 0 && n < N) {
+    part[((int64_t)blockIdx.y * N + n) * 2 + 0] = ((red[0][lane][0] + red[1][lane][0]) + red[2][lane][0]) + red[3][lane][0];
+    part[((int64_t)blockIdx.y * N + n) * 2 + 1] = ((red[0][lane][1] + red[1][lane][1]) + red[2][lane][1]) + red[3][lane][1];
   }
 }
 
@@ -794,6 +906,31 @@ constexpr unsigned bf16_lds_bytes() {
   return 2u * 2u * ((AR ? BM * (BK + 8) : BK * (BM + 32)) + (BR ? BN * (BK + 8) : BK * (BN + 32)));
 }
 
+// the fused Conv-BN stacks' bf16 GEMMs: BNOP 1 = forward conv (A = im2col of the previous
+// layer's pre-BN output, RK; B = Wf, RK), BNOP 2 = weight gradient (A = dy, CK; B = im2col
+// of that output, CK), slabs only (the reduce computes the statistics)
+template <int BM, int BN, int BK, int WM, int WN, int BNOP>
+void launch_bn_bf16(dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob, int kps, float* slab) {
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+  constexpr bool AR = BNOP == 1, BR = BNOP == 1;
+  constexpr bool DEEP = BM == 256 && !(BN == 256 && !AR && !BR);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, DEEP, BNOP>), grid, dim3(NT),
+                     dyn_lds_for(bf16_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, K, oa, ob, (float*)nullptr,
+                     (int64_t)N, (const float*)nullptr, (const float*)nullptr, 0, kps, slab, Batch{0, 0, 0, nullptr});
+}
+
+template <int BNOP>
+void launch_gemm_bn_bf16(int id, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob, int kps,
+                         float* slab) {
+  switch (id) {
+    case 0: launch_bn_bf16<128, 128, 64, 64, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    case 2: launch_bn_bf16<256, 128, 64, 64, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    case 3: launch_bn_bf16<256, 256, 64, 128, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    case 4: launch_bn_bf16<256, 256, 32, 128, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    default: launch_bn_bf16<64, 64, 64, 32, 32, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
+  }
+}
+
 template <int BM, int BN, int BK, int WM, int WN>
 void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                          float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
@@ -935,6 +1072,108 @@ extern "C" int autovc_gemm_bf16_splits(int M, int N, int K, int requested) {
   if (M <= 0 || N <= 0 || K <= 0) return requested < 1 ? 1 : requested;
   const PlanBf16 pl = plan_bf16(M, N, K, requested < 1 ? 1 : requested);
   return pl.splits;
+}
+
+// ------------------------------------------------------------------ fused Conv-BN stacks (bf16)
+// (autovc_amd.functional.ConvBNChainBf16Fn; model_vc_mel.py:49-59,92-102,132-169 under
+// BASELINE config 3's bf16 matmuls).  The conv GEMMs of a stack read the previous layer's
+// PRE-BN output and apply its BatchNorm + activation while staging (Opnd::coef), and their
+// split-K reduce emits the BatchNorm partials, so no BatchNorm pass reads or writes an
+// activation of its own.
+namespace {
+struct BnPlan { GemmShape cfg; int splits; int kps; };
+BnPlan plan_bn(int M, int N, int K) {
+  const PlanBf16 pl = plan_bf16(M, N, K, 1);
+  const GemmShape cfg = pl.cfg >= 0 ? kCfgBf16[pl.cfg] : pick_config_bf16(M, N, 1);
+  int splits = pl.cfg >= 0 ? pl.splits : 1;
+  int64_t kps = ((int64_t)K + splits - 1) / splits;
+  kps = (kps + cfg.bk - 1) / cfg.bk * cfg.bk;
+  splits = (int)std::max<int64_t>(1, ((int64_t)K + kps - 1) / kps);
+  return {cfg, splits, (int)kps};
+}
+constexpr int kStatsRows = 256;
+
+// bnop 0 plain / 1 forward (A with BN) / 2 weight gradient (B with BN); mode 0: plain reduce
+// (+ bias), 1 / 2: splitk_stats_kernel<mode> into part
+int bn_gemm(int bnop, int a_trans, int b_trans, int M, int N, int K, Opnd oa, Opnd ob, float* C, const float* bias,
+            int mode, const float* yp, const float* coefp, int actp, double* part, float* ws, hipStream_t st) {
+  const BnPlan pl = plan_bn(M, N, K);
+  const dim3 grid((N + pl.cfg.bn - 1) / pl.cfg.bn, (M + pl.cfg.bm - 1) / pl.cfg.bm, pl.splits);
+  g_batch = Batch{0, 0, 0, nullptr};
+  if (bnop == 1) launch_gemm_bn_bf16<1>(pl.cfg.id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (bnop == 2) launch_gemm_bn_bf16<2>(pl.cfg.id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else launch_gemm_bf16(pl.cfg.id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, N, nullptr, nullptr, 0, pl.kps, ws);
+  AVC_CHECK_LAUNCH("autovc_bnconv (gemm)");
+  if (mode == 0) {
+    const int gx = (N + 255) / 256;
+    const int gy = (int)std::max<int64_t>(1, std::min<int64_t>(M, 4096 / gx + 1));
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, (int64_t)M, (int64_t)N, pl.splits, ws, C,
+                       (int64_t)N, bias, nullptr, 0);
+  } else {
+    const dim3 g2((N + 63) / 64, (unsigned)std::min<int64_t>(kStatsRows, M));
+    if (mode == 1)
+      hipLaunchKernelGGL(splitk_stats_kernel<1>, g2, dim3(256), 0, st, (int64_t)M, (int64_t)N, pl.splits, ws, C,
+                         (int64_t)N, bias, nullptr, nullptr, 0, part);
+    else
+      hipLaunchKernelGGL(splitk_stats_kernel<2>, g2, dim3(256), 0, st, (int64_t)M, (int64_t)N, pl.splits, ws, C,
+                         (int64_t)N, nullptr, yp, coefp, actp, part);
+  }
+  AVC_CHECK_LAUNCH("autovc_bnconv (reduce)");
+  return avc::kOk;
+}
+
+bool bn_dims_ok(int B, int T, int Ci, int Co) {
+  return B > 0 && T > 0 && Ci > 0 && Co > 0 && Ci % 4 == 0 && Co % 4 == 0 &&
+         4 * ((int64_t)B * T * std::max(Ci, Co) * 5 + 4 * (int64_t)std::max(Ci, Co)) < (int64_t)kOOB;
+}
+}  // namespace
+
+extern "C" int autovc_bnconv_stats_rows(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(kStatsRows, M)); }
+
+extern "C" int64_t autovc_bnconv_workspace_floats(int B, int T, int Ci, int Co) {
+  if (B <= 0 || T <= 0 || Ci <= 0 || Co <= 0) return 0;
+  const int M = B * T;
+  const BnPlan f = plan_bn(M, Co, 5 * Ci), x = plan_bn(M, Ci, 5 * Co), w = plan_bn(Co, 5 * Ci, M);
+  return std::max({(int64_t)f.splits * M * Co, (int64_t)x.splits * M * Ci, (int64_t)w.splits * Co * 5 * Ci});
+}
+
+extern "C" int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const float* x, const float* x_coef, int x_act,
+                                          const float* Wf, const float* bias, float* y, double* part,
+                                          float* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && x && Wf && y && part && workspace, "autovc_bnconv_fwd_bf16_f32: bad args");
+  AVC_CHECK_ARG(x_act >= 0 && x_act <= 2 && AVC_ALIGNED16(x) && AVC_ALIGNED16(Wf) && (!x_coef || AVC_ALIGNED16(x_coef)),
+                "autovc_bnconv_fwd_bf16_f32: activation / alignment");
+  const int M = B * T;
+  const Opnd oa{x, Ci, T, Ci, -2, x_coef, x_act};
+  const Opnd ob{Wf, 5 * Ci, 0, 0, 0, nullptr, 0};
+  return bn_gemm(x_coef ? 1 : 0, 0, 0, M, Co, 5 * Ci, oa, ob, y, bias, 1, nullptr, nullptr, 0, part, workspace, stream);
+}
+
+extern "C" int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* Wd, float* dz,
+                                         const float* y_prev, const float* coef_prev, int act_prev, double* part,
+                                         float* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && dy && Wd && dz && workspace, "autovc_bnconv_dx_bf16_f32: bad args");
+  AVC_CHECK_ARG(!y_prev || (coef_prev && part && act_prev >= 0 && act_prev <= 2),
+                "autovc_bnconv_dx_bf16_f32: the BatchNorm sums need y_prev, coef_prev, part");
+  AVC_CHECK_ARG(AVC_ALIGNED16(dy) && AVC_ALIGNED16(Wd), "autovc_bnconv_dx_bf16_f32: alignment");
+  const int M = B * T;
+  const Opnd oa{dy, Co, T, Co, -2, nullptr, 0};
+  const Opnd ob{Wd, Ci, 0, 0, 0, nullptr, 0};
+  return bn_gemm(0, 0, 1, M, Ci, 5 * Co, oa, ob, dz, nullptr, y_prev ? 2 : 0, y_prev, coef_prev, act_prev, part,
+                 workspace, stream);
+}
+
+extern "C" int autovc_bnconv_dw_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* x,
+                                         const float* x_coef, int x_act, float* dWf, float* workspace,
+                                         hipStream_t stream) {
+  AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && dy && x && dWf && workspace, "autovc_bnconv_dw_bf16_f32: bad args");
+  AVC_CHECK_ARG(x_act >= 0 && x_act <= 2 && AVC_ALIGNED16(dy) && AVC_ALIGNED16(x) && (!x_coef || AVC_ALIGNED16(x_coef)),
+                "autovc_bnconv_dw_bf16_f32: activation / alignment");
+  const int M = B * T;
+  const Opnd oa{dy, Co, 0, 0, 0, nullptr, 0};
+  const Opnd ob{x, Ci, T, Ci, -2, x_coef, x_act};
+  return bn_gemm(x_coef ? 2 : 0, 1, 1, Co, 5 * Ci, M, oa, ob, dWf, nullptr, 0, nullptr, nullptr, 0, nullptr, workspace,
+                 stream);
 }
 
 extern "C" int autovc_gemm_set_lds_reserve(int bytes) {

@@ -47,21 +47,56 @@ __constant__ double kG[8][5] = {
 
 // out[i][r][c] (8, R, Cc): flip = 0: R = Co, Cc = Ci, tap k of W[r][c];  flip = 1: R = Ci,
 // Cc = Co, tap 4-k of W[c][r] (the input-gradient kernel).  W (Co, Ci, 5) contiguous.
+__device__ __forceinline__ void wino_weight_elem(int Co, int Ci, const float* __restrict__ W, int flip,
+                                                 float* __restrict__ out, int64_t n, int Cc, int64_t e) {
+  const int r = (int)(e / Cc), c = (int)(e % Cc);
+  const float* w = flip ? W + ((int64_t)c * Ci + r) * 5 : W + ((int64_t)r * Ci + c) * 5;
+  double g[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) g[k] = w[flip ? 4 - k : k];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v += kG[i][k] * g[k];
+    out[(int64_t)i * n + e] = (float)v;
+  }
+}
+
 __global__ void wino_weight_kernel(int Co, int Ci, const float* __restrict__ W, int flip, float* __restrict__ out) {
   const int R = flip ? Ci : Co, Cc = flip ? Co : Ci;
   const int64_t n = (int64_t)R * Cc;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(e / Cc), c = (int)(e % Cc);
-    const float* w = flip ? W + ((int64_t)c * Ci + r) * 5 : W + ((int64_t)r * Ci + c) * 5;
-    double g[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) g[k] = w[flip ? 4 - k : k];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      double v = 0.0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) v += kG[i][k] * g[k];
-      out[(int64_t)i * n + e] = (float)v;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
+    wino_weight_elem(Co, Ci, W, flip, out, n, Cc, e);
+}
+
+// Every conv weight transform of a training step in one launch (blockIdx.y = job):
+// kind 0 / 1 = the Winograd W~ (forward / flipped, as wino_weight_kernel), kind 2 / 3 =
+// the im2col GEMM packs Wf[co][k*Ci + ci] / Wd[(4-k)*Co + co][ci] (elementwise.hip's
+// conv_pack_kernel layouts).  Same arithmetic per element as the single-layer kernels.
+struct WJob { const float* W; float* out; int Co, Ci, kind; };
+constexpr int kMaxWJobs = 48;
+struct WJobs { WJob j[kMaxWJobs]; };
+
+__global__ __launch_bounds__(256) void conv_weights_batched_kernel(WJobs jobs) {
+  const WJob jb = jobs.j[blockIdx.y];
+  const int Co = jb.Co, Ci = jb.Ci;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (jb.kind <= 1) {
+    const int flip = jb.kind;
+    const int R = flip ? Ci : Co, Cc = flip ? Co : Ci;
+    const int64_t n = (int64_t)R * Cc;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride)
+      wino_weight_elem(Co, Ci, jb.W, flip, jb.out, n, Cc, e);
+  } else {
+    const int64_t total = (int64_t)Co * Ci * 5;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+      const int k = (int)(i % 5);
+      const int64_t r = i / 5;
+      const int ci = (int)(r % Ci), co = (int)(r / Ci);
+      const float w = jb.W[i];
+      if (jb.kind == 2) jb.out[(int64_t)co * 5 * Ci + (int64_t)k * Ci + ci] = w;
+      else jb.out[((int64_t)(4 - k) * Co + co) * Ci + ci] = w;
     }
   }
 }
@@ -470,6 +505,27 @@ extern "C" int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip
   hipLaunchKernelGGL(wino_weight_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
                      stream, Co, Ci, W, flip, out);
   AVC_CHECK_LAUNCH("autovc_wino5_weights_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_conv_weights_batched_f32(int n, const int* kinds, const int* Co, const int* Ci,
+                                               const float* const* W, float* const* out, hipStream_t stream) {
+  AVC_CHECK_ARG(n > 0 && kinds && Co && Ci && W && out, "autovc_conv_weights_batched_f32: bad args");
+  for (int j0 = 0; j0 < n; j0 += kMaxWJobs) {
+    WJobs jobs{};
+    const int m = std::min(n - j0, kMaxWJobs);
+    int64_t most = 1;
+    for (int q = 0; q < m; ++q) {
+      const int j = j0 + q;
+      AVC_CHECK_ARG(kinds[j] >= 0 && kinds[j] <= 3 && Co[j] > 0 && Ci[j] > 0 && W[j] && out[j],
+                    "autovc_conv_weights_batched_f32: bad job %d (kind %d, Co %d, Ci %d)", j, kinds[j], Co[j], Ci[j]);
+      jobs.j[q] = WJob{W[j], out[j], Co[j], Ci[j], kinds[j]};
+      most = std::max<int64_t>(most, (int64_t)Co[j] * Ci[j] * (kinds[j] <= 1 ? 1 : 5));
+    }
+    hipLaunchKernelGGL(conv_weights_batched_kernel, dim3((unsigned)std::min<int64_t>((most + 255) / 256, 1024), m),
+                       dim3(256), 0, stream, jobs);
+  }
+  AVC_CHECK_LAUNCH("autovc_conv_weights_batched_f32");
   return avc::kOk;
 }
 

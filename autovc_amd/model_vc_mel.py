@@ -201,7 +201,15 @@ class Generator(nn.Module):
         self.decoder = Decoder(dim_neck, dim_emb, dim_pre)
         self.postnet = Postnet()
 
+    def conv_layers(self):
+        """Every ConvNorm's nn.Conv1d (encoder, decoder, postnet)."""
+        return ([c[0].conv for c in self.encoder.convolutions] + [c[0].conv for c in self.decoder.convolutions]
+                + [c[0].conv for c in self.postnet.convolutions])
+
     def forward(self, x, c_org, c_trg):
+        if x.is_cuda:   # inside the Solver's weight scope: all weight transforms in one launch
+            AF.prepare_conv_weights(self.conv_layers() if c_trg is not None else
+                                    [c[0].conv for c in self.encoder.convolutions], x.shape[-2], self.training)
         code_real = self.encoder.encode(x, c_org)                       # :182
         if c_trg is None:
             return code_real                                            # :183-184

@@ -165,7 +165,9 @@ class Solver(object):
         return g_loss, g_loss_id, g_loss_id_psnt, g_loss_cd, x_identic_psnt
 
     def _forward_backward(self, x_real, emb_org):
-        with AF.precision(self.precision):
+        # the weights do not change until the optimizer step: each conv weight transform is
+        # computed once per step (AF.weight_scope)
+        with AF.precision(self.precision), AF.weight_scope():
             g_loss, l_id, l_psnt, l_cd, x_psnt = self.compute_losses(x_real, emb_org)
             self.reset_grad()
             g_loss.backward()

@@ -184,9 +184,16 @@ def blstm_roofline(dev, B, T, H=32):
         us = timed(fn)
         a = nbytes / (us * 1e-6) / 1e9
         out[name] = {"avg_launch_us": round(us, 2), "achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBS, 4)}
+        pmc = os.path.join(ROOT, "profiles", f"blstm_{name}_pmc.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                out[name]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
     out["achieved"], out["frac"] = out["fwd"]["achieved"], out["fwd"]["frac"]
+    out["traffic"] = out["fwd"].get("traffic")
     out["note"] = ("latency-bound: 128 dependent steps per launch; the 82 KB per step-direction the formula "
-                   "counts fit in L2/LDS, so HBM never limits this kernel (SURVEY §8d expects << 40 %)")
+                   "counts fit in L2/LDS, so HBM never limits this kernel (SURVEY §8d expects << 40 %); "
+                   "traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/blstm_{fwd,bwd}_pmc.json): "
+                   "the h/c/gates writes and the gx read, the formula's per-step W_hh/h re-reads stay on chip")
     return out
 
 

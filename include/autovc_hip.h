@@ -132,6 +132,12 @@ int autovc_gemm_batched_f32(int batch, int M, int N, int K, const float* A, int6
  * x (B,T,C) rows of ldx -> (8, B*T/4, C), zero outside each sequence.  output: (8,
  * B*T/4, C) -> y (B,T,C) rows of ldy, + bias (nullable).  T and C multiples of 4. */
 int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip, float* out, hipStream_t stream);
+/* Every conv weight transform of a training step in one launch: job j turns W[j] (Co[j],
+ * Ci[j], 5) into out[j] by kinds[j]: 0 / 1 = autovc_wino5_weights_f32 with flip 0 / 1,
+ * 2 / 3 = autovc_conv_pack_f32's Wf / Wd.  Host arrays of n entries.  Replaces the
+ * per-layer transforms of the ConvNorm calls (model_vc_mel.py:20-38) in one Solver step. */
+int autovc_conv_weights_batched_f32(int n, const int* kinds, const int* Co, const int* Ci,
+                                    const float* const* W, float* const* out, hipStream_t stream);
 int autovc_wino5_input_f32(int B, int T, int C, const float* x, int64_t ldx, float* out, hipStream_t stream);
 int autovc_wino5_output_f32(int B, int T, int C, const float* Yt, const float* bias, float* y, int64_t ldy,
                             hipStream_t stream);
@@ -208,6 +214,33 @@ int autovc_bn_bwd_finalize_f32(int RS, int C, const double* part, const float* v
                                float* dgamma, float* dbeta, int accumulate, hipStream_t stream);
 int autovc_colsum_f64_finalize_f32(int RS, int C, const double* part, float* out, int accumulate,
                                    hipStream_t stream);
+
+/* The same stacks under precision("bf16") (BASELINE config 3), where the convs are bf16
+ * im2col GEMMs (autovc_gemm_bf16_f32's conv operand forms; Ci, Co % 4 == 0):
+ *   fwd: y (B*T, Co) = conv(act(x * alpha + shift)) + bias — x is the previous layer's
+ *        pre-BN output and x_coef its coef (null: x used as is, the stack's first layer);
+ *        part (autovc_bnconv_stats_rows(B*T) x Co x 2 doubles) = its raw (sum y, sum y^2)
+ *        partials for autovc_bn_finalize_f32;
+ *   dx:  dz (B*T, Ci) = conv^T(dy); with y_prev (the previous layer's pre-BN output) also
+ *        part = that layer's BatchNorm-backward sums for autovc_bn_bwd_finalize_f32;
+ *   dw:  dWf (Co, 5 Ci) = dy^T im2col(act(x * alpha + shift)) (autovc_conv_unpack_grad_f32
+ *        turns it into (Co, Ci, 5));
+ *   autovc_bn_dy_f32: dy (M, C) of a layer from (dz, y, coef, sums) — BatchNorm and
+ *        activation backward — and its conv bias partials (autovc_bn_partial_rows(M) x C
+ *        doubles, for autovc_colsum_f64_finalize_f32).
+ * workspace: autovc_bnconv_workspace_floats(B, T, Ci, Co) floats (split-K slabs). */
+int autovc_bnconv_stats_rows(int64_t M);
+int64_t autovc_bnconv_workspace_floats(int B, int T, int Ci, int Co);
+int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const float* x, const float* x_coef, int x_act,
+                               const float* Wf, const float* bias, float* y, double* part, float* workspace,
+                               hipStream_t stream);
+int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* Wd, float* dz,
+                              const float* y_prev, const float* coef_prev, int act_prev, double* part,
+                              float* workspace, hipStream_t stream);
+int autovc_bnconv_dw_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* x, const float* x_coef,
+                              int x_act, float* dWf, float* workspace, hipStream_t stream);
+int autovc_bn_dy_f32(int64_t M, int C, const float* dz, const float* y, const float* coef, int act,
+                     const float* sums, float* dy, double* bias_part, hipStream_t stream);
 
 /* ---------------------------------------------------------------- LSTM recurrences
  * Replaces the cuDNN/mkldnn recurrence of nn.LSTM (model_vc_mel.py:61,90,104).

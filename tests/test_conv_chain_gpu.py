@@ -97,3 +97,66 @@ def test_chain_eval_mode_matches_per_layer_path(cuda):
         o1, _, _ = _run(copy.deepcopy(layers), x, None, x, chain=True, training=False)
         o0, _, _ = _run(copy.deepcopy(layers), x, None, x, chain=False, training=False)
     assert _rel(o1, o0) < 1e-6
+
+
+def _run_prec(layers, x, dz, residual, precision, chain_bf16, training=True):
+    from autovc_amd import functional as AF
+    prev = AF._CHAIN_BF16_ON
+    AF._CHAIN_BF16_ON = chain_bf16
+    try:
+        with AF.precision(precision):
+            return _run(layers, x, dz, residual, chain=True, training=training)
+    finally:
+        AF._CHAIN_BF16_ON = prev
+
+
+@pytest.mark.parametrize("name,chans,acts,res", [
+    ("encoder", [336, 512, 512, 512], ["relu"] * 3, False),
+    ("postnet", [80, 512, 512, 512, 512, 80], ["tanh"] * 4 + ["none"], True),
+])
+@pytest.mark.parametrize("B,T", [(2, 64), (8, 128), (64, 128)])
+def test_bf16_chain_as_accurate_as_per_layer_bf16(cuda, name, chans, acts, res, B, T):
+    """ConvBNChainBf16Fn (BatchNorm + activation applied while the bf16 conv GEMM stages its
+    operand, statistics from the split-K reduce, BN backward sums from the input-gradient
+    GEMM's reduce) against the fp32 per-layer path: its error is that of the per-layer bf16
+    path (conv GEMMs on bf16 operands, separate BatchNorm kernels) — outputs, every gradient
+    and the running statistics — and the forward is bit-identical from run to run."""
+    import copy
+    g = torch.Generator().manual_seed(1)
+    x = torch.clamp(torch.randn(B, T, chans[0], generator=g) * 0.18 + 0.43, 0, 1).to(cuda)
+    dz = (torch.randn(B, T, chans[-1], generator=g) * 1e-3).to(cuda)
+    residual = torch.randn(B, T, chans[-1], generator=g).to(cuda) if res else None
+    layers = _stack(chans, acts, seed=3)
+    ref, gref, sref = _run(copy.deepcopy(layers), x, dz, residual, chain=False)        # fp32 per layer
+    o1, g1, s1 = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", True)       # bf16 chain
+    o0, g0, s0 = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", False)      # bf16 per layer
+    o2, _, _ = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", True)
+    assert torch.equal(o1, o2)
+    e1, e0 = _rel(o1, ref), _rel(o0, ref)
+    assert e1 < 1e-2 and e1 < 1.5 * e0 + 1e-4, (e1, e0)
+    for k in gref:
+        if k.startswith("b") and not k.startswith("be"):
+            assert g1[k].abs().max().item() < 1e-5, k   # conv bias before a BatchNorm: zero true gradient
+            continue
+        e1, e0 = _rel(g1[k], gref[k]), _rel(g0[k], gref[k])
+        # (the stack's input gradient carries ~10 % bf16 error on both paths: BatchNorm
+        # backward cancellation of the zero-mean part)
+        assert e1 < 0.3 and e1 < 1.5 * e0 + 1e-3, (k, e1, e0)
+    for (m1, v1, n1), (m0, v0, n0), (mr, vr, nr) in zip(s1, s0, sref):
+        assert n1 == n0 == nr == 1
+        assert _rel(m1, mr) < 1.5 * _rel(m0, mr) + 1e-4 and _rel(v1, vr) < 1.5 * _rel(v0, vr) + 1e-4
+
+
+def test_bf16_chain_eval_mode(cuda):
+    import copy
+    g = torch.Generator().manual_seed(2)
+    layers = _stack([80, 512, 512, 80], ["tanh", "tanh", "none"], seed=4)
+    for _, bn, _ in layers:
+        bn.running_mean.uniform_(-0.2, 0.2, generator=g)
+        bn.running_var.uniform_(0.5, 1.5, generator=g)
+    x = torch.randn(4, 64, 80, generator=g).to(cuda)
+    with torch.no_grad():
+        ref, _, _ = _run(copy.deepcopy(layers), x, None, x, chain=False, training=False)
+        o1, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", True, training=False)
+        o0, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", False, training=False)
+    assert _rel(o1, ref) < 1.5 * _rel(o0, ref) + 1e-4

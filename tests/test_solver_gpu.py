@@ -170,3 +170,61 @@ def og_build_eval(cuda):
     g = Generator(32, 256, 512, 32)
     g.load_state_dict(og.make_weights())
     return g.to(cuda).eval()
+
+
+def test_batched_weight_transforms_bit_identical(cuda):
+    """autovc_conv_weights_batched_f32 (every conv weight transform of a step in one launch)
+    equals the per-layer kernels element for element, for all four kinds and the Generator's
+    channel shapes."""
+    import ctypes  # noqa: F401
+    from autovc_amd import _lib
+    from autovc_amd import functional as AF
+    g = torch.Generator().manual_seed(5)
+    shapes = [(512, 336), (512, 512), (80, 512), (512, 80), (516, 324)]
+    jobs, refs = [], []
+    for Co, Ci in shapes:
+        W = torch.randn(Co, Ci, 5, generator=g).to(cuda)
+        for kind in range(4):
+            out = torch.empty(AF._WSHAPE[kind](Co, Ci), device=cuda)
+            jobs.append((kind, W, out))
+            ref = torch.empty_like(out)
+            if kind <= 1:
+                _lib.call("autovc_wino5_weights_f32", Co, Ci, W.data_ptr(), kind, ref.data_ptr(), AF._s())
+            else:
+                _lib.call("autovc_conv_pack_f32", Co, Ci, 5, W.data_ptr(), ref.data_ptr() if kind == 2 else 0,
+                          ref.data_ptr() if kind == 3 else 0, AF._s())
+            refs.append(ref)
+    AF._run_weight_jobs(jobs)
+    torch.cuda.synchronize()
+    for (kind, _, out), ref in zip(jobs, refs):
+        assert torch.equal(out, ref), kind
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_weight_scope_step_bit_identical(cuda, precision):
+    """The step-scoped weight transforms (computed once per step, in one launch) leave two
+    Solver steps bit-identical to per-layer transforms (AVC_WEIGHT_BATCH=0)."""
+    import bench
+    from autovc_amd import functional as AF
+    res = []
+    prev = AF._WBATCH
+    try:
+        for on in (True, False):
+            AF._WBATCH = on
+            torch.manual_seed(0)
+            solver = bench.make_solver(cuda, 8)
+            solver.G.train()
+            solver.precision = precision
+            x, e = bench.synthetic_batch(8, 128, cuda, 99)
+            losses = [torch.stack([o.detach().reshape(()) for o in solver.train_step(x, e)]).clone()
+                      for _ in range(2)]
+            torch.cuda.synchronize()
+            res.append((losses, [f.clone() for f in solver.g_optimizer.flat_params()]))
+            del solver
+    finally:
+        AF._WBATCH = prev
+    (la, pa), (lb, pb) = res
+    for a, b in zip(la, lb):
+        assert torch.equal(a, b)
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)

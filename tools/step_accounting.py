@@ -18,11 +18,11 @@ CATS = [
     ("encoder BLSTM", r"blstm_"),
     ("GEMM fp32", r"gemm_kernel<"),
     ("GEMM bf16", r"gemm_bf16_kernel<"),
-    ("split-K reduce", r"splitk_reduce"),
+    ("split-K reduce", r"splitk_reduce|splitk_stats"),
     ("Winograd transforms", r"wino_"),
-    ("BatchNorm", r"stats_|apply_kernel|bwd_partial|bwd_finalize|bwd_apply"),
+    ("BatchNorm", r"stats_(partial|finalize)|apply_kernel|bwd_partial|bwd_finalize|bwd_apply|bn_dy"),
     ("bias column sums", r"colsum_"),
-    ("conv pack/unpack", r"conv_pack|conv_unpack|transpose_kernel"),
+    ("conv pack/unpack", r"conv_pack|conv_unpack|transpose_kernel|conv_weights_batched"),
     ("losses", r"loss_"),
     ("Adam", r"adam_kernel"),
     ("frame/code glue", r"frame_concat|code_gather"),
