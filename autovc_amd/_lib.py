@@ -54,12 +54,13 @@ sig("autovc_wino5_weights_f32", c_int, c_int, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_conv_weights_batched_f32", c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_bnconv_stats_rows", c_i64)
 sig("autovc_bnconv_workspace_floats", c_int, c_int, c_int, c_int)
-sig("autovc_bnconv_fwd_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-    c_ptr)
-sig("autovc_bnconv_dx_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr,
-    c_ptr)
-sig("autovc_bnconv_dw_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr)
-sig("autovc_bn_dy_f32", c_i64, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr)
+sig("autovc_bnconv_fwd_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int,
+    c_ptr, c_ptr)
+sig("autovc_bnconv_dx_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int,
+    c_ptr, c_ptr)
+sig("autovc_bnconv_dw_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int, c_ptr, c_ptr)
+sig("autovc_bn_dy_f32", c_i64, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
+sig("autovc_bn_apply_bf16", c_i64, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_wino5_input_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr)
 sig("autovc_wino5_output_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_i64, c_ptr)
 sig("autovc_wino5_dy_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_ptr)

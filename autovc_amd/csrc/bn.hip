@@ -277,15 +277,17 @@ __global__ __launch_bounds__(256) void colsum_f64_finalize_kernel(int C, int RS,
 
 // ---- fused Conv-BN stacks under bf16 (gemm.hip autovc_bnconv_*): the BatchNorm +
 // activation backward of one layer and its conv bias sums in one pass:
-//   g = act'(pre) dz, pre = alpha y + shift (relu' from pre > 0, tanh' = 1 - tanhf(pre)^2 as
-//   the forward computed it), dy = (g - sums0 / M - xhat sums1 / M) alpha,
+//   g = act'(pre) dz, pre = alpha y + shift (relu' from pre > 0, tanh' = 1 - avc_tanh_fast(pre)^2
+//   as the stack's GEMMs computed it), dy = (g - sums0 / M - xhat sums1 / M) alpha,
 //   xhat = (y - mean) invstd (bwd_apply_kernel's arithmetic; coef = [alpha|shift|mean|invstd]),
 //   bpart[rs][c] = sum of dy over row block rs (double, fixed order) for the conv bias.
+// dy is written as fp32 (dy) and / or as the bf16 copy the stack's GEMMs read (dyh).
 // grid (ceil(C/64), RS): 4 waves stride the rows of block rs.
+template <int ACT>
 __global__ __launch_bounds__(256) void bn_dy_kernel(int64_t M, int C, const float* __restrict__ dz,
                                                    const float* __restrict__ y, const float* __restrict__ coef,
-                                                   int act, const float* __restrict__ sums, float* __restrict__ dy,
-                                                   double* __restrict__ bpart) {
+                                                   const float* __restrict__ sums, float* __restrict__ dy,
+                                                   __bf16* __restrict__ dyh, double* __restrict__ bpart) {
   __shared__ double red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -301,17 +303,37 @@ __global__ __launch_bounds__(256) void bn_dy_kernel(int64_t M, int C, const floa
       const float yv = y[r * C + c], d = dz[r * C + c];
       const float pre = fmaf(yv, a, sh);
       float g = d;
-      if (act == kRelu) g = pre > 0.f ? d : 0.f;
-      else if (act == kTanh) { const float z = tanhf(pre); g = d * (1.f - z * z); }
+      if (ACT == kRelu) g = pre > 0.f ? d : 0.f;
+      else if (ACT == kTanh) { const float z = avc_tanh_fast(pre); g = d * (1.f - z * z); }
       const float xhat = (yv - mu) * invstd;
       const float v = (g - s0 - xhat * s1) * a;
-      dy[r * C + c] = v;
+      if (dy) dy[r * C + c] = v;
+      if (dyh) dyh[r * C + c] = (__bf16)v;
       sb += (double)v;
     }
   }
   red[w][lane] = sb;
   __syncthreads();
   if (w == 0 && c < C) bpart[(int64_t)rs * C + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// z = bf16(act(y alpha + shift)) — the bf16 copy of a stack layer's output that the next
+// layer's bf16 conv GEMMs (forward and weight gradient) read; tanh as the stack's backward
+// recomputes it.  4 channels per thread (C % 4 == 0), grid-stride over the (M, C/4) elements.
+template <int ACT>
+__global__ __launch_bounds__(256) void apply_bf16_kernel(int64_t n4, int C4, const float* __restrict__ y,
+                                                        const float* __restrict__ coef, __bf16* __restrict__ z) {
+  const int C = 4 * C4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = 4 * (int)(e % C4);
+    const float4 v = reinterpret_cast<const float4*>(y)[e];
+    const float4 a = *reinterpret_cast<const float4*>(coef + c), sh = *reinterpret_cast<const float4*>(coef + C + c);
+    float o[4] = {fmaf(v.x, a.x, sh.x), fmaf(v.y, a.y, sh.y), fmaf(v.z, a.z, sh.z), fmaf(v.w, a.w, sh.w)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = ACT == kRelu ? fmaxf(o[j], 0.f) : (ACT == kTanh ? avc_tanh_fast(o[j]) : o[j]);
+    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+    reinterpret_cast<bf16x4_t*>(z)[e] = bf16x4_t{(__bf16)o[0], (__bf16)o[1], (__bf16)o[2], (__bf16)o[3]};
+  }
 }
 
 // 2-D grid of the apply kernels: 64-channel column tiles x row groups (~8 rows per thread)
@@ -423,11 +445,29 @@ extern "C" int autovc_colsum_f64_finalize_f32(int RS, int C, const double* part,
 }
 
 extern "C" int autovc_bn_dy_f32(int64_t M, int C, const float* dz, const float* y, const float* coef, int act,
-                                const float* sums, float* dy, double* bias_part, hipStream_t stream) {
-  AVC_CHECK_ARG(M > 0 && C > 0 && dz && y && coef && sums && dy && bias_part, "autovc_bn_dy_f32: bad args");
+                                const float* sums, float* dy, void* dy_bf16, double* bias_part, hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && C > 0 && dz && y && coef && sums && (dy || dy_bf16) && bias_part, "autovc_bn_dy_f32: bad args");
   AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_bn_dy_f32: unknown activation %d", act);
-  hipLaunchKernelGGL(bn_dy_kernel, dim3((C + 63) / 64, autovc_bn_partial_rows(M)), dim3(256), 0, stream, M, C, dz, y,
-                     coef, act, sums, dy, bias_part);
+  const dim3 grid((C + 63) / 64, autovc_bn_partial_rows(M));
+  __bf16* dyh = static_cast<__bf16*>(dy_bf16);
+  if (act == kRelu) hipLaunchKernelGGL(bn_dy_kernel<kRelu>, grid, dim3(256), 0, stream, M, C, dz, y, coef, sums, dy, dyh, bias_part);
+  else if (act == kTanh) hipLaunchKernelGGL(bn_dy_kernel<kTanh>, grid, dim3(256), 0, stream, M, C, dz, y, coef, sums, dy, dyh, bias_part);
+  else hipLaunchKernelGGL(bn_dy_kernel<kNone>, grid, dim3(256), 0, stream, M, C, dz, y, coef, sums, dy, dyh, bias_part);
   AVC_CHECK_LAUNCH("autovc_bn_dy_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_apply_bf16(int64_t M, int C, const float* y, const float* coef, int act, void* z,
+                                    hipStream_t stream) {
+  AVC_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && y && coef && z && AVC_ALIGNED16(y) && AVC_ALIGNED16(coef),
+                "autovc_bn_apply_bf16: bad args");
+  AVC_CHECK_ARG(act >= 0 && act <= 2, "autovc_bn_apply_bf16: unknown activation %d", act);
+  const int64_t n4 = M * (C / 4);
+  const dim3 grid((unsigned)std::min<int64_t>((n4 + 255) / 256, 2048));
+  __bf16* zh = static_cast<__bf16*>(z);
+  if (act == kRelu) hipLaunchKernelGGL(apply_bf16_kernel<kRelu>, grid, dim3(256), 0, stream, n4, C / 4, y, coef, zh);
+  else if (act == kTanh) hipLaunchKernelGGL(apply_bf16_kernel<kTanh>, grid, dim3(256), 0, stream, n4, C / 4, y, coef, zh);
+  else hipLaunchKernelGGL(apply_bf16_kernel<kNone>, grid, dim3(256), 0, stream, n4, C / 4, y, coef, zh);
+  AVC_CHECK_LAUNCH("autovc_bn_apply_bf16");
   return avc::kOk;
 }

@@ -44,11 +44,19 @@ struct Opnd {
   int act;
 };
 
-// the fused Conv-BN stacks' transform of a stored pre-BN value (bn.hip apply_kernel's fmaf)
-__device__ __forceinline__ float bn_act(float x, float a, float s, int act) {
+// the fused Conv-BN stacks' transform of a stored pre-BN value (bn.hip apply_kernel's fmaf).
+// ACT is a template argument: with a runtime activation the compiler evaluated every branch
+// (two transcendentals per element) for every layer — 2.4x the GEMM time.
+// tanh: common.h's v_exp_f32 + v_rcp_f32 form (~1e-7 absolute); the value is rounded to
+// bf16 right away, and the stack's backward recomputes it the same way
+template <int ACT>
+__device__ __forceinline__ float bn_act(float x, float a, float s) {
   const float p = fmaf(x, a, s);
-  return act == 1 ? fmaxf(p, 0.f) : (act == 2 ? tanhf(p) : p);
+  return ACT == 1 ? fmaxf(p, 0.f) : (ACT == 2 ? avc_tanh_fast(p) : p);
 }
+
+// (alpha, shift) of a BN-on-load operand's channels, staged in LDS once per workgroup
+constexpr int kBnMaxC = 1024;
 
 // Batched launch (c != 0): blockIdx.z is the batch index, the operands and C of batch z
 // start z * (a, b, c) floats further (no split-K then).
@@ -134,18 +142,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)kOOB, 0x00020000);
 }
 
-template <bool RK, int ROWS, int BK, int NT>
+// EB: bytes per element of the operand in memory — 4 (fp32) or 2 (bf16, the bf16 kernel's
+// "bf16 source" operands: copies written by their producers, staged into the bf16 LDS image
+// as they are).  A slot is always 16 bytes: VE = 4 fp32 or 8 bf16 elements.
+template <bool RK, int ROWS, int BK, int NT, int EB = 4>
 struct OpTile {
+  static constexpr int VE = 16 / EB;                 // elements per 16-byte slot
   static constexpr int LD = RK ? BK + 4 : ROWS + 4;
   static constexpr int FLOATS = RK ? ROWS * LD : BK * LD;
-  static constexpr int F4 = ROWS * BK / 4;           // float4 per stage
+  static constexpr int F4 = ROWS * BK / VE;          // slots per stage
   static constexpr int PER = F4 / NT;
   static_assert(PER * NT == F4, "staging map");
-  static_assert(RK ? NT % (BK / 4) == 0 : NT % (ROWS / 4) == 0, "slots of a thread share k (RK) / row (CK)");
-  f32x4 v[PER];
+  static_assert(RK ? NT % (BK / VE) == 0 : NT % (ROWS / VE) == 0, "slots of a thread share k (RK) / row (CK)");
+  f32x4 v[PER];             // 16 raw bytes per slot (4 fp32 or 8 bf16)
   f32x4 v2[PER];            // second staging set (bf16 kernel: two stages in flight)
   __amdgpu_buffer_rsrc_t rsrc;
-  uint32_t off[PER];        // byte offset of the slot's next float4 (valid when unmasked)
+  uint32_t off[PER];        // byte offset of the slot's next 16 bytes (valid when unmasked)
   bool rok[PER];            // RK: row inside the operand
   int tpos[PER];            // conv: frame position in its sequence (RK: fixed; CK: advancing)
   int kpos[PER];            // CK: frame index of the slot
@@ -153,13 +165,13 @@ struct OpTile {
   int tap, kmod;            // conv: RK: k / C, k % C (advancing); CK: q / C (fixed)
   int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
   bool rowok;               // CK: the thread's row inside the operand
-  f32x4 al[2], sh[2];       // BN on load: the staged set's 4 channels' (alpha, shift) (CK: set 0, fixed)
+  int kch[2];               // BN on load: the staged set's first channel (RK: per stage; CK: fixed)
   uint32_t okm[2];          // BN on load: slots of the staged set inside their sequence
   // slot i of this thread -> (row r, k)
   __device__ __forceinline__ static void coords(int i, int& r, int& k) {
     const int e = threadIdx.x + i * NT;
-    if (RK) { r = e / (BK / 4); k = 4 * (e % (BK / 4)); }
-    else    { k = e / (ROWS / 4); r = 4 * (e % (ROWS / 4)); }
+    if (RK) { r = e / (BK / VE); k = VE * (e % (BK / VE)); }
+    else    { k = e / (ROWS / VE); r = VE * (e % (ROWS / VE)); }
   }
   __device__ __forceinline__ void init(const Opnd& o, int64_t r0, int64_t kbeg, int64_t R) {
     rsrc = make_rsrc(o.p);
@@ -175,7 +187,7 @@ struct OpTile {
       const int64_t r = r0 + rr, k = kbeg + kq;
       if (RK) {
         rok[i] = r < R;
-        off[i] = (uint32_t)((((r + shift) * o.ld) + k) * 4);
+        off[i] = (uint32_t)((((r + shift) * o.ld) + k) * EB);
         if (o.conv_T > 0) tpos[i] = (int)(r % o.conv_T);
         if (i == 0) {
           kk = (int)k;
@@ -183,16 +195,12 @@ struct OpTile {
         }
       } else {
         kpos[i] = (int)k;
-        off[i] = (uint32_t)((((k + shift) * o.ld) + r) * 4);
+        off[i] = (uint32_t)((((k + shift) * o.ld) + r) * EB);
         if (o.conv_T > 0) tpos[i] = (int)(k % o.conv_T);
         if (i == 0) {
           rowok = r < R;
           if (o.conv_T > 0) tap = (int)(r / o.conv_C);
-          if (o.coef && o.conv_T > 0 && rowok) {   // the thread's 4 rows = channels c .. c+3
-            const int c = (int)(r % o.conv_C);
-            al[0] = *reinterpret_cast<const f32x4*>(o.coef + c);
-            sh[0] = *reinterpret_cast<const f32x4*>(o.coef + o.conv_C + c);
-          }
+          if (o.conv_T > 0) kch[0] = kch[1] = rowok ? (int)(r % o.conv_C) : 0;   // rows = channels c .. c+3
         }
       }
     }
@@ -210,10 +218,7 @@ struct OpTile {
 #pragma unroll
         for (int i = 0; i < PER; ++i)
           if (rok[i] && kin && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T) m |= 1u << i;
-        if (kin) {
-          al[SET] = *reinterpret_cast<const f32x4*>(o.coef + kmod);
-          sh[SET] = *reinterpret_cast<const f32x4*>(o.coef + o.conv_C + kmod);
-        }
+        kch[SET] = kmod;
       } else {
         const int tt0 = tap + o.tap0;
 #pragma unroll
@@ -234,7 +239,7 @@ struct OpTile {
         bool ok = rok[i] && kin;
         if (o.conv_T > 0) ok = ok && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T;
         dst[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
-        off[i] += BK * 4;
+        off[i] += BK * EB;
       }
       kk += BK;
       if (o.conv_T > 0) {   // k += BK as (tap, kmod) with the uniform BK / C, BK % C
@@ -249,7 +254,7 @@ struct OpTile {
         bool ok = rowok && kpos[i] < K;
         if (o.conv_T > 0) ok = ok && (unsigned)(tpos[i] + tt0) < (unsigned)o.conv_T;
         dst[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
-        off[i] += (uint32_t)(BK * o.ld * 4);
+        off[i] += (uint32_t)(BK * o.ld * EB);
         kpos[i] += BK;
         if (o.conv_T > 0) {   // (frame + BK) % T with the uniform BK % T
           tpos[i] += step_r;
@@ -270,42 +275,91 @@ struct OpTile {
   }
   // bf16 image [row][LDB] (k contiguous) of an RK operand: each slot as one 8-byte write
   // BN: slot values become bn_act(value) (inside the sequence) or 0 before the rounding
-  template <bool BN, int SET>
-  __device__ __forceinline__ f32x4 staged(int i, int act) const {
+  // cl: the (alpha | shift) table in LDS (kBnMaxC floats each), al / sh: this set's channels
+  template <int ACT, int SET>
+  __device__ __forceinline__ f32x4 staged(int i, const f32x4& al, const f32x4& sh) const {
     const f32x4 x = SET ? v2[i] : v[i];
-    if constexpr (!BN) return x;
-    const int cs = RK ? SET : 0;
-    if (!((okm[SET] >> i) & 1u)) return f32x4{0.f, 0.f, 0.f, 0.f};
-    return f32x4{bn_act(x[0], al[cs][0], sh[cs][0], act), bn_act(x[1], al[cs][1], sh[cs][1], act),
-                 bn_act(x[2], al[cs][2], sh[cs][2], act), bn_act(x[3], al[cs][3], sh[cs][3], act)};
+    if constexpr (ACT < 0) return x;
+    else {
+      if (!((okm[SET] >> i) & 1u)) return f32x4{0.f, 0.f, 0.f, 0.f};
+      return f32x4{bn_act<ACT>(x[0], al[0], sh[0]), bn_act<ACT>(x[1], al[1], sh[1]),
+                   bn_act<ACT>(x[2], al[2], sh[2]), bn_act<ACT>(x[3], al[3], sh[3])};
+    }
   }
-  template <int LDB, int SET = 0, bool BN = false>
-  __device__ __forceinline__ void store_bf16(__bf16* lds, int act = 0) const {
+  template <bool BN, int SET>
+  __device__ __forceinline__ void coefs(const float* cl, f32x4& al, f32x4& sh) const {
+    if constexpr (BN) {
+      al = *reinterpret_cast<const f32x4*>(cl + kch[SET]);
+      sh = *reinterpret_cast<const f32x4*>(cl + kBnMaxC + kch[SET]);
+    }
+  }
+  // ACT < 0: no BatchNorm on load; else the activation of the BN operand (uniform branch in
+  // the callers below, so each path is straight-line code)
+  template <int LDB, int SET, int ACT>
+  __device__ __forceinline__ void store_bf16_act(__bf16* lds, const float* cl) const {
     static_assert(RK, "CK operands use store_bf16_kr");
+    if constexpr (EB == 2) {   // already bf16: one 16-byte write per slot
+      static_assert(ACT < 0, "BatchNorm on load needs an fp32 operand");
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        int r, k;
+        coords(i, r, k);
+        *reinterpret_cast<f32x4*>(lds + r * LDB + k) = SET ? v2[i] : v[i];
+      }
+      return;
+    }
+    f32x4 al, sh;
+    coefs<(ACT >= 0), SET>(cl, al, sh);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
       coords(i, r, k);
-      const f32x4 x = staged<BN, SET>(i, act);
+      const f32x4 x = staged<ACT, SET>(i, al, sh);
       const bf16x4 b = {(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
       *reinterpret_cast<bf16x4*>(lds + r * LDB + k) = b;
     }
+  }
+  template <int LDB, int SET = 0, bool BN = false>
+  __device__ __forceinline__ void store_bf16(__bf16* lds, int act = 0, const float* cl = nullptr) const {
+    if constexpr (!BN) store_bf16_act<LDB, SET, -1>(lds, cl);
+    else if (act == 1) store_bf16_act<LDB, SET, 1>(lds, cl);
+    else if (act == 2) store_bf16_act<LDB, SET, 2>(lds, cl);
+    else store_bf16_act<LDB, SET, 0>(lds, cl);
   }
   // bf16 image [k][ROWS + 32] (rows contiguous) of a CK operand: each slot's 4 rows as one
   // 8-byte write (a wave writes whole k rows: conflict-free); read back transposed with
   // ds_read_b64_tr_b16 (frag_tr below).  The 32-element pad makes the k-row stride 16 dwords
   // mod 64, so the 4 k rows one 32-lane half reads sit on disjoint banks.
   static constexpr int LDK = ROWS + 32;
-  template <int SET = 0, bool BN = false>
-  __device__ __forceinline__ void store_bf16_kr(__bf16* lds, int act = 0) const {
+  template <int SET, int ACT>
+  __device__ __forceinline__ void store_bf16_kr_act(__bf16* lds, const float* cl) const {
+    if constexpr (EB == 2) {   // 8 rows of one k, already bf16: one 16-byte write per slot
+      static_assert(ACT < 0, "BatchNorm on load needs an fp32 operand");
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        int r, k;
+        coords(i, r, k);
+        *reinterpret_cast<f32x4*>(lds + k * LDK + r) = SET ? v2[i] : v[i];
+      }
+      return;
+    }
+    f32x4 al, sh;
+    coefs<(ACT >= 0), SET>(cl, al, sh);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
       coords(i, r, k);
-      const f32x4 x = staged<BN, SET>(i, act);
+      const f32x4 x = staged<ACT, SET>(i, al, sh);
       const bf16x4 b = {(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
       *reinterpret_cast<bf16x4*>(lds + k * LDK + r) = b;
     }
+  }
+  template <int SET = 0, bool BN = false>
+  __device__ __forceinline__ void store_bf16_kr(__bf16* lds, int act = 0, const float* cl = nullptr) const {
+    if constexpr (!BN) store_bf16_kr_act<SET, -1>(lds, cl);
+    else if (act == 1) store_bf16_kr_act<SET, 1>(lds, cl);
+    else if (act == 2) store_bf16_kr_act<SET, 2>(lds, cl);
+    else store_bf16_kr_act<SET, 0>(lds, cl);
   }
   // fragment values of MFMAs p = 4g .. 4g+3 (k = h*BK/2 + p) for tile row `row`
   __device__ __forceinline__ f32x4 frag4(const float* lds, int row, int h, int g) const {
@@ -495,18 +549,29 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
 // the instruction, for A and B alike).
 // BNOP (fused Conv-BN stacks): 1 = A, 2 = B is a conv operand with BatchNorm + activation
 // applied on load (Opnd::coef / act).
-template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool DEEP = false, int BNOP = 0>
+// SRC: bit 0 = A, bit 1 = B is held in memory as bf16 (ld in bf16 elements; conv channel
+// counts multiples of 8).
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool DEEP = false, int BNOP = 0, int SRC = 0>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
     int k_per_split, float* __restrict__ slab, Batch bat) {
   constexpr bool ABN = BNOP == 1, BBN = BNOP == 2;
+  __shared__ __attribute__((aligned(16))) float cl[BNOP ? 2 * kBnMaxC : 4];
+  if constexpr (BNOP != 0) {   // the BN operand's (alpha | shift), staged once
+    const Opnd& o = ABN ? A : B;
+    for (int c = threadIdx.x; c < o.conv_C; c += blockDim.x) {
+      cl[c] = o.coef[c];
+      cl[kBnMaxC + c] = o.coef[o.conv_C + c];
+    }
+    __syncthreads();
+  }
   constexpr int NWN = BN / WN;
   constexpr int NT = 64 * (BM / WM) * NWN;
   constexpr int TI = WM / 32, TJ = WN / 32;
   constexpr int LDB = BK + 8;
-  using TA = OpTile<A_RK, BM, BK, NT>;
-  using TBt = OpTile<B_RK, BN, BK, NT>;
+  using TA = OpTile<A_RK, BM, BK, NT, (SRC & 1) ? 2 : 4>;
+  using TBt = OpTile<B_RK, BN, BK, NT, (SRC & 2) ? 2 : 4>;
   // RK operands: [row][BK + 8] images read with ds_read_b128; CK operands: [k][rows + 32]
   // images read with ds_read_b64_tr_b16
   constexpr int A_EL = A_RK ? BM * LDB : BK * TA::LDK;
@@ -542,16 +607,16 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   sa.init(A, m0, kbeg, M);
   sb.init(B, n0, kbeg, N);
   auto stage = [&](__bf16* img) {
-    if constexpr (A_RK) sa.template store_bf16<LDB, 0, ABN>(img, A.act);
-    else sa.template store_bf16_kr<0, ABN>(img, A.act);
-    if constexpr (B_RK) sb.template store_bf16<LDB, 0, BBN>(img + A_EL, B.act);
-    else sb.template store_bf16_kr<0, BBN>(img + A_EL, B.act);
+    if constexpr (A_RK) sa.template store_bf16<LDB, 0, ABN>(img, A.act, cl);
+    else sa.template store_bf16_kr<0, ABN>(img, A.act, cl);
+    if constexpr (B_RK) sb.template store_bf16<LDB, 0, BBN>(img + A_EL, B.act, cl);
+    else sb.template store_bf16_kr<0, BBN>(img + A_EL, B.act, cl);
   };
   auto stage2 = [&](__bf16* img) {   // from the second staging set
-    if constexpr (A_RK) sa.template store_bf16<LDB, 1, ABN>(img, A.act);
-    else sa.template store_bf16_kr<1, ABN>(img, A.act);
-    if constexpr (B_RK) sb.template store_bf16<LDB, 1, BBN>(img + A_EL, B.act);
-    else sb.template store_bf16_kr<1, BBN>(img + A_EL, B.act);
+    if constexpr (A_RK) sa.template store_bf16<LDB, 1, ABN>(img, A.act, cl);
+    else sa.template store_bf16_kr<1, ABN>(img, A.act, cl);
+    if constexpr (B_RK) sb.template store_bf16<LDB, 1, BBN>(img + A_EL, B.act, cl);
+    else sb.template store_bf16_kr<1, BBN>(img + A_EL, B.act, cl);
   };
   auto load1 = [&]() { sa.template load_s<ABN, 0>(A, kend); sb.template load_s<BBN, 0>(B, kend); };
   auto load2 = [&]() { sa.template load_s<ABN, 1>(A, kend); sb.template load_s<BBN, 1>(B, kend); };
@@ -692,16 +757,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int64_t M, int64_t N
 //   MODE 2: (sum g, sum g (yp - mean)), g = act'(pre) v, pre = alpha yp + shift — the
 //           BatchNorm backward sums of the layer whose pre-BN output yp (M x N) this input
 //           gradient v belongs to (bn.hip bwd_partial_kernel's sums; relu' from pre > 0,
-//           tanh' = 1 - tanhf(pre)^2 recomputed as the forward computed it).
+//           tanh' = 1 - avc_tanh_fast(pre)^2 recomputed as the forward computed it).
 // Block = 64 columns x 4 waves; wave w takes rows r0 + w, r0 + w + 4, ... of the block's
 // range (the loads of 4 rows in flight per thread), the 4 waves' sums are added in wave
 // order through LDS (deterministic).
-template <int MODE>
+template <int MODE, int ACTP>
 __global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N, int splits,
                                                           const float* __restrict__ slab, float* __restrict__ C,
                                                           int64_t ldc, const float* __restrict__ bias,
                                                           const float* __restrict__ yp, const float* __restrict__ coefp,
-                                                          int actp, double* __restrict__ part) {
+                                                          double* __restrict__ part) {
   __shared__ double red[4][64][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 64 + lane;
@@ -726,8 +791,8 @@ __global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N,
         const float y = yp[i];
         const float pre = fmaf(y, a, sh);
         float g = v;
-        if (actp == 1) g = pre > 0.f ? v : 0.f;
-        else if (actp == 2) { const float z = tanhf(pre); g = v * (1.f - z * z); }
+        if (ACTP == 1) g = pre > 0.f ? v : 0.f;
+        else if (ACTP == 2) { const float z = avc_tanh_fast(pre); g = v * (1.f - z * z); }
         s1 += (double)g;
         s2 += (double)g * (double)(y - mu);
       }
@@ -906,28 +971,28 @@ constexpr unsigned bf16_lds_bytes() {
   return 2u * 2u * ((AR ? BM * (BK + 8) : BK * (BM + 32)) + (BR ? BN * (BK + 8) : BK * (BN + 32)));
 }
 
-// the fused Conv-BN stacks' bf16 GEMMs: BNOP 1 = forward conv (A = im2col of the previous
-// layer's pre-BN output, RK; B = Wf, RK), BNOP 2 = weight gradient (A = dy, CK; B = im2col
-// of that output, CK), slabs only (the reduce computes the statistics)
-template <int BM, int BN, int BK, int WM, int WN, int BNOP>
+// the fused Conv-BN stacks' bf16 GEMMs (slabs only: the reduce writes C and the statistics):
+// forward (A = im2col of the previous layer's output, RK; B = Wf, RK), input gradient (A =
+// im2col(dy), RK; B = Wd, CK), weight gradient (A = dy, CK; B = im2col(x), CK).  BNOP 1 / 2:
+// BatchNorm + activation applied on load to A / B (fp32 operand); SRC: bf16-source operands.
+template <int BM, int BN, int BK, int WM, int WN, bool AR, bool BR, int BNOP, int SRC>
 void launch_bn_bf16(dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-  constexpr bool AR = BNOP == 1, BR = BNOP == 1;
   constexpr bool DEEP = BM == 256 && !(BN == 256 && !AR && !BR);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, DEEP, BNOP>), grid, dim3(NT),
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, DEEP, BNOP, SRC>), grid, dim3(NT),
                      dyn_lds_for(bf16_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, K, oa, ob, (float*)nullptr,
                      (int64_t)N, (const float*)nullptr, (const float*)nullptr, 0, kps, slab, Batch{0, 0, 0, nullptr});
 }
 
-template <int BNOP>
+template <bool AR, bool BR, int BNOP, int SRC>
 void launch_gemm_bn_bf16(int id, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob, int kps,
                          float* slab) {
   switch (id) {
-    case 0: launch_bn_bf16<128, 128, 64, 64, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
-    case 2: launch_bn_bf16<256, 128, 64, 64, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
-    case 3: launch_bn_bf16<256, 256, 64, 128, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
-    case 4: launch_bn_bf16<256, 256, 32, 128, 64, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
-    default: launch_bn_bf16<64, 64, 64, 32, 32, BNOP>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    case 0: launch_bn_bf16<128, 128, 64, 64, 64, AR, BR, BNOP, SRC>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    case 2: launch_bn_bf16<256, 128, 64, 64, 64, AR, BR, BNOP, SRC>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    case 3: launch_bn_bf16<256, 256, 64, 128, 64, AR, BR, BNOP, SRC>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    case 4: launch_bn_bf16<256, 256, 32, 128, 64, AR, BR, BNOP, SRC>(grid, st, M, N, K, oa, ob, kps, slab); break;
+    default: launch_bn_bf16<64, 64, 64, 32, 32, AR, BR, BNOP, SRC>(grid, st, M, N, K, oa, ob, kps, slab); break;
   }
 }
 
@@ -1082,10 +1147,20 @@ extern "C" int autovc_gemm_bf16_splits(int M, int N, int K, int requested) {
 // activation of its own.
 namespace {
 struct BnPlan { GemmShape cfg; int splits; int kps; };
+// split-K of the small outputs plan_bf16 leaves to the caller (functional._splits_for's rule:
+// >= 1024 64x64 tile-splits while each keeps >= 1024 k, deep splits for < 64 tiles)
+int small_splits(int M, int N, int K) {
+  const int64_t tiles = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
+  int s = 1;
+  while (tiles * s < 1024 && K / (s + 1) >= 1024 && s < 8) ++s;
+  if (tiles < 64) s = std::max<int>(s, (int)std::min<int64_t>({64, K / 256, std::max<int64_t>(1, 1024 / tiles)}));
+  return std::max(1, s);
+}
+
 BnPlan plan_bn(int M, int N, int K) {
-  const PlanBf16 pl = plan_bf16(M, N, K, 1);
-  const GemmShape cfg = pl.cfg >= 0 ? kCfgBf16[pl.cfg] : pick_config_bf16(M, N, 1);
-  int splits = pl.cfg >= 0 ? pl.splits : 1;
+  const PlanBf16 pl = plan_bf16(M, N, K, small_splits(M, N, K));
+  int splits = pl.splits;
+  const GemmShape cfg = pl.cfg >= 0 ? kCfgBf16[pl.cfg] : pick_config_bf16(M, N, splits);
   int64_t kps = ((int64_t)K + splits - 1) / splits;
   kps = (kps + cfg.bk - 1) / cfg.bk * cfg.bk;
   splits = (int)std::max<int64_t>(1, ((int64_t)K + kps - 1) / kps);
@@ -1095,14 +1170,27 @@ constexpr int kStatsRows = 256;
 
 // bnop 0 plain / 1 forward (A with BN) / 2 weight gradient (B with BN); mode 0: plain reduce
 // (+ bias), 1 / 2: splitk_stats_kernel<mode> into part
-int bn_gemm(int bnop, int a_trans, int b_trans, int M, int N, int K, Opnd oa, Opnd ob, float* C, const float* bias,
-            int mode, const float* yp, const float* coefp, int actp, double* part, float* ws, hipStream_t st) {
+int bn_gemm(int bnop, int src, int a_trans, int b_trans, int M, int N, int K, Opnd oa, Opnd ob, float* C,
+            const float* bias, int mode, const float* yp, const float* coefp, int actp, double* part, float* ws,
+            hipStream_t st) {
   const BnPlan pl = plan_bn(M, N, K);
   const dim3 grid((N + pl.cfg.bn - 1) / pl.cfg.bn, (M + pl.cfg.bm - 1) / pl.cfg.bm, pl.splits);
   g_batch = Batch{0, 0, 0, nullptr};
-  if (bnop == 1) launch_gemm_bn_bf16<1>(pl.cfg.id, grid, st, M, N, K, oa, ob, pl.kps, ws);
-  else if (bnop == 2) launch_gemm_bn_bf16<2>(pl.cfg.id, grid, st, M, N, K, oa, ob, pl.kps, ws);
-  else launch_gemm_bf16(pl.cfg.id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, N, nullptr, nullptr, 0, pl.kps, ws);
+  const int id = pl.cfg.id;
+  // (layout, BNOP, SRC) combinations of the stacks; anything else is the plain fp32-source GEMM
+  if (!a_trans && !b_trans && bnop == 1 && src == 0) launch_gemm_bn_bf16<true, true, 1, 0>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (!a_trans && !b_trans && bnop == 0 && src == 2) launch_gemm_bn_bf16<true, true, 0, 2>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (!a_trans && !b_trans && bnop == 0 && src == 3) launch_gemm_bn_bf16<true, true, 0, 3>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (!a_trans && b_trans && bnop == 0 && src == 3) launch_gemm_bn_bf16<true, false, 0, 3>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (a_trans && b_trans && bnop == 2 && src == 0) launch_gemm_bn_bf16<false, false, 2, 0>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (a_trans && b_trans && bnop == 0 && src == 1) launch_gemm_bn_bf16<false, false, 0, 1>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (a_trans && b_trans && bnop == 0 && src == 3) launch_gemm_bn_bf16<false, false, 0, 3>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);
+  else if (bnop == 0 && src == 0)
+    launch_gemm_bf16(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, N, nullptr, nullptr, 0, pl.kps, ws);
+  else {
+    avc::set_error("autovc_bnconv: unsupported operand combination (bnop %d, src %d)", bnop, src);
+    return avc::kErrArg;
+  }
   AVC_CHECK_LAUNCH("autovc_bnconv (gemm)");
   if (mode == 0) {
     const int gx = (N + 255) / 256;
@@ -1111,12 +1199,13 @@ int bn_gemm(int bnop, int a_trans, int b_trans, int M, int N, int K, Opnd oa, Op
                        (int64_t)N, bias, nullptr, 0);
   } else {
     const dim3 g2((N + 63) / 64, (unsigned)std::min<int64_t>(kStatsRows, M));
-    if (mode == 1)
-      hipLaunchKernelGGL(splitk_stats_kernel<1>, g2, dim3(256), 0, st, (int64_t)M, (int64_t)N, pl.splits, ws, C,
-                         (int64_t)N, bias, nullptr, nullptr, 0, part);
-    else
-      hipLaunchKernelGGL(splitk_stats_kernel<2>, g2, dim3(256), 0, st, (int64_t)M, (int64_t)N, pl.splits, ws, C,
-                         (int64_t)N, nullptr, yp, coefp, actp, part);
+#define AVC_STATS(MODE, ACT) hipLaunchKernelGGL((splitk_stats_kernel<MODE, ACT>), g2, dim3(256), 0, st, (int64_t)M, \
+                                               (int64_t)N, pl.splits, ws, C, (int64_t)N, bias, yp, coefp, part)
+    if (mode == 1) AVC_STATS(1, 0);
+    else if (actp == 1) AVC_STATS(2, 1);
+    else if (actp == 2) AVC_STATS(2, 2);
+    else AVC_STATS(2, 0);
+#undef AVC_STATS
   }
   AVC_CHECK_LAUNCH("autovc_bnconv (reduce)");
   return avc::kOk;
@@ -1137,43 +1226,53 @@ extern "C" int64_t autovc_bnconv_workspace_floats(int B, int T, int Ci, int Co) 
   return std::max({(int64_t)f.splits * M * Co, (int64_t)x.splits * M * Ci, (int64_t)w.splits * Co * 5 * Ci});
 }
 
-extern "C" int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const float* x, const float* x_coef, int x_act,
-                                          const float* Wf, const float* bias, float* y, double* part,
+// src: bit 0 = the activation operand (x / dy), bit 1 = the other (W / x) is bf16 in memory
+// (2-byte elements, same strides in elements); a BN-on-load operand (x_coef) must be fp32
+bool bn_src_ok(int src, int Ci, int Co) { return src >= 0 && src <= 3 && (src == 0 || (Ci % 8 == 0 && Co % 8 == 0)); }
+
+extern "C" int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef, int x_act,
+                                          const void* Wf, const float* bias, float* y, double* part, int src,
                                           float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && x && Wf && y && part && workspace, "autovc_bnconv_fwd_bf16_f32: bad args");
   AVC_CHECK_ARG(x_act >= 0 && x_act <= 2 && AVC_ALIGNED16(x) && AVC_ALIGNED16(Wf) && (!x_coef || AVC_ALIGNED16(x_coef)),
                 "autovc_bnconv_fwd_bf16_f32: activation / alignment");
+  AVC_CHECK_ARG(bn_src_ok(src, Ci, Co) && !(x_coef && (src & 1)), "autovc_bnconv_fwd_bf16_f32: bad src %d", src);
+  AVC_CHECK_ARG(!x_coef || Ci <= kBnMaxC, "autovc_bnconv_fwd_bf16_f32: BatchNorm input channels > %d", kBnMaxC);
   const int M = B * T;
-  const Opnd oa{x, Ci, T, Ci, -2, x_coef, x_act};
-  const Opnd ob{Wf, 5 * Ci, 0, 0, 0, nullptr, 0};
-  return bn_gemm(x_coef ? 1 : 0, 0, 0, M, Co, 5 * Ci, oa, ob, y, bias, 1, nullptr, nullptr, 0, part, workspace, stream);
+  const Opnd oa{(const float*)x, Ci, T, Ci, -2, x_coef, x_act};
+  const Opnd ob{(const float*)Wf, 5 * Ci, 0, 0, 0, nullptr, 0};
+  return bn_gemm(x_coef ? 1 : 0, src, 0, 0, M, Co, 5 * Ci, oa, ob, y, bias, 1, nullptr, nullptr, 0, part, workspace,
+                 stream);
 }
 
-extern "C" int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* Wd, float* dz,
+extern "C" int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* Wd, float* dz,
                                          const float* y_prev, const float* coef_prev, int act_prev, double* part,
-                                         float* workspace, hipStream_t stream) {
+                                         int src, float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && dy && Wd && dz && workspace, "autovc_bnconv_dx_bf16_f32: bad args");
   AVC_CHECK_ARG(!y_prev || (coef_prev && part && act_prev >= 0 && act_prev <= 2),
                 "autovc_bnconv_dx_bf16_f32: the BatchNorm sums need y_prev, coef_prev, part");
   AVC_CHECK_ARG(AVC_ALIGNED16(dy) && AVC_ALIGNED16(Wd), "autovc_bnconv_dx_bf16_f32: alignment");
+  AVC_CHECK_ARG(bn_src_ok(src, Ci, Co) && (src == 0 || src == 3), "autovc_bnconv_dx_bf16_f32: bad src %d", src);
   const int M = B * T;
-  const Opnd oa{dy, Co, T, Co, -2, nullptr, 0};
-  const Opnd ob{Wd, Ci, 0, 0, 0, nullptr, 0};
-  return bn_gemm(0, 0, 1, M, Ci, 5 * Co, oa, ob, dz, nullptr, y_prev ? 2 : 0, y_prev, coef_prev, act_prev, part,
+  const Opnd oa{(const float*)dy, Co, T, Co, -2, nullptr, 0};
+  const Opnd ob{(const float*)Wd, Ci, 0, 0, 0, nullptr, 0};
+  return bn_gemm(0, src, 0, 1, M, Ci, 5 * Co, oa, ob, dz, nullptr, y_prev ? 2 : 0, y_prev, coef_prev, act_prev, part,
                  workspace, stream);
 }
 
-extern "C" int autovc_bnconv_dw_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* x,
-                                         const float* x_coef, int x_act, float* dWf, float* workspace,
+extern "C" int autovc_bnconv_dw_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* x,
+                                         const float* x_coef, int x_act, float* dWf, int src, float* workspace,
                                          hipStream_t stream) {
   AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && dy && x && dWf && workspace, "autovc_bnconv_dw_bf16_f32: bad args");
   AVC_CHECK_ARG(x_act >= 0 && x_act <= 2 && AVC_ALIGNED16(dy) && AVC_ALIGNED16(x) && (!x_coef || AVC_ALIGNED16(x_coef)),
                 "autovc_bnconv_dw_bf16_f32: activation / alignment");
+  AVC_CHECK_ARG(bn_src_ok(src, Ci, Co) && !(x_coef && (src & 2)), "autovc_bnconv_dw_bf16_f32: bad src %d", src);
+  AVC_CHECK_ARG(!x_coef || Ci <= kBnMaxC, "autovc_bnconv_dw_bf16_f32: BatchNorm input channels > %d", kBnMaxC);
   const int M = B * T;
-  const Opnd oa{dy, Co, 0, 0, 0, nullptr, 0};
-  const Opnd ob{x, Ci, T, Ci, -2, x_coef, x_act};
-  return bn_gemm(x_coef ? 2 : 0, 1, 1, Co, 5 * Ci, M, oa, ob, dWf, nullptr, 0, nullptr, nullptr, 0, nullptr, workspace,
-                 stream);
+  const Opnd oa{(const float*)dy, Co, 0, 0, 0, nullptr, 0};
+  const Opnd ob{(const float*)x, Ci, T, Ci, -2, x_coef, x_act};
+  return bn_gemm(x_coef ? 2 : 0, src, 1, 1, Co, 5 * Ci, M, oa, ob, dWf, nullptr, 0, nullptr, nullptr, 0, nullptr,
+                 workspace, stream);
 }
 
 extern "C" int autovc_gemm_set_lds_reserve(int bytes) {

@@ -73,7 +73,8 @@ __global__ void wino_weight_kernel(int Co, int Ci, const float* __restrict__ W, 
 // Every conv weight transform of a training step in one launch (blockIdx.y = job):
 // kind 0 / 1 = the Winograd W~ (forward / flipped, as wino_weight_kernel), kind 2 / 3 =
 // the im2col GEMM packs Wf[co][k*Ci + ci] / Wd[(4-k)*Co + co][ci] (elementwise.hip's
-// conv_pack_kernel layouts).  Same arithmetic per element as the single-layer kernels.
+// conv_pack_kernel layouts), kind 4 / 5 = the same packs as bf16 (the bf16 GEMMs' bf16-source
+// weight operands).  Same arithmetic per element as the single-layer kernels.
 struct WJob { const float* W; float* out; int Co, Ci, kind; };
 constexpr int kMaxWJobs = 48;
 struct WJobs { WJob j[kMaxWJobs]; };
@@ -95,8 +96,10 @@ __global__ __launch_bounds__(256) void conv_weights_batched_kernel(WJobs jobs) {
       const int64_t r = i / 5;
       const int ci = (int)(r % Ci), co = (int)(r / Ci);
       const float w = jb.W[i];
-      if (jb.kind == 2) jb.out[(int64_t)co * 5 * Ci + (int64_t)k * Ci + ci] = w;
-      else jb.out[((int64_t)(4 - k) * Co + co) * Ci + ci] = w;
+      const int64_t of = jb.kind == 2 || jb.kind == 4 ? (int64_t)co * 5 * Ci + (int64_t)k * Ci + ci
+                                                       : ((int64_t)(4 - k) * Co + co) * Ci + ci;
+      if (jb.kind <= 3) jb.out[of] = w;
+      else reinterpret_cast<__bf16*>(jb.out)[of] = (__bf16)w;   // RNE, as the GEMM's staging rounds
     }
   }
 }
@@ -517,7 +520,7 @@ extern "C" int autovc_conv_weights_batched_f32(int n, const int* kinds, const in
     int64_t most = 1;
     for (int q = 0; q < m; ++q) {
       const int j = j0 + q;
-      AVC_CHECK_ARG(kinds[j] >= 0 && kinds[j] <= 3 && Co[j] > 0 && Ci[j] > 0 && W[j] && out[j],
+      AVC_CHECK_ARG(kinds[j] >= 0 && kinds[j] <= 5 && Co[j] > 0 && Ci[j] > 0 && W[j] && out[j],
                     "autovc_conv_weights_batched_f32: bad job %d (kind %d, Co %d, Ci %d)", j, kinds[j], Co[j], Ci[j]);
       jobs.j[q] = WJob{W[j], out[j], Co[j], Ci[j], kinds[j]};
       most = std::max<int64_t>(most, (int64_t)Co[j] * Ci[j] * (kinds[j] <= 1 ? 1 : 5));

@@ -295,7 +295,12 @@ _WINO_KEEP_XT = os.environ.get("AVC_WINO_KEEP_XT", "1") != "0"
 _WSCOPE = [None]
 _WBATCH = os.environ.get("AVC_WEIGHT_BATCH", "1") != "0"
 _WSHAPE = {0: lambda Co, Ci: (8, Co, Ci), 1: lambda Co, Ci: (8, Ci, Co),
-           2: lambda Co, Ci: (Co, KS * Ci), 3: lambda Co, Ci: (KS * Co, Ci)}
+           2: lambda Co, Ci: (Co, KS * Ci), 3: lambda Co, Ci: (KS * Co, Ci),
+           4: lambda Co, Ci: (Co, KS * Ci), 5: lambda Co, Ci: (KS * Co, Ci)}   # 4 / 5: bf16 packs
+
+
+def _wdtype(kind):
+    return torch.bfloat16 if kind >= 4 else torch.float32
 
 
 @contextlib.contextmanager
@@ -334,12 +339,14 @@ def conv_weight(W, kind):
     cache = _WSCOPE[0] if _cacheable(W) else None
     if cache is not None and key in cache:
         return cache[key]
-    out = torch.empty(_WSHAPE[kind](Co, Ci), device=W.device, dtype=torch.float32)
+    out = torch.empty(_WSHAPE[kind](Co, Ci), device=W.device, dtype=_wdtype(kind))
     if kind <= 1:
         _lib.call("autovc_wino5_weights_f32", Co, Ci, W.data_ptr(), kind, out.data_ptr(), _s())
-    else:
+    elif kind <= 3:
         _lib.call("autovc_conv_pack_f32", Co, Ci, KS, W.data_ptr(), _p(out if kind == 2 else None),
                   _p(out if kind == 3 else None), _s())
+    else:
+        _run_weight_jobs([(kind, W, out)])
     if cache is not None:
         cache[key] = out
     return out
@@ -358,11 +365,18 @@ def prepare_conv_weights(convs, T, training):
         if not _cacheable(W) or W.shape[2] != KS:
             continue
         Co, Ci = W.shape[0], W.shape[1]
-        kinds = (0, 1) if _wino_ok(T, Ci, Co) else ((2, 3) if (Co % 4 == 0 and Ci % 4 == 0) else ())
+        if _wino_ok(T, Ci, Co):
+            kinds = (0, 1)
+        elif _PRECISION[0] == "bf16" and _CHAIN_BF16_MODE == 2 and Co % 8 == 0 and Ci % 8 == 0:
+            kinds = (4, 5)
+        elif Co % 4 == 0 and Ci % 4 == 0:
+            kinds = (2, 3)
+        else:
+            kinds = ()
         for kind in kinds[:2 if training else 1]:
             key = (kind, W.data_ptr(), Co, Ci)
             if key not in cache:
-                out = torch.empty(_WSHAPE[kind](Co, Ci), device=W.device, dtype=torch.float32)
+                out = torch.empty(_WSHAPE[kind](Co, Ci), device=W.device, dtype=_wdtype(kind))
                 cache[key] = out
                 jobs.append((kind, W, out))
     if jobs:
@@ -747,16 +761,21 @@ class ConvBNChainFn(torch.autograd.Function):
         return (None, dx, dres, *grads)
 
 
-_CHAIN_BF16_ON = os.environ.get("AVC_CONV_CHAIN_BF16", "0") != "0"
+# AVC_CONV_CHAIN_BF16: 0 = per-layer ConvBNActFn under bf16; 1 = the stacks with BatchNorm
+# applied while the GEMMs stage fp32 operands; 2 = the stacks on bf16 copies written by the
+# producers (BatchNorm + activation -> bf16 z, dy -> bf16, bf16 weight packs)
+_CHAIN_BF16_MODE = int(os.environ.get("AVC_CONV_CHAIN_BF16", "2"))
+_CHAIN_BF16_ON = _CHAIN_BF16_MODE != 0
 
 
 def _chain_ok_bf16(x, layers, training):
+    q = 8 if _CHAIN_BF16_MODE == 2 else 4
     if not (_CHAIN_BF16_ON and _PRECISION[0] == "bf16" and x.is_cuda and x.dim() == 3
-            and x.dtype == torch.float32 and x.shape[2] % 4 == 0):
+            and x.dtype == torch.float32 and x.shape[2] % q == 0):
         return False
     for conv, bn, _ in layers:
         if (conv.kernel_size[0] != KS or conv.padding[0] != PAD or conv.stride[0] != 1 or conv.dilation[0] != 1
-                or conv.groups != 1 or conv.out_channels % 4 or conv.in_channels % 4):
+                or conv.groups != 1 or conv.out_channels % q or conv.in_channels % q):
             return False
         if bn.training != training or not bn.track_running_stats or bn.running_mean is None or not bn.affine:
             return False
@@ -765,18 +784,22 @@ def _chain_ok_bf16(x, layers, training):
 
 class ConvBNChainBf16Fn(torch.autograd.Function):
     """The Conv-BN-act stack under precision("bf16") (BASELINE config 3), where the convs
-    are bf16 im2col GEMMs (csrc/gemm.hip "fused Conv-BN stacks (bf16)"): each layer's conv
-    GEMM reads the previous layer's PRE-BN output y and applies that layer's BatchNorm +
-    activation while staging its operand, and its split-K reduce writes y together with
-    y's BatchNorm partials; backward, the input-gradient GEMM's reduce emits the previous
-    layer's BatchNorm-backward sums, one kernel per layer turns (dz, y) into dy and the
-    conv bias partials, and the weight-gradient GEMM re-applies the forward's BatchNorm to
-    its im2col operand.  Only the stack's output is materialised.  Same apply(spec, x,
-    residual, *tensors) as ConvBNChainFn."""
+    are bf16 im2col GEMMs (csrc/gemm.hip "fused Conv-BN stacks (bf16)").  Every conv GEMM's
+    split-K reduce writes its pre-BN output y together with y's BatchNorm partials (no
+    statistics pass), the input-gradient GEMM's reduce emits the previous layer's
+    BatchNorm-backward sums, and one kernel per layer turns (dz, y) into dy and the conv
+    bias partials.  How the next GEMMs get act(BN(y)):
+      mode 1: applied while they stage y (fp32) into their bf16 LDS tiles;
+      mode 2: one pass writes a bf16 copy z = bf16(act(BN(y))) that they read as is (as
+              dy and the packed weights: bf16-source operands, half the operand bytes).
+    Only the stack's output is materialised in fp32.  Same apply(spec, x, residual,
+    *tensors) as ConvBNChainFn."""
 
     @staticmethod
     def forward(ctx, spec, x, residual, *tensors):
         training, acts, moms, epss = spec
+        mode = _CHAIN_BF16_MODE
+        h = mode == 2
         L = len(acts)
         x = x.contiguous()
         B, T, _ = x.shape
@@ -784,17 +807,22 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
         dev = x.device
         lib = _lib.load()
         RS = int(lib.autovc_bnconv_stats_rows(M))
-        ys, coefs, means, varis = [], [], [], []
+        ys, coefs, means, varis, zbs = [], [], [], [], []
         for l in range(L):
             W, b, g, be, rm, rv, nbt = tensors[7 * l:7 * l + 7]
             Co, Ci = W.shape[0], W.shape[1]
-            Wf = conv_weight(W, 2)
+            Wf = conv_weight(W, 4 if h else 2)
             y = torch.empty((B, T, Co), device=dev, dtype=torch.float32)
             part = _ws(dev, RS * Co * 16, "chain_fwd")
             ws = _ws(dev, 4 * lib.autovc_bnconv_workspace_floats(B, T, Ci, Co), "bnconv")
-            xin, xcoef, xact = (x, None, 0) if l == 0 else (ys[-1], coefs[-1], ACT[acts[l - 1]])
+            if l == 0:
+                xin, xcoef, xact, src = x, None, 0, (2 if h else 0)
+            elif h:
+                xin, xcoef, xact, src = zbs[-1], None, 0, 3
+            else:
+                xin, xcoef, xact, src = ys[-1], coefs[-1], ACT[acts[l - 1]], 0
             _lib.call("autovc_bnconv_fwd_bf16_f32", B, T, Ci, Co, xin.data_ptr(), _p(xcoef), xact, Wf.data_ptr(),
-                      _p(b), y.data_ptr(), part, ws, _s())
+                      _p(b), y.data_ptr(), part, src, ws, _s())
             coef = torch.empty((4, Co), device=dev, dtype=torch.float32)
             if training:
                 mean = torch.empty(Co, device=dev, dtype=torch.float32)
@@ -805,6 +833,11 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                 mean, var = rm, rv
                 _lib.call("autovc_bn_coef_f32", Co, rm.data_ptr(), rv.data_ptr(), _p(g), _p(be), float(epss[l]),
                           coef.data_ptr(), _s())
+            if h and l < L - 1:
+                zb = torch.empty((B, T, Co), device=dev, dtype=torch.bfloat16)
+                _lib.call("autovc_bn_apply_bf16", M, Co, y.data_ptr(), coef.data_ptr(), ACT[acts[l]], zb.data_ptr(),
+                          _s())
+                zbs.append(zb)
             ys.append(y)
             coefs.append(coef)
             means.append(mean)
@@ -816,8 +849,8 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
         _lib.call("autovc_bn_act_fwd_f32", M, C, ys[-1].data_ptr(), C, means[-1].data_ptr(), varis[-1].data_ptr(),
                   _p(g), _p(be), float(epss[-1]), ACT[acts[-1]], _p(res), C, z.data_ptr(), C, _s())
         if training:
-            ctx.spec = spec
-            ctx.ys, ctx.coefs, ctx.means, ctx.varis = ys, coefs, means, varis
+            ctx.spec, ctx.mode = spec, mode
+            ctx.ys, ctx.coefs, ctx.means, ctx.varis, ctx.zbs = ys, coefs, means, varis, zbs
             ctx.x = x
             ctx.z = z if acts[-1] != "none" else None
             ctx.has_res = residual is not None
@@ -831,9 +864,10 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
         if ctx.spec is None:
             raise NotImplementedError("autovc_amd: backward through eval-mode BatchNorm is not supported")
         training, acts, moms, epss = ctx.spec
+        h = ctx.mode == 2
         L = len(acts)
         needs = ctx.needs_input_grad
-        x, ys, coefs, means, varis = ctx.x, ctx.ys, ctx.coefs, ctx.means, ctx.varis
+        x, ys, coefs, means, varis, zbs = ctx.x, ctx.ys, ctx.coefs, ctx.means, ctx.varis, ctx.zbs
         tensors = ctx.params
         B, T, _ = x.shape
         M = B * T
@@ -869,42 +903,48 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                 grads[7 * l + 2] = gg.result()
             if gb is not None:
                 grads[7 * l + 3] = gb.result()
-            dy = torch.empty((B, T, Co), device=dev, dtype=torch.float32)
+            dy = torch.empty((B, T, Co), device=dev, dtype=torch.bfloat16 if h else torch.float32)
             bpart = _ws(dev, PR * Co * 8, "chain_bias")
             _lib.call("autovc_bn_dy_f32", M, Co, dz.data_ptr(), y.data_ptr(), coefs[l].data_ptr(), ACT[acts[l]], sums,
-                      dy.data_ptr(), bpart, _s())
+                      0 if h else dy.data_ptr(), dy.data_ptr() if h else 0, bpart, _s())
             if b is not None and needs[3 + 7 * l + 1]:
                 go = _GradOut(b, (Co,), dev)
                 _lib.call("autovc_colsum_f64_finalize_f32", PR, Co, bpart, go.buf.data_ptr(), int(go.acc), _s())
                 grads[7 * l + 1] = go.result()
-            xin, xcoef, xact = (x, None, 0) if l == 0 else (ys[l - 1], coefs[l - 1], ACT[acts[l - 1]])
+            if l == 0:
+                xin, xcoef, xact, wsrc = x, None, 0, (1 if h else 0)
+            elif h:
+                xin, xcoef, xact, wsrc = zbs[l - 1], None, 0, 3
+            else:
+                xin, xcoef, xact, wsrc = ys[l - 1], coefs[l - 1], ACT[acts[l - 1]], 0
             if needs[3 + 7 * l]:
                 go = _GradOut(W, (Co, Ci, KS), dev)
 
-                def dw(go=go, dy=dy, xin=xin, xcoef=xcoef, xact=xact, Co=Co, Ci=Ci):
+                def dw(go=go, dy=dy, xin=xin, xcoef=xcoef, xact=xact, wsrc=wsrc, Co=Co, Ci=Ci):
                     dWf = torch.empty((Co, KS * Ci), device=dev, dtype=torch.float32)
                     ws = _ws(dev, 4 * _lib.load().autovc_bnconv_workspace_floats(B, T, Ci, Co), "bnconv")
                     _lib.call("autovc_bnconv_dw_bf16_f32", B, T, Co, Ci, dy.data_ptr(), xin.data_ptr(), _p(xcoef),
-                              xact, dWf.data_ptr(), ws, _s())
+                              xact, dWf.data_ptr(), wsrc, ws, _s())
                     _lib.call("autovc_conv_unpack_grad_f32", Co, Ci, KS, dWf.data_ptr(), go.buf.data_ptr(),
                               int(go.acc), _s())
                 _grad_launch(dev, go.acc, dw, dy, xin, xcoef)
                 grads[7 * l] = go.result()
             if l > 0 or needs[1]:
-                Wd = conv_weight(W, 3)
+                Wd = conv_weight(W, 5 if h else 3)
                 dzp = torch.empty((B, T, Ci), device=dev, dtype=torch.float32)
                 ws = _ws(dev, 4 * lib.autovc_bnconv_workspace_floats(B, T, Ci, Co), "bnconv")
+                src = 3 if h else 0
                 if l > 0:
                     rows = RS
                     part = _ws(dev, max(PR, RS) * Ci * 16, "chain_bwd")
                     _lib.call("autovc_bnconv_dx_bf16_f32", B, T, Co, Ci, dy.data_ptr(), Wd.data_ptr(), dzp.data_ptr(),
-                              ys[l - 1].data_ptr(), coefs[l - 1].data_ptr(), ACT[acts[l - 1]], part, ws, _s())
+                              ys[l - 1].data_ptr(), coefs[l - 1].data_ptr(), ACT[acts[l - 1]], part, src, ws, _s())
                     dz = dzp
                 else:
                     _lib.call("autovc_bnconv_dx_bf16_f32", B, T, Co, Ci, dy.data_ptr(), Wd.data_ptr(), dzp.data_ptr(),
-                              0, 0, 0, 0, ws, _s())
+                              0, 0, 0, 0, src, ws, _s())
                     dx = dzp
-        ctx.ys = ctx.coefs = None
+        ctx.ys = ctx.coefs = ctx.zbs = None
         return (None, dx, dres, *grads)
 
 

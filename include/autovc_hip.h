@@ -134,7 +134,8 @@ int autovc_gemm_batched_f32(int batch, int M, int N, int K, const float* A, int6
 int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip, float* out, hipStream_t stream);
 /* Every conv weight transform of a training step in one launch: job j turns W[j] (Co[j],
  * Ci[j], 5) into out[j] by kinds[j]: 0 / 1 = autovc_wino5_weights_f32 with flip 0 / 1,
- * 2 / 3 = autovc_conv_pack_f32's Wf / Wd.  Host arrays of n entries.  Replaces the
+ * 2 / 3 = autovc_conv_pack_f32's Wf / Wd, 4 / 5 = the same packs as bf16 (RNE).  Host arrays
+ * of n entries.  Replaces the
  * per-layer transforms of the ConvNorm calls (model_vc_mel.py:20-38) in one Solver step. */
 int autovc_conv_weights_batched_f32(int n, const int* kinds, const int* Co, const int* Ci,
                                     const float* const* W, float* const* out, hipStream_t stream);
@@ -228,19 +229,27 @@ int autovc_colsum_f64_finalize_f32(int RS, int C, const double* part, float* out
  *   autovc_bn_dy_f32: dy (M, C) of a layer from (dz, y, coef, sums) — BatchNorm and
  *        activation backward — and its conv bias partials (autovc_bn_partial_rows(M) x C
  *        doubles, for autovc_colsum_f64_finalize_f32).
+ * src: bit 0 = the activation operand (x / dy), bit 1 = the other (Wf / Wd / x) is a bf16
+ * copy in memory (2-byte elements; Ci, Co % 8 == 0): the producers' bf16 copies
+ * (autovc_bn_apply_bf16, autovc_bn_dy_f32's dy_bf16, kind 4 / 5 weight packs) are staged as
+ * they are.  A BatchNorm-on-load operand (x_coef) is fp32.  dx: src 0 or 3.
  * workspace: autovc_bnconv_workspace_floats(B, T, Ci, Co) floats (split-K slabs). */
 int autovc_bnconv_stats_rows(int64_t M);
 int64_t autovc_bnconv_workspace_floats(int B, int T, int Ci, int Co);
-int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const float* x, const float* x_coef, int x_act,
-                               const float* Wf, const float* bias, float* y, double* part, float* workspace,
+int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef, int x_act,
+                               const void* Wf, const float* bias, float* y, double* part, int src, float* workspace,
                                hipStream_t stream);
-int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* Wd, float* dz,
-                              const float* y_prev, const float* coef_prev, int act_prev, double* part,
+int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* Wd, float* dz,
+                              const float* y_prev, const float* coef_prev, int act_prev, double* part, int src,
                               float* workspace, hipStream_t stream);
-int autovc_bnconv_dw_bf16_f32(int B, int T, int Co, int Ci, const float* dy, const float* x, const float* x_coef,
-                              int x_act, float* dWf, float* workspace, hipStream_t stream);
+int autovc_bnconv_dw_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* x, const float* x_coef,
+                              int x_act, float* dWf, int src, float* workspace, hipStream_t stream);
 int autovc_bn_dy_f32(int64_t M, int C, const float* dz, const float* y, const float* coef, int act,
-                     const float* sums, float* dy, double* bias_part, hipStream_t stream);
+                     const float* sums, float* dy, void* dy_bf16, double* bias_part, hipStream_t stream);
+/* z (M, C) bf16 = act(y * alpha + shift): the bf16 copy of a stack layer's output read by
+ * the next layer's bf16-source GEMMs (C % 4 == 0). */
+int autovc_bn_apply_bf16(int64_t M, int C, const float* y, const float* coef, int act, void* z,
+                         hipStream_t stream);
 
 /* ---------------------------------------------------------------- LSTM recurrences
  * Replaces the cuDNN/mkldnn recurrence of nn.LSTM (model_vc_mel.py:61,90,104).

@@ -100,14 +100,15 @@ def test_chain_eval_mode_matches_per_layer_path(cuda):
 
 
 def _run_prec(layers, x, dz, residual, precision, chain_bf16, training=True):
+    """chain_bf16: 0 = per-layer bf16 path, 1 / 2 = ConvBNChainBf16Fn mode 1 / 2."""
     from autovc_amd import functional as AF
-    prev = AF._CHAIN_BF16_ON
-    AF._CHAIN_BF16_ON = chain_bf16
+    prev = AF._CHAIN_BF16_ON, AF._CHAIN_BF16_MODE
+    AF._CHAIN_BF16_ON, AF._CHAIN_BF16_MODE = bool(chain_bf16), int(chain_bf16)
     try:
         with AF.precision(precision):
             return _run(layers, x, dz, residual, chain=True, training=training)
     finally:
-        AF._CHAIN_BF16_ON = prev
+        AF._CHAIN_BF16_ON, AF._CHAIN_BF16_MODE = prev
 
 
 @pytest.mark.parametrize("name,chans,acts,res", [
@@ -115,7 +116,8 @@ def _run_prec(layers, x, dz, residual, precision, chain_bf16, training=True):
     ("postnet", [80, 512, 512, 512, 512, 80], ["tanh"] * 4 + ["none"], True),
 ])
 @pytest.mark.parametrize("B,T", [(2, 64), (8, 128), (64, 128)])
-def test_bf16_chain_as_accurate_as_per_layer_bf16(cuda, name, chans, acts, res, B, T):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_bf16_chain_as_accurate_as_per_layer_bf16(cuda, name, chans, acts, res, B, T, mode):
     """ConvBNChainBf16Fn (BatchNorm + activation applied while the bf16 conv GEMM stages its
     operand, statistics from the split-K reduce, BN backward sums from the input-gradient
     GEMM's reduce) against the fp32 per-layer path: its error is that of the per-layer bf16
@@ -128,9 +130,9 @@ def test_bf16_chain_as_accurate_as_per_layer_bf16(cuda, name, chans, acts, res, 
     residual = torch.randn(B, T, chans[-1], generator=g).to(cuda) if res else None
     layers = _stack(chans, acts, seed=3)
     ref, gref, sref = _run(copy.deepcopy(layers), x, dz, residual, chain=False)        # fp32 per layer
-    o1, g1, s1 = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", True)       # bf16 chain
-    o0, g0, s0 = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", False)      # bf16 per layer
-    o2, _, _ = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", True)
+    o1, g1, s1 = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", mode)       # bf16 chain
+    o0, g0, s0 = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", 0)          # bf16 per layer
+    o2, _, _ = _run_prec(copy.deepcopy(layers), x, dz, residual, "bf16", mode)
     assert torch.equal(o1, o2)
     e1, e0 = _rel(o1, ref), _rel(o0, ref)
     assert e1 < 1e-2 and e1 < 1.5 * e0 + 1e-4, (e1, e0)
@@ -147,7 +149,8 @@ def test_bf16_chain_as_accurate_as_per_layer_bf16(cuda, name, chans, acts, res, 
         assert _rel(m1, mr) < 1.5 * _rel(m0, mr) + 1e-4 and _rel(v1, vr) < 1.5 * _rel(v0, vr) + 1e-4
 
 
-def test_bf16_chain_eval_mode(cuda):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_bf16_chain_eval_mode(cuda, mode):
     import copy
     g = torch.Generator().manual_seed(2)
     layers = _stack([80, 512, 512, 80], ["tanh", "tanh", "none"], seed=4)
@@ -157,6 +160,6 @@ def test_bf16_chain_eval_mode(cuda):
     x = torch.randn(4, 64, 80, generator=g).to(cuda)
     with torch.no_grad():
         ref, _, _ = _run(copy.deepcopy(layers), x, None, x, chain=False, training=False)
-        o1, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", True, training=False)
-        o0, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", False, training=False)
+        o1, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", mode, training=False)
+        o0, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", 0, training=False)
     assert _rel(o1, ref) < 1.5 * _rel(o0, ref) + 1e-4

@@ -184,30 +184,31 @@ def test_batched_weight_transforms_bit_identical(cuda):
     jobs, refs = [], []
     for Co, Ci in shapes:
         W = torch.randn(Co, Ci, 5, generator=g).to(cuda)
-        for kind in range(4):
-            out = torch.empty(AF._WSHAPE[kind](Co, Ci), device=cuda)
+        for kind in range(6):
+            out = torch.empty(AF._WSHAPE[kind](Co, Ci), device=cuda, dtype=AF._wdtype(kind))
             jobs.append((kind, W, out))
-            ref = torch.empty_like(out)
+            ref = torch.empty(AF._WSHAPE[kind](Co, Ci), device=cuda)
             if kind <= 1:
                 _lib.call("autovc_wino5_weights_f32", Co, Ci, W.data_ptr(), kind, ref.data_ptr(), AF._s())
             else:
-                _lib.call("autovc_conv_pack_f32", Co, Ci, 5, W.data_ptr(), ref.data_ptr() if kind == 2 else 0,
-                          ref.data_ptr() if kind == 3 else 0, AF._s())
-            refs.append(ref)
+                _lib.call("autovc_conv_pack_f32", Co, Ci, 5, W.data_ptr(), ref.data_ptr() if kind % 2 == 0 else 0,
+                          ref.data_ptr() if kind % 2 == 1 else 0, AF._s())
+            refs.append(ref.to(AF._wdtype(kind)))   # kinds 4 / 5: the RNE bf16 of the fp32 pack
     AF._run_weight_jobs(jobs)
     torch.cuda.synchronize()
     for (kind, _, out), ref in zip(jobs, refs):
         assert torch.equal(out, ref), kind
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_weight_scope_step_bit_identical(cuda, precision):
+@pytest.mark.parametrize("precision,chain", [("fp32", 0), ("bf16", 0), ("bf16", 2)])
+def test_weight_scope_step_bit_identical(cuda, precision, chain):
     """The step-scoped weight transforms (computed once per step, in one launch) leave two
     Solver steps bit-identical to per-layer transforms (AVC_WEIGHT_BATCH=0)."""
     import bench
     from autovc_amd import functional as AF
     res = []
-    prev = AF._WBATCH
+    prev = AF._WBATCH, AF._CHAIN_BF16_ON, AF._CHAIN_BF16_MODE
+    AF._CHAIN_BF16_ON, AF._CHAIN_BF16_MODE = bool(chain), chain
     try:
         for on in (True, False):
             AF._WBATCH = on
@@ -222,7 +223,7 @@ def test_weight_scope_step_bit_identical(cuda, precision):
             res.append((losses, [f.clone() for f in solver.g_optimizer.flat_params()]))
             del solver
     finally:
-        AF._WBATCH = prev
+        AF._WBATCH, AF._CHAIN_BF16_ON, AF._CHAIN_BF16_MODE = prev
     (la, pa), (lb, pb) = res
     for a, b in zip(la, lb):
         assert torch.equal(a, b)
