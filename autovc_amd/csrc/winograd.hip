@@ -79,10 +79,42 @@ struct WJob { const float* W; float* out; int Co, Ci, kind; };
 constexpr int kMaxWJobs = 48;
 struct WJobs { WJob j[kMaxWJobs]; };
 
+// kinds 6 / 7 / 8 take W as an (Co rows x Ci cols) matrix (the LSTM weights, model_vc_mel.py
+// :90,104): 6 = its RNE bf16 copy, 7 = its fp32 transpose (Ci x Co), 8 = the bf16 transpose
+// (32 x 32 LDS tiles, grid-stride over the tiles: the trip count is uniform per block).
 __global__ __launch_bounds__(256) void conv_weights_batched_kernel(WJobs jobs) {
+  __shared__ float tile[32][33];
   const WJob jb = jobs.j[blockIdx.y];
   const int Co = jb.Co, Ci = jb.Ci;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (jb.kind == 6) {
+    const int64_t n = (int64_t)Co * Ci;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+      reinterpret_cast<__bf16*>(jb.out)[i] = (__bf16)jb.W[i];
+    return;
+  }
+  if (jb.kind >= 7) {
+    const int R = Co, C = Ci, tc = (C + 31) / 32;
+    const int64_t ntiles = (int64_t)tc * ((R + 31) / 32);
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+      const int c0 = (int)(t % tc) * 32, r0 = (int)(t / tc) * 32;
+      for (int k = ty; k < 32; k += 8) {
+        const int r = r0 + k, c = c0 + tx;
+        if (r < R && c < C) tile[k][tx] = jb.W[(int64_t)r * C + c];
+      }
+      __syncthreads();
+      for (int k = ty; k < 32; k += 8) {
+        const int c = c0 + k, r = r0 + tx;
+        if (r < R && c < C) {
+          if (jb.kind == 7) jb.out[(int64_t)c * R + r] = tile[tx][k];
+          else reinterpret_cast<__bf16*>(jb.out)[(int64_t)c * R + r] = (__bf16)tile[tx][k];
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
   if (jb.kind <= 1) {
     const int flip = jb.kind;
     const int R = flip ? Ci : Co, Cc = flip ? Co : Ci;
@@ -520,10 +552,14 @@ extern "C" int autovc_conv_weights_batched_f32(int n, const int* kinds, const in
     int64_t most = 1;
     for (int q = 0; q < m; ++q) {
       const int j = j0 + q;
-      AVC_CHECK_ARG(kinds[j] >= 0 && kinds[j] <= 5 && Co[j] > 0 && Ci[j] > 0 && W[j] && out[j],
+      AVC_CHECK_ARG(kinds[j] >= 0 && kinds[j] <= 8 && Co[j] > 0 && Ci[j] > 0 && W[j] && out[j],
                     "autovc_conv_weights_batched_f32: bad job %d (kind %d, Co %d, Ci %d)", j, kinds[j], Co[j], Ci[j]);
       jobs.j[q] = WJob{W[j], out[j], Co[j], Ci[j], kinds[j]};
-      most = std::max<int64_t>(most, (int64_t)Co[j] * Ci[j] * (kinds[j] <= 1 ? 1 : 5));
+      const int64_t work = kinds[j] <= 1 ? (int64_t)Co[j] * Ci[j]
+                         : kinds[j] <= 5 ? (int64_t)Co[j] * Ci[j] * 5
+                         : kinds[j] == 6 ? (int64_t)Co[j] * Ci[j]
+                                         : 256 * (int64_t)((Co[j] + 31) / 32) * ((Ci[j] + 31) / 32);   // a block per tile
+      most = std::max<int64_t>(most, work);
     }
     hipLaunchKernelGGL(conv_weights_batched_kernel, dim3((unsigned)std::min<int64_t>((most + 255) / 256, 1024), m),
                        dim3(256), 0, stream, jobs);

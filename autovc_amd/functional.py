@@ -296,11 +296,13 @@ _WSCOPE = [None]
 _WBATCH = os.environ.get("AVC_WEIGHT_BATCH", "1") != "0"
 _WSHAPE = {0: lambda Co, Ci: (8, Co, Ci), 1: lambda Co, Ci: (8, Ci, Co),
            2: lambda Co, Ci: (Co, KS * Ci), 3: lambda Co, Ci: (KS * Co, Ci),
-           4: lambda Co, Ci: (Co, KS * Ci), 5: lambda Co, Ci: (KS * Co, Ci)}   # 4 / 5: bf16 packs
+           4: lambda Co, Ci: (Co, KS * Ci), 5: lambda Co, Ci: (KS * Co, Ci),   # 4 / 5: bf16 packs
+           # 2-D (LSTM) weights (R, C): 6 = bf16 copy, 7 = fp32 transpose, 8 = bf16 transpose
+           6: lambda R, C: (R, C), 7: lambda R, C: (C, R), 8: lambda R, C: (C, R)}
 
 
 def _wdtype(kind):
-    return torch.bfloat16 if kind >= 4 else torch.float32
+    return torch.float32 if kind in (0, 1, 2, 3, 7) else torch.bfloat16
 
 
 @contextlib.contextmanager
@@ -346,20 +348,40 @@ def conv_weight(W, kind):
         _lib.call("autovc_conv_pack_f32", Co, Ci, KS, W.data_ptr(), _p(out if kind == 2 else None),
                   _p(out if kind == 3 else None), _s())
     else:
-        _run_weight_jobs([(kind, W, out)])
+        _run_weight_jobs([(kind, W.contiguous(), out)])
     if cache is not None:
         cache[key] = out
     return out
 
 
-def prepare_conv_weights(convs, T, training):
+def prepare_weights(convs, lstms, T, training):
     """Inside a weight_scope: compute, in one launch, every transform the ConvNorm layers
     `convs` (nn.Conv1d, k=5) will use for sequences of T frames — the Winograd pair for
-    fp32 Winograd shapes, else the im2col packs — and cache them for the scope."""
+    fp32 Winograd shapes, else the im2col packs — and the large-H LSTMs `lstms` (model_vc_mel
+    LSTM modules) their recurrences use — bf16 copies of the recurrent weights under bf16,
+    the transposes the backward reads — and cache them for the scope."""
     cache = _WSCOPE[0]
     if cache is None:
         return
     jobs = []
+
+    def add(kind, W):
+        key = (kind, W.data_ptr(), W.shape[0], W.shape[1])
+        if key not in cache:
+            out = torch.empty(_WSHAPE[kind](W.shape[0], W.shape[1]), device=W.device, dtype=_wdtype(kind))
+            cache[key] = out
+            jobs.append((kind, W, out))
+
+    for m in lstms:
+        H = m.hidden_size
+        if m.bidirectional or m.num_layers not in (1, 2) or H < 256:
+            continue
+        mats = [m.weight_hh_l0] if m.num_layers == 1 else [m.weight_hh_l0, m.weight_ih_l1, m.weight_hh_l1]
+        kinds = ((6, 8) if training else (6,)) if _bf16_rec(H) else ((7,) if training else ())
+        for W in mats:
+            if _cacheable(W):
+                for kind in kinds:
+                    add(kind, W)
     for conv in convs:
         W = conv.weight
         if not _cacheable(W) or W.shape[2] != KS:
@@ -374,13 +396,13 @@ def prepare_conv_weights(convs, T, training):
         else:
             kinds = ()
         for kind in kinds[:2 if training else 1]:
-            key = (kind, W.data_ptr(), Co, Ci)
-            if key not in cache:
-                out = torch.empty(_WSHAPE[kind](Co, Ci), device=W.device, dtype=_wdtype(kind))
-                cache[key] = out
-                jobs.append((kind, W, out))
+            add(kind, W)
     if jobs:
         _run_weight_jobs(jobs)
+
+
+def prepare_conv_weights(convs, T, training):
+    prepare_weights(convs, [], T, training)
 
 
 def _wino_conv(x, Wp, bias, T, flip, keep_xt=False):
@@ -1077,13 +1099,13 @@ class LSTMLayerFn(torch.autograd.Function):
         c = torch.empty((B, T, H), device=dev, dtype=torch.float32)
         gates = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
         if _bf16_rec(H) and lstm_xcd(B, H):
-            Wb = _bf(W_hh)
+            Wb = conv_weight(W_hh, 6)
             ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmx")
             _lib.call("autovc_lstm_fwd_xcd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),
                       h.data_ptr(), T * H, H, c.data_ptr(), _p(gates), ws, _s())
         elif _bf16_rec(H):
             hb = torch.empty((B, T, H), device=dev, dtype=torch.bfloat16)
-            Wb = _bf(W_hh)   # held until the launches are enqueued (stream-ordered reuse after)
+            Wb = conv_weight(W_hh, 6)   # held until the launches are enqueued (stream-ordered reuse after)
             _lib.call("autovc_lstm_fwd_bf16", B, T, H, gx.data_ptr(), T * 4 * H, 4 * H, Wb.data_ptr(),
                       h.data_ptr(), hb.data_ptr(), c.data_ptr(), _p(gates), 0, _s())
         elif lstm_xcd(B, H):
@@ -1112,11 +1134,6 @@ def _bf16_rec(H):
     return _PRECISION[0] == "bf16" and H % 128 == 0
 
 
-def _bf(t):
-    """RNE bf16 copy (contiguous) of an fp32 weight for the bf16 recurrences."""
-    return t.detach().contiguous().to(torch.bfloat16)
-
-
 def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     """BPTT of one large-H layer: recurrence (C-ABI), weight/bias gradients straight into
     the flat gradient buffer where the optimizer owns one, dx.  Returns (dx, dW_ih, dW_hh,
@@ -1140,8 +1157,8 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
         elif _XCD_FLUSH == "after":
             _flush_grad_queue()
         return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs)
-    WT = torch.empty((H, 4 * H), device=dev, dtype=torch.float32)
-    _lib.call("autovc_transpose_f32", 4 * H, H, W_hh.data_ptr(), WT.data_ptr(), _s())
+    # W_hh^T (fp32, or its bf16 copy under bf16): from the step's weight scope when there is one
+    WT = conv_weight(W_hh, 8 if _bf16_rec(H) else 7)
     # split-K of the recurrent product (same box, alternating): fp32 4 ways at H=1024 (256
     # workgroups; 8 ways: +0.1 ms/step), 8 ways at H=512 (fills the chip: -0.15 ms); bf16
     # 8 ways everywhere (half the bytes per workgroup: -0.15 ms).  AVC_LSTM_SPLITS overrides.
@@ -1155,9 +1172,8 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     mark = _grad_mark(dev)   # queued weight gradients run beside this latency-bound recurrence
     if _bf16_rec(H):
         dGb = torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16)
-        WTb = _bf(WT)
         _lib.call("autovc_lstm_bwd_bf16", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
-                  WTb.data_ptr(), dG.data_ptr(), dGb.data_ptr(), 0, splits, ws, _s())
+                  WT.data_ptr(), dG.data_ptr(), dGb.data_ptr(), 0, splits, ws, _s())
     else:
         _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
                   WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
@@ -1281,7 +1297,7 @@ class LSTM2StackFn(torch.autograd.Function):
             h0b, h1b = (torch.empty((B, T, H), device=dev, dtype=torch.bfloat16) for _ in range(2))
             # the bf16 weight copies must be alive together (a temporary's block would be
             # reused by the next conversion before the launches read it)
-            W0b, Wi1b, W1b = _bf(W_hh0), _bf(W_ih1), _bf(W_hh1)
+            W0b, Wi1b, W1b = conv_weight(W_hh0, 6), conv_weight(W_ih1, 6), conv_weight(W_hh1, 6)
             if lstm2_persistent(B, H):
                 ws = _ws(dev, _lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), "lstm2p")
                 _lib.call("autovc_lstm2_fwd_persist_bf16", B, T, H, gx0.data_ptr(), T * 4 * H, 4 * H,
@@ -1332,9 +1348,9 @@ class LSTM2StackFn(torch.autograd.Function):
         B, T, _ = x.shape
         H = W_hh0.shape[1]
         dev = x.device
-        WT1, WIT1, WT0 = (torch.empty((H, 4 * H), device=dev, dtype=torch.float32) for _ in range(3))
-        for W, WT in ((W_hh1, WT1), (W_ih1, WIT1), (W_hh0, WT0)):
-            _lib.call("autovc_transpose_f32", 4 * H, H, W.data_ptr(), WT.data_ptr(), _s())
+        # the (H, 4H) transposes (bf16 copies under bf16), from the step's weight scope if any
+        kt = 8 if _bf16_rec(H) else 7
+        WT1, WIT1, WT0 = conv_weight(W_hh1, kt), conv_weight(W_ih1, kt), conv_weight(W_hh0, kt)
         # the stacked backward kernel is built for split-K 2 or 4 only (autovc_lstm2_bwd_f32)
         splits = 4 if int(os.environ.get("AVC_LSTM2_SPLITS", "4")) >= 4 else 2
         if (4 * H) % (64 * splits):
@@ -1344,10 +1360,9 @@ class LSTM2StackFn(torch.autograd.Function):
         dG0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         mark = _grad_mark(dev)   # queued weight gradients run beside the recurrences
         if _bf16_rec(H):
-            WTb = [_bf(w) for w in (WT1, WIT1, WT0)]   # alive together until the launches are queued
             dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
             _lib.call("autovc_lstm2_bwd_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                      g0.data_ptr(), c0.data_ptr(), WTb[0].data_ptr(), WTb[1].data_ptr(), WTb[2].data_ptr(),
+                      g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(),
                       dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), splits, ws, _s())
         else:
             _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),

@@ -208,8 +208,9 @@ class Generator(nn.Module):
 
     def forward(self, x, c_org, c_trg):
         if x.is_cuda:   # inside the Solver's weight scope: all weight transforms in one launch
-            AF.prepare_conv_weights(self.conv_layers() if c_trg is not None else
-                                    [c[0].conv for c in self.encoder.convolutions], x.shape[-2], self.training)
+            full = c_trg is not None
+            AF.prepare_weights(self.conv_layers() if full else [c[0].conv for c in self.encoder.convolutions],
+                               [self.decoder.lstm1, self.decoder.lstm2] if full else [], x.shape[-2], self.training)
         code_real = self.encoder.encode(x, c_org)                       # :182
         if c_trg is None:
             return code_real                                            # :183-184

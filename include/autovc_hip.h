@@ -134,8 +134,9 @@ int autovc_gemm_batched_f32(int batch, int M, int N, int K, const float* A, int6
 int autovc_wino5_weights_f32(int Co, int Ci, const float* W, int flip, float* out, hipStream_t stream);
 /* Every conv weight transform of a training step in one launch: job j turns W[j] (Co[j],
  * Ci[j], 5) into out[j] by kinds[j]: 0 / 1 = autovc_wino5_weights_f32 with flip 0 / 1,
- * 2 / 3 = autovc_conv_pack_f32's Wf / Wd, 4 / 5 = the same packs as bf16 (RNE).  Host arrays
- * of n entries.  Replaces the
+ * 2 / 3 = autovc_conv_pack_f32's Wf / Wd, 4 / 5 = the same packs as bf16 (RNE); for a 2-D
+ * W (Co rows x Ci cols: the LSTM weights) 6 = its bf16 copy, 7 = its transpose (Ci x Co, as
+ * autovc_transpose_f32), 8 = the bf16 transpose.  Host arrays of n entries.  Replaces the
  * per-layer transforms of the ConvNorm calls (model_vc_mel.py:20-38) in one Solver step. */
 int autovc_conv_weights_batched_f32(int n, const int* kinds, const int* Co, const int* Ci,
                                     const float* const* W, float* const* out, hipStream_t stream);

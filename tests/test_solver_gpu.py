@@ -173,9 +173,10 @@ def og_build_eval(cuda):
 
 
 def test_batched_weight_transforms_bit_identical(cuda):
-    """autovc_conv_weights_batched_f32 (every conv weight transform of a step in one launch)
-    equals the per-layer kernels element for element, for all four kinds and the Generator's
-    channel shapes."""
+    """autovc_conv_weights_batched_f32 (every weight transform of a step in one launch)
+    equals the per-layer kernels / torch element for element: Winograd pairs, im2col packs
+    (fp32 and bf16) at the Generator's channel shapes, and the LSTM weights' bf16 copies and
+    transposes."""
     import ctypes  # noqa: F401
     from autovc_amd import _lib
     from autovc_amd import functional as AF
@@ -194,6 +195,11 @@ def test_batched_weight_transforms_bit_identical(cuda):
                 _lib.call("autovc_conv_pack_f32", Co, Ci, 5, W.data_ptr(), ref.data_ptr() if kind % 2 == 0 else 0,
                           ref.data_ptr() if kind % 2 == 1 else 0, AF._s())
             refs.append(ref.to(AF._wdtype(kind)))   # kinds 4 / 5: the RNE bf16 of the fp32 pack
+    for R, C in [(4096, 1024), (2048, 512), (100, 36)]:   # LSTM weights: bf16 copy, transposes
+        W = torch.randn(R, C, generator=g).to(cuda)
+        for kind, ref in ((6, W.to(torch.bfloat16)), (7, W.t().contiguous()), (8, W.t().contiguous().to(torch.bfloat16))):
+            jobs.append((kind, W, torch.empty(AF._WSHAPE[kind](R, C), device=cuda, dtype=AF._wdtype(kind))))
+            refs.append(ref)
     AF._run_weight_jobs(jobs)
     torch.cuda.synchronize()
     for (kind, _, out), ref in zip(jobs, refs):
