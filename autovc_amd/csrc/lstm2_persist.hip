@@ -661,6 +661,14 @@ constexpr int XC_PAD_LDS = 96 * 1024;  // dynamic LDS that keeps one workgroup p
 #ifndef XCD_DIRECT
 #define XCD_DIRECT 0
 #endif
+// 1: fp32 products on v_mfma_f32_4x4x1_16b_f32: the group's 8 batch rows fill all 16 blocks
+// (4 column groups x 2 row groups x 2 halves of K), where the 16x16x4 form computes 16 batch
+// lanes of which 8 are real — half the MFMA cycles, the W fragments in 256 registers.  Measured
+// 3.90 vs 3.85 us per step and 15.38-15.46 vs 15.44-15.46 ms per training step
+// (profiles/r03/ab_xcd_mf4.txt): the products are not what bounds the step; diagnostic build.
+#ifndef XCD_MF4
+#define XCD_MF4 0
+#endif
 #if XCD_STAMP
 constexpr int kXS = 16, kXP = 8;
 __device__ unsigned long long g_xcd_stamp[XNX * XSL * kXS * kXP];
@@ -741,9 +749,23 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
     return;
   }
   // W fragments: wave = gate, lane -> column u0 + lane % 16, k = 128 (lane / 16) + q
-  float wf[BF ? 1 : KG];
+  constexpr bool MF4 = !BF && XCD_MF4 && !XCD_DIRECT;
+  constexpr int KH = HH / 2;             // 4x4x1 form: k per half
+  float wf[BF || MF4 ? 1 : KG];
   bf16x8 wb[BF ? KG / 8 : 1];
-  if constexpr (BF) {
+  // 4x4x1 form: lane 4 b + i, block b = (column group cg = b & 3, row group rg = (b >> 2) & 1,
+  // K half kh = b >> 3): A = W[gate][u0 + 4 cg + i][kh KH + s], B = h[4 rg + i][kh KH + s]
+  [[maybe_unused]] const int m4b = lane >> 2, m4i = lane & 3;
+  [[maybe_unused]] const int m4cg = m4b & 3, m4rg = (m4b >> 2) & 1, m4kh = m4b >> 3;
+  float w4[MF4 ? KH : 1];
+  if constexpr (MF4) {
+    const float* src = a.W + (int64_t)(wave * HH + u0 + 4 * m4cg + m4i) * HH + KH * m4kh;
+#pragma unroll
+    for (int q = 0; q < KH; q += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + q);
+      w4[q] = v[0]; w4[q + 1] = v[1]; w4[q + 2] = v[2]; w4[q + 3] = v[3];
+    }
+  } else if constexpr (BF) {
     // k of MFMA q, lane group g, element e: KG g + 8 q + e (A and B alike)
     const __bf16* src = a.Wb + (int64_t)(wave * HH + u0 + (lane & 15)) * HH + KG * (lane >> 4);
 #pragma unroll
@@ -866,7 +888,22 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
       }
       __syncthreads();
       XSTAMP(t, 2);
-      if constexpr (BF) {
+      if constexpr (MF4) {
+        // four independent accumulator chains, then the two K halves (lanes l and l ^ 32)
+        const float* hb4 = hs + (4 * m4rg + m4i) * HS + KH * m4kh;
+        f32x4 a4[4] = {};
+#pragma unroll
+        for (int q = 0; q < KH; q += 4) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(hb4 + q);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a4[e] = __builtin_amdgcn_mfma_f32_4x4x1f32(w4[q + e], bv[e], a4[e], 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[r] = (a4[0][r] + a4[1][r]) + (a4[2][r] + a4[3][r]);
+          acc[r] += __shfl_xor(acc[r], 32);
+        }
+      } else if constexpr (BF) {
 #pragma unroll
         for (int q = 0; q < KG / 8; ++q)
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[q], *reinterpret_cast<const bf16x8*>(hrowb + 8 * q), acc,
@@ -884,10 +921,17 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
     }
 #endif
     XSTAMP(t, 3);
-    // C[unit 4 (lane / 16) + r][batch lane % 16] of gate `wave`
-    if ((lane & 15) < XRB)
+    if constexpr (MF4) {
+      // block b < 8 (K half 0, both halves summed): D[r][j] in lane 4 b + j, register r =
+      // column 4 cg + r, batch row 4 rg + j
+      if (lane < 32)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pre[(wave * U + 4 * m4cg + r) * (XRB + 1) + 4 * m4rg + m4i] = acc[r];
+    } else if ((lane & 15) < XRB) {
+      // C[unit 4 (lane / 16) + r][batch lane % 16] of gate `wave`
 #pragma unroll
       for (int r = 0; r < 4; ++r) pre[(wave * U + 4 * (lane >> 4) + r) * (XRB + 1) + (lane & 15)] = acc[r];
+    }
     __syncthreads();
     XSTAMP(t, 4);
     if (cown) {
