@@ -902,6 +902,362 @@ __global__ __launch_bounds__(256) void wn_upsample_kernel(UpArgs u, const float*
   }
 }
 
+// ================================================================ XCD-local generation
+// (B <= 8, the r9y9 shapes R = 512, G = 512, S = 256, 3 taps).  Each utterance is an
+// independent chain, so XCD x can run utterance x on its own: its 32 workgroups ("slots",
+// one per CU) step through the layers, the skip tail and the head with every per-layer
+// hand-off (g_l, x_l(t): 3 KB) written into and read from that XCD's L2, separated by a
+// per-XCD phase counter (L2-local atomics) instead of a kernel boundary.  Per layer a slot
+// owns 8 gate units (16 gate rows over the 1792 inputs [x_l(t-2d) | x_l(t-d) | g_(l-1) |
+// x_(l-1)(t)] of wn_layer_kernel's folded-current-tap form: the ring taps enter the GEMV
+// directly, no past-tap launches), 16 residual rows and 8 skip rows of the previous layer.
+// The weights (136 KB per slot and phase) are the bulk of a phase's bytes, so they are moved
+// off the critical chain: 4 "loader" waves fetch the NEXT phase's rows into registers while
+// the phase runs and write them to LDS once the 4 "compute" waves have read the current ones;
+// the compute waves' chain per phase is wait -> hand-off loads (sc1) -> dot products from
+// LDS -> gate / residual -> stores -> arrive.  Every slot draws the sample itself from the
+// previous step's h1 (same Philox stream, the same value in all 32).  26 phases per sample
+// step: layers 0..L-1, the last layer's skip rows, h1.
+__device__ int g_wn_fault = 0;         // sticky: an XCD-local generation timed out (autovc_wavenet_fault)
+constexpr int kXW = 8;                 // waves per slot workgroup: 4 compute + 4 loader
+constexpr int kXCW = 4;                // compute waves
+constexpr int kXUW = 8 / kXCW;         // gate units per compute wave (2)
+constexpr int kXGR = 2 * kXUW;         // gate rows per compute wave (4)
+constexpr int kXXR = 16 / kXCW;        // residual x rows per compute wave (4)
+constexpr int kXSR = 8 / kXCW;         // skip / head rows per compute wave (2)
+constexpr int kXSlots = 32;            // slots per XCD
+constexpr int kXLn = 32;               // ints per barrier line (128 B)
+constexpr int kXBarLines = 17;         // census (lines 0..7), phase counters (8..15), error (16)
+static_assert(kCtrSlots % kXLn == 0, "barrier block starts on a line");
+constexpr int kXKX = 1792;             // gate width K*R + H
+constexpr int kXC = kXKX / 256;        // 256-float chunks of the gate GEMV (7)
+constexpr int kXG4 = 16 * kXKX / 4;    // float4 of the gate rows of a slot (7168)
+constexpr int kXR4 = 24 * 256 / 4;     // float4 of the residual / skip / head rows (1536)
+constexpr int kXLd = (kXG4 + kXR4) / (64 * (kXW - kXCW));   // float4 per loader lane (34)
+static_assert(kXLd * 64 * (kXW - kXCW) == kXG4 + kXR4, "loader map");
+
+__device__ __forceinline__ f32x4 ld4_l2(const float* base, int off) {
+  // an L1-bypassing (sc1) 16-byte load of data another workgroup of this XCD wrote: `base` is
+  // wave-uniform (the descriptor lives in SGPRs; a per-lane base would make the compiler
+  // loop over the lanes), `off` the lane's float offset
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff,
+                                                                     0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)off * 4u, 0, 16));
+}
+
+__device__ __forceinline__ f32x4 ld4_ro(const float* base, int off) {
+  // a 16-byte load of read-only weights through a wave-uniform buffer descriptor
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff,
+                                                                     0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)off * 4u, 0, 0));
+}
+
+__global__ __launch_bounds__(64 * kXW, 1) void wn_xcd_kernel(WnArgs a, int t0, int t1, int* bar, int timeout_ticks) {
+  constexpr int R = 512, H = 256, S = 256;
+  __shared__ __attribute__((aligned(16))) float s_w[4 * (kXG4 + kXR4)];   // this phase's weight rows
+  __shared__ float s_mol[kMaxNO];
+  __shared__ float s_in;
+  __shared__ float s_x[16];              // this slot's rows of the residual input x_{l-1}(t)
+  __shared__ float s_skip[8];            // this slot's skip accumulator rows
+  __shared__ int s_info[3];              // xcc, slot, status
+  __shared__ int s_ok;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool compute = w < kXCW;
+  if (tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    const int xcc = (int)(x & 15);
+    const int slot = xcc < 8 ? __hip_atomic_fetch_add(bar + xcc * kXLn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 99;
+    s_info[0] = xcc;
+    s_info[1] = slot;
+    s_info[2] = (xcc < 8 && slot < kXSlots) ? 0 : 1;
+    if (s_info[2]) __hip_atomic_store(bar + 16 * kXLn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const int u = __builtin_amdgcn_readfirstlane(s_info[0]), slot = __builtin_amdgcn_readfirstlane(s_info[1]);
+  if (s_info[2] || u >= a.B) return;     // a group short of slots times out below
+  const int L = a.n_layers, T = a.T, RING = a.RING, NPH = L + 2;
+  int* ctr = bar + (8 + u) * kXLn;
+  int* err = bar + 16 * kXLn;
+  int phase = 0;                          // phases every slot of the XCD has arrived at
+  bool ok = true;
+  const float* W2 = head_base(a) + (int64_t)S * S + S;
+  const float* b2 = W2 + (int64_t)a.NO * S;
+  const float* b1 = head_base(a) + (int64_t)S * S;
+
+  // ---- loader waves: the next phase's rows, registers -> LDS.  Loader wave lw owns gate
+  // rows kGRL lw .. (each 7 float4 per lane) and residual rows kRRL lw .. (1 float4 per lane):
+  // every load is a wave-uniform row base plus a lane offset, so the addressing stays scalar.
+  constexpr int kNLW = kXW - kXCW, kGRL = 16 / kNLW, kRRL = 24 / kNLW;
+  static_assert(kGRL * kXC + kRRL == kXLd, "loader rows");
+  const int lw = w - kXCW;
+  f32x4 lreg[kXLd];                      // (loader waves only)
+  auto load_next = [&](int ph) {          // global -> registers
+    if (ph < L) {
+#pragma unroll
+      for (int k = 0; k < kGRL; ++k) {
+        const int row = kGRL * lw + k, unit = 8 * slot + (row >> 1);
+        const float* base = layer_base(a, ph) + (int64_t)(unit + (row & 1) * H) * kXKX;
+#pragma unroll
+        for (int c = 0; c < kXC; ++c) lreg[kXC * k + c] = ld4_ro(base, 256 * c + 4 * lane);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kRRL; ++k) {
+      const int row = kRRL * lw + k;     // residual block row 0..23
+      const float* base = nullptr;
+      if (ph == L + 1) {
+        if (row >= 16) base = head_base(a) + (int64_t)(8 * slot + row - 16) * 256;
+      } else if (ph >= 1 && (ph < L || row >= 16)) {
+        const int prow = row < 16 ? 16 * slot + row : R + 8 * slot + (row - 16);
+        base = layer_base(a, ph - 1) + (int64_t)a.G * kXKX + (int64_t)prow * H;
+      }
+      if (base != nullptr) lreg[kGRL * kXC + k] = ld4_ro(base, 4 * lane);
+    }
+  };
+  auto store_next = [&]() {               // registers -> LDS (rows a phase does not read get stale data)
+#pragma unroll
+    for (int k = 0; k < kGRL; ++k)
+#pragma unroll
+      for (int c = 0; c < kXC; ++c)
+        *reinterpret_cast<f32x4*>(s_w + (kGRL * lw + k) * kXKX + 256 * c + 4 * lane) = lreg[kXC * k + c];
+#pragma unroll
+    for (int k = 0; k < kRRL; ++k)
+      *reinterpret_cast<f32x4*>(s_w + 4 * kXG4 + (kRRL * lw + k) * 256 + 4 * lane) = lreg[kGRL * kXC + k];
+  };
+  if (!compute) {
+    load_next(0);
+    store_next();
+    load_next(1 % NPH);
+  }
+  __syncthreads();
+
+  auto arrive = [&]() {
+    if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the hand-off stores are in L2
+    lds_barrier();
+    if (tid == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    ++phase;
+  };
+  auto wait = [&]() {
+    if (tid == 0) {
+      const uint64_t c0 = __builtin_amdgcn_s_memrealtime();
+      int good = 1;
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < kXSlots * phase) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - c0 > (uint64_t)timeout_ticks ||
+            __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          good = 0;
+          break;
+        }
+      }
+      s_ok = good;
+    }
+    lds_barrier();
+    ok = s_ok != 0;
+  };
+  // end of a phase: loaders move the next phase's rows into LDS (the compute waves read the
+  // current ones before the arrive) and fetch the one after
+  int gph = 0;                            // global phase index of this launch (0 = step t0, layer 0)
+  auto finish_phase = [&]() {
+    arrive();
+    ++gph;
+  };
+
+  if (!compute) {
+    // the loader waves' loop: the same barriers as the compute waves' (wait, the two of the
+    // sampling phase, arrive), with the register rows live only here
+    for (int t = t0; t < t1 && ok; ++t)
+      for (int ph = 0; ph < NPH && ok; ++ph) {
+        if (gph > 0) wait();
+        if (!ok) break;
+        if (ph == 0) { lds_barrier(); lds_barrier(); }
+        arrive();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        store_next();
+        load_next((gph + 2) % NPH);
+        ++gph;
+      }
+    return;
+  }
+  for (int t = t0; t < t1 && ok; ++t) {
+    const int ts = t & (RING - 1), prow = t % a.Tch;
+    for (int ph = 0; ph < NPH && ok; ++ph) {
+      if (gph > 0) wait();
+      if (!ok) break;
+      if (ph < L) {
+        const int l = ph, d = 1 << (l % a.lps);
+        // ---- compute waves: wave w owns units 8 slot + kXUW w .. +kXUW (gate rows kXGR w ..
+        // of the LDS block: [unit tanh, unit sigmoid] pairs), residual x rows kXXR w .. and
+        // skip rows 16 + kXSR w .. of the LDS residual block
+        f32x4 in[kXC];
+        float pre[kXGR];
+        if (compute) {
+          const float* x2 = ring_row(a, l, (t - 2 * d) & (RING - 1)) + (int64_t)u * R;
+          const float* x1 = ring_row(a, l, (t - d) & (RING - 1)) + (int64_t)u * R;
+          in[0] = ld4_l2(x2, 4 * lane);
+          in[1] = ld4_l2(x2, 256 + 4 * lane);
+          in[2] = ld4_l2(x1, 4 * lane);
+          in[3] = ld4_l2(x1, 256 + 4 * lane);
+          const float* pr = a.pre + ((int64_t)prow * a.B + u) * ((int64_t)L * a.G) + (int64_t)l * a.G;
+          const int u0 = 8 * slot + kXUW * w;
+#pragma unroll
+          for (int q = 0; q < kXUW; ++q) { pre[2 * q] = pr[u0 + q]; pre[2 * q + 1] = pr[H + u0 + q]; }
+          if (l >= 1) {
+            const float* gp = gbuf_of(a, l - 1) + (int64_t)u * H;
+            const float* xp = ring_row(a, l - 1, ts) + (int64_t)u * R;
+            in[4] = ld4_l2(gp, 4 * lane);
+            in[5] = ld4_l2(xp, 4 * lane);
+            in[6] = ld4_l2(xp, 256 + 4 * lane);
+          }
+        }
+        if (l == 0) {
+          // ---- the sample of step t-1 from its h1 (every slot draws the same value), then x_0(t)
+          const int tp = t - 1;
+          constexpr int MR = 32 / kXCW;        // MoL rows per compute wave (16)
+          if (compute && tp >= 0) {
+            const f32x4 hv = ld4_l2(a.h1 + (int64_t)u * S, 4 * lane);
+            float accm[MR];
+#pragma unroll
+            for (int q = 0; q < MR; ++q) {
+              const int row = min(MR * w + q, a.NO - 1);
+              accm[q] = dot4(ld4(W2 + (int64_t)row * S + 4 * lane), hv, 0.f);
+            }
+            const float v = wave_reduce_multi<MR>(accm, lane);
+            const int r = MR * w + lane / (64 / MR);
+            if ((lane & (64 / MR - 1)) == 0 && r < a.NO) s_mol[r] = v + b2[r];
+          }
+          lds_barrier();
+          if (tid == 0) {
+            float smp = 0.f, in_v = 0.f;
+            if (tp >= 0) smp = mol_sample(s_mol, a.NO / 3, tp, a.utt_base + u, a);
+            if (a.teacher != nullptr && t < a.teacher_len) in_v = a.teacher[(int64_t)u * a.teacher_len + t];
+            else if (tp >= 0) in_v = smp;
+            s_in = in_v;
+            if (slot == 0) {
+              a.yin[(int64_t)u * T + t] = in_v;
+              if (tp >= 0) {
+                a.y_out[(int64_t)u * T + tp] = smp;
+                if (a.mol_out)
+                  for (int j = 0; j < a.NO; ++j) a.mol_out[((int64_t)u * T + tp) * a.NO + j] = s_mol[j];
+              }
+            }
+          }
+          lds_barrier();
+          if (compute) {
+            const float in_v = s_in;
+            in[4] = f32x4{0.f, 0.f, 0.f, 0.f};   // layer 0: no g_(l-1) block (its weights are zero)
+#pragma unroll
+            for (int c = 5; c < 7; ++c) {
+              const int i = 256 * (c - 5) + 4 * lane;
+              const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + R + i);
+              in[c] = f32x4{in_v * fw[0] + fb[0], in_v * fw[1] + fb[1], in_v * fw[2] + fb[2], in_v * fw[3] + fb[3]};
+            }
+            if (tid < 16) {                   // x_0(t): this slot's 16 rows
+              const int row = 16 * slot + tid;
+              const float xv = in_v * a.packed[row] + a.packed[R + row];
+              ring_row(a, 0, ts)[(int64_t)u * R + row] = xv;
+              s_x[tid] = xv;
+            }
+          }
+        }
+        if (compute) {
+          // ---- dot products from the LDS rows
+          float accg[kXGR];
+#pragma unroll
+          for (int r = 0; r < kXGR; ++r) accg[r] = 0.f;
+#pragma unroll
+          for (int c = 0; c < kXC; ++c)
+#pragma unroll
+            for (int r = 0; r < kXGR; ++r)
+              accg[r] = dot4(*reinterpret_cast<const f32x4*>(s_w + (kXGR * w + r) * kXKX + 256 * c + 4 * lane), in[c],
+                             accg[r]);
+          // lane (64 / kXGR) r holds gate row r; the sigmoid row of a pair sits 64 / kXGR lanes up
+          constexpr int GS = 64 / kXGR;
+          const float zv = wave_reduce_multi<kXGR>(accg, lane);
+          const float zs = __shfl(zv, (lane + GS) & 63);
+          if (lane % (2 * GS) == 0) {
+            const int q = lane / (2 * GS), un = 8 * slot + kXUW * w + q;
+            float pt = pre[0], ps = pre[1];   // pre[2 q], pre[2 q + 1] without a dynamic register index
+#pragma unroll
+            for (int k = 1; k < kXUW; ++k)
+              if (q == k) { pt = pre[2 * k]; ps = pre[2 * k + 1]; }
+            gbuf_of(a, l)[(int64_t)u * H + un] = tanhf(zv + pt) * avc_sigmoid(zs + ps);
+          }
+          if (l >= 1) {
+            constexpr int RR = kXXR + kXSR <= 8 ? 8 : 16;   // residual values per wave, padded
+            float accr[RR];
+#pragma unroll
+            for (int r = 0; r < RR; ++r) accr[r] = 0.f;
+            const float* rw = s_w + 4 * kXG4;
+#pragma unroll
+            for (int r = 0; r < kXXR; ++r)
+              accr[r] = dot4(*reinterpret_cast<const f32x4*>(rw + (kXXR * w + r) * 256 + 4 * lane), in[4], 0.f);
+#pragma unroll
+            for (int r = 0; r < kXSR; ++r)
+              accr[kXXR + r] = dot4(*reinterpret_cast<const f32x4*>(rw + (16 + kXSR * w + r) * 256 + 4 * lane), in[4], 0.f);
+            const float v = wave_reduce_multi<RR>(accr, lane);   // lane (64 / RR) j: value j
+            const float* pbias = layer_base(a, l - 1) + (int64_t)a.G * kXKX + (int64_t)(R + S) * H;
+            const int j = lane / (64 / RR);
+            if (lane % (64 / RR) == 0 && j < kXXR) {
+              const int xr = 16 * slot + kXXR * w + j;
+              const float xv = (v + pbias[xr] + s_x[kXXR * w + j]) * kSqrtHalf;
+              ring_row(a, l, ts)[(int64_t)u * R + xr] = xv;
+              s_x[kXXR * w + j] = xv;
+            } else if (lane % (64 / RR) == 0 && j < kXXR + kXSR) {
+              const int k = kXSR * w + j - kXXR;
+              const float sv = v + pbias[R + 8 * slot + k];
+              s_skip[k] = l - 1 == 0 ? sv : (a.legacy ? (s_skip[k] + sv) * kSqrtHalf : s_skip[k] + sv);
+            }
+          }
+        }
+      } else if (ph == L) {
+        // ---- tail: the last layer's skip rows (LDS residual rows 16..23) -> the global skip sum
+        if (compute) {
+          const f32x4 g = ld4_l2(gbuf_of(a, L - 1) + (int64_t)u * H, 4 * lane);
+          const float* rw = s_w + 4 * kXG4;
+          float acc[kXSR];
+#pragma unroll
+          for (int r = 0; r < kXSR; ++r)
+            acc[r] = dot4(*reinterpret_cast<const f32x4*>(rw + (16 + kXSR * w + r) * 256 + 4 * lane), g, 0.f);
+          const float v = wave_reduce_multi<kXSR>(acc, lane);
+          if (lane % (64 / kXSR) == 0) {
+            const int k = kXSR * w + lane / (64 / kXSR);
+            const float* pbias = layer_base(a, L - 1) + (int64_t)a.G * kXKX + (int64_t)(R + S) * H;
+            const float sv = v + pbias[R + 8 * slot + k];
+            const float sk = L - 1 == 0 ? sv : (a.legacy ? (s_skip[k] + sv) * kSqrtHalf : s_skip[k] + sv);
+            a.skip[(int64_t)u * S + 8 * slot + k] = sk;
+          }
+        }
+      } else {
+        // ---- head: h1 = relu(W1 relu(skip) + b1), this slot's 8 rows (LDS rows 16..23)
+        if (compute) {
+          f32x4 x = ld4_l2(a.skip + (int64_t)u * S, 4 * lane);
+          x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
+          const float* rw = s_w + 4 * kXG4;
+          float acc[kXSR];
+#pragma unroll
+          for (int r = 0; r < kXSR; ++r)
+            acc[r] = dot4(*reinterpret_cast<const f32x4*>(rw + (16 + kXSR * w + r) * 256 + 4 * lane), x, 0.f);
+          const float v = wave_reduce_multi<kXSR>(acc, lane);
+          if (lane % (64 / kXSR) == 0) {
+            const int hr = 8 * slot + kXSR * w + lane / (64 / kXSR);
+            a.h1[(int64_t)u * S + hr] = fmaxf(v + b1[hr], 0.f);
+          }
+        }
+      }
+      finish_phase();
+    }
+  }
+  if (!ok) {
+    // a phase timed out (the XCD's 32 workgroups were not all resident): poison this
+    // utterance's outputs of the call and raise the device fault word the host checks
+    if (slot == 0)
+      for (int t = t0 + tid; t < t1; t += blockDim.x) a.y_out[(int64_t)u * T + t] = __builtin_nanf("");
+    if (tid == 0) __hip_atomic_fetch_or(&g_wn_fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---- graph cache: a captured S-step graph depends only on WnArgs and S.
 struct GraphKey {
   WnArgs a;
@@ -974,6 +1330,21 @@ int get_graph(const WnArgs& a, int steps, int slot0, int prow0, hipGraphExec_t* 
   return avc::kOk;
 }
 
+// XCD-local generation: AVC_WN_XCD=0 / autovc_wavenet_set_xcd(0) select the per-layer launches
+int g_wn_xcd = [] { const char* e = getenv("AVC_WN_XCD"); return e ? atoi(e) : 0; }();
+int g_wn_timeout_ticks = 100000000;   // 1 s of s_memrealtime (100 MHz) per phase wait
+
+bool xcd_eligible(int B, int n_layers, int taps, int R, int G, int S) {
+  if (!g_wn_xcd || B > 8 || n_layers < 1 || taps != 3 || R != 512 || G != 512 || S != 256) return false;
+  static const bool dev_ok = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    return cus == 8 * kXSlots;              // 8 XCDs x 32 CUs (MI355X)
+  }();
+  return dev_ok;
+}
+
 int64_t ring_frames(int n_layers, int lps, int K) {
   const int64_t dmax = (int64_t)1 << (std::min(n_layers, lps) - 1);
   const int64_t need = (K - 1) * dmax + 1;
@@ -1004,6 +1375,31 @@ int autovc_wavenet_stamps(unsigned long long* host, int64_t n) {
 }
 #endif
 
+int autovc_wavenet_set_xcd(int on) {
+  AVC_CHECK_ARG(on == 0 || on == 1, "autovc_wavenet_set_xcd: 0 or 1");
+  g_wn_xcd = on;
+  return avc::kOk;
+}
+
+int autovc_wavenet_get_xcd(void) { return g_wn_xcd; }
+
+int autovc_wavenet_set_timeout_ticks(int ticks) {
+  AVC_CHECK_ARG(ticks >= 0, "autovc_wavenet_set_timeout_ticks: ticks >= 0");
+  g_wn_timeout_ticks = ticks > 0 ? ticks : 100000000;
+  return avc::kOk;
+}
+
+int autovc_wavenet_fault(int clear, int* out) {
+  AVC_CHECK_ARG(out != nullptr, "autovc_wavenet_fault: null out");
+  AVC_HIP(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  AVC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wn_fault), sizeof(int)), "hipMemcpyFromSymbol");
+  if (clear) {
+    const int zero = 0;
+    AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wn_fault), &zero, sizeof(int)), "hipMemcpyToSymbol");
+  }
+  return avc::kOk;
+}
+
 int64_t autovc_wavenet_ring_frames(int n_layers, int layers_per_stack, int taps) {
   if (n_layers <= 0 || layers_per_stack <= 0 || layers_per_stack > 16 || taps <= 0) return -1;
   return ring_frames(n_layers, layers_per_stack, taps);
@@ -1022,7 +1418,7 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
   const int64_t ring = (int64_t)(n_layers + 1) * ring_frames(n_layers, layers_per_stack, taps) * B * R;
   const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + 2 * (int64_t)B * (G / 2) +
                          2 * (int64_t)n_layers * B * G + (int64_t)(S / kHR) * B * kMaxNO + 7 * 64;
-  return floats * 4 + kCtrSlots * 4 + 256;
+  return floats * 4 + kCtrSlots * 4 + (int64_t)kXBarLines * kXLn * 4 + 256;
 }
 
 int autovc_wavenet_upsample_f32(int B, int Tc, int C, int n_stages, const int* scales, const float* c,
@@ -1088,15 +1484,28 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   a.ptap = ws;                 ws += round64(2 * (int64_t)n_layers * B * G);
   a.molp = ws;                 ws += round64((int64_t)(S / kHR) * B * kMaxNO);
   a.ctr = reinterpret_cast<int*>(ws);
+  int* xbar = a.ctr + kCtrSlots;   // the XCD-local generation's census / phase counters
   a.teacher = teacher; a.teacher_len = teacher ? teacher_len : 0;
   a.y_out = y_out; a.mol_out = mol_out;
   a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32);
   a.utt_base = utt_base; a.log_scale_min = log_scale_min;
-  const int64_t used = reinterpret_cast<char*>(a.ctr + kCtrSlots) - static_cast<char*>(workspace);
+  const int64_t used = reinterpret_cast<char*>(xbar + kXBarLines * kXLn) - static_cast<char*>(workspace);
   AVC_CHECK_ARG(used <= autovc_wavenet_workspace_bytes(B, T, n_layers, layers_per_stack, taps, R, G, S),
                 "%s: workspace layout overflow", fn);
 
   if (t0 == 0) AVC_HIP(hipMemsetAsync(workspace, 0, (size_t)used, stream), "hipMemsetAsync");
+  if (xcd_eligible(B, n_layers, taps, R, G, S)) {
+    // one persistent launch for the whole call: utterance x on XCD x (see wn_xcd_kernel)
+    AVC_HIP(hipMemsetAsync(xbar, 0, (size_t)kXBarLines * kXLn * 4, stream), "hipMemsetAsync");
+    hipLaunchKernelGGL(wn_xcd_kernel, dim3(8 * kXSlots), dim3(64 * kXW), 0, stream, a, t0, t1, xbar,
+                       g_wn_timeout_ticks);
+    AVC_CHECK_LAUNCH(fn);
+    if (t1 == T) {
+      hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);
+      AVC_CHECK_LAUNCH(fn);
+    }
+    return avc::kOk;
+  }
   hipLaunchKernelGGL(wn_set_ctr_kernel, dim3(1), dim3(1), 0, stream, a.ctr, t0);
   AVC_CHECK_LAUNCH(fn);
   // graph replays cover runs of graph_steps steps inside the conditioning chunk (a graph

@@ -25,6 +25,7 @@ Training-mode forward is not part of the path (the reference only synthesises).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import warnings
 
@@ -330,6 +331,14 @@ class WaveNet(nn.Module):
                       pre.data_ptr(), chunk, int(seed) & ((1 << 64) - 1), int(utt_base), float(log_scale_min),
                       _lib.ptr(tch), 0 if tch is None else tch.shape[1], y.data_ptr(), _lib.ptr(mol),
                       ws.data_ptr(), int(graph_steps), stream)
+        # the XCD-local generation poisons its outputs and sets a fault word if a phase wait
+        # timed out (its 32 workgroups per XCD were not all resident): surface it here
+        fault = ctypes.c_int(0)
+        _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(fault))
+        if fault.value:
+            raise RuntimeError("wn_xcd_kernel (XCD-local WaveNet generation): a per-XCD phase wait timed out — "
+                               "its workgroups were not all resident (another process on this GPU?); outputs are NaN. "
+                               "Set AVC_WN_XCD=0 to use the per-layer launches.")
         return (y, mol) if return_mol else y
 
     def incremental_forward(self, initial_input=None, c=None, g=None, T=100, test_inputs=None,

@@ -489,6 +489,16 @@ int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, 
  *   autovc_wavenet_ring_frames: frames of the per-layer input rings (power of two >=
  *            (taps-1) * max dilation + 1).
  */
+/* XCD-local generation (B <= 8, R = G = 512, S = 256, 3 taps, 8 XCDs x 32 CUs): utterance x
+ * runs on XCD x as ONE persistent launch per autovc_wavenet_generate_f32 call, every per-layer
+ * hand-off inside that XCD's L2.  set_xcd(1/0) selects it (default: AVC_WN_XCD, 0 if unset);
+ * a phase wait that times out (set_timeout_ticks: s_memrealtime ticks, 0 = 1 s) writes NaN
+ * over the utterance's outputs of the call and sets the fault word autovc_wavenet_fault reads
+ * (synchronising; clear != 0 resets it). */
+int autovc_wavenet_set_xcd(int on);
+int autovc_wavenet_get_xcd(void);
+int autovc_wavenet_set_timeout_ticks(int ticks);
+int autovc_wavenet_fault(int clear, int* out);
 int64_t autovc_wavenet_ring_frames(int n_layers, int layers_per_stack, int taps);
 int64_t autovc_wavenet_packed_floats(int n_layers, int taps, int R, int G, int S, int n_out);
 int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_per_stack, int taps,

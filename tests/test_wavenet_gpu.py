@@ -36,6 +36,17 @@ def _cond(B, Tc, seed=4321):
     return torch.from_numpy(np.clip(rs.normal(0.43, 0.18, (B, 80, Tc)), 0, 1).astype(np.float32))
 
 
+@pytest.fixture(params=[0, 1], ids=["launches", "xcd"])
+def xcd(request):
+    """Run a test with the per-layer launches and with the XCD-local persistent generation
+    (wn_xcd_kernel: B <= 8 on 8 XCDs x 32 CUs; larger batches use the launches either way)."""
+    from autovc_amd import _lib
+    prev = _lib.load().autovc_wavenet_get_xcd()
+    _lib.call("autovc_wavenet_set_xcd", request.param)
+    yield request.param
+    _lib.call("autovc_wavenet_set_xcd", prev)
+
+
 def rel(a, b):
     a = a.double().cpu()
     b = b.double().cpu()
@@ -53,7 +64,7 @@ def test_upsample_matches_oracle(cuda):
 
 
 @pytest.mark.parametrize("B,layers,stacks", [(3, 24, 4), (9, 6, 2)])
-def test_teacher_forced_mol_and_samples(cuda, B, layers, stacks):
+def test_teacher_forced_mol_and_samples(cuda, B, layers, stacks, xcd):
     hp = ow.small_hparams(layers=layers, stacks=stacks)
     m, W = _model(hp, cuda)
     c = _cond(B, 2)
@@ -69,7 +80,7 @@ def test_teacher_forced_mol_and_samples(cuda, B, layers, stacks):
     assert (y.double().cpu() - y_ref).abs().max().item() < 1e-4
 
 
-def test_free_running_matches_oracle(cuda):
+def test_free_running_matches_oracle(cuda, xcd):
     hp = ow.HPARAMS
     m, W = _model(hp, cuda)
     c = _cond(2, 2, seed=7)
@@ -92,7 +103,7 @@ def test_graph_replay_is_bit_exact(cuda):
     assert torch.equal(a, b) and torch.equal(a, d)
 
 
-def test_batch_shard_and_chunk_invariance(cuda):
+def test_batch_shard_and_chunk_invariance(cuda, xcd):
     hp = ow.small_hparams()
     m, _ = _model(hp, cuda)
     c = _cond(3, 2).to(cuda)
@@ -103,7 +114,7 @@ def test_batch_shard_and_chunk_invariance(cuda):
     assert (full - chunked).abs().max().item() < 1e-5
 
 
-def test_wavegen_api(cuda):
+def test_wavegen_api(cuda, xcd):
     from autovc_amd import synthesis
     torch.manual_seed(0)
     model = synthesis.build_model().to(cuda)      # r9y9 init, weight norm still attached
@@ -133,7 +144,7 @@ def test_error_behaviour(cuda):
         m.generate(c.cpu())
 
 
-def test_full_size_config4_shard_invariance(cuda):
+def test_full_size_config4_shard_invariance(cuda, xcd):
     """BASELINE config 4 at full size (8 utterances x 32,768 samples, 24 layers): sharding the
     batch by rank (utt_base) reproduces the single-batch run over 256 ring wraps and 256
     conditioning chunks; every sample finite and in [-1, 1]."""
@@ -162,3 +173,57 @@ def test_two_tiles_direct_launches_equal_graphs(cuda):
     d = m.generate(c, seed=3, log_scale_min=LSM, graph_steps=7)
     assert a.shape == (16, 4096)
     assert torch.equal(a, b) and torch.equal(a, d)
+
+
+def test_xcd_generation_matches_launches(cuda):
+    """The XCD-local persistent generation (one utterance per XCD, per-layer hand-offs in the
+    XCD's L2) against the per-layer launches: 8 utterances, 24 layers, 2,048 free-running
+    samples (16 ring wraps, 16 conditioning chunks) within fp32 summation-order noise, and
+    the MoL parameters of a teacher-forced run within 1e-5; no fault recorded."""
+    import ctypes
+    from autovc_amd import _lib
+    if _lib.load().autovc_lstm_xcd_supported(64, 512) == 0:
+        pytest.skip("needs 8 XCDs x 32 CUs")
+    hp = ow.HPARAMS
+    m, _ = _model(hp, cuda)
+    c = _cond(8, 8, seed=29).to(cuda)
+    rs = np.random.RandomState(5)
+    teacher = torch.from_numpy(rs.uniform(-0.9, 0.9, (8, 2048)).astype(np.float32)).to(cuda)
+    prev = _lib.load().autovc_wavenet_get_xcd()
+    out = {}
+    try:
+        for mode in (0, 1):
+            _lib.call("autovc_wavenet_set_xcd", mode)
+            y = m.generate(c, seed=13, log_scale_min=LSM)
+            _, mol = m.generate(c, seed=13, log_scale_min=LSM, teacher=teacher, return_mol=True)
+            out[mode] = (y, mol)
+    finally:
+        _lib.call("autovc_wavenet_set_xcd", prev)
+    (y0, m0), (y1, m1) = out[0], out[1]
+    assert torch.isfinite(y1).all() and torch.isfinite(m1).all()
+    assert rel(m1, m0) < 1e-5
+    assert (y1 - y0).abs().max().item() < 1e-4
+    f = ctypes.c_int(0)
+    _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(f))
+    assert f.value == 0
+
+
+def test_xcd_generation_timeout_surfaces(cuda):
+    """A phase wait that gives up (forced: a 1-tick timeout) poisons the outputs and raises."""
+    from autovc_amd import _lib
+    if _lib.load().autovc_lstm_xcd_supported(64, 512) == 0:
+        pytest.skip("needs 8 XCDs x 32 CUs")
+    hp = ow.small_hparams()
+    m, _ = _model(hp, cuda)
+    c = _cond(2, 1).to(cuda)
+    prev = _lib.load().autovc_wavenet_get_xcd()
+    try:
+        _lib.call("autovc_wavenet_set_xcd", 1)
+        _lib.call("autovc_wavenet_set_timeout_ticks", 1)
+        with pytest.raises(RuntimeError, match="wn_xcd_kernel"):
+            m.generate(c, seed=1, log_scale_min=LSM)
+    finally:
+        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
+        _lib.call("autovc_wavenet_set_xcd", prev)
+    y = m.generate(c, seed=1, log_scale_min=LSM)          # the next call runs clean
+    assert torch.isfinite(y).all()
