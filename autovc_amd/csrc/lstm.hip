@@ -484,6 +484,137 @@ __global__ __launch_bounds__(64 * NW_) void lstm2_bwd_rec_kernel(int B, int T, i
   }
 }
 
+// Wide-tile recurrent products of the stacked backward (splits = 8): a workgroup owns all
+// 64 batch rows x 64 output columns over 4H / 8 of K, so every weight row is fetched once
+// per step instead of once per 32-row batch tile, and the per-CU operand bytes for the
+// step's 3 x 64 x H outputs halve ((64 + 64) / (64 x 64) against (32 + 32) / (32 x 32) per
+// output and k).  8 waves: wave w computes the 32 x 32 block (w & 3) of the tile over the
+// k-half w >> 2 of each chunk as 2 x 2 v_mfma_f32_16x16x4_f32 (bf16: 16x16x32) tiles (four
+// LDS fragment reads per 16 MFMAs instead of two per 4); the halves are summed through LDS.
+// Staging, swizzle and prefetch are tile_gemm2's.
+constexpr int TBW = 64, TNW = 64;
+template <int KCH_, int D_, bool BF>
+__device__ __forceinline__ void bwd_rec_body_wide(int B, int T, int H, const float* dG, int t, const float* WT,
+                                                  float* P, int j0) {
+  constexpr int NT = 512, SLOTS = KCH_ / 4, PER = TBW * SLOTS / NT, CF = (TBW + TNW) * KCH_;
+  constexpr int SUB = KCH_ / 32;                           // 16-k sub-blocks per wave per chunk
+  static_assert(PER * NT == TBW * SLOTS && TBW == TNW && SUB >= 1, "wide staging map");
+  __shared__ __attribute__((aligned(16))) float lds[2 * CF];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blockIdx.y * TBW, s = blockIdx.z, S = gridDim.z;
+  const int K4 = BF ? 2 * H : 4 * H, ks = K4 / S, kb = s * ks;
+  const float* arow[PER];
+  const float* brow[PER];
+  int srow[PER], spos[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + i * NT, r = e / SLOTS, sl = e % SLOTS;
+    srow[i] = r;
+    spos[i] = swz(sl, r);
+    arow[i] = dG + ((int64_t)min(b0 + r, B - 1) * T + t) * K4 + kb + 4 * sl;
+    brow[i] = WT + (int64_t)(j0 + r) * K4 + kb + 4 * sl;
+  }
+  const int nc = ks / KCH_;
+  f32x4 sa[D_][PER], sb[D_][PER];
+#pragma unroll
+  for (int d = 0; d < D_; ++d) {
+    const int cl = min(d, nc - 1);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + cl * KCH_);
+      sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + cl * KCH_);
+    }
+  }
+  const int q = w & 3, kh = w >> 2, g = lane >> 4;
+  const int ra0 = (q >> 1) * 32 + (lane & 15), rb0 = (q & 1) * 32 + (lane & 15);
+  f32x4 acc[2][2] = {};
+  for (int c0 = 0; c0 < nc; c0 += D_) {
+#pragma unroll
+    for (int d = 0; d < D_; ++d) {
+      const int c = c0 + d;
+      float* L = lds + (c & 1) * CF;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        *reinterpret_cast<f32x4*>(L + srow[i] * KCH_ + 4 * spos[i]) = sa[d][i];
+        *reinterpret_cast<f32x4*>(L + (TBW + srow[i]) * KCH_ + 4 * spos[i]) = sb[d][i];
+      }
+      __syncthreads();
+      const int cn = min(c + D_, nc - 1);
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        sa[d][i] = *reinterpret_cast<const f32x4*>(arow[i] + cn * KCH_);
+        sb[d][i] = *reinterpret_cast<const f32x4*>(brow[i] + cn * KCH_);
+      }
+      if (c < nc) {
+#pragma unroll
+        for (int sub = 0; sub < SUB; ++sub) {
+          const int sl = (kh * SUB + sub) * 4 + g;
+          f32x4 av[2], bv[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int ra = ra0 + 16 * i, rb = rb0 + 16 * i;
+            av[i] = *reinterpret_cast<const f32x4*>(L + ra * KCH_ + 4 * swz(sl, ra));
+            bv[i] = *reinterpret_cast<const f32x4*>(L + (TBW + rb) * KCH_ + 4 * swz(sl, rb));
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jn = 0; jn < 2; ++jn) {
+              if constexpr (BF) {
+                acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av[i]),
+                                                                     __builtin_bit_cast(bf16x8, bv[jn]), acc[i][jn],
+                                                                     0, 0, 0);
+              } else {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                  acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][jj], bv[jn][jj], acc[i][jn], 0, 0, 0);
+              }
+            }
+        }
+      }
+    }
+  }
+  // k-halves: waves 4..7 leave their blocks in the (now idle) chunk buffers, waves 0..3 add
+  __syncthreads();
+  float* red = lds + q * 1024;
+  if (kh == 1)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) *reinterpret_cast<f32x4*>(red + ((2 * i + jn) * 64 + lane) * 4) = acc[i][jn];
+  __syncthreads();
+  if (kh == 1) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const f32x4 o = *reinterpret_cast<const f32x4*>(red + ((2 * i + jn) * 64 + lane) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = b0 + (q >> 1) * 32 + 16 * i + 4 * g + r;
+        if (b < B) P[((int64_t)s * B + b) * H + j0 + (q & 1) * 32 + 16 * jn + (lane & 15)] = acc[i][jn][r] + o[r];
+      }
+    }
+}
+
+// grid (3 H / 64, ceil(B / 64), S): x-tiles as lstm2_bwd_rec_kernel's, 64 columns each
+template <int KCH_ = KCH, int D_ = DPF, bool BF = false>
+__global__ __launch_bounds__(512) void lstm2_bwd_rec_wide_kernel(int B, int T, int H, const float* dG1,
+                                                                 const float* dG0, int t1, int t0,
+                                                                 const float* WT1, const float* WIT1,
+                                                                 const float* WT0, float* P1, float* PQ0) {
+  const int nt = H / TNW, prod = blockIdx.x / nt, j0 = (blockIdx.x % nt) * TNW;
+  const int64_t slabs = (int64_t)gridDim.z * B * H;
+  if (prod < 2) {
+    if (t1 < 0) return;
+    if (prod == 0) bwd_rec_body_wide<KCH_, D_, BF>(B, T, H, dG1, t1, WT1, P1, j0);
+    else bwd_rec_body_wide<KCH_, D_, BF>(B, T, H, dG1, t1, WIT1, PQ0 + slabs, j0);
+  } else {
+    if (t0 >= T) return;
+    bwd_rec_body_wide<KCH_, D_, BF>(B, T, H, dG0, t0, WT0, PQ0, j0);
+  }
+}
+
 // ------------------------------------------------------------------ small H (BLSTM)
 // Whole sequence, both directions in one launch.  grid = (ceil(B/2), ndir); block 256 =
 // 2 batch rows x 32 units x 4 k-quarters.  gx: (B,T,ndir*4H) [dir-major blocks]; h out:
@@ -748,8 +879,9 @@ extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, i
                                     const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
                                     float* dG0, int splits, float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H), "autovc_lstm2_bwd_f32: bad dims");
-  AVC_CHECK_ARG((splits == 2 || splits == 4) && (4 * H) % (KCH * splits) == 0,
-                "autovc_lstm2_bwd_f32: splits must be 2 or 4 with 4H a multiple of %d x splits", KCH);
+  AVC_CHECK_ARG((splits == 2 || splits == 4 || splits == 8) && (4 * H) % (KCH * splits) == 0 &&
+                    (splits < 8 || H % TNW == 0),
+                "autovc_lstm2_bwd_f32: splits must be 2, 4 or 8 with 4H a multiple of %d x splits", KCH);
   AVC_CHECK_ARG(dh1_out && gates1 && c1 && gates0 && c0 && W_hh1_T && W_ih1_T && W_hh0_T && dG1 && dG0 && workspace,
                 "autovc_lstm2_bwd_f32: null pointer");
   AVC_CHECK_ARG(d_ldb % 4 == 0 && d_ldt % 4 == 0 && AVC_ALIGNED16(dh1_out) && AVC_ALIGNED16(W_hh1_T) &&
@@ -766,14 +898,21 @@ extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, i
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits};
   const dim3 pgrid((H / 4 + 63) / 64, B, 2);
-  const dim3 rgrid(3 * H / TN, (B + TB - 1) / TB, splits);
+  // splits 8: the wide-tile products (64 x 64 per workgroup); 2 / 4: 32 x 32 tiles
+  const bool wide = splits == 8;
+  const dim3 rgrid = wide ? dim3(3 * H / TNW, (B + TBW - 1) / TBW, splits) : dim3(3 * H / TN, (B + TB - 1) / TB, splits);
   for (int s = 0; s <= T; ++s) {
     const int t1 = T - 1 - s, t0 = T - s;
-    if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    if (splits == 8) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<8>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    else if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
     else hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<2>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
     if (s == T) break;
-    hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
-                       (const float*)dG1, (const float*)dG0, t1, t0, W_hh1_T, W_ih1_T, W_hh0_T, P1, PQ0);
+    if (wide)
+      hipLaunchKernelGGL((lstm2_bwd_rec_wide_kernel<KCH, DPF>), rgrid, dim3(512), 0, stream, B, T, H,
+                         (const float*)dG1, (const float*)dG0, t1, t0, W_hh1_T, W_ih1_T, W_hh0_T, P1, PQ0);
+    else
+      hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
+                         (const float*)dG1, (const float*)dG0, t1, t0, W_hh1_T, W_ih1_T, W_hh0_T, P1, PQ0);
   }
   AVC_CHECK_LAUNCH("autovc_lstm2_bwd_f32");
   return avc::kOk;
@@ -931,8 +1070,9 @@ extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, 
                                      float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits,
                                      float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(T > 0 && bf16_shape_ok(B, H), "autovc_lstm2_bwd_bf16: bad dims");
-  AVC_CHECK_ARG((splits == 2 || splits == 4) && (2 * H) % (KCH * splits) == 0,
-                "autovc_lstm2_bwd_bf16: splits must be 2 or 4 with 2H a multiple of %d x splits", KCH);
+  AVC_CHECK_ARG((splits == 2 || splits == 4 || splits == 8) && (2 * H) % (KCH * splits) == 0 &&
+                    (splits < 8 || H % TNW == 0),
+                "autovc_lstm2_bwd_bf16: splits must be 2, 4 or 8 with 2H a multiple of %d x splits", KCH);
   AVC_CHECK_ARG(dh1_out && gates1 && c1 && gates0 && c0 && W_hh1_T_b && W_ih1_T_b && W_hh0_T_b && dG1 && dG1_b &&
                 dG0 && dG0_b && workspace, "autovc_lstm2_bwd_bf16: null pointer");
   AVC_CHECK_ARG(d_ldb % 4 == 0 && d_ldt % 4 == 0 && AVC_ALIGNED16(dh1_out) && AVC_ALIGNED16(W_hh1_T_b) &&
@@ -948,16 +1088,25 @@ extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, 
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits, reinterpret_cast<__bf16*>(dG1_b)};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits, reinterpret_cast<__bf16*>(dG0_b)};
   const dim3 pgrid((H / 4 + 63) / 64, B, 2);
-  const dim3 rgrid(3 * H / TN, (B + TB - 1) / TB, splits);
+  const bool wide = splits == 8;
+  const dim3 rgrid = wide ? dim3(3 * H / TNW, (B + TBW - 1) / TBW, splits) : dim3(3 * H / TN, (B + TB - 1) / TB, splits);
+  const float* d1 = reinterpret_cast<const float*>(dG1_b);
+  const float* d0 = reinterpret_cast<const float*>(dG0_b);
+  const float* w1 = reinterpret_cast<const float*>(W_hh1_T_b);
+  const float* wi = reinterpret_cast<const float*>(W_ih1_T_b);
+  const float* w0 = reinterpret_cast<const float*>(W_hh0_T_b);
   for (int s = 0; s <= T; ++s) {
     const int t1 = T - 1 - s, t0 = T - s;
-    if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    if (splits == 8) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<8>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    else if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
     else hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<2>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
     if (s == T) break;
-    hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF, true>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
-                       reinterpret_cast<const float*>(dG1_b), reinterpret_cast<const float*>(dG0_b), t1, t0,
-                       reinterpret_cast<const float*>(W_hh1_T_b), reinterpret_cast<const float*>(W_ih1_T_b),
-                       reinterpret_cast<const float*>(W_hh0_T_b), P1, PQ0);
+    if (wide)
+      hipLaunchKernelGGL((lstm2_bwd_rec_wide_kernel<KCH, DPF, true>), rgrid, dim3(512), 0, stream, B, T, H, d1, d0,
+                         t1, t0, w1, wi, w0, P1, PQ0);
+    else
+      hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF, true>), rgrid, dim3(64 * NWV), 0, stream, B, T, H, d1,
+                         d0, t1, t0, w1, wi, w0, P1, PQ0);
   }
   AVC_CHECK_LAUNCH("autovc_lstm2_bwd_bf16");
   return avc::kOk;

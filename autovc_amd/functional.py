@@ -1351,10 +1351,14 @@ class LSTM2StackFn(torch.autograd.Function):
         # the (H, 4H) transposes (bf16 copies under bf16), from the step's weight scope if any
         kt = 8 if _bf16_rec(H) else 7
         WT1, WIT1, WT0 = conv_weight(W_hh1, kt), conv_weight(W_ih1, kt), conv_weight(W_hh0, kt)
-        # the stacked backward kernel is built for split-K 2 or 4 only (autovc_lstm2_bwd_f32)
-        splits = 4 if int(os.environ.get("AVC_LSTM2_SPLITS", "4")) >= 4 else 2
-        if (4 * H) % (64 * splits):
-            splits = 2
+        # split-K of the stacked backward products (autovc_lstm2_bwd_f32): 4 / 2 = 32 x 32 tiles;
+        # 8 = the wide-tile kernel (64 x 64 per workgroup), measured slower (fp32 23.5 vs 20.0 us
+        # per launch, 15.87 vs 15.49 ms/step; bf16 9.6 vs 9.46 ms/step:
+        # profiles/r03/ab_lstm2_bwd_wide.txt); AVC_LSTM2_SPLITS overrides
+        kdim = 2 * H if _bf16_rec(H) else 4 * H
+        splits = {8: 8, 4: 4}.get(int(os.environ.get("AVC_LSTM2_SPLITS", "4")), 2)
+        while splits > 2 and (kdim % (64 * splits) or (splits == 8 and H % 64)):
+            splits //= 2
         ws = _ws(dev, 4 * _lib.load().autovc_lstm2_bwd_workspace_floats(B, H, splits), "lstm")
         dG1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         dG0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)

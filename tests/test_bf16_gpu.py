@@ -143,3 +143,29 @@ def test_lstm_bf16_recurrence(cuda, B, T, I, H, stacked):
     for a, b in zip(dps, ps):
         assert rel(a, b.grad) < 5e-2
     assert rel(outs["bf16"][0], outs["fp32"][0]) > 1e-5
+
+
+@pytest.mark.parametrize("B,H", [(64, 1024), (9, 512)])
+def test_lstm2_bf16_stacked_backward_wide_tiles(cuda, monkeypatch, B, H):
+    """bf16 stacked backward: the wide-tile products (split-K 8, 64 x 64 per workgroup)
+    against the 32 x 32 tiles (split-K 4) — the same bf16 operands, so the gradients differ
+    only by the fp32 summation order of the partials."""
+    from autovc_amd import functional as AF
+    torch.manual_seed(8)
+    T, I = 10, 512
+    s = 1 / H ** 0.5
+    shapes = [(4 * H, I), (4 * H, H), (4 * H,), (4 * H,), (4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]
+    ps = [((torch.rand(*sh) * 2 - 1) * s).to(cuda) for sh in shapes]
+    x = torch.randn(B, T, I, device=cuda)
+    gh = torch.randn(B, T, H, device=cuda)
+    grads = {}
+    for splits in ("4", "8"):
+        monkeypatch.setenv("AVC_LSTM2_SPLITS", splits)
+        xd = x.clone().requires_grad_()
+        pd = [p.clone().requires_grad_() for p in ps]
+        with AF.precision("bf16"):
+            AF.LSTM2StackFn.apply(xd, *pd, True).backward(gh)
+            AF.join_grad_stream()
+        grads[splits] = [xd.grad] + [p.grad for p in pd]
+    for a, b in zip(grads["8"], grads["4"]):
+        assert rel(a, b) < 5e-3   # a partial sum order flips a few bf16 roundings of dG

@@ -199,11 +199,12 @@ def test_lstm2_stack_fwd_bwd(cuda, B, T, I, H):
         assert rel(a.grad, b.grad) < 1e-4
 
 
-@pytest.mark.parametrize("splits", ["2", "4"])
+@pytest.mark.parametrize("splits", ["2", "4", "8"])
 def test_lstm2_stacked_backward_matches_layerwise(cuda, monkeypatch, splits):
     """The backward wavefront (autovc_lstm2_bwd_f32) against the layer-by-layer backward
     (two autovc_lstm_bwd_f32 recurrences + the input-gradient GEMM) at decoder lstm2's
-    size: the same sums up to the order of layer 0's dh partials."""
+    size: the same sums up to the order of layer 0's dh partials (splits 8: the wide-tile
+    product kernel, 64 x 64 per workgroup)."""
     from autovc_amd import functional as AF
     torch.manual_seed(6)
     B, T, I, H = 64, 12, 512, 1024
