@@ -209,6 +209,32 @@ __device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int
   return *status == 0;
 }
 
+// grid_sync (LP_BARRIER 0) in two halves, so a workgroup can work between its arrival and
+// the release: grid_arrive publishes this workgroup's hand-off (the last arriver of the last
+// XCC opens every gate), grid_wait polls this XCC's gate
+__device__ __forceinline__ void grid_arrive(const PArgs& a, int xcc, int mine, int nx, int gen) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
+    if (old == mine * (gen + 1) - 1) {
+      const int top = add_rlx(a.bar + BAR_TOP * L, 1);
+      if (top == nx * (gen + 1) - 1)
+        for (int x = 0; x < 16; ++x) st_rlx(a.bar + (BAR_GEN + x) * L, gen + 1);
+    }
+  }
+}
+
+__device__ __forceinline__ bool grid_wait(const PArgs& a, int xcc, int* status, int gen) {
+  if (threadIdx.x == 0) {
+    const bool ok = wait_ge(a.bar + (BAR_GEN + xcc) * L, gen + 1, a.bar + BAR_ERR * L, a.timeout_ticks);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)
+    *status = ok ? 0 : 1;
+  }
+  __syncthreads();
+  return *status == 0;
+}
+
 // Sticky per-device fault word: a launch whose grid barrier timed out (its workgroups were
 // not all resident at once — e.g. another process's kernels held part of the chip) ORs
 // kFaultPersistBarrier into it, after writing NaN over every h and c it owns, so the
@@ -393,7 +419,7 @@ __device__ __forceinline__ void gemm_wave_bf(const __bf16* __restrict__ hk0_t, c
 // that layer and whose iteration t is its step t (no lag, T iterations).
 // BF: bf16 weights and hand-off copies (the products' numerics of autovc_lstm2_fwd_bf16);
 // cell math, c, h, gates fp32 either way.
-template <int HH, bool TWO, bool BF = false>
+template <int HH, bool TWO, bool BF = false, bool LAG2 = false>
 __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
   constexpr int KW = PK<HH>::KW, KL = PK<HH>::KL, GR = PK<HH>::GR, NS = KW / 32;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -509,6 +535,108 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
     }
   };
 
+  if constexpr (TWO && LAG2) {
+    // Two-step wavefront: iteration t runs layer 0 at step t and layer 1 at step t - 2, so
+    // layer 1's input product W_ih1 h0_(t-1) (for its step t - 1, done in iteration t + 1)
+    // reads rows released one barrier earlier and runs between this workgroup's arrival at
+    // barrier t and the release: a third of the MFMA work under the barrier's latency, for a
+    // second (L2-hot) read of h0_(t-1).  After the release: W_hh0 h0_(t-1) and W_hh1 h1_(t-3).
+    auto store_outputs2 = [&](int t0) {
+      if (!eown) return;
+      if (t0 >= 2 && t0 - 2 < T) {
+        const int t1 = t0 - 2;
+        const int64_t o = ((int64_t)eb * T + t1) * H + ej;
+        cell_store(out1, a.c1 + o, a.h1 + o, a.g1 ? a.g1 + ((int64_t)eb * T + t1) * 4 * H + ej : nullptr, H);
+      }
+      if (t0 < T) {
+        const int64_t o = ((int64_t)eb * T + t0) * H + ej;
+        cell_store(out0, a.c0 + o, a.h0 + (int64_t)eb * a.h0_ldb + (int64_t)t0 * a.h0_ldt + ej,
+                   a.g0 ? a.g0 + ((int64_t)eb * T + t0) * 4 * H + ej : nullptr, H);
+      }
+    };
+    const int last2 = T + 1;
+    f32x4 acc1[PRBW] = {};                                            // layer 1's carried input product
+    for (int t = 0; t <= last2; ++t) {
+      const bool l0 = t < T, l1 = t >= 2;
+      if (t >= 1) store_outputs2(t - 1);
+      float gxv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (eown && l0) {
+        const float* g = a.gx0 + (int64_t)eb * a.gx_ldb + (int64_t)t * a.gx_ldt;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gxv[q] = g[q * H + ej];
+      }
+      f32x4 acc0[PRBW] = {};
+      const int th0 = t >= 1 ? t - 1 : 0, th1 = t >= 3 ? t - 3 : 0;
+      const bool pl0 = l0 && t >= 1, ps1 = t >= 3;
+      if constexpr (BF) {
+        const __bf16* hk0b = a.hk0b + (int64_t)th0 * BH;
+        const __bf16* hk1b = a.hk1b + (int64_t)th1 * BH;
+        if (pl0 && ps1) gemm_wave_bf<NS, false, true, true>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
+        else if (pl0) gemm_wave_bf<NS, false, true, false>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
+        else if (ps1) gemm_wave_bf<NS, false, false, true>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
+      } else {
+        const float* hk0 = a.hk0 + (int64_t)th0 * BH;
+        const float* hk1 = a.hk1 + (int64_t)th1 * BH;
+        if (pl0 && ps1) gemm_wave<KL, false, true, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+        else if (pl0) gemm_wave<KL, false, true, false>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+        else if (ps1) gemm_wave<KL, false, false, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
+      }
+      auto sum = [&](int g) {
+        const float* r = red + eb * RED_LD + g * PU + eu;
+        return ((r[0] + r[RED_SLOT]) + r[2 * RED_SLOT]) + r[3 * RED_SLOT];
+      };
+      auto reduce_put = [&](const f32x4 (&acc)[PRBW]) {
+        if (kw < 4) put_tile(red + (kw & 3) * RED_SLOT, acc, rb0, lane);
+#pragma unroll
+        for (int ph = 1; ph < PKWN / 4; ++ph) {
+          __syncthreads();
+          if (kw / 4 == ph) add_tile(red + (kw & 3) * RED_SLOT, acc, rb0, lane);
+        }
+      };
+      if (l1) {                                                       // layer 1 at step t - 2
+        reduce_put(acc1);
+        __syncthreads();
+        if (wave < 4) {
+          float pre[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) pre[g] = sum(g) + bias1[g];
+          out1 = cell(pre, out1.c);
+          handoff<BF>(out1.h, a.hk1 + (int64_t)(t - 2) * BH, a.hk1b + (int64_t)(t - 2) * BH, B, eb, ej, lane);
+        }
+        __syncthreads();
+      }
+      if (l0) {                                                       // layer 0 at step t
+        reduce_put(acc0);
+        __syncthreads();
+        if (wave < 4) {
+          float pre[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) pre[g] = sum(g) + gxv[g];
+          out0 = cell(pre, out0.c);
+          handoff<BF>(out0.h, a.hk0 + (int64_t)t * BH, a.hk0b + (int64_t)t * BH, B, eb, ej, lane);
+        }
+      }
+      if (t == last2) break;
+      grid_arrive(a, xcc_id, xcc_wgs, xcc_n, t);
+      // under the barrier: layer 1's input product for its step t - 1 from h0_(t-1)
+#pragma unroll
+      for (int rb = 0; rb < PRBW; ++rb) acc1[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t >= 1 && t - 1 < T) {
+        if constexpr (BF)
+          gemm_wave_bf<NS, true, false, false>(a.hk0b + (int64_t)(t - 1) * BH, a.hk1b, whb, W0b, W1b, k8_0, B, rb0,
+                                               lane, acc1, acc0);
+        else
+          gemm_wave<KL, true, false, false>(a.hk0 + (int64_t)(t - 1) * BH, a.hk1, wh, W0, W1, kb0, B, rb0, lane, acc1,
+                                            acc0);
+      }
+      if (!grid_wait(a, xcc_id, status, t)) {
+        fail();
+        return;
+      }
+    }
+    store_outputs2(last2);
+    return;
+  }
   const int last = TWO ? T : T - 1;                                 // final iteration
   for (int t = 0; t <= last; ++t) {
     const bool l0 = t < T, l1 = TWO && t >= 1;
@@ -601,6 +729,14 @@ bool persist_fits() {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_persist_kernel<HH, TWO, BF>, PNT,
                                                      lds_bytes<HH, TWO, BF>()) != hipSuccess)
       per = 0;
+    int per2 = 0;                         // the two-step wavefront form must fit the same way
+    const void* k2 = reinterpret_cast<const void*>(lstm_persist_kernel<HH, TWO, BF, true>);
+    if (TWO && (hipFuncSetAttribute(k2, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<HH, TWO, BF>()) !=
+                    hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, lstm_persist_kernel<HH, TWO, BF, true>, PNT,
+                                                             lds_bytes<HH, TWO, BF>()) != hipSuccess ||
+                per2 < 1))
+      per = 0;
   }
   if (g_cus < 0) {
     int dev = 0;
@@ -609,6 +745,18 @@ bool persist_fits() {
                 ? p.multiProcessorCount : 0;
   }
   return per >= 1 && HH / PU <= g_cus;
+}
+
+// The two-step wavefront of the stacked forward (LAG2 above): the fp32 default (20.7-21.0 ->
+// 18.1-18.2 us per wavefront step, 15.39 -> 14.99 ms per training step, alternating on one box:
+// profiles/r03/ab_lstm2_lag2.txt); not under bf16, whose 8x cheaper products leave the
+// barrier nothing to hide and the second h0 read costs (10.5 -> 14.1 us).  AVC_LSTM2_LAG2=0 /
+// =1 forces it off / on for both; read per launch (one per forward), so tests compare both.
+bool lag2_on(bool bf) {
+  const char* e = getenv("AVC_LSTM2_LAG2");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return !bf;
 }
 
 template <int HH, bool TWO, bool BF = false>
@@ -620,8 +768,12 @@ void launch_persist(PArgs& a, void* workspace, hipStream_t stream) {
   a.hk1b = TWO ? a.hk0b + (int64_t)a.T * a.B * HH : nullptr;
   // 1 s of s_memrealtime (100 MHz) per wait: a safety net, never a schedule
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
-  hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO, BF>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO, BF>()), stream,
-                     a);
+  if (TWO && lag2_on(BF))
+    hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO, BF, true>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO, BF>()),
+                       stream, a);
+  else
+    hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO, BF>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO, BF>()), stream,
+                       a);
 }
 
 // ================================================================ XCD-local recurrences

@@ -106,7 +106,13 @@ def lstm_roofline(solver, B, T, dev):
             xs.append(e0.elapsed_time(e1) * 1e3)
         launch_us = sorted(xs[1:])[1]
         flop_launch, bytes_launch = flop2 * T, 2 * per_layer_step * T
-        kernel = "lstm_persist_kernel<1024, true, false> (decoder lstm2 forward, both layers, whole sequence per launch, H=1024, B=64)"
+        # the fp32 default is the two-step wavefront form (layer 1 two steps behind layer 0: T + 2
+        # iterations); AVC_LSTM2_LAG2=0 selects the one-step form (T + 1)
+        lag2 = os.environ.get("AVC_LSTM2_LAG2", "") != "0"
+        iters = T + 2 if lag2 else T + 1
+        kernel = (f"lstm_persist_kernel<1024, true, false, {'true' if lag2 else 'false'}> (decoder lstm2 forward, "
+                  "both layers, whole sequence per launch, H=1024, B=64"
+                  + (", two-step wavefront)" if lag2 else ")"))
         pmc_file = "lstm2_persist_pmc.json"
     else:
         launch_us, flop_launch, bytes_launch = us2, flop2, 2 * per_layer_step
@@ -137,7 +143,7 @@ def lstm_roofline(solver, B, T, dev):
                             "hbm_frac": round(per_layer_step / (us1 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                             "mfma_frac": round(2 * B * 4 * H * H / (us1 * 1e-6) / 1e12 / MFMA_F32_PEAK_TF, 4)}}
     if persistent:
-        out["us_per_wavefront_step"] = round(launch_us / (T + 1), 3)
+        out["us_per_wavefront_step"] = round(launch_us / iters, 3)
     return out
 
 

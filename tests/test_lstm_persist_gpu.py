@@ -40,8 +40,17 @@ def _supported(B, H):
     return bool(_lib.load().autovc_lstm2_persist_supported(B, H))
 
 
+@pytest.fixture(params=["0", "1"], ids=["lag1", "lag2"])
+def lag2(request, monkeypatch):
+    """Both wavefront forms of the persistent stacked forward: layer 1 one step behind layer 0
+    (AVC_LSTM2_LAG2=0, the bf16 default) and two steps behind (=1, the fp32 default: layer 1's
+    input product runs while the workgroup waits at the grid barrier)."""
+    monkeypatch.setenv("AVC_LSTM2_LAG2", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("T", [3, 128])
-def test_persistent_matches_per_step_launches(cuda, T):
+def test_persistent_matches_per_step_launches(cuda, T, lag2):
     from autovc_amd import _lib
     B, H = 64, 1024
     if not _supported(B, H):
@@ -107,7 +116,7 @@ def test_single_layer_persistent_matches_per_step_launches(cuda, H, T):
 
 
 @pytest.mark.parametrize("T", [3, 128])
-def test_bf16_persistent_matches_bf16_per_step_launches(cuda, T):
+def test_bf16_persistent_matches_bf16_per_step_launches(cuda, T, lag2):
     """autovc_lstm2_fwd_persist_bf16 against the per-step bf16 wavefront (autovc_lstm2_fwd_bf16):
     the same RNE-rounded weights and h copies, fp32 accumulation in a different order."""
     from autovc_amd import _lib
