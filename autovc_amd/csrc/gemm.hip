@@ -877,11 +877,13 @@ GemmShape pick_config(int M, int N, int K, int splits) {
   if (t128 >= 512) return kCfg[big >= 0 && big < NCFG ? big : 2];
   // deep-K outputs that fill the chip once with 128-tiles (the LSTM weight gradients,
   // 4096 x 1024 over K = B*T = 8192, on the gradient side stream): 128x128/BK32 measured
-  // 17.86 vs 17.98 ms/step against 64x64 (tools/ab_gemm_bigk.sh; AVC_GEMM_BIGK=<cfg id>
-  // overrides, -1 = the 64x64 path)
+  // 17.86 vs 17.98 ms/step against 64x64 (round 2, tools/ab_gemm_bigk.sh); its 8-wave form
+  // (cfg 9: 64x32 per wave, pipelined fragment reads) 14.82-14.89 vs 14.95-14.98 ms/step in
+  // round 3, where these GEMMs run at the end of the replayed step with the chip to themselves
+  // (profiles/r03/ab_gemm_bigk.txt; AVC_GEMM_BIGK=<cfg id> overrides, -1 = the 64x64 path)
   static const int bigk = [] {
     const char* e = getenv("AVC_GEMM_BIGK");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 9;
   }();
   if (bigk >= 0 && bigk < NCFG && t128 >= 256 && K >= 4096) return kCfg[bigk];
   if (splits > 1) return kCfg[3];
