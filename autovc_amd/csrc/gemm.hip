@@ -871,7 +871,9 @@ GemmShape pick_config(int M, int N, int K, int splits) {
   // (8-wave tiles, cfg 9/11, won 5-7 % in the isolated sweep but nothing inside the step:
   // 21.62 vs 21.52 ms, same box, alternating)
   constexpr int NCFG = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
-  static const int big = [] { const char* e = getenv("AVC_GEMM_BIG"); return e ? atoi(e) : 2; }();
+  // round 3 (whole step, alternating): cfg 9 for the big grids too, 14.80-14.83 vs
+  // 14.86-14.89 ms/step with identical losses (profiles/r03/ab_gemm_bigk.txt)
+  static const int big = [] { const char* e = getenv("AVC_GEMM_BIG"); return e ? atoi(e) : 9; }();
   static const int small = [] { const char* e = getenv("AVC_GEMM_SMALL"); return e ? atoi(e) : 8; }();
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
   if (t128 >= 512) return kCfg[big >= 0 && big < NCFG ? big : 2];
