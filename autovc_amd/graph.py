@@ -16,9 +16,19 @@ update: those buffers are snapshotted and restored around it.
 """
 from __future__ import annotations
 
+import collections
+import os
+
 import torch
 
 from . import functional as AF
+
+# Replays the host may have queued ahead of the GPU.  Unbounded, back-to-back replays of a
+# graph with no side-stream branch (AVC_GRAD_STREAM=0) aborted a 25-step bench run with a
+# GPU memory fault in round 3 (and gave run-to-run different losses in round 2) while the
+# short tests passed; waiting on the event of the replay MAX_AHEAD steps back keeps the
+# queue short at no cost to throughput (the GPU still holds MAX_AHEAD steps of work).
+MAX_AHEAD = int(os.environ.get("AVC_GRAPH_MAX_AHEAD", "2"))
 
 
 class StepGraphs:
@@ -26,6 +36,7 @@ class StepGraphs:
         self.fn = fn            # fn(*inputs) -> tuple of device tensors
         self.module = module    # holds the BatchNorm buffers the warm-up must not advance
         self._graphs = {}
+        self._inflight = collections.deque()
 
     def _capture(self, inputs):
         dev = inputs[0].device
@@ -55,7 +66,14 @@ class StepGraphs:
         for s, t in zip(static, inputs):
             if s.data_ptr() != t.data_ptr():
                 s.copy_(t)
+        if MAX_AHEAD > 0:
+            while len(self._inflight) >= MAX_AHEAD:
+                self._inflight.popleft().synchronize()
         graph.replay()
+        if MAX_AHEAD > 0:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(inputs[0].device))
+            self._inflight.append(ev)
         return out
 
     def reset(self):

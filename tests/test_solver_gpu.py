@@ -103,8 +103,9 @@ def test_hip_graph_step_bit_identical(cuda, precision, grad_stream, B):
     """Solver(hip_graph=True) replays the captured forward+backward: three steps (the first
     captures) give bit-identical losses, parameters and BatchNorm running stats to eager,
     and a second input batch of the same shape is picked up by the replay — with the
-    weight-gradient side stream on and off (AVC_GRAD_STREAM), and at B=64, where the
-    persistent lstm2 forward is in the graph."""
+    weight-gradient side stream on and off (AVC_GRAD_STREAM; off, the Solver runs the step
+    eagerly even with hip_graph), and at B=64, where the persistent lstm2 forward is in the
+    graph."""
     import bench
     from autovc_amd import functional as AF
     res = []
