@@ -829,10 +829,7 @@ constexpr GemmShape kCfg[] = {
     {14, 128, 128, 32},  // cfg 9 with two k-stages of loads in flight
 };
 
-#ifndef AVC_GEMM_FORCE_CFG
-#define AVC_GEMM_FORCE_CFG -1
-#endif
-int g_force_cfg = AVC_GEMM_FORCE_CFG;  // tools/gemm_bench.hip overrides this
+int g_force_cfg = -1;  // tools/gemm_bench.hip overrides this
 // LDS (bytes per CU) that GEMM launches leave free for a latency-bound kernel on another
 // stream (autovc_gemm_set_lds_reserve): each workgroup is padded with unused dynamic LDS
 // so that the largest count that still fits in 160 KiB - reserve is also the most that fit.

@@ -169,17 +169,9 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
   return tile_gemm2<KCH, NW, D, BF>(lds, arow_of, brow_of, K, arow_of, brow_of, 0);
 }
 
-// configuration used by the product kernels (chosen with tools/lstm_step_bench.hip)
-#ifndef AVC_LSTM_KCH
-#define AVC_LSTM_KCH 64
-#endif
-#ifndef AVC_LSTM_NW
-#define AVC_LSTM_NW 8
-#endif
-#ifndef AVC_LSTM_D
-#define AVC_LSTM_D 2
-#endif
-constexpr int KCH = AVC_LSTM_KCH, NWV = AVC_LSTM_NW, DPF = AVC_LSTM_D;
+// configuration used by the product kernels (chosen with tools/lstm_step_bench.hip): k chunk,
+// waves per workgroup, chunks of loads in flight
+constexpr int KCH = 64, NWV = 8, DPF = 2;
 using TileP = Tile<KCH, NWV, DPF>;
 
 struct StepArgs {

@@ -43,44 +43,19 @@
 
 #include <hip/hip_runtime.h>
 
-// Diagnostic ablations (tools/lp_ablate.sh builds them into separate libraries; the product
-// build is LP_ABLATE 0): 1 = no grid barrier, 2 = no products, 3 = products without the h
-// loads (constant operands), 4 = no epilogue (no reduction, cell update or stores).
-#ifndef LP_ABLATE
-#define LP_ABLATE 0
-#endif
-// h groups in flight per stream
-#ifndef LP_PWIN
-#define LP_PWIN 1
-#endif
-// waves per workgroup: 4 (one per SIMD) or 8 (two per SIMD: one wave's MFMAs run while the
-// other waits for its h loads)
-#ifndef LP_NW
-#define LP_NW 8
-#endif
-// grid barrier: 0 = XCC counters -> top counter -> generation words (two atomic round trips
-// on the critical path); 2 = one counter replicated on 16 lines: every workgroup adds to
-// all 16 with one wave instruction (16 lanes) and polls its own XCC's replica (one atomic
-// round trip: MI355X_MICROARCH.md's replicated-counter hand-off); 1 = XCC counters only,
-// every waiting workgroup polls all of them —
-// measured 24.1 vs 20.2 us per wavefront step (256 pollers x 8 counters contend with the
-// arrivals: profiles/r02/lstm2_persist_ab_8wave.txt), kept as a diagnostic build only
-#ifndef LP_BARRIER
-#define LP_BARRIER 0
-#endif
-
 namespace {
 
 constexpr int PB = 64;             // batch rows per tile (all of them)
 constexpr int PU = 4;              // hidden units per tile (x 4 gates = 16 columns)
 constexpr int PC = 4 * PU;         // tile columns
-constexpr int PNW = LP_NW;         // waves per workgroup
+constexpr int PNW = 8;             // waves per workgroup: two per SIMD (one wave's MFMAs run
+                                   // while the other waits for its h loads)
 constexpr int PNT = 64 * PNW;
 constexpr int PRH = PNW == 16 ? 2 : 1;   // row halves: 16 waves = 8 k ranges x 2 row halves
 constexpr int PKWN = PNW / PRH;    // k ranges
 constexpr int PRB = PB / 16;       // 16-row blocks of the tile (4)
 constexpr int PRBW = PRB / PRH;    // 16-row blocks per wave
-constexpr int PWIN = LP_PWIN;      // h groups in flight per stream
+constexpr int PWIN = 1;            // h groups in flight per stream
 constexpr int RED_LD = PC + 1;     // padded row of a 64 x 16 partial tile in LDS
 constexpr int RED_SLOT = PB * RED_LD;
 constexpr int NSLOT = 4;                            // partial-tile slots (one layer at a time)
@@ -108,8 +83,7 @@ constexpr int BAR_ARRIVE = 17;     // 16 lines: per-XCC arrivals (cumulative)
 constexpr int BAR_TOP = 33;        // 1 line: XCC leaders arrived (cumulative)
 constexpr int BAR_GEN = 34;        // 16 lines: per-XCC generation released
 constexpr int BAR_ERR = 50;        // 1 line: timeout / error code
-constexpr int BAR_REP = 52;        // 16 lines: replicated arrival counters (LP_BARRIER 2)
-constexpr int BAR_LINES = 68;
+constexpr int BAR_LINES = 52;
 constexpr int64_t BAR_BYTES = BAR_LINES * L * 4;
 
 struct PArgs {
@@ -158,42 +132,11 @@ __device__ __noinline__ bool wait_ge(int* p, int target, int* err, int timeout_t
 // workgroup timed out (then every workgroup leaves the kernel).
 // xcc / mine / nx: this workgroup's XCC, the workgroups on it and the XCCs in use (held by
 // thread 0); *status: an LDS word broadcasting the outcome to the workgroup
-// polls every XCC's arrival counter (census[x] = workgroups on XCC x, 0 = unused) until each
-// has reached census[x] * (gen + 1); bounded like wait_ge
-__device__ __noinline__ bool wait_all_xcc(int* bar, const int (&census)[16], int gen, int timeout_ticks) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    bool all = true;
-    for (int x = 0; x < 16; ++x)
-      if (census[x] > 0 && ld_rlx(bar + (BAR_ARRIVE + x) * L) < census[x] * (gen + 1)) all = false;
-    if (all) return true;
-    if (ld_rlx(bar + BAR_ERR * L) != 0) return false;
-    __builtin_amdgcn_s_sleep(1);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)timeout_ticks) {
-      st_rlx(bar + BAR_ERR * L, 1);
-      return false;
-    }
-  }
-}
-
 __device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int nx, const int (&census)[16],
                                           int* status, int gen) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's stores are in L2
   __syncthreads();
-  if (LP_BARRIER == 2) {
-    if (threadIdx.x < 16) add_rlx(a.bar + (BAR_REP + threadIdx.x) * L, 1);   // one wave instruction, 16 replicas
-    if (threadIdx.x == 0) {
-      const bool ok = wait_ge(a.bar + (BAR_REP + xcc) * L, (int)gridDim.x * (gen + 1), a.bar + BAR_ERR * L,
-                              a.timeout_ticks);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)
-      *status = ok ? 0 : 1;
-    }
-  } else if (threadIdx.x == 0 && LP_BARRIER == 1) {
-    add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
-    const bool ok = wait_all_xcc(a.bar, census, gen, a.timeout_ticks);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only (sc1 loads follow)
-    *status = ok ? 0 : 1;
-  } else if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     bool ok = true;
     const int old = add_rlx(a.bar + (BAR_ARRIVE + xcc) * L, 1);
     if (old == mine * (gen + 1) - 1) {                    // last of this XCC
@@ -209,7 +152,7 @@ __device__ __forceinline__ bool grid_sync(const PArgs& a, int xcc, int mine, int
   return *status == 0;
 }
 
-// grid_sync (LP_BARRIER 0) in two halves, so a workgroup can work between its arrival and
+// grid_sync in two halves, so a workgroup can work between its arrival and
 // the release: grid_arrive publishes this workgroup's hand-off (the last arriver of the last
 // XCC opens every gate), grid_wait polls this XCC's gate
 __device__ __forceinline__ void grid_arrive(const PArgs& a, int xcc, int mine, int nx, int gen) {
@@ -236,12 +179,15 @@ __device__ __forceinline__ bool grid_wait(const PArgs& a, int xcc, int* status, 
 }
 
 // Sticky per-device fault word: a launch whose grid barrier timed out (its workgroups were
-// not all resident at once — e.g. another process's kernels held part of the chip) ORs
-// kFaultPersistBarrier into it, after writing NaN over every h and c it owns, so the
-// failure reaches the loss.  The host reads and clears it at its sync points
-// (autovc_fault_status: Solver log steps, bench.py) and raises.
+// not all resident at once — e.g. another process's kernels held part of the chip) ORs its
+// kernel family's bit into it, after writing NaN over every output it owns, so the failure
+// reaches the loss.  The host reads and clears it at its sync points (autovc_fault_status:
+// Solver log steps, bench.py) and raises, naming the kernel (autovc_amd.functional).
 __device__ int g_avc_fault = 0;
-constexpr int kFaultPersistBarrier = 1;
+constexpr int kFaultLstm2Persist = 1;    // lstm_persist_kernel, two layers (decoder lstm2 forward)
+constexpr int kFaultLstmXcdFwd = 2;      // lstm_xcd_fwd_kernel (decoder lstm1 forward)
+constexpr int kFaultLstmXcdBwd = 4;      // lstm_xcd_bwd_kernel (decoder lstm1 backward, opt-in)
+constexpr int kFaultLstm1Persist = 8;    // lstm_persist_kernel, one layer (opt-in)
 int g_timeout_ticks = 0;             // 0 = the default 1 s; tests force a timeout with a tiny value
 
 // per-step cell update of one (batch row b, unit j) from its 4 gate pre-activations
@@ -322,7 +268,6 @@ __device__ __forceinline__ void gemm_wave(const float* __restrict__ hk0_t, const
   const uint32_t off0 = (uint32_t)((kb0 * B + 16 * rb0 + (lane & 15)) * 16);
   const uint32_t gstride = (uint32_t)B * 16;
   auto ld = [&](__amdgpu_buffer_rsrc_t r, int g, int rb) {
-    if (LP_ABLATE == 3) return f32x4{0.5f, 0.25f, (float)g, (float)rb};
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off0 + g * gstride + rb * 256, 0, 16));
   };
   f32x4 a0[PWIN][PRBW], a1[PWIN][PRBW];
@@ -453,7 +398,9 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
           a.c1[((int64_t)eb * T + t) * H + ej] = nan;
         }
       }
-    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0)
+      __hip_atomic_fetch_or(&g_avc_fault, TWO ? kFaultLstm2Persist : kFaultLstm1Persist, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
   };
 
   // ---- start: census of workgroups per XCC (the barrier's groups)
@@ -653,7 +600,7 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
     const float* hk1 = a.hk1 + (int64_t)(t >= 2 ? t - 2 : 0) * BH;   // h1_{t-2}
     const __bf16* hk0b = a.hk0b + (int64_t)(t >= 1 ? t - 1 : 0) * BH;
     const __bf16* hk1b = a.hk1b + (int64_t)(t >= 2 ? t - 2 : 0) * BH;
-    if (LP_ABLATE == 2 || t == 0) {                                  // h0_{-1} = 0: no products
+    if (t == 0) {                                                    // h0_{-1} = 0: no products
     } else if constexpr (BF) {
       if (!TWO) gemm_wave_bf<NS, false, true, false>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
       else if (t == 1) gemm_wave_bf<NS, true, true, false>(hk0b, hk1b, whb, W0b, W1b, k8_0, B, rb0, lane, acc1, acc0);
@@ -665,49 +612,44 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
       else if (t < T) gemm_wave<KL, true, true, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);
       else gemm_wave<KL, true, false, true>(hk0, hk1, wh, W0, W1, kb0, B, rb0, lane, acc1, acc0);   // t == T
     }
-    if (LP_ABLATE != 4) {
-      // the 4 waves' partial tiles summed through LDS in fixed order
-      auto sum = [&](int layer, int g) {
-        const float* r = red + layer * NSLOT * RED_SLOT + eb * RED_LD + g * PU + eu;
-        return ((r[0] + r[RED_SLOT]) + r[2 * RED_SLOT]) + r[3 * RED_SLOT];
-      };
-      // more than 4 waves: wave w < 4 stores its tile into slot w, then waves 4..7 add into
-      // slots 0..3, then waves 8..11, ... (fixed order)
-      auto reduce_put = [&](float* slots, const f32x4 (&acc)[PRBW]) {
-        if (kw < 4) put_tile(slots + (kw & 3) * RED_SLOT, acc, rb0, lane);
+    // the 4 waves' partial tiles summed through LDS in fixed order
+    auto sum = [&](int layer, int g) {
+      const float* r = red + layer * NSLOT * RED_SLOT + eb * RED_LD + g * PU + eu;
+      return ((r[0] + r[RED_SLOT]) + r[2 * RED_SLOT]) + r[3 * RED_SLOT];
+    };
+    // more than 4 waves: wave w < 4 stores its tile into slot w, then waves 4..7 add into
+    // slots 0..3, then waves 8..11, ... (fixed order)
+    auto reduce_put = [&](float* slots, const f32x4 (&acc)[PRBW]) {
+      if (kw < 4) put_tile(slots + (kw & 3) * RED_SLOT, acc, rb0, lane);
 #pragma unroll
-        for (int ph = 1; ph < PKWN / 4; ++ph) {
-          __syncthreads();
-          if (kw / 4 == ph) add_tile(slots + (kw & 3) * RED_SLOT, acc, rb0, lane);
-        }
-      };
-      if (TWO) {
-        reduce_put(red, acc1);
+      for (int ph = 1; ph < PKWN / 4; ++ph) {
         __syncthreads();
-        if (wave < 4 && l1) {                                        // layer 1 at step t - 1 (eown)
-          float pre[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + bias1[g];
-          const int t1 = t - 1;
-          out1 = cell(pre, out1.c);
-          handoff<BF>(out1.h, a.hk1 + (int64_t)t1 * BH, a.hk1b + (int64_t)t1 * BH, B, eb, ej, lane);
-        }
-        __syncthreads();                                             // slots reused for layer 0
+        if (kw / 4 == ph) add_tile(slots + (kw & 3) * RED_SLOT, acc, rb0, lane);
       }
-      reduce_put(red, acc0);
+    };
+    if (TWO) {
+      reduce_put(red, acc1);
       __syncthreads();
-      if (wave < 4 && l0) {                                          // layer 0 at step t (eown)
+      if (wave < 4 && l1) {                                        // layer 1 at step t - 1 (eown)
         float pre[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + gxv[g];
-        out0 = cell(pre, out0.c);
-        handoff<BF>(out0.h, a.hk0 + (int64_t)t * BH, a.hk0b + (int64_t)t * BH, B, eb, ej, lane);
+        for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + bias1[g];
+        const int t1 = t - 1;
+        out1 = cell(pre, out1.c);
+        handoff<BF>(out1.h, a.hk1 + (int64_t)t1 * BH, a.hk1b + (int64_t)t1 * BH, B, eb, ej, lane);
       }
-    } else if (wave == 0 && acc1[0][0] == 12345.f && acc0[1][1] == 12345.f) {
-      a.h0[0] = 0.f;                                                  // keep the products live
+      __syncthreads();                                             // slots reused for layer 0
     }
-    if (LP_ABLATE == 1) __syncthreads();
-    else if (t < last && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, census, status, t)) {
+    reduce_put(red, acc0);
+    __syncthreads();
+    if (wave < 4 && l0) {                                          // layer 0 at step t (eown)
+      float pre[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pre[g] = sum(0, g) + gxv[g];
+      out0 = cell(pre, out0.c);
+      handoff<BF>(out0.h, a.hk0 + (int64_t)t * BH, a.hk0b + (int64_t)t * BH, B, eb, ej, lane);
+    }
+    if (t < last && !grid_sync(a, xcc_id, xcc_wgs, xcc_n, census, status, t)) {
       fail();
       return;
     }
@@ -801,37 +743,6 @@ constexpr int XNT = 256;               // 4 waves
 constexpr int XC_CENSUS = 0, XC_STEP = 16, XC_ERR = 32, XC_LINES = 33;
 constexpr int64_t XC_BYTES = XC_LINES * L * 4;
 constexpr int XC_PAD_LDS = 96 * 1024;  // dynamic LDS that keeps one workgroup per CU
-// Diagnostic timeline (tools only: tools/build_variant.sh xstamp -DXCD_STAMP=1, then
-// tools/xcd_stamps.py): thread 0 of every workgroup records s_memrealtime at the phase
-// boundaries of steps 1..kXS of the forward kernel; the product build is XCD_STAMP 0.
-#ifndef XCD_STAMP
-#define XCD_STAMP 0
-#endif
-// 1: B fragments loaded per wave straight from global memory (plain loads, no LDS staging):
-// measured 5.05 / 3.96 us per step (fp32 / bf16) against 3.86 / 1.98 for the coalesced LDS
-// staging (profiles/r03/lstm_xcd_time.txt) — diagnostic build only
-#ifndef XCD_DIRECT
-#define XCD_DIRECT 0
-#endif
-// 1: fp32 products on v_mfma_f32_4x4x1_16b_f32: the group's 8 batch rows fill all 16 blocks
-// (4 column groups x 2 row groups x 2 halves of K), where the 16x16x4 form computes 16 batch
-// lanes of which 8 are real — half the MFMA cycles, the W fragments in 256 registers.  Measured
-// 3.90 vs 3.85 us per step and 15.38-15.46 vs 15.44-15.46 ms per training step
-// (profiles/r03/ab_xcd_mf4.txt): the products are not what bounds the step; diagnostic build.
-#ifndef XCD_MF4
-#define XCD_MF4 0
-#endif
-#if XCD_STAMP
-constexpr int kXS = 16, kXP = 8;
-__device__ unsigned long long g_xcd_stamp[XNX * XSL * kXS * kXP];
-#define XSTAMP(t, ph)                                                                                \
-  do {                                                                                              \
-    if (tid == 0 && (t) >= 1 && (t) <= kXS)                                                         \
-      g_xcd_stamp[((xcc * XSL + slot) * kXS + (t) - 1) * kXP + (ph)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define XSTAMP(t, ph) do { } while (0)
-#endif
 
 struct XArgs {
   int B, T;
@@ -893,31 +804,17 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
         a.h[(int64_t)(r0 + cb) * a.h_ldb + (int64_t)t * a.h_ldt + u0 + cu] = nan;
         a.c[((int64_t)(r0 + cb) * T + t) * HH + u0 + cu] = nan;
       }
-    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdFwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   if (s_info[2]) {
     if (s_info[0] < XNX && s_info[1] < XSL) fail();   // an in-range slot of a failed group
-    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdFwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   // W fragments: wave = gate, lane -> column u0 + lane % 16, k = 128 (lane / 16) + q
-  constexpr bool MF4 = !BF && XCD_MF4 && !XCD_DIRECT;
-  constexpr int KH = HH / 2;             // 4x4x1 form: k per half
-  float wf[BF || MF4 ? 1 : KG];
+  float wf[BF ? 1 : KG];
   bf16x8 wb[BF ? KG / 8 : 1];
-  // 4x4x1 form: lane 4 b + i, block b = (column group cg = b & 3, row group rg = (b >> 2) & 1,
-  // K half kh = b >> 3): A = W[gate][u0 + 4 cg + i][kh KH + s], B = h[4 rg + i][kh KH + s]
-  [[maybe_unused]] const int m4b = lane >> 2, m4i = lane & 3;
-  [[maybe_unused]] const int m4cg = m4b & 3, m4rg = (m4b >> 2) & 1, m4kh = m4b >> 3;
-  float w4[MF4 ? KH : 1];
-  if constexpr (MF4) {
-    const float* src = a.W + (int64_t)(wave * HH + u0 + 4 * m4cg + m4i) * HH + KH * m4kh;
-#pragma unroll
-    for (int q = 0; q < KH; q += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + q);
-      w4[q] = v[0]; w4[q + 1] = v[1]; w4[q + 2] = v[2]; w4[q + 3] = v[3];
-    }
-  } else if constexpr (BF) {
+  if constexpr (BF) {
     // k of MFMA q, lane group g, element e: KG g + 8 q + e (A and B alike)
     const __bf16* src = a.Wb + (int64_t)(wave * HH + u0 + (lane & 15)) * HH + KG * (lane >> 4);
 #pragma unroll
@@ -946,7 +843,6 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
   int* step_ctr = a.bar + (XC_STEP + xcc) * L;
   for (int t = 0; t < T; ++t) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    XSTAMP(t, 0);
     if (t > 0) {
       // ---- XCD barrier: all 32 slots stored h_{t-1}
       if (tid == 0) {
@@ -963,57 +859,10 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
         s_info[2] = ok ? 0 : 1;
       }
       __syncthreads();
-      XSTAMP(t, 1);
       if (s_info[2]) {
         fail();
         return;
       }
-#if XCD_DIRECT
-      // ---- every wave loads its own B fragments straight from global memory, a chunk
-      // ahead of its MFMAs: lane (batch l % 16, k group l / 16) reads h_{t-1}[row][KG g ..
-      // KG g + KG) — PLAIN loads: every h_{t-1} address is read once per launch, after the
-      // barrier, by a CU that never loaded it before in this launch (and a kernel start
-      // invalidates L1), so no L1 line can be stale; the line then serves the wave's next
-      // 16-B pieces from L1 and the other 3 waves of the CU
-      {
-        const bool bval = (lane & 15) < XRB;
-        const float* src = a.h + (int64_t)(r0 + (bval ? (lane & 15) : 0)) * a.h_ldb + (int64_t)(t - 1) * a.h_ldt +
-                           KG * (lane >> 4);
-        constexpr int CH = BF ? 16 : 8;            // floats per chunk
-        constexpr int NC = KG / CH;
-        f32x4 nb[CH / 4];
-        auto ld = [&](int c) {
-#pragma unroll
-          for (int i = 0; i < CH / 4; ++i)
-            nb[i] = bval ? *reinterpret_cast<const f32x4*>(src + c * CH + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
-        };
-        ld(0);
-        XSTAMP(t, 2);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          f32x4 cur[CH / 4];
-#pragma unroll
-          for (int i = 0; i < CH / 4; ++i) cur[i] = nb[i];
-          if (c + 1 < NC) ld(c + 1);
-          if constexpr (BF) {
-#pragma unroll
-            for (int j = 0; j < CH / 8; ++j) {
-              const f32x4 lo = cur[2 * j], hi = cur[2 * j + 1];
-              const bf16x8 bv = {(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
-                                 (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[c * (CH / 8) + j], bv, acc, 0, 0, 0);
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < CH / 4; ++i)
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c * CH + 4 * i + e], cur[i][e], acc, 0, 0, 0);
-          }
-        }
-      }
-    }
-#else
       // ---- stage h_{t-1} of the group's 8 rows (sc1 loads: L1 bypassed, L2-served)
       {
         // wave-instruction i of wave w moves 1 KB chunk 4w + i of the 8 rows (whole lines per
@@ -1039,23 +888,7 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
         }
       }
       __syncthreads();
-      XSTAMP(t, 2);
-      if constexpr (MF4) {
-        // four independent accumulator chains, then the two K halves (lanes l and l ^ 32)
-        const float* hb4 = hs + (4 * m4rg + m4i) * HS + KH * m4kh;
-        f32x4 a4[4] = {};
-#pragma unroll
-        for (int q = 0; q < KH; q += 4) {
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(hb4 + q);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) a4[e] = __builtin_amdgcn_mfma_f32_4x4x1f32(w4[q + e], bv[e], a4[e], 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          acc[r] = (a4[0][r] + a4[1][r]) + (a4[2][r] + a4[3][r]);
-          acc[r] += __shfl_xor(acc[r], 32);
-        }
-      } else if constexpr (BF) {
+      if constexpr (BF) {
 #pragma unroll
         for (int q = 0; q < KG / 8; ++q)
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[q], *reinterpret_cast<const bf16x8*>(hrowb + 8 * q), acc,
@@ -1071,21 +904,12 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
         }
       }
     }
-#endif
-    XSTAMP(t, 3);
-    if constexpr (MF4) {
-      // block b < 8 (K half 0, both halves summed): D[r][j] in lane 4 b + j, register r =
-      // column 4 cg + r, batch row 4 rg + j
-      if (lane < 32)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pre[(wave * U + 4 * m4cg + r) * (XRB + 1) + 4 * m4rg + m4i] = acc[r];
-    } else if ((lane & 15) < XRB) {
+    if ((lane & 15) < XRB) {
       // C[unit 4 (lane / 16) + r][batch lane % 16] of gate `wave`
 #pragma unroll
       for (int r = 0; r < 4; ++r) pre[(wave * U + 4 * (lane >> 4) + r) * (XRB + 1) + (lane & 15)] = acc[r];
     }
     __syncthreads();
-    XSTAMP(t, 4);
     if (cown) {
       float p[4];
 #pragma unroll
@@ -1100,10 +924,8 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
     // ---- arrive once h_t (only it) is in the XCD's L2; c / gates and the next gx loads
     // go out after the arrive, under the next step's wait
     if (t + 1 < T) {
-      XSTAMP(t, 5);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      XSTAMP(t, 6);
       if (tid == 0) add_l2(step_ctr, 1);
     }
     if (cown) {
@@ -1175,11 +997,11 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
       for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q) a.dG[(cell0 + t) * K4 + q * HH + u0 + cu] = nan;
-    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdBwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   if (s_info[2]) {
     if (s_info[0] < XNX && s_info[1] < XSL) fail();
-    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultPersistBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdBwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   // A fragments: lane -> unit u0 + lane % 16, k = KW wave + KG (lane / 16) + q: W_hh[k][unit]
@@ -1489,7 +1311,7 @@ extern "C" int autovc_lstm_persist_set_timeout_ticks(int ticks) {
   return avc::kOk;
 }
 
-// The device fault word (bit 0: a persistent LSTM launch's grid barrier timed out) after
+// The device fault word (one bit per persistent kernel family whose barrier timed out) after
 // everything queued on `stream`; synchronises the stream.  clear != 0 resets it.
 extern "C" int autovc_fault_status(hipStream_t stream, int clear, int* out) {
   AVC_CHECK_ARG(out != nullptr, "autovc_fault_status: null out");
@@ -1507,9 +1329,3 @@ extern "C" int autovc_fault_status(hipStream_t stream, int clear, int* out) {
   return avc::kOk;
 }
 
-#if XCD_STAMP
-extern "C" int autovc_xcd_stamps(unsigned long long* out) {
-  AVC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xcd_stamp), sizeof(g_xcd_stamp)), "autovc_xcd_stamps");
-  return avc::kOk;
-}
-#endif

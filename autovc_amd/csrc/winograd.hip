@@ -278,16 +278,10 @@ __global__ void wino_wgrad_kernel(int64_t n, const float* __restrict__ Mt, float
 // atomics), every load of a wave is issued before its first use, and the input-type
 // transforms read each frame of the wave's window (4 kTPW + 4 frames) once instead of
 // twice (neighbouring tiles share their 4 halo frames).
-#ifndef WINO_TPW
-#define WINO_TPW 1
-#endif
-#ifndef WINO_WAVES
-#define WINO_WAVES 8
-#endif
-constexpr int kTPW = WINO_TPW;           // tiles per wave: 4 (1024 waves, halo frames shared)
+constexpr int kTPW = 1;                  // tiles per wave: 4 (1024 waves, halo frames shared)
                                          // measured 16.11-16.21 vs 16.00 ms/step for 1 (4096 waves),
                                          // profiles/r03/ab_conv_chain.txt
-constexpr int kWaves = WINO_WAVES;       // waves per block
+constexpr int kWaves = 8;                // waves per block
 constexpr int kThreads = 64 * kWaves;
 constexpr int kTPB = kWaves * kTPW;
 constexpr int kWin = 4 * kTPW + 4;       // frames of a wave's window: 4q0 - 2 .. 4(q0 + kTPW) + 1

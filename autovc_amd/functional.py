@@ -1228,20 +1228,30 @@ class DeviceFault(RuntimeError):
     """A kernel reported a failure through the device fault word (autovc_fault_status)."""
 
 
+# fault-word bits (csrc/lstm2_persist.hip) -> (kernel, what it overwrote, the switch that avoids it)
+_FAULT_BITS = (
+    (1, "lstm_persist_kernel, two layers (decoder lstm2 forward)", "h/c", "AVC_LSTM2_PERSIST=0"),
+    (2, "lstm_xcd_fwd_kernel (decoder lstm1 forward)", "h/c", "AVC_LSTM_XCD=0"),
+    (4, "lstm_xcd_bwd_kernel (decoder lstm1 backward)", "gate gradients", "AVC_LSTM_XCD_BWD=0"),
+    (8, "lstm_persist_kernel, one layer (decoder lstm1 forward)", "h/c", "AVC_LSTM_PERSIST=0"),
+)
+
+
 def check_device_faults(device=None):
     """Raise DeviceFault if a persistent LSTM launch's grid barrier timed out since the
-    last check (the launch then wrote NaN over its h / c, so the losses are NaN too).
+    last check (the launch then wrote NaN over its outputs, so the losses are NaN too).
     Synchronises the current stream: called at the Solver's log steps and by bench.py,
     never per iteration."""
     import ctypes
     v = ctypes.c_int(0)
     _lib.call("autovc_fault_status", _lib.stream_ptr(device), 1, ctypes.byref(v))
-    if v.value & 1:
+    hit = [f for f in _FAULT_BITS if v.value & f[0]]
+    if hit:
+        names = "; ".join(f"{k} (its {what} were overwritten with NaN; {env} avoids it)" for _, k, what, env in hit)
         raise DeviceFault(
-            "lstm_persist_kernel (decoder lstm2 forward): a grid barrier timed out — its 256 workgroups were "
-            "not all resident at once (another process's kernels held part of the GPU?); the forward's h/c were "
-            "overwritten with NaN.  Run one training process per GPU (INTEGRATION.md, Co-residency) or set "
-            "AVC_LSTM2_PERSIST=0.")
+            f"persistent kernel grid barrier timed out: {names}.  Its workgroups were not all resident at once "
+            "(another process's kernels held part of the GPU?): run one training process per GPU "
+            "(INTEGRATION.md, Co-residency).")
 
 
 # the single-layer recurrence (decoder lstm1, H = 512) the same way — opt-in

@@ -331,10 +331,12 @@ class WaveNet(nn.Module):
                       pre.data_ptr(), chunk, int(seed) & ((1 << 64) - 1), int(utt_base), float(log_scale_min),
                       _lib.ptr(tch), 0 if tch is None else tch.shape[1], y.data_ptr(), _lib.ptr(mol),
                       ws.data_ptr(), int(graph_steps), stream)
-        # the XCD-local generation poisons its outputs and sets a fault word if a phase wait
-        # timed out (its 32 workgroups per XCD were not all resident): surface it here
+        # the XCD-local generation (opt-in) poisons its outputs and sets a fault word if a phase
+        # wait timed out (its 32 workgroups per XCD were not all resident): surface it here.
+        # Reading the word synchronises the device, so only that mode pays for it.
         fault = ctypes.c_int(0)
-        _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(fault))
+        if lib.autovc_wavenet_get_xcd():
+            _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(fault))
         if fault.value:
             raise RuntimeError("wn_xcd_kernel (XCD-local WaveNet generation): a per-XCD phase wait timed out — "
                                "its workgroups were not all resident (another process on this GPU?); outputs are NaN. "

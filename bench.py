@@ -568,12 +568,14 @@ def main():
 
     # test hook (tests/test_bench_multirank, 1-GPU boxes): every rank on cuda:0 over gloo, to
     # exercise the N > 1 flow (sharding, barriers, max-over-ranks timing) without 2 GPUs.
-    # The persistent lstm2 forward needs every CU to itself (all 256 workgroups co-resident,
-    # INTEGRATION.md "Co-residency"): two processes' grids on one device could each hold
-    # part of the chip, so ranks sharing a device use the per-step launches.
+    # Every persistent kernel (lstm2 forward, XCD-local lstm1 forward / backward, the opt-in
+    # single-layer persistent forward) needs every CU to itself (all 256 workgroups
+    # co-resident, INTEGRATION.md "Co-residency"): two processes' grids on one device could
+    # each hold part of the chip, so ranks sharing a device use the per-step launches.
     share = os.environ.get("AVC_BENCH_SHARE_DEVICE") == "1"
     if share:
-        os.environ["AVC_LSTM2_PERSIST"] = "0"
+        for k in ("AVC_LSTM2_PERSIST", "AVC_LSTM_XCD", "AVC_LSTM_XCD_BWD", "AVC_LSTM_PERSIST"):
+            os.environ[k] = "0"
     from autovc_amd import ddp
     rank, world = ddp.init_from_env(backend="gloo" if share else None)
     if world != args.gpus:

@@ -2,7 +2,7 @@
 (/root/reference/model_vc_mel.py, model_vc_stft.py and solver_encoder.Solver.train), in the
 build container only.  The reference never travels: only the arrays written here do.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_generator_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_generator_golden.py [--spread | --b64]
 
 Inputs: the bundled spmel crops spmel/p225/p225_003.npy[:128], spmel/p226/p226_003.npy[:128]
 (also under tests/golden/frontend/) and the bundled embeddings emb_org_mel.npy (2, 256).
@@ -212,8 +212,37 @@ def main_spread(out_path=os.path.join(HERE, "generator_spread.npz")):
     print("wrote", out_path)
 
 
+def main_b64(out_path=os.path.join(HERE, "generator_b64_traj.npz")):
+    """The reference at BASELINE config 2's shape (B=64, T=128): the Solver-composed step
+    (+ torch Adam) for 10 steps on bench.py's synthetic batch (seed 1234, one
+    batch reused every step, as bench.py times it), from the same deterministic weights —
+    in float32 on 8 threads (the pin), float64 and float32 on 1 thread (the reference's own
+    spread, which sets the tolerance as for the B=2 trajectory).  The batch itself is not
+    stored (2.6 MB): its float64 sum and a hash pin that the GPU test regenerated the same
+    one."""
+    import hashlib
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    _stub_modules()
+    sys.path.insert(0, REF)
+    import model_vc_mel as ref_mel  # reference
+    sys.path.insert(0, ROOT)
+    import bench
+    xt, et = bench.synthetic_batch(64, 128, torch.device("cpu"), 1234)
+    sd = deterministic_state_dict(ref_mel.Generator(32, 256, 512, 32).state_dict())
+    traj32, _ = _reference_steps(ref_mel, sd, xt, et, torch.float32, 8, 10)
+    traj64, _ = _reference_steps(ref_mel, sd, xt, et, torch.float64, 8, 10)
+    traj_t1, _ = _reference_steps(ref_mel, sd, xt, et, torch.float32, 1, 10)
+    digest = hashlib.sha256(xt.numpy().tobytes() + et.numpy().tobytes()).hexdigest()
+    np.savez_compressed(out_path, traj=traj32, traj_f64=traj64, traj_t1=traj_t1, batch_sha256=np.array(digest),
+                        x_sum=np.float64(xt.double().sum()), e_sum=np.float64(et.double().sum()))
+    print("wrote", out_path, traj32.tolist())
+
+
 if __name__ == "__main__":
     if "--spread" in sys.argv:
         main_spread()
+    elif "--b64" in sys.argv:
+        main_b64()
     else:
         main()

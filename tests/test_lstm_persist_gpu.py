@@ -247,8 +247,10 @@ def test_xcd_local_lstm_timeout_surfaces(cuda):
     finally:
         _lib.call("autovc_lstm_persist_set_timeout_ticks", 0)
     assert bool(torch.isnan(h[:, -1]).any())
-    with pytest.raises(AF.DeviceFault):
+    # the fault names this kernel and its own switch (not the lstm2 forward's)
+    with pytest.raises(AF.DeviceFault, match="lstm_xcd_fwd_kernel.*AVC_LSTM_XCD=0") as ei:
         AF.check_device_faults(cuda)
+    assert "AVC_LSTM2_PERSIST" not in str(ei.value)
 
 
 @pytest.mark.parametrize("T", [1, 2, 128])

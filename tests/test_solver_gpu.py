@@ -236,3 +236,55 @@ def test_weight_scope_step_bit_identical(cuda, precision, chain):
         assert torch.equal(a, b)
     for a, b in zip(pa, pb):
         assert torch.equal(a, b)
+
+
+B64 = os.path.join(GOLDEN, "generator_b64_traj.npz")
+
+
+def _b64_tolerance(R):
+    """max(5 %, 2 x the reference's own divergence envelope at B=64) per step and loss, as
+    parity_tol.trajectory_tolerance does for the B=2 golden (float64 and float32-on-1-thread
+    reruns of the reference against its float32 pin, generator_b64_traj.npz)."""
+    ref = R["traj"]
+    spread = np.maximum(np.abs(R["traj_f64"] - ref), np.abs(R["traj_t1"] - ref)) / np.abs(ref)
+    return np.maximum(0.05, 2.0 * np.maximum.accumulate(spread, axis=0))
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_b64_graph_trajectory_matches_reference(cuda, precision):
+    """BASELINE config 2's product path — B=64, T=128, every step a captured-graph replay
+    (persistent lstm2 two-step wavefront, XCD-local lstm1 forward, fused Conv-BN stacks, the
+    weight-gradient side stream) — for 10 Solver steps against the REFERENCE Generator +
+    Solver loss + Adam run at the same shape from the same weights and batch
+    (tests/golden/make_generator_golden.py --b64).  Step 1 within 1e-4 rel; steps 2-10
+    within the reference's own spread bound (>= 5 %).  bf16 (config 3): within 5 % of the
+    fp32 reference's g_loss at every step."""
+    import hashlib
+    import bench
+    R = np.load(B64)
+    x, e = bench.synthetic_batch(64, 128, torch.device("cpu"), 1234)
+    assert hashlib.sha256(x.numpy().tobytes() + e.numpy().tobytes()).hexdigest() == str(R["batch_sha256"])
+    s = _solver()
+    s.G.train()
+    s.precision = precision
+    s.hip_graph = True
+    x, e = x.to(cuda), e.to(cuda)
+    traj = []
+    for _ in range(10):
+        _, a, b, c = s.train_step(x, e)
+        traj.append(torch.stack([a.reshape(()), b.reshape(()), c.reshape(())]).clone())
+    torch.cuda.synchronize()
+    from autovc_amd import functional as AF
+    AF.check_device_faults(cuda)
+    traj = torch.stack(traj).double().cpu().numpy()
+    ref = R["traj"]
+    dev = np.abs(traj - ref) / np.abs(ref)
+    if precision == "fp32":
+        assert dev[0].max() < 1e-4, dev[0]
+        tol = _b64_tolerance(R)
+        assert np.all(dev <= tol), {"deviation": dev.round(5).tolist(), "tolerance": tol.round(4).tolist()}
+    else:
+        # the Solver's objective g_loss = id + id_psnt + cd (lambda_cd = 1), as
+        # test_bf16_gpu.py::test_bf16_training_loss_tracks_fp32 bounds it
+        gap = np.abs(traj.sum(1) - ref.sum(1)) / ref.sum(1)
+        assert np.all(gap <= 0.05), {"g_loss gap": gap.round(5).tolist(), "per-loss": dev.round(4).tolist()}
