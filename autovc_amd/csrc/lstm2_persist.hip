@@ -380,7 +380,13 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
   constexpr int H = HH;
   const int B = a.B, T = a.T;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j0 = blockIdx.x * PU;
+  // XCD-aware unit blocks: workgroups are dispatched round-robin over the 8 XCDs, so block
+  // b (on XCD b % 8) owns unit block (b % 8) * (grid / 8) + b / 8 — each XCD's workgroups own
+  // one contiguous run of H / 8 units, and the 16-B row pieces of h / c / gates that
+  // neighbouring units write meet in that XCD's (write-back) L2 as whole lines instead of
+  // leaving it as partial-line writes (PMC WRITE_SIZE 853 MB per launch with b -> block b)
+  const int nxb = (int)gridDim.x / 8;
+  const int j0 = ((int)blockIdx.x % 8 * nxb + (int)blockIdx.x / 8) * PU;
   auto grow = [&](int col) { return (col >> 2) * H + j0 + (col & 3); };   // tile column -> gate row
   // epilogue ownership: thread e owns (batch row e / 4, unit j0 + e % 4) of both layers
   const int eb = tid >> 2, ej = j0 + (tid & 3), eu = tid & 3;

@@ -47,22 +47,6 @@
 
 namespace {
 
-// Diagnostic timeline (tools/wn_stamps.sh builds it into a separate library; the product
-// build is WN_STAMP 0): lane 0 of wave 0 (gate) and of wave kGW (residual) of every
-// workgroup records s_memrealtime (100 MHz, one clock for the whole chip) at the phase
-// boundaries of the kernel for ONE chosen sample step; autovc_wavenet_stamps reads them.
-#ifndef WN_STAMP
-#define WN_STAMP 0
-#endif
-#if WN_STAMP
-constexpr int kStampLaunch = 64, kStampWG = 512, kStampN = 8;
-__device__ unsigned long long g_wn_stamp[kStampLaunch * kStampWG * kStampN];
-__device__ int g_wn_stamp_t = -1;
-#define WN_NOW() __builtin_amdgcn_s_memrealtime()
-// the value must have arrived before the clock is read
-#define WN_AFTER(v) asm volatile("" ::"v"(v))
-#endif
-
 constexpr float kSqrtHalf = 0.70710677f;  // float(math.sqrt(0.5))
 constexpr int kBT = 8;                    // utterances per batch tile
 constexpr int kMaxNO = 32;                // MoL head width limit (3 x up to 10 mixtures)
@@ -308,27 +292,15 @@ constexpr int kRP = 2;                    // gate pairs per workgroup
 constexpr int kUB = 4;                    // utterances per workgroup
 constexpr int kGC = 3;                    // chunks of the critical GEMV [g_(l-1) | x_(l-1)(t)]:
                                           // H + R = 768 = 3 x 256 for r9y9
-#ifndef WN_GSPLIT
-#define WN_GSPLIT 2
-#endif
-constexpr int kGS = WN_GSPLIT;            // gate-row groups: 1 = a wave takes all 4 rows of its
+constexpr int kGS = 2;            // gate-row groups: 1 = a wave takes all 4 rows of its
                                           // chunk, 2 = two waves per chunk, 2 rows each
 constexpr int kGW = kGC * kGS;            // gate waves
 constexpr int kWR = 2 * kRP / kGS;        // gate rows per gate wave
-#ifndef WN_RW
-#define WN_RW 2
-#endif
-constexpr int kRW = WN_RW;                // residual waves
+constexpr int kRW = 2;                // residual waves
 constexpr int kResRows = 8 / kRW;         // residual rows per residual wave (>= kRP*(R+S)/H / kRW)
 constexpr int kLayerThreads = 64 * (kGW + kRW);
-#ifndef WN_TW
-#define WN_TW 4
-#endif
-constexpr int kTailWaves = WN_TW;         // tail / head: one wave per output row
-#ifndef WN_PR
-#define WN_PR 32
-#endif
-constexpr int kPR = WN_PR;                // past-tap workgroups: gate rows per workgroup (16, 32 or 64)
+constexpr int kTailWaves = 4;         // tail / head: one wave per output row
+constexpr int kPR = 32;                // past-tap workgroups: gate rows per workgroup (16, 32 or 64)
 constexpr int kPRT = kPR / 16;            // 16-row MFMA tiles per workgroup
 
 // MoL head output of the previous step: the head kernel's row-block workgroups (kHR rows
@@ -394,10 +366,6 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   __shared__ float s_in[kUB];
   __shared__ float s_red[kGW][kWR * kUB];
   __shared__ int s_arrived;
-#if WN_STAMP
-  unsigned long long st[kStampN] = {};
-  st[0] = WN_NOW();
-#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kUB;
   const int nb = min(kUB, a.B - b0);
@@ -513,12 +481,6 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
   }
   if (threadIdx.x == 0) s_arrived = 0;
   lds_barrier();                            // (layer >= 1: the loads above stay in flight)
-#if WN_STAMP
-  st[1] = WN_NOW();
-  if (gate) { const float xf = x0[0][0] + x0[kUB - 1][3] + w0[0][0] + w0[kWR - 1][3] + pre_a; WN_AFTER(xf); }
-  if (resid) { const float xf = rres + rg[0][0] + rw[0][0] + rskip; WN_AFTER(xf); }
-  st[2] = WN_NOW();
-#endif
 
   // ---------------- layer 0: sample the previous step's output; x_0(t) is its current tap
   if (L0) {
@@ -573,9 +535,6 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
         for (int b = 0; b < kUB; ++b) acc[r * kUB + b] = dot4(w, x[b], acc[r * kUB + b]);
       }
     }
-#if WN_STAMP
-    { const float af = acc[0] + acc[kWR * kUB - 1]; WN_AFTER(af); st[3] = WN_NOW(); }
-#endif
     const float s = wave_reduce_multi<kWR * kUB>(acc, lane);
     if ((lane & (64 / (kWR * kUB) - 1)) == 0) s_red[wave][lane / (64 / (kWR * kUB))] = s;
     // the last gate wave to arrive finishes the gate (no barrier with the residual waves)
@@ -583,9 +542,6 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
     int prev = 0;
     if (lane == 0) prev = atomicAdd(&s_arrived, 1);
     prev = __shfl(prev, 0);
-#if WN_STAMP
-    st[4] = WN_NOW();
-#endif
     if (prev == kGW - 1) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       if (lane < kRP * kUB && fb < nb) {
@@ -607,9 +563,6 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
     for (int q = 0; q < kResRows; ++q)
 #pragma unroll
       for (int b = 0; b < kUB; ++b) acc[q * kUB + b] = dot4(rw[q], rg[b], 0.f);
-#if WN_STAMP
-    { const float af = acc[0]; WN_AFTER(af); st[3] = WN_NOW(); }
-#endif
     const float v0 = wave_reduce_multi<kResRows * kUB>(acc, lane);
     const int j = rwave + my_q * kRW;
     if (lane % kRStep == 0 && j < kRP * nrp && my_b < nb) {
@@ -623,21 +576,7 @@ __global__ __launch_bounds__(kLayerThreads) void wn_layer_kernel(WnArgs a, int l
         else *sp = a.legacy ? (rskip + v) * kSqrtHalf : (rskip + v);
       }
     }
-#if WN_STAMP
-    st[4] = WN_NOW();
-#endif
   }
-#if WN_STAMP
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  st[6] = WN_NOW();
-  if (lane == 0 && (wave == 0 || wave == kGW)) {
-    if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1))) {
-      const int wg = blockIdx.x + blockIdx.y * gridDim.x;
-      unsigned long long* o = g_wn_stamp + ((int64_t)(layer * 2 + (wave == kGW)) * kStampWG + wg) * kStampN;
-      for (int i = 0; i < kStampN; ++i) o[i] = st[i];
-    }
-  }
-#endif
 }
 
 // Past taps of the NEXT sample step: P_l(t+1) = sum_{j < K-1} W_j x_l(t+1 - (K-1-j) d_l), for
@@ -724,9 +663,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1)))
     past_taps<NW>(a, 0, blockIdx.x - own, slot);
     return;
   }
-#if WN_STAMP
-  const unsigned long long st0 = WN_NOW();
-#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
@@ -752,13 +688,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1)))
     for (int b = 0; b < kBT; ++b) acc[b] = dot4(wv, g[b], acc[b]);
   }
   const float s = wave_reduce_multi<kBT>(acc, lane);
-#if WN_STAMP
-  if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1)) && lane == 0) {
-    WN_AFTER(s);
-    unsigned long long* o = g_wn_stamp + ((int64_t)(2 * a.n_layers) * kStampWG + blockIdx.x + blockIdx.y * gridDim.x) * kStampN;
-    o[0] = st0; o[6] = WN_NOW();
-  }
-#endif
   (void)slot;
   if ((lane & 7) != 0 || blockIdx.x * NW + wave >= a.S) return;
   const int b = lane >> 3;
@@ -783,9 +712,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1)))
     past_taps<NW>(a, a.n_layers / 2, blockIdx.x - own, slot);
     return;
   }
-#if WN_STAMP
-  const unsigned long long st0 = WN_NOW();
-#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b0 = blockIdx.y * kBT;
   const int nb = min(kBT, a.B - b0);
@@ -835,12 +761,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1)))
     for (int r = 0; r < kHR; ++r) p += w2[r] * s_h1[r][mb];
     a.molp[((int64_t)blockIdx.x * a.B + b0 + mb) * kMaxNO + mj] = p;
   }
-#if WN_STAMP
-  if (g_wn_stamp_t >= 0 && slot == (g_wn_stamp_t & (a.RING - 1)) && lane == 0 && wave == 0) {
-    unsigned long long* o = g_wn_stamp + ((int64_t)(2 * a.n_layers + 1) * kStampWG + blockIdx.x + blockIdx.y * gridDim.x) * kStampN;
-    o[0] = st0; o[6] = WN_NOW();
-  }
-#endif
   (void)slot;
 }
 
@@ -1357,23 +1277,6 @@ int64_t ring_frames(int n_layers, int lps, int K) {
 
 extern "C" {
 
-#if WN_STAMP
-// Diagnostic build only: choose the sample step to record (-1 = none) / copy the stamps out
-// ([launch slot = 2 layer + (residual wave), tail 2L, head 2L+1][workgroup][stamp]).
-int autovc_wavenet_stamp_set(int t) {
-  AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wn_stamp_t), &t, sizeof(int)), "hipMemcpyToSymbol");
-  static const unsigned long long zero[1024] = {};
-  for (size_t off = 0; off < sizeof(g_wn_stamp); off += sizeof(zero))
-    AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wn_stamp), zero, std::min(sizeof(zero), sizeof(g_wn_stamp) - off), off),
-            "hipMemcpyToSymbol");
-  return avc::kOk;
-}
-int autovc_wavenet_stamps(unsigned long long* host, int64_t n) {
-  if (n * sizeof(unsigned long long) > sizeof(g_wn_stamp)) return avc::kErrArg;
-  AVC_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wn_stamp), n * sizeof(unsigned long long)), "hipMemcpyFromSymbol");
-  return avc::kOk;
-}
-#endif
 
 int autovc_wavenet_set_xcd(int on) {
   AVC_CHECK_ARG(on == 0 || on == 1, "autovc_wavenet_set_xcd: 0 or 1");
