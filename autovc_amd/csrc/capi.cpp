@@ -39,4 +39,48 @@ int autovc_stream_destroy(hipStream_t stream) {
   return avc::kOk;
 }
 
+// ---- gradient-ready marks (autovc_amd.functional / ddp): events that eager work outside a
+// captured step graph (the data-parallel collectives) can wait on
+int autovc_event_create(hipEvent_t* out) {
+  AVC_CHECK_ARG(out != nullptr, "autovc_event_create: null out");
+  AVC_HIP(hipEventCreateWithFlags(out, hipEventDisableTiming), "hipEventCreateWithFlags");
+  return avc::kOk;
+}
+
+int autovc_event_destroy(hipEvent_t ev) {
+  AVC_HIP(hipEventDestroy(ev), "hipEventDestroy");
+  return avc::kOk;
+}
+
+// Record `ev` on `stream`.  While the stream is being captured into a graph, an event-record
+// node is added after the stream's current capture dependencies and becomes the stream's only
+// dependency (hipEventRecord itself is refused inside a capture for an event meant to be
+// waited on outside the graph): every replay of the graph records `ev` at that point.
+int autovc_event_record_any(hipEvent_t ev, hipStream_t stream) {
+  AVC_CHECK_ARG(ev != nullptr, "autovc_event_record_any: null event");
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  unsigned long long id = 0;
+  AVC_HIP(hipStreamGetCaptureInfo_v2(stream, &st, &id, &graph, &deps, &ndeps), "hipStreamGetCaptureInfo_v2");
+  if (st == hipStreamCaptureStatusNone) {
+    AVC_HIP(hipEventRecord(ev, stream), "hipEventRecord");
+    return avc::kOk;
+  }
+  AVC_CHECK_ARG(st == hipStreamCaptureStatusActive && graph != nullptr,
+                "autovc_event_record_any: stream capture is invalidated");
+  hipGraphNode_t node = nullptr;
+  AVC_HIP(hipGraphAddEventRecordNode(&node, graph, deps, ndeps, ev), "hipGraphAddEventRecordNode");
+  AVC_HIP(hipStreamUpdateCaptureDependencies(stream, &node, 1, hipStreamSetCaptureDependencies),
+          "hipStreamUpdateCaptureDependencies");
+  return avc::kOk;
+}
+
+int autovc_stream_wait_event(hipStream_t stream, hipEvent_t ev) {
+  AVC_CHECK_ARG(ev != nullptr, "autovc_stream_wait_event: null event");
+  AVC_HIP(hipStreamWaitEvent(stream, ev, 0), "hipStreamWaitEvent");
+  return avc::kOk;
+}
+
 }  // extern "C"

@@ -7,12 +7,19 @@ and adds the one real exchange of the step: an all-reduce (mean) of the gradient
 Because FusedAdam keeps every gradient in ONE contiguous buffer, the exchange is a few
 bucketed collectives over that buffer (no per-parameter calls).
 
-Overlap: the buckets are all-reduced asynchronously, and each bucket's Adam update is
-queued as soon as its collective is done (`reduce_and_step`), so the update of bucket i
-runs while bucket i+1 is still on the wire.  The forward+backward itself is replayed as
-one captured HIP graph (autovc_amd.graph): collectives are kept OUT of that graph (RCCL
-under stream capture is not exercised on the single-GPU boxes this build is tested on),
-which is why the exchange cannot start inside the backward in graph mode.
+Overlap with the backward: while the exchange is attached (world > 1), the backward records
+gradient-ready marks (functional.GradMarks): an event at every recurrence and at the final
+join, each flat-buffer gradient logged with the mark after which it is final.  The step's
+forward+backward is one captured HIP graph (autovc_amd.graph) whose marks are event-record
+nodes, so the collectives stay OUT of the graph (eager RCCL, never captured) and still start
+inside the backward: after the replay is enqueued, `reduce_and_step` issues every bucket's
+collective on a communication stream that first waits for that bucket's mark — the buckets
+of postnet / linear / lstm2 / decoder convs (about 80 % of the bytes) become final when
+lstm1's backward recurrence releases their weight-gradient GEMMs, and their exchange runs
+beside the rest of the backward (lstm1, the encoder BLSTMs and convs, the side stream's
+remaining GEMMs).  Each bucket's Adam update is queued on the compute stream as its mean
+lands.  Without marks (overlap=False or a recording off) every collective waits for the whole
+backward, as before.
 
 Exchange precision: fp32 (113.7 MB per step, one ring all-reduce per bucket) or bf16
 (BASELINE config 3) with fp32 accumulation: each rank rounds its bucket to
@@ -32,6 +39,7 @@ import torch
 import torch.distributed as dist
 
 DEFAULT_BUCKET_BYTES = 16 << 20
+last_schedule: list = []      # (bucket key, gradient-ready mark) of the last overlapped step, in issue order
 
 
 def init_from_env(backend=None):
@@ -99,6 +107,9 @@ class _Bf16Mean:
     def finish(self):
         self.work.wait()
         self.chunk.copy_(self.gathered[:self.chunk.numel()])
+        if self.chunk.is_cuda:   # buffers from the communication stream, read on this one
+            for t in (self.send, self.recv, self.gathered):
+                t.record_stream(torch.cuda.current_stream(self.chunk.device))
 
 
 class _Fp32Mean:
@@ -124,13 +135,59 @@ def _exchange(grad_dtype):
     raise ValueError(f"gradient exchange dtype must be float32 or bfloat16, got {grad_dtype}")
 
 
-def _run_exchange(items, grad_dtype, world, after=None):
+_COMM_STREAMS: dict = {}
+
+
+def _comm_stream(dev):
+    st = _COMM_STREAMS.get(dev.index)
+    if st is None:
+        st = torch.cuda.Stream(dev)
+        _COMM_STREAMS[dev.index] = st
+    return st
+
+
+def _run_exchange(items, grad_dtype, world, after=None, gates=None):
     """items: (key, fp32 chunk) pairs.  Every bucket's first collective is issued before
-    any is waited on; `after(key)` runs as each bucket's mean lands (the Adam slice)."""
+    any is waited on; `after(key)` runs as each bucket's mean lands (the Adam slice).
+    gates (CUDA only): key -> callable(stream_ptr) that makes the communication stream wait
+    until the bucket's gradients are final (functional.GradMarks.wait); the collectives and
+    the bf16 shard sums are then issued on that stream, in gate order, and only the
+    compute stream's finish (mean / copy back, Adam) waits for them."""
     cls = _exchange(grad_dtype)
-    ex = [(k, cls(chunk, world)) for k, chunk in items]
-    for _, e in ex:
-        e.reduce()
+    if not gates:
+        ex = [(k, cls(chunk, world)) for k, chunk in items]
+        for _, e in ex:
+            e.reduce()
+        for k, e in ex:
+            e.finish()
+            if after is not None:
+                after(k)
+        return
+    dev = items[0][1].device
+    if dev.type != "cuda":        # host tensors (tests): the gates only order the issue
+        ex = []
+        for k, chunk in items:
+            gates[k](None)
+            ex.append((k, cls(chunk, world)))
+        for _, e in ex:
+            e.reduce()
+        for k, e in ex:
+            e.finish()
+            if after is not None:
+                after(k)
+        return
+    comm = _comm_stream(dev)
+    # no wait on the compute stream as a whole (that would wait for the entire backward): each
+    # bucket's gate is an event recorded after the bucket's last gradient write of this step,
+    # which the compute stream issued after everything earlier that touched the bucket (the
+    # previous step's Adam and copy-back, this step's zero_grad)
+    ex = []
+    with torch.cuda.stream(comm):
+        for k, chunk in items:
+            gates[k](comm.cuda_stream)
+            ex.append((k, cls(chunk, world)))
+        for _, e in ex:
+            e.reduce()
     for k, e in ex:
         e.finish()
         if after is not None:
@@ -149,11 +206,14 @@ def allreduce_gradients(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype
     _run_exchange(items, grad_dtype, world)
 
 
-def reduce_and_step(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None):
+def reduce_and_step(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None, marks=None):
     """All-reduce (mean) + Adam, bucket by bucket: every bucket's collective is issued up
     front; bucket i's update is queued on the compute stream once its collective is done,
     overlapping the collectives of the later buckets.  Identical arithmetic to
-    allreduce_gradients() followed by optimizer.step() (Adam is elementwise)."""
+    allreduce_gradients() followed by optimizer.step() (Adam is elementwise).
+    marks (functional.GradMarks of the step just issued): each bucket's collective waits
+    only for its own gradient-ready mark, not for the whole backward, and buckets are issued
+    in mark order."""
     world = _world()
     optimizer.begin_step()          # joins the gradient side stream first
     if world == 1:
@@ -163,12 +223,20 @@ def reduce_and_step(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=Non
         return
     items = [((gi, s, c), f["g"][s:s + c]) for gi, f in enumerate(optimizer._flat) if f is not None
              for s, c in _buckets(f["g"].numel(), bucket_bytes)]
-    _run_exchange(items, grad_dtype, world, after=lambda k: optimizer.update_range(*k))
+    gates = None
+    if marks is not None and marks.n > 0:
+        ready = {k: marks.ready_mark(chunk.data_ptr(), chunk.numel() * 4) for k, chunk in items}
+        items.sort(key=lambda kc: ready[kc[0]])
+        gates = {k: (lambda sp, r=ready[k]: marks.wait(sp, r)) for k, _ in items}
+        global last_schedule
+        last_schedule = [(k, ready[k]) for k, _ in items]
+    _run_exchange(items, grad_dtype, world, after=lambda k: optimizer.update_range(*k), gates=gates)
 
 
 def make_data_parallel(solver, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype="auto", overlap=True):
     """Attach the gradient exchange to an autovc_amd Solver and sync its initial weights.
-    overlap=True: reduce_and_step (bucketed exchange interleaved with the Adam update);
+    overlap=True: reduce_and_step with the backward's gradient-ready marks (each bucket's
+    collective starts inside the backward, interleaved with the Adam update);
     overlap=False: allreduce_gradients after backward, then one Adam launch.
     grad_dtype "auto": bf16 while solver.precision is "bf16" (BASELINE config 3), else fp32;
     or torch.float32 / torch.bfloat16 for a fixed exchange precision."""
@@ -180,7 +248,10 @@ def make_data_parallel(solver, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype="au
         return grad_dtype
 
     if overlap:
-        solver._optimizer_step = lambda: reduce_and_step(solver.g_optimizer, bucket_bytes, dtype())
+        from .functional import MARKS
+        MARKS.active = bool(torch.cuda.is_available())
+        solver._optimizer_step = lambda: reduce_and_step(solver.g_optimizer, bucket_bytes, dtype(),
+                                                         marks=MARKS if MARKS.active else None)
     else:
         solver._after_backward = lambda: allreduce_gradients(solver.g_optimizer, bucket_bytes, dtype())
     solver._ddp_grad_dtype = dtype

@@ -104,16 +104,19 @@ _GRAD_QUEUE: list = []
 _GRAD_PENDING: set = set()   # device indices whose side stream has work not yet joined
 
 
-def _grad_launch(dev, use, fn, *inputs):
-    """Queue the gradient launches `fn` for the side stream when `use` (the gradient is
-    accumulated into the flat buffer) and the side stream is enabled; else run them now.
-    Queued work is released at the next recurrence (_flush_grad_queue) so that it runs
-    beside a latency-bound chain rather than beside the main stream's own GEMMs (measured:
-    released immediately it only competed with them: 22.2 -> 22.9 ms/step)."""
-    if not (use and _GRAD_STREAM_ON):
+def _grad_launch(dev, outs, fn, *inputs):
+    """Queue the gradient launches `fn` for the side stream when their destinations `outs`
+    (a _GradOut or a tuple of them) accumulate into the flat buffer and the side stream is
+    enabled; else run them now.  Queued work is released at the next recurrence
+    (_flush_grad_queue) so that it runs beside a latency-bound chain rather than beside the
+    main stream's own GEMMs (measured: released immediately it only competed with them:
+    22.2 -> 22.9 ms/step)."""
+    outs = outs if isinstance(outs, tuple) else (outs,)
+    if not (all(o.acc for o in outs) and _GRAD_STREAM_ON):
         fn()
         return
-    _GRAD_QUEUE.append((dev, fn, inputs, _PRECISION[0]))   # run later under the same precision
+    # run later under the same precision; the destinations are final once the batch is done
+    _GRAD_QUEUE.append((dev, fn, inputs, _PRECISION[0], outs))
 
 
 def _grad_mark(dev):
@@ -135,6 +138,8 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
     inputs), inputs marked as in use by the side stream.  The LDS reserve only pays beside
     a recurrence; the final flush (join) runs unpadded."""
     if not _GRAD_QUEUE:
+        if MARKS.active and beside_recurrence:
+            MARKS.mark(torch.device("cuda", torch.cuda.current_device()), None, [])
         return
     items = list(_GRAD_QUEUE)
     _GRAD_QUEUE.clear()
@@ -151,7 +156,7 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
     _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0)
     try:
         with torch.cuda.stream(side):
-            for _, fn, inputs, prec in items:
+            for _, fn, inputs, prec, _outs in items:
                 for t in inputs:
                     if t is not None:
                         t.record_stream(side)
@@ -161,6 +166,8 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
         _PRECISION[0] = prev_prec
         _lib.call("autovc_gemm_set_lds_reserve", 0)
         _GRAD_STREAM_ACTIVE[0] = False
+    if MARKS.active:
+        MARKS.mark(dev, side, [o for item in items for o in item[4]])
 
 
 def join_grad_stream(dev=None):
@@ -177,6 +184,82 @@ def join_grad_stream(dev=None):
         # capture (autovc_amd.graph) the wait must be on work of the same capture
         torch.cuda.current_stream(dev).wait_stream(st)
         _GRAD_PENDING.discard(idx)
+
+
+class GradMarks:
+    """Gradient-ready marks of the backward, for the data-parallel exchange (autovc_amd.ddp)
+    to overlap with the rest of the backward (not in the reference, which is single-device).
+
+    While `active`, every backward recurrence (where the queued weight gradients are released
+    to the side stream) and the final join record a mark: an event on the main stream and,
+    when the side stream has work, one on the side stream, both through
+    autovc_event_record_any — inside a step-graph capture these become event-record nodes that
+    every replay re-records.  Every flat-buffer gradient destination (_GradOut with acc) is
+    logged with the first mark after which it is final: a main-stream write at the next mark,
+    a side-stream batch at the mark taken right after it is issued.  ddp.reduce_and_step then
+    starts each bucket's collective as soon as the events of its latest write's mark fire."""
+
+    def __init__(self):
+        self.active = False
+        self.events = []          # mark k (1-based) -> (main event handle, side event handle)
+        self.n = 0                # marks recorded in the current backward
+        self.ready = {}           # flat-buffer byte range (ptr, nbytes) -> mark index
+        self.side_at = {}         # mark index -> whether its side event was recorded
+
+    def begin(self):
+        self.n = 0
+        self.ready = {}
+        self.side_at = {}
+
+    def _event(self, k, which):
+        import ctypes
+        while len(self.events) < k:
+            pair = []
+            for _ in range(2):
+                h = ctypes.c_void_p()
+                _lib.call("autovc_event_create", ctypes.byref(h))
+                pair.append(h.value)
+            self.events.append(tuple(pair))
+        return self.events[k - 1][which]
+
+    def log(self, buf, k):
+        key = (buf.data_ptr(), buf.numel() * buf.element_size())
+        self.ready[key] = max(self.ready.get(key, 0), k)
+
+    def mark(self, dev, side, outs):
+        self.n += 1
+        k = self.n
+        _lib.call("autovc_event_record_any", self._event(k, 0), torch.cuda.current_stream(dev).cuda_stream)
+        self.side_at[k] = side is not None
+        if side is not None:
+            _lib.call("autovc_event_record_any", self._event(k, 1), side.cuda_stream)
+        for o in outs:
+            self.log(o.buf, k)
+
+    def final(self, dev):
+        """The join at the end of the backward: everything is final at this mark."""
+        self.n += 1
+        _lib.call("autovc_event_record_any", self._event(self.n, 0), torch.cuda.current_stream(dev).cuda_stream)
+        self.side_at[self.n] = False
+        return self.n
+
+    def ready_mark(self, ptr, nbytes):
+        """Mark index after which the flat-buffer bytes [ptr, ptr + nbytes) are final (the
+        last mark when nothing wrote them)."""
+        r = 0
+        for (p, n), k in self.ready.items():
+            if p < ptr + nbytes and ptr < p + n:
+                r = max(r, k)
+        return r if r else self.n
+
+    def wait(self, stream_ptr, k):
+        """Make `stream_ptr` wait for mark k's events."""
+        _lib.call("autovc_stream_wait_event", stream_ptr, self._event(k, 0))
+        if self.side_at.get(k):
+            _lib.call("autovc_stream_wait_event", stream_ptr, self._event(k, 1))
+
+
+MARKS = GradMarks()
 
 
 _PRECISION = ["fp32"]
@@ -255,6 +338,8 @@ class _GradOut:
         g = param.grad if (param is not None and getattr(param, "_avc_flat", False)) else None
         self.acc = g is not None and tuple(g.shape) == tuple(shape) and g.is_contiguous()
         self.buf = g if self.acc else torch.empty(shape, device=device, dtype=torch.float32)
+        if self.acc and MARKS.active:
+            MARKS.log(self.buf, MARKS.n + 1)      # a main-stream write: final at the next mark
 
     def result(self):
         return None if self.acc else self.buf
@@ -478,7 +563,7 @@ def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None, Xt=None):
     padded = W is None or tuple(W.shape) != tuple(Wp.shape)
     if need_b:
         go = _GradOut(None if padded else b, (Cop,), dev)
-        _grad_launch(dev, go.acc, lambda go=go: colsum(dy.view(M, Cop), go.buf, accumulate=go.acc), dy)
+        _grad_launch(dev, go, lambda go=go: colsum(dy.view(M, Cop), go.buf, accumulate=go.acc), dy)
         db = go.result()
     if need_w:
         go = _GradOut(None if padded else W, (Cop, Cip, KS), dev)
@@ -492,7 +577,7 @@ def _conv_bwd(dy, x, Wp, need_x, need_w, need_b, W=None, b=None, Xt=None):
                  splits=_splits_for(Cop, KS * Cip, M))
             _lib.call("autovc_conv_unpack_grad_f32", Cop, Cip, KS, dWf.data_ptr(), go.buf.data_ptr(), int(go.acc),
                       _s())
-        _grad_launch(dev, go.acc, dw, dy, x, *(() if Xt is None else (Xt,)))
+        _grad_launch(dev, go, dw, dy, x, *(() if Xt is None else (Xt,)))
         dW = go.result()
     if need_x:
         if _wino_ok(T, Cip, Cop) and dy.is_contiguous():
@@ -759,7 +844,7 @@ class ConvBNChainFn(torch.autograd.Function):
                     _lib.call("autovc_gemm_batched_f32", 8, Co, Ci, nt, Dt.data_ptr(), Co, nt * Co, 1, Xt.data_ptr(),
                               Ci, nt * Ci, 1, Mt.data_ptr(), Ci, Co * Ci, 0, _s())
                     _lib.call("autovc_wino5_wgrad_f32", Co, Ci, Mt.data_ptr(), go.buf.data_ptr(), int(go.acc), _s())
-                _grad_launch(dev, go.acc, dw, Dt, Xt)
+                _grad_launch(dev, go, dw, Dt, Xt)
                 grads[7 * l] = go.result()
             xts[l] = None
             if need_dx:
@@ -949,7 +1034,7 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                               xact, dWf.data_ptr(), wsrc, ws, _s())
                     _lib.call("autovc_conv_unpack_grad_f32", Co, Ci, KS, dWf.data_ptr(), go.buf.data_ptr(),
                               int(go.acc), _s())
-                _grad_launch(dev, go.acc, dw, dy, xin, xcoef)
+                _grad_launch(dev, go, dw, dy, xin, xcoef)
                 grads[7 * l] = go.result()
             if l > 0 or needs[1]:
                 Wd = conv_weight(W, 5 if h else 3)
@@ -1063,13 +1148,13 @@ class LinearFn(torch.autograd.Function):
         dx = dW = db = None
         if ctx.needs_input_grad[1]:
             go = _GradOut(W_param if Np == N else None, (Np, K), dev)
-            _grad_launch(dev, go.acc, lambda go=go: gemm(Np, K, M, dy, Np, 1, x, K, 1, go.buf, K,
+            _grad_launch(dev, go, lambda go=go: gemm(Np, K, M, dy, Np, 1, x, K, 1, go.buf, K,
                                                          splits=_splits_for(Np, K, M), accumulate=go.acc), dy, x)
             dW = go.result()
             dW = dW if (dW is None or Np == N) else dW[:N].contiguous()
         if ctx.has_b and ctx.needs_input_grad[2]:
             go = _GradOut(b_param if Np == N else None, (Np,), dev)
-            _grad_launch(dev, go.acc, lambda go=go: colsum(dy, go.buf, accumulate=go.acc), dy)
+            _grad_launch(dev, go, lambda go=go: colsum(dy, go.buf, accumulate=go.acc), dy)
             db = go.result()
             db = db if (db is None or Np == N) else db[:N].contiguous()
         if ctx.needs_input_grad[0]:
@@ -1192,19 +1277,19 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
     dx = dWih = dWhh = dbih = dbhh = None
     if needs[1]:
         go = _GradOut(p_ih, W_ih.shape, dev)
-        _grad_launch(dev, go.acc, lambda go=go: gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I,
+        _grad_launch(dev, go, lambda go=go: gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I,
                                                      splits=_splits_for(4 * H, I, M), accumulate=go.acc), dG, x)
         dWih = go.result()
     if needs[2]:
         go = _GradOut(p_hh, (4 * H, H), dev)
-        _grad_launch(dev, go.acc, lambda go=go: gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
+        _grad_launch(dev, go, lambda go=go: gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
                                                      splits=_splits_for(4 * H, H, M), accumulate=go.acc), dG, h)
         dWhh = go.result()
     if needs[3] or needs[4]:
         gi, gh = _GradOut(p_bih, (4 * H,), dev), _GradOut(p_bhh, (4 * H,), dev)
         if gi.acc != gh.acc:
             gi, gh = _GradOut(None, (4 * H,), dev), _GradOut(None, (4 * H,), dev)
-        _grad_launch(dev, gi.acc, lambda gi=gi, gh=gh: colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc),
+        _grad_launch(dev, (gi, gh), lambda gi=gi, gh=gh: colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc),
                      dG)
         dbih, dbhh = gi.result(), gh.result()
     if needs[0]:

@@ -167,11 +167,15 @@ class Solver(object):
     def _forward_backward(self, x_real, emb_org):
         # the weights do not change until the optimizer step: each conv weight transform is
         # computed once per step (AF.weight_scope)
+        if AF.MARKS.active:     # data parallel: gradient-ready marks for the exchange (ddp)
+            AF.MARKS.begin()
         with AF.precision(self.precision), AF.weight_scope():
             g_loss, l_id, l_psnt, l_cd, x_psnt = self.compute_losses(x_real, emb_org)
             self.reset_grad()
             g_loss.backward()
         AF.join_grad_stream()   # weight gradients (side stream) complete before they are read
+        if AF.MARKS.active:
+            AF.MARKS.final(x_real.device)
         return g_loss, l_id, l_psnt, l_cd, x_psnt
 
     def train_step(self, x_real, emb_org):

@@ -103,6 +103,17 @@ int autovc_gemm_set_lds_reserve(int bytes);
  * reference counterpart (torch.cuda streams are unmasked). */
 int autovc_stream_create_cu_mask(int n_words, const uint32_t* mask, hipStream_t* out);
 int autovc_stream_destroy(hipStream_t stream);
+/* Gradient-ready marks of the data-parallel step (not in the reference, which is
+ * single-device: solver_encoder.py:101,128 / :293-300 backward then step).  The step's
+ * backward records an event whenever a group of parameter gradients is complete;
+ * autovc_event_record_any adds an event-record node when `stream` is being captured into a
+ * hipGraph (so every replay records it) and is hipEventRecord otherwise.  The eager
+ * gradient exchange waits on those events (autovc_stream_wait_event) before each bucket's
+ * collective, overlapping the exchange with the rest of the backward (autovc_amd/ddp.py). */
+int autovc_event_create(hipEvent_t* out);
+int autovc_event_destroy(hipEvent_t ev);
+int autovc_event_record_any(hipEvent_t ev, hipStream_t stream);
+int autovc_stream_wait_event(hipStream_t stream, hipEvent_t ev);
 /* Same contract, bf16 compute (BASELINE config 3, "bf16 with fp32 master"): the fp32
  * operands are rounded to bf16 (RNE) as they are staged, v_mfma_f32_32x32x16_bf16
  * accumulates in fp32, C / bias / accumulate stay fp32 — the numerics of a torch.autocast

@@ -118,3 +118,71 @@ def test_bf16_exchange_fp32_accumulate(world):
         err = (got.double() - exact).abs()
         bound = 2 * 2.0 ** -8 * torch.stack([_rank_grads(r).double().abs() for r in range(world)]).max(0).values
         assert bool((err <= bound + 1e-30).all()), float((err - bound).max())
+
+
+class _FakeMarks:
+    """GradMarks stand-in for host tensors: fixed ready marks per flat-buffer range, and a log
+    of the gates the exchange waited on (in issue order)."""
+
+    def __init__(self, flat, cuts):
+        self.n = len(cuts) + 1
+        self.flat = flat
+        self.cuts = cuts            # element offsets where the ready mark changes
+        self.waited = []
+
+    def ready_mark(self, ptr, nbytes):
+        start = (ptr - self.flat.data_ptr()) // 4
+        end = start + nbytes // 4
+        # later ranges of the flat buffer are final earlier (the backward runs the model in
+        # reverse): mark 1 for the tail, the last mark for the head
+        return max(self.n - sum(1 for c in self.cuts if e > c) for e in range(start, end, max(1, (end - start) // 8)))
+
+    def wait(self, stream, k):
+        self.waited.append(k)
+
+
+class _AdamLog:
+    """FusedAdam stand-in: one flat group, update_range records the issue order."""
+
+    def __init__(self, g):
+        self._flat = [dict(g=g, p=torch.zeros_like(g))]
+        self.updates = []
+
+    def begin_step(self):
+        pass
+
+    def update_range(self, gi, s, c):
+        self.updates.append(s)
+
+
+def _marked_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from autovc_amd import ddp
+    out = {}
+    for dtype in (None, torch.bfloat16):
+        plain = _AdamLog(_rank_grads(rank, 40003))
+        ddp.reduce_and_step(plain, bucket_bytes=4 * 4000, grad_dtype=dtype)
+        marked = _AdamLog(_rank_grads(rank, 40003))
+        marks = _FakeMarks(marked._flat[0]["g"], cuts=[12000, 30000])
+        ddp.reduce_and_step(marked, bucket_bytes=4 * 4000, grad_dtype=dtype, marks=marks)
+        out[str(dtype)] = (plain._flat[0]["g"].clone(), marked._flat[0]["g"].clone(), marks.waited,
+                           marked.updates, list(ddp.last_schedule))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_marked_exchange_equals_plain_gloo_world2():
+    """The exchange gated by gradient-ready marks (buckets issued in mark order, each after
+    its own gate; the overlap with the backward on the GPU) gives the same means, bit for
+    bit, as the plain exchange, for the fp32 and the bf16 exchange; buckets final earlier
+    (the flat buffer's tail) are issued and updated first."""
+    res = _run(_marked_worker, 2)
+    for rank, out in res:
+        for dtype, (plain, marked, waited, updates, sched) in out.items():
+            assert torch.equal(plain, marked), (rank, dtype)
+            assert waited == sorted(waited) and waited[0] == 1 and waited[-1] == 3, waited
+            assert updates[0] > updates[-1]                  # tail bucket first, head bucket last
+            assert [r for _, r in sched] == waited

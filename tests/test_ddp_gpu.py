@@ -50,6 +50,7 @@ def _worker(rank, world, port, out_dir, grad_dtype, overlap):
         solver.train_step(x, e)
     torch.cuda.synchronize()
     torch.save([f.cpu() for f in solver.g_optimizer.flat_params()], os.path.join(out_dir, f"rank{rank}.pt"))
+    torch.save([r for _, r in ddp.last_schedule], os.path.join(out_dir, f"sched{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -64,6 +65,7 @@ def _run_ranks(tmp_path, grad_dtype, overlap):
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0, p.exitcode
+    _run_ranks.schedule = torch.load(os.path.join(tmp_path, "sched0.pt"), weights_only=True)
     return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
 
 
@@ -89,7 +91,13 @@ def _reference(cuda):
 
 @pytest.mark.parametrize("overlap", [True, False])
 def test_two_rank_graph_step_equals_mean_gradient_step(cuda, tmp_path, overlap):
+    """overlap=True: each bucket's collective waits only for its gradient-ready mark inside
+    the replayed backward (functional.GradMarks); the buckets of the late layers must be
+    gated on an earlier mark than the encoder's, which is final only at the end."""
     ranks = _run_ranks(tmp_path, "fp32", overlap)
+    if overlap:
+        sched = _run_ranks.schedule
+        assert sched == sorted(sched) and len(set(sched)) >= 2 and sched[0] < sched[-1], sched
     ref = _reference(cuda)
     for a, b in zip(ranks[0], ranks[1]):
         assert torch.equal(a, b)                     # the ranks stay in lockstep
