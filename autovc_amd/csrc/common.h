@@ -14,6 +14,13 @@ namespace avc {
 
 void set_error(const char* fmt, ...);
 
+// Zero `bytes` (a multiple of 4) at `p` on `stream` with a kernel (elementwise.hip).  Used
+// instead of hipMemsetAsync on every path a step graph captures: a captured memset becomes
+// a memset node, and replays of a single-stream (linear) step graph holding memset nodes
+// faulted the GPU on this runtime; kernel nodes are the only
+// node kind the graphs then contain.
+hipError_t zero_async(void* p, size_t bytes, hipStream_t stream);
+
 constexpr int kOk = 0;
 constexpr int kErrArg = -1;     // bad shape / pointer / alignment
 constexpr int kErrLaunch = -2;  // hip launch or runtime failure

@@ -22,6 +22,11 @@ int grid_for(int64_t total, int per = 256) { return (int)std::min<int64_t>((tota
 #define GRID_STRIDE(i, total) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (total); i += (int64_t)gridDim.x * blockDim.x)
 
+__global__ __launch_bounds__(256) void zero_words_kernel(uint32_t* __restrict__ p, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0u;
+}
+
 __global__ void frame_concat_kernel(int B, int T, int C1, int C2, int rep, const float* __restrict__ X,
                                     int64_t ldx, const float* __restrict__ E, float* __restrict__ out) {
   const int C = C1 + C2;
@@ -408,4 +413,12 @@ extern "C" int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, f
                      (const float*)workspace, out, out2, accumulate);
   AVC_CHECK_LAUNCH("autovc_colsum_f32");
   return avc::kOk;
+}
+
+hipError_t avc::zero_async(void* p, size_t bytes, hipStream_t stream) {
+  const int64_t n = (int64_t)(bytes / 4);
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, static_cast<uint32_t*>(p), n);
+  return hipGetLastError();
 }

@@ -885,8 +885,8 @@ extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, i
   float* dcs1 = PQ0 + 2 * splits * BH;
   float* dcs0 = dcs1 + BH;
   // layer 0's first processed step has no recurrent partials and no carried cell gradient
-  AVC_HIP(hipMemsetAsync(PQ0, 0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_f32");
-  AVC_HIP(hipMemsetAsync(dcs0, 0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_f32");
+  AVC_HIP(avc::zero_async(PQ0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_f32");
+  AVC_HIP(avc::zero_async(dcs0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_f32");
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits};
   const dim3 pgrid((H / 4 + 63) / 64, B, 2);
@@ -1075,8 +1075,8 @@ extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, 
   float* PQ0 = P1 + splits * BH;
   float* dcs1 = PQ0 + 2 * splits * BH;
   float* dcs0 = dcs1 + BH;
-  AVC_HIP(hipMemsetAsync(PQ0, 0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_bf16");
-  AVC_HIP(hipMemsetAsync(dcs0, 0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_bf16");
+  AVC_HIP(avc::zero_async(PQ0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_bf16");
+  AVC_HIP(avc::zero_async(dcs0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_bf16");
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits, reinterpret_cast<__bf16*>(dG1_b)};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits, reinterpret_cast<__bf16*>(dG0_b)};
   const dim3 pgrid((H / 4 + 63) / 64, B, 2);

@@ -1158,7 +1158,7 @@ extern "C" int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int
   a.h = h; a.c = c_all; a.g = gates; a.h_ldb = h_ldb; a.h_ldt = h_ldt;
   a.bar = static_cast<int*>(workspace);
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
-  AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
+  AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
   hipLaunchKernelGGL((lstm_xcd_fwd_kernel<512, false>), dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
@@ -1179,7 +1179,7 @@ extern "C" int autovc_lstm_fwd_xcd_bf16(int B, int T, int H, const float* gx, in
   a.h = h; a.c = c_all; a.g = gates; a.h_ldb = h_ldb; a.h_ldt = h_ldt;
   a.bar = static_cast<int*>(workspace);
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
-  AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
+  AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
   hipLaunchKernelGGL((lstm_xcd_fwd_kernel<512, true>), dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
@@ -1198,7 +1198,7 @@ extern "C" int autovc_lstm_bwd_xcd_f32(int B, int T, int H, const float* dh_out,
   a.dG = dG;
   a.bar = static_cast<int*>(workspace);
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
-  AVC_HIP(hipMemsetAsync(workspace, 0, XC_BYTES, stream), fn);
+  AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
   hipLaunchKernelGGL(lstm_xcd_bwd_kernel<512>, dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
@@ -1232,7 +1232,7 @@ extern "C" int autovc_lstm2_fwd_persist_f32(int B, int T, int H, const float* gx
   a.W_hh0 = W_hh0; a.b_ih1 = b_ih1; a.b_hh1 = b_hh1; a.W_ih1 = W_ih1; a.W_hh1 = W_hh1;
   a.h0 = h0; a.c0 = c0; a.g0 = gates0; a.h1 = h1; a.c1 = c1; a.g1 = gates1;
   a.h0_ldb = (int64_t)T * H; a.h0_ldt = H;
-  AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
+  AVC_HIP(avc::zero_async(workspace, BAR_BYTES, stream), fn);
   launch_persist<1024, true>(a, workspace, stream);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
@@ -1260,7 +1260,7 @@ extern "C" int autovc_lstm2_fwd_persist_bf16(int B, int T, int H, const float* g
   a.W1b = reinterpret_cast<const __bf16*>(W_hh1_b);
   a.h0 = h0; a.c0 = c0; a.g0 = gates0; a.h1 = h1; a.c1 = c1; a.g1 = gates1;
   a.h0_ldb = (int64_t)T * H; a.h0_ldt = H;
-  AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
+  AVC_HIP(avc::zero_async(workspace, BAR_BYTES, stream), fn);
   launch_persist<1024, true, true>(a, workspace, stream);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
@@ -1293,7 +1293,7 @@ extern "C" int autovc_lstm_fwd_persist_f32(int B, int T, int H, const float* gx,
   a.W_hh0 = W_hh;
   a.h0 = h; a.c0 = c_all; a.g0 = gates;
   a.h0_ldb = h_ldb; a.h0_ldt = h_ldt;
-  AVC_HIP(hipMemsetAsync(workspace, 0, BAR_BYTES, stream), fn);
+  AVC_HIP(avc::zero_async(workspace, BAR_BYTES, stream), fn);
   if (H == 512) launch_persist<512, false>(a, workspace, stream);
   else launch_persist<1024, false>(a, workspace, stream);
   AVC_CHECK_LAUNCH(fn);

@@ -1396,10 +1396,10 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   AVC_CHECK_ARG(used <= autovc_wavenet_workspace_bytes(B, T, n_layers, layers_per_stack, taps, R, G, S),
                 "%s: workspace layout overflow", fn);
 
-  if (t0 == 0) AVC_HIP(hipMemsetAsync(workspace, 0, (size_t)used, stream), "hipMemsetAsync");
+  if (t0 == 0) AVC_HIP(avc::zero_async(workspace, (size_t)used, stream), "zero_async");
   if (xcd_eligible(B, n_layers, taps, R, G, S)) {
     // one persistent launch for the whole call: utterance x on XCD x (see wn_xcd_kernel)
-    AVC_HIP(hipMemsetAsync(xbar, 0, (size_t)kXBarLines * kXLn * 4, stream), "hipMemsetAsync");
+    AVC_HIP(avc::zero_async(xbar, (size_t)kXBarLines * kXLn * 4, stream), "zero_async");
     hipLaunchKernelGGL(wn_xcd_kernel, dim3(8 * kXSlots), dim3(64 * kXW), 0, stream, a, t0, t1, xbar,
                        g_wn_timeout_ticks);
     AVC_CHECK_LAUNCH(fn);

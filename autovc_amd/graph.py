@@ -23,18 +23,18 @@ import torch
 
 from . import functional as AF
 
-# Replays the host may have queued ahead of the GPU.  Unbounded, back-to-back replays of a
-# graph with no side-stream branch (AVC_GRAD_STREAM=0) aborted a 25-step bench run with a
-# GPU memory fault in round 3 (and gave run-to-run different losses in round 2) while the
-# short tests passed; waiting on the event of the replay MAX_AHEAD steps back keeps the
-# queue short at no cost to throughput (the GPU still holds MAX_AHEAD steps of work).
-MAX_AHEAD = int(os.environ.get("AVC_GRAPH_MAX_AHEAD", "2"))
+# Replays the host may queue ahead of the GPU (0 = unbounded, the default).  Round 3 bounded
+# it at 2 while looking for the cause of GPU memory faults in replays of step graphs without
+# a side-stream branch; the cause was the memset nodes those single-stream graphs held
+# (DESIGN.md section 9, round 4), not the queue depth, so the bound is off by default.
+MAX_AHEAD = int(os.environ.get("AVC_GRAPH_MAX_AHEAD", "0"))
 
 
 class StepGraphs:
-    def __init__(self, fn, module):
+    def __init__(self, fn, module, debug_dot=None):
         self.fn = fn            # fn(*inputs) -> tuple of device tensors
         self.module = module    # holds the BatchNorm buffers the warm-up must not advance
+        self.debug_dot = debug_dot   # path: write each captured graph as DOT (tools only)
         self._graphs = {}
         self._inflight = collections.deque()
 
@@ -49,8 +49,12 @@ class StepGraphs:
             self.fn(*static)
         cur.wait_stream(warm)
         graph = torch.cuda.CUDAGraph()
+        if self.debug_dot:
+            graph.enable_debug_mode()
         with torch.cuda.graph(graph):
             out = self.fn(*static)
+        if self.debug_dot:
+            graph.debug_dump(self.debug_dot)
         with torch.no_grad():
             for b, s in zip(self.module.buffers(), saved):
                 b.copy_(s)

@@ -183,13 +183,9 @@ class Solver(object):
         scalars (g_loss, loss_id, loss_id_psnt, loss_cd); nothing synchronises.  With
         `hip_graph` the forward+backward is a graph replay (its outputs are the graph's
         static tensors, overwritten by the next step)."""
-        # the captured step is bit-identical to eager with the weight-gradient side stream on
-        # and off (tests/test_solver_gpu.py::test_hip_graph_step_bit_identical)
-        # a step graph without the side-stream branch (AVC_GRAD_STREAM=0) runs eagerly: its
-        # back-to-back replays gave run-to-run different losses in round 2 and aborted a
-        # 25-step run with a GPU memory fault in round 3 (graph.MAX_AHEAD now bounds the
-        # replays in flight; this mode stays eager until that is shown to cure it)
-        if self.hip_graph and AF._GRAD_STREAM_ON:
+        # the captured step replays bit-identically to eager with the weight-gradient side
+        # stream on and off (tests/test_solver_gpu.py::test_hip_graph_replays_without_host_sync)
+        if self.hip_graph:
             if self._graphs is None:
                 from .graph import StepGraphs
                 self._graphs = StepGraphs(self._forward_backward, self.G)

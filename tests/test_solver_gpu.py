@@ -103,40 +103,64 @@ def test_hip_graph_step_bit_identical(cuda, precision, grad_stream, B):
     """Solver(hip_graph=True) replays the captured forward+backward: three steps (the first
     captures) give bit-identical losses, parameters and BatchNorm running stats to eager,
     and a second input batch of the same shape is picked up by the replay — with the
-    weight-gradient side stream on and off (AVC_GRAD_STREAM; off, the Solver runs the step
-    eagerly even with hip_graph), and at B=64, where the persistent lstm2 forward is in the
-    graph."""
+    weight-gradient side stream on and off (AVC_GRAD_STREAM: off, the step graph is one
+    single-stream chain), and at B=64, where the persistent lstm2 forward is in the graph."""
+    res = [_graph_vs_eager_run(cuda, precision, grad_stream, B, graph, 3, switch_batches=True)
+           for graph in (False, True)]
+    _assert_same(*res)
+
+
+def _graph_vs_eager_run(cuda, precision, grad_stream, B, graph, steps, switch_batches=False):
     import bench
     from autovc_amd import functional as AF
-    res = []
     prev = AF._GRAD_STREAM_ON
     try:
         AF._GRAD_STREAM_ON = grad_stream
-        for graph in (False, True):
-            torch.manual_seed(0)
-            solver = bench.make_solver(cuda, B)
-            solver.G.train()
-            solver.precision = precision
-            solver.hip_graph = graph
-            xa, ea = bench.synthetic_batch(B, 128, cuda, 99)
-            xb, eb = bench.synthetic_batch(B, 128, cuda, 100)
-            losses = []
-            for x, e in ((xa, ea), (xb, eb), (xa, ea)):
-                out = solver.train_step(x, e)
-                losses.append(torch.stack([o.detach().reshape(()) for o in out]).clone())
-            torch.cuda.synchronize()
-            res.append((losses, [f.clone() for f in solver.g_optimizer.flat_params()],
-                        [b.clone() for b in solver.G.buffers()]))
-            del solver
+        torch.manual_seed(0)
+        solver = bench.make_solver(cuda, B)
+        solver.G.train()
+        solver.precision = precision
+        solver.hip_graph = graph
+        xa, ea = bench.synthetic_batch(B, 128, cuda, 99)
+        xb, eb = bench.synthetic_batch(B, 128, cuda, 100)
+        losses = []
+        for i in range(steps):
+            x, e = (xb, eb) if (switch_batches and i % 2 == 1) else (xa, ea)
+            out = solver.train_step(x, e)      # no host synchronisation between steps
+            losses.append(torch.stack([o.detach().reshape(()) for o in out]).clone())
+        torch.cuda.synchronize()
+        AF.check_device_faults(cuda)
+        res = (losses, [f.clone() for f in solver.g_optimizer.flat_params()], [b.clone() for b in solver.G.buffers()])
+        del solver
+        return res
     finally:
         AF._GRAD_STREAM_ON = prev
-    (la, pa, ba), (lb, pb, bb) = res
-    for a, b in zip(la, lb):
-        assert torch.equal(a, b)
-    for a, b in zip(pa, pb):
-        assert torch.equal(a, b)
-    for a, b in zip(ba, bb):
-        assert torch.equal(a, b)
+
+
+def _assert_same(a, b):
+    (la, pa, ba), (lb, pb, bb) = a, b
+    for i, (x, y) in enumerate(zip(la, lb)):
+        assert torch.equal(x, y), (i, x, y)
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+    for x, y in zip(ba, bb):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("grad_stream", [True, False])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_hip_graph_replays_without_host_sync(cuda, precision, grad_stream):
+    """30 back-to-back replays of the B=64 step graph (bench.py's path) with no host
+    synchronisation between them (the host runs ahead, graph.MAX_AHEAD = 0 = unbounded),
+    side stream on and off: every step's losses, the final parameters and BatchNorm buffers
+    bit-identical to 30 eager steps.  With the side stream off the step graph is a single
+    stream chain; round 3's replays of such graphs faulted the GPU because they held memset
+    nodes — the step path now zeroes with kernels only."""
+    from autovc_amd import graph as G
+    assert G.MAX_AHEAD == 0
+    eager = _graph_vs_eager_run(cuda, precision, grad_stream, 64, False, 30)
+    replay = _graph_vs_eager_run(cuda, precision, grad_stream, 64, True, 30)
+    _assert_same(eager, replay)
 
 
 def test_graph_replay_survives_workspace_growth(cuda):
@@ -276,7 +300,7 @@ def test_b64_graph_trajectory_matches_reference(cuda, precision):
     torch.cuda.synchronize()
     from autovc_amd import functional as AF
     AF.check_device_faults(cuda)
-    traj = torch.stack(traj).double().cpu().numpy()
+    traj = torch.stack(traj).detach().double().cpu().numpy()
     ref = R["traj"]
     dev = np.abs(traj - ref) / np.abs(ref)
     if precision == "fp32":

@@ -32,9 +32,7 @@ for STEP in ${1//,/ }; do
            python tools/pmc_summarize.py gpurun_out/xpmc_f gpurun_out/xpmc_w xcd > gpurun_out/lstm_xcd_pmc.json ;;
     wnpersist) timeout -k 10 120 tools/pbin/wn_persist_ubench > gpurun_out/wn_persist_ubench.txt 2>&1 && \
                timeout -k 10 300 tools/pbin/chain_ubench > gpurun_out/chain_ubench.txt 2>&1 ;;
-    audit) timeout -k 10 300 python -u tools/graph_ptr_audit.py ${AUDIT_B:-64} 0 fp32 > gpurun_out/audit.log 2>&1 && \
-           timeout -k 10 300 python -u tools/graph_ptr_audit.py ${AUDIT_B:-64} 1 fp32 >> gpurun_out/audit.log 2>&1 && \
-           timeout -k 10 300 python -u tools/graph_ptr_audit.py ${AUDIT_B:-64} 0 bf16 >> gpurun_out/audit.log 2>&1 ;;
+    audit) timeout -k 10 300 python -u tools/graph_ptr_audit.py ${AUDIT_B:-64} ${AUDIT_SIDE:-1} ${AUDIT_PREC:-fp32} >> gpurun_out/audit.log 2>&1 ;;
     ring) timeout -k 10 120 python -u tools/graph_ring_probe.py ${RING_N:-2000} ${RING_R:-1,2,4,8,16,32} ${RING_F:-1,0} > gpurun_out/ring.log 2>&1 ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac

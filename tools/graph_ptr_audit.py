@@ -103,7 +103,9 @@ def main():
     x, e = bench.synthetic_batch(B, 128, dev, 1234)
     rec = Recorder()
     _lib.call = rec
-    graphs = G.StepGraphs(s._forward_backward, s.G)
+    dot = os.path.join(ROOT, "gpurun_out", f"step_graph_{prec}_side{int(stream_on)}.dot")
+    os.makedirs(os.path.dirname(dot), exist_ok=True)
+    graphs = G.StepGraphs(s._forward_backward, s.G, debug_dot=dot)
     orig_capture = graphs._capture
 
     def capture(inputs):
@@ -133,6 +135,14 @@ def main():
     print(f"B={B} side_stream={'on' if stream_on else 'off'} precision={prec}: {len(rec.rec)} pointer "
           f"arguments recorded in the capture ({len(uniq)} distinct), graph pool {pool}", flush=True)
     bad = report("after capture", classify(uniq, pool))
+    if os.path.exists(dot):
+        import re
+        text = open(dot).read()
+        counts = {k: len(re.findall(k, text, re.I)) for k in ("kernel", "memset", "memcpy", "event")}
+        print(f"graph DOT ({os.path.basename(dot)}): mentions per node kind {counts}", flush=True)
+        if counts["memset"] or counts["memcpy"]:
+            print("   graph holds memset / memcpy nodes", flush=True)
+            bad += 1
     for _ in range(3):
         graphs.run(prec, x, e)
         s._after_backward()
