@@ -439,12 +439,13 @@ def conv_weight(W, kind):
     return out
 
 
-def prepare_weights(convs, lstms, T, training):
+def prepare_weights(convs, lstms, T, training, B=None):
     """Inside a weight_scope: compute, in one launch, every transform the ConvNorm layers
     `convs` (nn.Conv1d, k=5) will use for sequences of T frames — the Winograd pair for
     fp32 Winograd shapes, else the im2col packs — and the large-H LSTMs `lstms` (model_vc_mel
     LSTM modules) their recurrences use — bf16 copies of the recurrent weights under bf16,
-    the transposes the backward reads — and cache them for the scope."""
+    the transposes the backward reads (B: the batch, which decides whether the persistent
+    lstm2 backward, reading the untransposed weights, runs) — and cache them for the scope."""
     cache = _WSCOPE[0]
     if cache is None:
         return
@@ -463,6 +464,9 @@ def prepare_weights(convs, lstms, T, training):
             continue
         mats = [m.weight_hh_l0] if m.num_layers == 1 else [m.weight_hh_l0, m.weight_ih_l1, m.weight_hh_l1]
         kinds = ((6, 8) if training else (6,)) if _bf16_rec(H) else ((7,) if training else ())
+        if m.num_layers == 2 and training and B is not None and lstm2_bwd_persistent(B, H):
+            # the persistent backward reads the (4H, H) weights (or the bf16 copies) as they are
+            kinds = tuple(k for k in kinds if k not in (7, 8))
         for W in mats:
             if _cacheable(W):
                 for kind in kinds:
@@ -1319,6 +1323,7 @@ _FAULT_BITS = (
     (2, "lstm_xcd_fwd_kernel (decoder lstm1 forward)", "h/c", "AVC_LSTM_XCD=0"),
     (4, "lstm_xcd_bwd_kernel (decoder lstm1 backward)", "gate gradients", "AVC_LSTM_XCD_BWD=0"),
     (8, "lstm_persist_kernel, one layer (decoder lstm1 forward)", "h/c", "AVC_LSTM_PERSIST=0"),
+    (16, "lstm2_bwd_persist_kernel (decoder lstm2 backward)", "gate gradients", "AVC_LSTM2_BWD_PERSIST=0"),
 )
 
 
@@ -1443,9 +1448,6 @@ class LSTM2StackFn(torch.autograd.Function):
         B, T, _ = x.shape
         H = W_hh0.shape[1]
         dev = x.device
-        # the (H, 4H) transposes (bf16 copies under bf16), from the step's weight scope if any
-        kt = 8 if _bf16_rec(H) else 7
-        WT1, WIT1, WT0 = conv_weight(W_hh1, kt), conv_weight(W_ih1, kt), conv_weight(W_hh0, kt)
         # split-K of the stacked backward products (autovc_lstm2_bwd_f32): 4 / 2 = 32 x 32 tiles;
         # 8 = the wide-tile kernel (64 x 64 per workgroup), measured slower (fp32 23.5 vs 20.0 us
         # per launch, 15.87 vs 15.49 ms/step; bf16 9.6 vs 9.46 ms/step:
@@ -1454,9 +1456,17 @@ class LSTM2StackFn(torch.autograd.Function):
         splits = {8: 8, 4: 4}.get(int(os.environ.get("AVC_LSTM2_SPLITS", "4")), 2)
         while splits > 2 and (kdim % (64 * splits) or (splits == 8 and H % 64)):
             splits //= 2
-        ws = _ws(dev, 4 * _lib.load().autovc_lstm2_bwd_workspace_floats(B, H, splits), "lstm")
         dG1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         dG0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+        if lstm2_bwd_persistent(B, H):
+            LSTM2StackFn._backward_persistent(ctx, dh1, dG1, dG0)
+            grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
+            grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)
+            return (grads0[0], *grads0[1:], *grads1[1:], None)
+        # the (H, 4H) transposes (bf16 copies under bf16), from the step's weight scope if any
+        kt = 8 if _bf16_rec(H) else 7
+        WT1, WIT1, WT0 = conv_weight(W_hh1, kt), conv_weight(W_ih1, kt), conv_weight(W_hh0, kt)
+        ws = _ws(dev, 4 * _lib.load().autovc_lstm2_bwd_workspace_floats(B, H, splits), "lstm")
         mark = _grad_mark(dev)   # queued weight gradients run beside the recurrences
         if _bf16_rec(H):
             dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
@@ -1471,6 +1481,45 @@ class LSTM2StackFn(torch.autograd.Function):
         grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
         grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)
         return (grads0[0], *grads0[1:], *grads1[1:], None)
+
+
+    @staticmethod
+    def _backward_persistent(ctx, dh1, dG1, dG0):
+        """Both recurrences' backward as ONE persistent weight-stationary launch
+        (autovc_lstm2_bwd_persist_*: the (4H, H) weights themselves, or their bf16 copies
+        under bf16).  The weight gradients queued before it stay queued and are released at
+        the next recurrence (lstm1's backward): launched beside a kernel that needs every CU
+        they would only delay its start (AVC_LSTM2_BWD_FLUSH=beside releases them here)."""
+        x, W_ih0, W_hh0, h0, c0, g0, W_ih1, W_hh1, h1, c1, g1 = ctx.saved_tensors
+        B, T, _ = x.shape
+        H = W_hh0.shape[1]
+        dev = x.device
+        lib = _lib.load()
+        ws = _ws(dev, lib.autovc_lstm2_bwd_persist_workspace_bytes(B, T, H), "lstm2bp")
+        mark = _grad_mark(dev) if _BWD_FLUSH == "beside" else None
+        if _bf16_rec(H):
+            W1b, Wi1b, W0b = conv_weight(W_hh1, 6), conv_weight(W_ih1, 6), conv_weight(W_hh0, 6)
+            dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
+            _lib.call("autovc_lstm2_bwd_persist_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
+                      g0.data_ptr(), c0.data_ptr(), W1b.data_ptr(), Wi1b.data_ptr(), W0b.data_ptr(), dG1.data_ptr(),
+                      dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), ws, _s())
+        else:
+            _lib.call("autovc_lstm2_bwd_persist_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
+                      g0.data_ptr(), c0.data_ptr(), W_hh1.data_ptr(), W_ih1.data_ptr(), W_hh0.data_ptr(),
+                      dG1.data_ptr(), dG0.data_ptr(), ws, _s())
+        if mark is not None:
+            _flush_grad_queue(after=mark)
+
+
+# decoder lstm2 backward as ONE persistent launch (lstm2_bwd_persist_kernel) where the shape
+# and device allow it (B = 64, H = 1024, 256 CUs); AVC_LSTM2_BWD_PERSIST=0 selects the
+# per-step product + pointwise launches
+_BWD_PERSIST_ON = os.environ.get("AVC_LSTM2_BWD_PERSIST", "1") != "0"
+_BWD_FLUSH = os.environ.get("AVC_LSTM2_BWD_FLUSH", "defer")
+
+
+def lstm2_bwd_persistent(B, H):
+    return _BWD_PERSIST_ON and bool(_lib.load().autovc_lstm2_bwd_persist_supported(B, H))
 
 
 class BLSTMLayerFn(torch.autograd.Function):

@@ -210,7 +210,8 @@ class Generator(nn.Module):
         if x.is_cuda:   # inside the Solver's weight scope: all weight transforms in one launch
             full = c_trg is not None
             AF.prepare_weights(self.conv_layers() if full else [c[0].conv for c in self.encoder.convolutions],
-                               [self.decoder.lstm1, self.decoder.lstm2] if full else [], x.shape[-2], self.training)
+                               [self.decoder.lstm1, self.decoder.lstm2] if full else [], x.shape[-2], self.training,
+                               B=x.shape[0])
         code_real = self.encoder.encode(x, c_org)                       # :182
         if c_trg is None:
             return code_real                                            # :183-184

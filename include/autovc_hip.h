@@ -411,6 +411,27 @@ int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ld
                          const float* gates1, const float* c1, const float* gates0, const float* c0,
                          const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
                          float* dG0, int splits, float* workspace, hipStream_t stream);
+/* autovc_lstm2_bwd_f32 / _bf16 as ONE persistent, weight-stationary launch
+ * (csrc/lstm2_persist.hip, lstm2_bwd_persist_kernel; replaces the BPTT of nn.LSTM(512, 1024,
+ * 2) at model_vc_mel.py:104,118 as the reference's autograd runs it, solver_encoder.py:296):
+ * 256 workgroups (one per CU, 8 XCDs x 32), each holding a (512 gate rows x 32 units) slice
+ * of W_hh1, W_ih1 and W_hh0 in registers for the whole sequence; per wavefront step the
+ * three products over its K slice, the group's K-slice partials summed inside the XCD, the
+ * cell backward of the 4 x 64 cells it owns, and a grid barrier.  Weights are the (4H, H)
+ * parameters themselves (fp32) or their RNE bf16 copies (_bf16, which also writes dG*_b).
+ * Needs B = 64, H = 1024, 256 CUs (autovc_lstm2_bwd_persist_supported) and every workgroup
+ * resident at once (Co-residency; fault bit 16). */
+int autovc_lstm2_bwd_persist_supported(int B, int H);
+int64_t autovc_lstm2_bwd_persist_workspace_bytes(int B, int T, int H);
+int autovc_lstm2_bwd_persist_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                 const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                 const float* W_hh1, const float* W_ih1, const float* W_hh0, float* dG1,
+                                 float* dG0, void* workspace, hipStream_t stream);
+int autovc_lstm2_bwd_persist_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                  const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                  const uint16_t* W_hh1_b, const uint16_t* W_ih1_b, const uint16_t* W_hh0_b,
+                                  float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, void* workspace,
+                                  hipStream_t stream);
 int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
                          const float* W_hh_b, float* h, float* c_all, float* gates,
                          hipStream_t stream);

@@ -33,6 +33,7 @@ for STEP in ${1//,/ }; do
     wnpersist) timeout -k 10 120 tools/pbin/wn_persist_ubench > gpurun_out/wn_persist_ubench.txt 2>&1 && \
                timeout -k 10 300 tools/pbin/chain_ubench > gpurun_out/chain_ubench.txt 2>&1 ;;
     audit) timeout -k 10 300 python -u tools/graph_ptr_audit.py ${AUDIT_B:-64} ${AUDIT_SIDE:-1} ${AUDIT_PREC:-fp32} >> gpurun_out/audit.log 2>&1 ;;
+    bench_nss) AVC_GRAD_STREAM=0 timeout -k 10 300 python bench.py --steps 25 --warmup 5 --no-wavenet --no-cpu-baseline --no-e2e --no-roofline > gpurun_out/bench_grad_stream0.json 2> gpurun_out/bench_grad_stream0.err ;;
     ring) timeout -k 10 120 python -u tools/graph_ring_probe.py ${RING_N:-2000} ${RING_R:-1,2,4,8,16,32} ${RING_F:-1,0} > gpurun_out/ring.log 2>&1 ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac

@@ -25,7 +25,7 @@ CATS = [
     ("conv pack/unpack", r"conv_pack|conv_unpack|transpose_kernel|conv_weights_batched"),
     ("losses", r"loss_"),
     ("Adam", r"adam_kernel"),
-    ("frame/code glue", r"frame_concat|code_gather"),
+    ("frame/code glue", r"frame_concat|code_gather|zero_words"),
 ]
 
 
