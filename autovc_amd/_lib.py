@@ -83,6 +83,8 @@ sig("autovc_bn_partial_rows", c_i64)
 sig("autovc_bn_bwd_partial_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_bn_bwd_finalize_f32", c_int, c_int, c_ptr, c_ptr, c_f32, c_ptr, c_ptr, c_ptr, c_int, c_ptr)
 sig("autovc_colsum_f64_finalize_f32", c_int, c_int, c_ptr, c_ptr, c_int, c_ptr)
+sig("autovc_bn_bwd_finalize_bias_f32", c_int, c_int, c_ptr, c_ptr, c_f32, c_ptr, c_ptr, c_ptr, c_int, c_int, c_int,
+    c_ptr, c_ptr, c_int, c_ptr)
 sig("autovc_gemm_f32", c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,

@@ -171,11 +171,11 @@ __global__ __launch_bounds__(256) void bwd_partial_kernel(int64_t M, int C, cons
 }
 
 // sums -> dbeta = sum dy_act, dgamma = sum dy_act * xhat ; keeps the raw sums for apply
-__global__ __launch_bounds__(256) void bwd_finalize_kernel(int C, const double* __restrict__ part, int RS,
-                                                          const float* __restrict__ var, float eps,
-                                                          float* __restrict__ sums, float* __restrict__ dgamma,
-                                                          float* __restrict__ dbeta, int accumulate) {
-  const int c = fin_channel();
+__device__ __forceinline__ void bwd_finalize_body(int blk, int C, const double* __restrict__ part, int RS,
+                                                  const float* __restrict__ var, float eps, float* __restrict__ sums,
+                                                  float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                  int accumulate) {
+  const int c = blk * kFinCh + (threadIdx.x & 15);
   double a, b;
   if (!sum_partials(part, RS, C, c, a, b)) return;
   const float invstd = 1.0f / sqrtf(var[c] + eps);
@@ -184,6 +184,13 @@ __global__ __launch_bounds__(256) void bwd_finalize_kernel(int C, const double* 
   sums[2 * c + 1] = sdyx;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + sdy : sdy;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + sdyx : sdyx;
+}
+
+__global__ __launch_bounds__(256) void bwd_finalize_kernel(int C, const double* __restrict__ part, int RS,
+                                                          const float* __restrict__ var, float eps,
+                                                          float* __restrict__ sums, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta, int accumulate) {
+  bwd_finalize_body(blockIdx.x, C, part, RS, var, eps, sums, dgamma, dbeta, accumulate);
 }
 
 // dy = (dy_act - sdy/M - xhat * sdyx/M) * invstd * gamma   (2-D launch as apply_kernel)
@@ -257,11 +264,11 @@ __global__ void coef_kernel(int C, const float* __restrict__ mean, const float* 
 }
 
 // column sums of RS fp64 partial rows (the fused conv bias gradient), fixed order
-__global__ __launch_bounds__(256) void colsum_f64_finalize_kernel(int C, int RS, const double* __restrict__ part,
-                                                                 float* __restrict__ out, int accumulate) {
+__device__ __forceinline__ void colsum_f64_body(int blk, int C, int RS, const double* __restrict__ part,
+                                                float* __restrict__ out, int accumulate) {
   __shared__ double red[16][kFinCh];
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = fin_channel();
+  const int c = blk * kFinCh + cl;
   double s = 0.0;
   if (c < C)
 #pragma unroll 8
@@ -273,6 +280,24 @@ __global__ __launch_bounds__(256) void colsum_f64_finalize_kernel(int C, int RS,
   for (int q = 0; q < 16; ++q) t += red[q][cl];
   const float v = (float)t;
   out[c] = accumulate ? out[c] + v : v;
+}
+
+__global__ __launch_bounds__(256) void colsum_f64_finalize_kernel(int C, int RS, const double* __restrict__ part,
+                                                                 float* __restrict__ out, int accumulate) {
+  colsum_f64_body(blockIdx.x, C, RS, part, out, accumulate);
+}
+
+// One launch for two independent finalizes of the Conv-BN stack backward: blocks [0, nb_bn)
+// finish this layer's BatchNorm-backward sums, the rest the previous (deeper) layer's conv
+// bias sums, which no kernel in between reads.
+__global__ __launch_bounds__(256) void bwd_finalize_bias_kernel(int C, const double* __restrict__ part, int RS,
+                                                               const float* __restrict__ var, float eps,
+                                                               float* __restrict__ sums, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta, int accumulate, int nb_bn,
+                                                               int Cb, int RSb, const double* __restrict__ bpart,
+                                                               float* __restrict__ db, int acc_b) {
+  if ((int)blockIdx.x < nb_bn) bwd_finalize_body(blockIdx.x, C, part, RS, var, eps, sums, dgamma, dbeta, accumulate);
+  else colsum_f64_body(blockIdx.x - nb_bn, Cb, RSb, bpart, db, acc_b);
 }
 
 // ---- fused Conv-BN stacks under bf16 (gemm.hip autovc_bnconv_*): the BatchNorm +
@@ -432,6 +457,19 @@ extern "C" int autovc_bn_bwd_finalize_f32(int RS, int C, const double* part, con
   hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, stream, C, part, RS, var, eps, sums,
                      dgamma, dbeta, accumulate);
   AVC_CHECK_LAUNCH("autovc_bn_bwd_finalize_f32");
+  return avc::kOk;
+}
+
+extern "C" int autovc_bn_bwd_finalize_bias_f32(int RS, int C, const double* part, const float* var, float eps,
+                                               float* sums, float* dgamma, float* dbeta, int accumulate, int RSb,
+                                               int Cb, const double* bias_part, float* db, int acc_b,
+                                               hipStream_t stream) {
+  AVC_CHECK_ARG(RS > 0 && C > 0 && part && var && sums && RSb > 0 && Cb > 0 && bias_part && db,
+                "autovc_bn_bwd_finalize_bias_f32: bad args");
+  const int nb = (C + kFinCh - 1) / kFinCh, nbb = (Cb + kFinCh - 1) / kFinCh;
+  hipLaunchKernelGGL(bwd_finalize_bias_kernel, dim3(nb + nbb), dim3(256), 0, stream, C, part, RS, var, eps, sums,
+                     dgamma, dbeta, accumulate, nb, Cb, RSb, bias_part, db, acc_b);
+  AVC_CHECK_LAUNCH("autovc_bn_bwd_finalize_bias_f32");
   return avc::kOk;
 }
 

@@ -714,6 +714,25 @@ def _chain_ok(x, layers, training):
     return True
 
 
+def _bn_bwd_finalize(pending, rows, C, part, var, eps, sums, gg, gb, acc):
+    """A stack layer's BatchNorm-backward sums (+ dgamma / dbeta), in the same launch as the
+    deeper layer's pending conv bias finalize when there is one."""
+    if pending is None:
+        _lib.call("autovc_bn_bwd_finalize_f32", rows, C, part, var.data_ptr(), float(eps), sums,
+                  _p(gg.buf if gg else None), _p(gb.buf if gb else None), int(acc), _s())
+        return
+    rs_b, c_b, bpart, go = pending
+    _lib.call("autovc_bn_bwd_finalize_bias_f32", rows, C, part, var.data_ptr(), float(eps), sums,
+              _p(gg.buf if gg else None), _p(gb.buf if gb else None), int(acc), rs_b, c_b, bpart,
+              go.buf.data_ptr(), int(go.acc), _s())
+
+
+def _bias_finalize(pending):
+    if pending is not None:
+        rs_b, c_b, bpart, go = pending
+        _lib.call("autovc_colsum_f64_finalize_f32", rs_b, c_b, bpart, go.buf.data_ptr(), int(go.acc), _s())
+
+
 class ConvBNChainFn(torch.autograd.Function):
     """Forward / backward of a Conv-BN-act stack (see above).  apply(spec, x, residual,
     *per-layer (W, b, gamma, beta, running_mean, running_var, num_batches_tracked));
@@ -801,6 +820,7 @@ class ConvBNChainFn(torch.autograd.Function):
         grads = [None] * len(tensors)
         dx = None
         part, rows = None, 0
+        pending = None   # the previous layer's conv bias partials, finalized in the next launch
         for l in range(L - 1, -1, -1):
             W, b, g, be = tensors[7 * l:7 * l + 4]
             Co, Ci = W.shape[0], W.shape[1]
@@ -821,8 +841,8 @@ class ConvBNChainFn(torch.autograd.Function):
                 gg = _GradOut(None, (Co,), dev) if ng else None
                 gb = _GradOut(None, (Co,), dev) if nb else None
             sums = _ws(dev, 8 * Co, "chain_sums")
-            _lib.call("autovc_bn_bwd_finalize_f32", rows, Co, part, varis[l].data_ptr(), float(epss[l]), sums,
-                      _p(gg.buf if gg else None), _p(gb.buf if gb else None), int(acc), _s())
+            _bn_bwd_finalize(pending, rows, Co, part, varis[l], epss[l], sums, gg, gb, acc)
+            pending = None
             if gg is not None:
                 grads[7 * l + 2] = gg.result()
             if gb is not None:
@@ -835,9 +855,9 @@ class ConvBNChainFn(torch.autograd.Function):
             if Dt is not None or Xd is not None or need_b:
                 _lib.call("autovc_wino5_bnbwd_f32", B, T, Co, dz.data_ptr(), Co, y.data_ptr(), Co,
                           coefs[l].data_ptr(), act, sums, _p(Dt), _p(Xd), bpart, _s())
-            if need_b:
+            if need_b:   # finalized with the next layer's BatchNorm sums (one launch) or after the loop
                 go = _GradOut(b, (Co,), dev)
-                _lib.call("autovc_colsum_f64_finalize_f32", RS, Co, bpart, go.buf.data_ptr(), int(go.acc), _s())
+                pending = (RS, Co, bpart, go)
                 grads[7 * l + 1] = go.result()
             if need_w:
                 go = _GradOut(W, (Co, Ci, KS), dev)
@@ -868,6 +888,7 @@ class ConvBNChainFn(torch.autograd.Function):
                     _lib.call("autovc_wino5_output_f32", B, T, Ci, Yd.data_ptr(), 0, dzp.data_ptr(), Ci, _s())
                     dx = dzp
                 del Yd
+        _bias_finalize(pending)
         ctx.ys = ctx.xts = ctx.coefs = None
         return (None, dx, dres, *grads)
 
@@ -991,6 +1012,7 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
         grads = [None] * len(tensors)
         dx = None
         part, rows = None, 0
+        pending = None   # the previous layer's conv bias partials, finalized in the next launch
         for l in range(L - 1, -1, -1):
             W, b, g, be = tensors[7 * l:7 * l + 4]
             Co, Ci = W.shape[0], W.shape[1]
@@ -1008,8 +1030,8 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                 gg = _GradOut(None, (Co,), dev) if ng else None
                 gb = _GradOut(None, (Co,), dev) if nb else None
             sums = _ws(dev, 8 * Co, "chain_sums")
-            _lib.call("autovc_bn_bwd_finalize_f32", rows, Co, part, varis[l].data_ptr(), float(epss[l]), sums,
-                      _p(gg.buf if gg else None), _p(gb.buf if gb else None), int(acc), _s())
+            _bn_bwd_finalize(pending, rows, Co, part, varis[l], epss[l], sums, gg, gb, acc)
+            pending = None
             if gg is not None:
                 grads[7 * l + 2] = gg.result()
             if gb is not None:
@@ -1020,7 +1042,7 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                       0 if h else dy.data_ptr(), dy.data_ptr() if h else 0, bpart, _s())
             if b is not None and needs[3 + 7 * l + 1]:
                 go = _GradOut(b, (Co,), dev)
-                _lib.call("autovc_colsum_f64_finalize_f32", PR, Co, bpart, go.buf.data_ptr(), int(go.acc), _s())
+                pending = (PR, Co, bpart, go)
                 grads[7 * l + 1] = go.result()
             if l == 0:
                 xin, xcoef, xact, wsrc = x, None, 0, (1 if h else 0)
@@ -1055,6 +1077,7 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                     _lib.call("autovc_bnconv_dx_bf16_f32", B, T, Co, Ci, dy.data_ptr(), Wd.data_ptr(), dzp.data_ptr(),
                               0, 0, 0, 0, src, ws, _s())
                     dx = dzp
+        _bias_finalize(pending)
         ctx.ys = ctx.coefs = ctx.zbs = None
         return (None, dx, dres, *grads)
 

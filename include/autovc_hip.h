@@ -225,6 +225,13 @@ int autovc_bn_bwd_partial_f32(int64_t M, int C, const float* dz, int64_t lddz, c
                               hipStream_t stream);
 int autovc_bn_bwd_finalize_f32(int RS, int C, const double* part, const float* var, float eps, float* sums,
                                float* dgamma, float* dbeta, int accumulate, hipStream_t stream);
+/* autovc_bn_bwd_finalize_f32 and, in the same launch, autovc_colsum_f64_finalize_f32 of the
+ * previous (deeper) layer's conv bias partials (RSb rows x Cb, fp64) into db — the Conv-BN
+ * stack backward's two per-layer finalizes as one launch (model_vc_mel.py:49-59,132-169
+ * backward: BatchNorm1d's and the Conv1d bias's gradients). */
+int autovc_bn_bwd_finalize_bias_f32(int RS, int C, const double* part, const float* var, float eps, float* sums,
+                                    float* dgamma, float* dbeta, int accumulate, int RSb, int Cb,
+                                    const double* bias_part, float* db, int acc_b, hipStream_t stream);
 int autovc_colsum_f64_finalize_f32(int RS, int C, const double* part, float* out, int accumulate,
                                    hipStream_t stream);
 
