@@ -43,6 +43,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace {
 
 constexpr int PB = 64;             // batch rows per tile (all of them)
@@ -1167,6 +1169,7 @@ constexpr int BKW = BKS / 8;       // gate rows per wave (64)
 constexpr int BNT = 512;           // 8 waves
 constexpr int BROW = 64;           // batch rows (all of them)
 constexpr int BPLD = BJ + 1;       // padded LDS row of a 64 x 32 partial tile
+constexpr int BSLOTS = 8 * BROW * BPLD;        // floats of the 8 waves' partial-tile slots
 constexpr int BB_GROUP = BAR_LINES;          // 32 lines: per-group partial counters
 constexpr int BB_LINES = BAR_LINES + 32;
 constexpr int64_t BB_BYTES = BB_LINES * L * 4;
@@ -1194,7 +1197,7 @@ __device__ __forceinline__ void st_wt(float* p, float v) {
 template <bool BF>
 __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
   constexpr int H = 1024, G4 = 4 * H;
-  extern __shared__ __attribute__((aligned(16))) float lds[];   // [8 waves][2 products][64][BPLD]
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [8 waves][64][BPLD] slots + fp32 W_hh0 slice
   __shared__ int s_info[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
@@ -1252,8 +1255,12 @@ __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
   const int g = lane >> 4, jl = lane & 15;
   const int kw = k0 + BKW * wave;
   constexpr int NM = BF ? 2 : 16;
-  float wf[3][2][BF ? 1 : 16];
+  // fp32: W_hh1 and W_ih1 slices in VGPRs (64 per lane), W_hh0's in LDS after the reduction
+  // slots (w0s, 64 KB, [wave][cb][g][m / 4][16 lanes][4]: a lane's 4 consecutive m as one
+  // conflict-free ds_read_b128); bf16: all three in VGPRs (48 per lane)
+  float wf[2][2][BF ? 1 : 16];
   bf16x8 wb[3][2][BF ? 2 : 1];
+  float* w0s = lds + BSLOTS;
   {
     const float* Ws[3] = {a.W1, a.Wi1, a.W0};
     const __bf16* Wbs[3] = {a.W1b, a.Wi1b, a.W0b};
@@ -1267,12 +1274,18 @@ __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
           for (int m = 0; m < 2; ++m)
 #pragma unroll
             for (int e = 0; e < 8; ++e) wb[p][cb][m][e] = Wbs[p][(int64_t)(kw + 32 * m + 8 * g + e) * H + col];
-        } else {
+        } else if (p < 2) {
 #pragma unroll
           for (int m = 0; m < 16; ++m) wf[p][cb][m] = Ws[p][(int64_t)(kw + 16 * g + m) * H + col];
+        } else {
+#pragma unroll
+          for (int m = 0; m < 16; ++m)
+            w0s[((((wave * 2 + cb) * 4 + g) * 4 + (m >> 2)) * 16 + jl) * 4 + (m & 3)] =
+                Ws[p][(int64_t)(kw + 16 * g + m) * H + col];
         }
       }
   }
+  __syncthreads();
   // ---- cell operands of the next cell update, prefetched (they do not depend on the recurrence)
   const float* gsrc = l1cell ? a.g1 : a.g0;
   const float* csrc = l1cell ? a.c1 : a.c0;
@@ -1284,102 +1297,123 @@ __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
     cp = t > 0 ? csrc[((int64_t)cb_ * T + t - 1) * H + cu] : 0.f;
     dho = l1cell ? a.dh1[(int64_t)cb_ * a.d_ldb + (int64_t)t * a.d_ldt + cu] : 0.f;
   };
-  if (l1cell) load_cell(T - 1);
-  float* slots = lds;                                 // [wave][product][64][BPLD]
+  float* slots = lds;                                 // [wave][64][BPLD]
   constexpr int SLOT = BROW * BPLD;
   float* mypart = a.part + (int64_t)(jb * BKB + kb) * 3 * BROW * BJ;
   int* grp = a.bar + (BB_GROUP + jb) * L;
-  // one MFMA tile of the product: A = dG rows (sc1 buffer loads), B = the weight registers
-  auto products = [&](const float* dGt, const __bf16* dGbt, bool two, int p_first, f32x4 (&acc)[2][4][2]) {
-    // dGt / dGbt: dG at step t (row b at + b * T * 4H); two: also the second product (P1 and Q
-    // share the dG1 operand)
+  // ---- the products.  A = this wave's 64 rows x 64 k of a dG row block (sc1 buffer loads
+  // from a wave-uniform base), B = the weight registers.  All of a tensor's A fragments are
+  // issued at once (fp32: 16 x 16 B per lane, bf16: 8), and as each 16-row block of dG1 has
+  // fed its P1 / Q MFMAs its registers are refilled with dG0's block for P0, so the dG0
+  // loads are in flight under the P1 / Q MFMAs.
+  constexpr int NA = BF ? 2 : 4;                       // 16-B A loads per row block per lane
+  f32x4 A[4][NA];
+  auto issue = [&](const void* dGrow0, int rb) {       // dGrow0: element (b = 0, t, k = 0)
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(dGrow0), (short)0,
+                                                                       0x7fffffff, 0x00020000);
+    const uint32_t off = BF ? (uint32_t)((((int64_t)(16 * rb + jl) * T) * G4 + kw + 8 * g) * 2)
+                            : (uint32_t)((((int64_t)(16 * rb + jl) * T) * G4 + kw + 16 * g) * 4);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) acc[i][rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NA; ++i)
+      A[rb][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off + (BF ? 64 : 16) * i, 0, 16));
+  };
+  // acc[i][rb][cb] += A[rb] x W[p + i] over this wave's 64 k (NP products, first P)
+  auto mfma_rb = [&](auto np_tag, auto p_tag, int rb, f32x4 (&acc)[2][4][2]) {
+    constexpr int NP = decltype(np_tag)::value, P = decltype(p_tag)::value;
     if constexpr (BF) {
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(dGbt), (short)0,
-                                                                         0x7fffffff, 0x00020000);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        bf16x8 av[2];
-        const uint32_t off = (uint32_t)((((int64_t)(16 * rb + jl) * T) * G4 + kw + 8 * g) * 2);
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
-          av[m] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off + 64 * m, 0, 16));
+        for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+          for (int i = 0; i < NP; ++i)
+            acc[i][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, A[rb][m]),
+                                                                     wb[P + i][cb][m], acc[i][rb][cb], 0, 0, 0);
+    } else if constexpr (P == 2) {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) {
-            acc[0][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], wb[p_first][cb][m], acc[0][rb][cb], 0, 0, 0);
-            if (two)
-              acc[1][rb][cb] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], wb[p_first + 1][cb][m], acc[1][rb][cb], 0, 0, 0);
-          }
+      for (int mq = 0; mq < 4; ++mq) {
+        f32x4 bw[2];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          bw[cb] = *reinterpret_cast<const f32x4*>(w0s + ((((wave * 2 + cb) * 4 + g) * 4 + mq) * 16 + jl) * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            acc[0][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[rb][mq][e], bw[cb][e], acc[0][rb][cb], 0, 0, 0);
       }
     } else {
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dGt), (short)0,
-                                                                         0x7fffffff, 0x00020000);
-      f32x4 av[2][4];
-      auto ld = [&](int rb, f32x4 (&v)[4]) {
-        const uint32_t off = (uint32_t)((((int64_t)(16 * rb + jl) * T) * G4 + kw + 16 * g) * 4);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * i, 0, 16));
-      };
-      ld(0, av[0]);
+      for (int m = 0; m < 16; ++m)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        if (rb + 1 < 4) ld(rb + 1, av[(rb + 1) & 1]);
+        for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int m = 0; m < 16; ++m)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) {
-            const float x = av[rb & 1][m >> 2][m & 3];
-            acc[0][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x, wf[p_first][cb][m], acc[0][rb][cb], 0, 0, 0);
-            if (two)
-              acc[1][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x, wf[p_first + 1][cb][m], acc[1][rb][cb], 0, 0, 0);
-          }
-      }
+          for (int i = 0; i < NP; ++i)
+            acc[i][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[rb][m >> 2][m & 3], wf[P + i][cb][m],
+                                                                  acc[i][rb][cb], 0, 0, 0);
     }
   };
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I0 = std::integral_constant<int, 0>;
   // this wave's partial tiles -> LDS slots, then every thread sums the 8 waves' slots in wave
   // order for (np) products and stores the workgroup's partial tiles (plain stores: the group
   // reads them from this XCD's L2)
   auto reduce_store = [&](f32x4 (&acc)[2][4][2], int np, int p_first) {
-    for (int i = 0; i < np; ++i)
+    for (int i = 0; i < np; ++i) {
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            slots[(wave * 2 + i) * SLOT + (16 * rb + 4 * g + r) * BPLD + 16 * cb + jl] = acc[i][rb][cb][r];
-    __syncthreads();
-    for (int e = tid; e < np * BROW * BJ; e += BNT) {
-      const int i = e / (BROW * BJ), rc = e % (BROW * BJ), row = rc / BJ, col = rc % BJ;
-      float s = 0.f;
+            slots[wave * SLOT + (16 * rb + 4 * g + r) * BPLD + 16 * cb + jl] = acc[i][rb][cb][r];
+      __syncthreads();
+      for (int e = tid; e < BROW * BJ; e += BNT) {
+        const int row = e / BJ, col = e % BJ;
+        float sum = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) s += slots[(w * 2 + i) * SLOT + row * BPLD + col];
-      mypart[(int64_t)(p_first + i) * BROW * BJ + rc] = s;
+        for (int w = 0; w < 8; ++w) sum += slots[w * SLOT + row * BPLD + col];
+        mypart[(int64_t)(p_first + i) * BROW * BJ + e] = sum;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   };
   for (int s = 0; s <= T; ++s) {
     const int t1 = T - 1 - s, t0 = T - s;
     const bool act1 = t1 >= 0, act0 = s >= 1, doP1Q = s >= 1, doP0 = s >= 2;
+    // this iteration's cell operands (independent of the recurrence): issued first, they land
+    // under the products (issued before the grid barrier they only lengthened its wait)
+    if (l1cell ? act1 : act0) load_cell(l1cell ? t1 : t0);
     // ---- products over this workgroup's K slice
     if (doP1Q) {
+      const void* d1 = BF ? (const void*)(a.dG1b + (int64_t)t0 * G4) : (const void*)(a.dG1 + (int64_t)t0 * G4);
+      const void* d0 = BF ? (const void*)(a.dG0b + (int64_t)(t0 + 1) * G4)
+                          : (const void*)(a.dG0 + (int64_t)(t0 + 1) * G4);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) issue(d1, rb);
       f32x4 acc[2][4][2];
-      products(a.dG1 + (int64_t)t0 * G4, a.dG1b + (int64_t)t0 * G4, true, 0, acc);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[i][rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        mfma_rb(I2{}, I0{}, rb, acc);                      // P1 (W_hh1) and Q (W_ih1) on dG1
+        if (doP0) issue(d0, rb);
+      }
       reduce_store(acc, 2, 0);
-    }
-    if (doP0) {
-      f32x4 acc[2][4][2];
-      products(a.dG0 + (int64_t)(t0 + 1) * G4, a.dG0b + (int64_t)(t0 + 1) * G4, false, 2, acc);
-      reduce_store(acc, 1, 2);
+      if (doP0) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[0][rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) mfma_rb(I1{}, I2{}, rb, acc);   // P0 (W_hh0) on dG0
+        reduce_store(acc, 1, 2);
+      }
     }
     // ---- the group's 8 K-slice partials are in this XCD's L2
     if (doP1Q) {
@@ -1411,13 +1445,16 @@ __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
     if (act) {
       float dh = dho;
       if (l1cell ? doP1Q : true) {
-        const float* base = a.part + (int64_t)jb * BKB * 3 * BROW * BJ + cb_ * BJ + kb * 4 + (ce & 3);
+        // the group's partial tiles: a wave-uniform buffer base (a per-lane base would force a
+        // waterfall loop over the 64 lanes' descriptors), the cell's offset in voffset
+        const float* base = a.part + (int64_t)jb * BKB * 3 * BROW * BJ;
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
                                                                            0x7fffffff, 0x00020000);
+        const uint32_t cell_off = (uint32_t)((cb_ * BJ + kb * 4 + (ce & 3)) * 4);
         float sq = 0.f, sp = 0.f;
 #pragma unroll
         for (int k2 = 0; k2 < BKB; ++k2) {
-          const uint32_t o = (uint32_t)(k2 * 3 * BROW * BJ * 4);
+          const uint32_t o = cell_off + (uint32_t)(k2 * 3 * BROW * BJ * 4);
           if (l1cell) {
             sp += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 16));
           } else {
@@ -1443,23 +1480,11 @@ __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
         __bf16* db = (l1cell ? a.dG1b : a.dG0b) + ((int64_t)cb_ * T + t) * G4 + cu;
         const float v4[4] = {di, df, dgg, dO};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          // the 4 units of a row sit in 4 consecutive lanes: one 8-byte write-through store
-          const int v = (int)__builtin_bit_cast(unsigned short, (__bf16)v4[q]);
-          const int q0 = lane & ~3;
-          const unsigned long long w =
-              (unsigned long long)(unsigned)(__shfl(v, q0, 64) | (__shfl(v, q0 + 1, 64) << 16)) |
-              ((unsigned long long)(unsigned)(__shfl(v, q0 + 2, 64) | (__shfl(v, q0 + 3, 64) << 16)) << 32);
-          if ((lane & 3) == 0)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(db + q * H), w, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (int q = 0; q < 4; ++q)
+          __hip_atomic_store(reinterpret_cast<unsigned short*>(db + q * H),
+                             __builtin_bit_cast(unsigned short, (__bf16)v4[q]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       }
-    }
-    // next cell's operands: layer 1 at t1 - 1, layer 0 at t0 - 1 (= T - 1 for s = 0)
-    {
-      const int tn = l1cell ? t1 - 1 : (s == 0 ? T - 1 : t0 - 1);
-      if (tn >= 0) load_cell(tn);
     }
     if (s < T && !grid_sync(pa, xcc_id, xcc_wgs, xcc_n, census, status, s)) {
       fail();
@@ -1469,7 +1494,7 @@ __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
 }
 
 int g_bwd_ok = -1;
-constexpr int kBwdLds = 8 * 2 * BROW * BPLD * 4;
+constexpr int kBwdLds = (BSLOTS + 8 * 2 * 4 * 4 * 16 * 4) * 4;   // slots + the fp32 W_hh0 slice
 
 template <bool BF>
 bool bwd_fits_one() {

@@ -1534,10 +1534,14 @@ class LSTM2StackFn(torch.autograd.Function):
             _flush_grad_queue(after=mark)
 
 
-# decoder lstm2 backward as ONE persistent launch (lstm2_bwd_persist_kernel) where the shape
-# and device allow it (B = 64, H = 1024, 256 CUs); AVC_LSTM2_BWD_PERSIST=0 selects the
-# per-step product + pointwise launches
-_BWD_PERSIST_ON = os.environ.get("AVC_LSTM2_BWD_PERSIST", "1") != "0"
+# decoder lstm2 backward as ONE persistent launch (lstm2_bwd_persist_kernel) — opt-in
+# (AVC_LSTM2_BWD_PERSIST=1, B = 64, H = 1024, 256 CUs): measured slower than the per-step
+# product + pointwise launches (T = 128: fp32 28.9 vs 24.4 us per wavefront step, bf16 21.0
+# vs 14.8; training step 20.0 vs 14.6 ms before the reduction / prefetch fixes,
+# profiles/r04/lstm2_bwd_persist_time.txt): the per-step group reduction of the K-slice
+# partials, the write-through dG hand-off and the grid barrier cost ~11 us per step, against
+# the launch pair's ~5 us
+_BWD_PERSIST_ON = os.environ.get("AVC_LSTM2_BWD_PERSIST", "0") != "0"
 _BWD_FLUSH = os.environ.get("AVC_LSTM2_BWD_FLUSH", "defer")
 
 
