@@ -199,14 +199,27 @@ int g_timeout_ticks = 0;             // 0 = the default 1 s; tests force a timeo
 // for the hand-off stores alone).  The cell state is carried in registers, never re-read.
 struct CellOut { float c, h, i, f, g, o; };
 
+// Every multiply-add is spelled out (contraction off): the kernels that share this update
+// (lstm_persist_kernel, lstm2_rs_kernel) then round it identically whatever the compiler
+// would fuse in each context.
+__device__ __forceinline__ float tanh_fast_nc(float x) {
+#pragma clang fp contract(off)
+  return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(x * 2.88539008f) + 1.0f), 1.0f);
+}
+__device__ __forceinline__ float sigmoid_fast_nc(float x) {
+#pragma clang fp contract(off)
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504f));
+}
+
 __device__ __forceinline__ CellOut cell(const float (&pre)[4], float cp) {
+#pragma clang fp contract(off)
   CellOut r;
-  r.i = avc_sigmoid_fast(pre[0]);
-  r.f = avc_sigmoid_fast(pre[1]);
-  r.g = avc_tanh_fast(pre[2]);
-  r.o = avc_sigmoid_fast(pre[3]);
-  r.c = r.f * cp + r.i * r.g;
-  r.h = r.o * avc_tanh_fast(r.c);
+  r.i = sigmoid_fast_nc(pre[0]);
+  r.f = sigmoid_fast_nc(pre[1]);
+  r.g = tanh_fast_nc(pre[2]);
+  r.o = sigmoid_fast_nc(pre[3]);
+  r.c = __builtin_fmaf(r.f, cp, r.i * r.g);
+  r.h = r.o * tanh_fast_nc(r.c);
   return r;
 }
 
@@ -665,6 +678,407 @@ __global__ __launch_bounds__(PNT, 1) void lstm_persist_kernel(PArgs a) {
   store_outputs(last);                                               // the final iteration's outputs
 }
 
+// ---------------------------------------------------------------- row-split stacked forward
+// lstm_persist_kernel gives each workgroup all 64 batch rows x 16 gate columns, so every CU
+// streams the whole h0_{t-1} and h1_{t-2} (512 KB fp32) out of L2 every step.  Here the two
+// workgroups of a pair split the rows instead (32 rows each) and each owns twice the columns
+// (8 units x 4 gates = 32): the same MFMA work per CU, half the per-CU h fill, twice the
+// stationary weights — W_hh0's 32 rows in LDS (128 KB fp32, [k/4][32][4]), W_ih1's and W_hh1's
+// as MFMA B fragments in VGPRs (128 per lane fp32, 64 bf16).  Wave w = k range w (128 k),
+// 2 row blocks x 2 column blocks per wave; the 8 partial tiles summed through LDS in fixed order
+// (the k order of lstm_persist_kernel: same sums), cell update by waves 0-3 (thread e: row
+// e / 8, unit e % 8).  Iteration structure, barrier, hand-off and fault path are those of
+// lstm_persist_kernel (both wavefront forms).
+constexpr int RS_ROWS = 32;                 // batch rows per workgroup
+constexpr int RS_U = 8;                     // hidden units per workgroup
+constexpr int RS_C = 4 * RS_U;              // tile columns
+constexpr int RS_RB = RS_ROWS / 16;         // 16-row blocks
+constexpr int RS_CB = RS_C / 16;            // 16-column blocks
+constexpr int RS_LD = RS_C + 1;             // padded partial-tile row
+constexpr int RS_SLOT = RS_ROWS * RS_LD;
+static_assert(PNW == 8 && PRH == 1, "row-split form: 8 waves, one k range each");
+
+constexpr int RS_KEEP = 2 * 6 * 256;        // cell outputs kept between iterations: [layer][6][thread]
+
+template <int HH, bool BF>
+constexpr int rs_lds_bytes() {
+  return (BF ? 2 : 4) * HH * RS_C + 4 * (NSLOT * RS_SLOT + RS_KEEP);
+}
+static_assert(rs_lds_bytes<1024, false>() <= 160 * 1024, "LDS budget (row split)");
+
+using RsAcc = f32x4[RS_RB][RS_CB];
+
+// fp32 products over this wave's k range.  S0: layer 1's input product (h0_{t-1}, W_ih1 from
+// VGPRs), L0: layer 0's recurrent product (h0_{t-1}, W_hh0 from LDS), S1: layer 1's recurrent
+// product (h1, W_hh1 from VGPRs).  Lane l: k slot l >> 4 covers k = kbase + 64... as in
+// gemm_wave (KL consecutive k per slot), A row r0 + 16 rb + (l & 15), B column 16 cb + (l & 15).
+template <int KL, bool S0, bool L0, bool S1>
+__device__ __forceinline__ void rs_gemm(const float* __restrict__ hk0_t, const float* __restrict__ hk1_t,
+                                        const float (&wi)[RS_CB][KL], const float (&wh)[RS_CB][KL],
+                                        const float* W0, int kb0, int B, int r0, int lane, RsAcc& acc1,
+                                        RsAcc& acc0) {
+  const __amdgpu_buffer_rsrc_t q0 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hk0_t), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t q1 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hk1_t), (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t off0 = (uint32_t)((kb0 * B + r0 + (lane & 15)) * 16);
+  const uint32_t gstride = (uint32_t)B * 16;
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int g, int rb) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off0 + g * gstride + rb * 256, 0, 16));
+  };
+  f32x4 a0[RS_RB], a1[RS_RB];
+#pragma unroll
+  for (int rb = 0; rb < RS_RB; ++rb) {
+    if (S0 || L0) a0[rb] = ld(q0, 0, rb);
+    if (S1) a1[rb] = ld(q1, 0, rb);
+  }
+  const float* w0p = W0 + (kb0 * RS_C + (lane & 15)) * 4;
+#pragma unroll
+  for (int g = 0; g < KL / 4; ++g) {
+    f32x4 x0[RS_RB], x1[RS_RB];
+#pragma unroll
+    for (int rb = 0; rb < RS_RB; ++rb) {
+      x0[rb] = a0[rb];
+      x1[rb] = a1[rb];
+    }
+    if (g + 1 < KL / 4) {
+#pragma unroll
+      for (int rb = 0; rb < RS_RB; ++rb) {
+        if (S0 || L0) a0[rb] = ld(q0, g + 1, rb);
+        if (S1) a1[rb] = ld(q1, g + 1, rb);
+      }
+    }
+    f32x4 bv0[RS_CB] = {};
+    if (L0)
+#pragma unroll
+      for (int cb = 0; cb < RS_CB; ++cb) bv0[cb] = *reinterpret_cast<const f32x4*>(w0p + (g * RS_C + 16 * cb) * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int rb = 0; rb < RS_RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < RS_CB; ++cb) {
+          if (S0) acc1[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], wi[cb][4 * g + q], acc1[rb][cb], 0, 0, 0);
+          if (S1) acc1[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[rb][q], wh[cb][4 * g + q], acc1[rb][cb], 0, 0, 0);
+          if (L0) acc0[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[rb][q], bv0[cb][q], acc0[rb][cb], 0, 0, 0);
+        }
+  }
+}
+
+// bf16 products (v_mfma_f32_16x16x32_bf16), operand maps of gemm_wave_bf: lane l supplies the
+// 8 k of block k8_0 + 4 st of row r0 + 16 rb + (l & 15); B fragments W_hh0 [H/8][32][8] (LDS),
+// W_ih1 / W_hh1 (VGPRs)
+template <int NS, bool S0, bool L0, bool S1>
+__device__ __forceinline__ void rs_gemm_bf(const __bf16* __restrict__ hk0_t, const __bf16* __restrict__ hk1_t,
+                                           const bf16x8 (&wi)[RS_CB][NS], const bf16x8 (&wh)[RS_CB][NS],
+                                           const __bf16* W0, int k8_0, int B, int r0, int lane, RsAcc& acc1,
+                                           RsAcc& acc0) {
+  const __amdgpu_buffer_rsrc_t q0 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(hk0_t), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t q1 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(hk1_t), (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t off0 = (uint32_t)((k8_0 * B + r0 + (lane & 15)) * 16);
+  const uint32_t sstride = (uint32_t)B * 64;
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int st, int rb) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off0 + st * sstride + rb * 256, 0, 16));
+  };
+  bf16x8 a0[RS_RB], a1[RS_RB];
+#pragma unroll
+  for (int rb = 0; rb < RS_RB; ++rb) {
+    if (S0 || L0) a0[rb] = ld(q0, 0, rb);
+    if (S1) a1[rb] = ld(q1, 0, rb);
+  }
+  const __bf16* w0p = W0 + (k8_0 * RS_C + (lane & 15)) * 8;
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    bf16x8 x0[RS_RB], x1[RS_RB];
+#pragma unroll
+    for (int rb = 0; rb < RS_RB; ++rb) {
+      x0[rb] = a0[rb];
+      x1[rb] = a1[rb];
+    }
+    if (st + 1 < NS) {
+#pragma unroll
+      for (int rb = 0; rb < RS_RB; ++rb) {
+        if (S0 || L0) a0[rb] = ld(q0, st + 1, rb);
+        if (S1) a1[rb] = ld(q1, st + 1, rb);
+      }
+    }
+    bf16x8 bv0[RS_CB] = {};
+    if (L0)
+#pragma unroll
+      for (int cb = 0; cb < RS_CB; ++cb)
+        bv0[cb] = *reinterpret_cast<const bf16x8*>(w0p + (st * 4 * RS_C + 16 * cb) * 8);
+#pragma unroll
+    for (int rb = 0; rb < RS_RB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < RS_CB; ++cb) {
+        if (S0) acc1[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0[rb], wi[cb][st], acc1[rb][cb], 0, 0, 0);
+        if (S1) acc1[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[rb], wh[cb][st], acc1[rb][cb], 0, 0, 0);
+        if (L0) acc0[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0[rb], bv0[cb], acc0[rb][cb], 0, 0, 0);
+      }
+  }
+}
+
+// partial tile (acc[rb][cb], C/D map col = lane & 15, row = 4 (lane >> 4) + r) -> LDS slot
+template <bool ADD>
+__device__ __forceinline__ void rs_tile(float* slot, const RsAcc& acc, int lane) {
+#pragma unroll
+  for (int rb = 0; rb < RS_RB; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RS_CB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* p = slot + (16 * rb + 4 * (lane >> 4) + r) * RS_LD + 16 * cb + (lane & 15);
+        if (ADD) *p += acc[rb][cb][r];
+        else *p = acc[rb][cb][r];
+      }
+}
+
+template <int HH, bool BF, bool LAG2>
+__global__ __launch_bounds__(PNT, 1) void lstm2_rs_kernel(PArgs a) {
+  constexpr int H = HH, KW = HH / PNW, KL = KW / 4, NS = KW / 32;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* W0 = lds;                                          // fp32 [H/4][32][4]
+  __bf16* W0b = reinterpret_cast<__bf16*>(lds);             // bf16 [H/8][32][8]
+  float* red = lds + (BF ? HH * RS_C / 2 : HH * RS_C);      // NSLOT partial-tile slots
+  int* status = reinterpret_cast<int*>(red + RS_C);         // pad column of slot 0's row 0
+  // the epilogue threads' cell outputs (c, h, i, f, g, o of both layers) wait in LDS for the
+  // next iteration's stores instead of holding 12 VGPRs across the products
+  float* keep = red + NSLOT * RS_SLOT;
+  int xcc_id = 0, xcc_wgs = 0, xcc_n = 0;
+  int census[16] = {};
+  const int B = a.B, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware ownership (see lstm_persist_kernel): block b runs on XCD b % 8; that XCD's 32
+  // workgroups own 16 consecutive unit blocks of 8 units, two row halves each
+  const int nxb = (int)gridDim.x / 8, slot = (int)blockIdx.x / 8;
+  const int j0 = ((int)blockIdx.x % 8 * (nxb / 2) + slot / 2) * RS_U;
+  const int r0 = (slot & 1) * RS_ROWS;
+  auto grow = [&](int col) { return (col >> 3) * H + j0 + (col & 7); };   // tile column -> gate row
+  // epilogue ownership: thread e < 256 owns (batch row r0 + e / 8, unit j0 + e % 8)
+  const int er = tid >> 3, eu = tid & 7, eb = r0 + er, ej = j0 + eu;
+  const bool eown = tid < 4 * 64 && eb < B;
+  auto fail = [&]() {
+    const float nan = __builtin_nanf("");
+    if (eown)
+      for (int t = 0; t < T; ++t) {
+        a.h0[(int64_t)eb * a.h0_ldb + (int64_t)t * a.h0_ldt + ej] = nan;
+        a.c0[((int64_t)eb * T + t) * H + ej] = nan;
+        a.h1[((int64_t)eb * T + t) * H + ej] = nan;
+        a.c1[((int64_t)eb * T + t) * H + ej] = nan;
+      }
+    if (tid == 0)
+      __hip_atomic_fetch_or(&g_avc_fault, kFaultLstm2Persist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  if (tid == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 15;
+    add_rlx(a.bar + (BAR_CENSUS + xcc) * L, 1);
+    add_rlx(a.bar + BAR_START * L, 1);
+    const bool ok = wait_ge(a.bar + BAR_START * L, gridDim.x, a.bar + BAR_ERR * L, a.timeout_ticks);
+    int nx = 0;
+    for (int x = 0; x < 16; ++x) {
+      census[x] = ld_rlx(a.bar + (BAR_CENSUS + x) * L);
+      nx += census[x] > 0;
+    }
+    xcc_id = (int)xcc;
+    xcc_wgs = ld_rlx(a.bar + (BAR_CENSUS + xcc) * L);
+    xcc_n = nx;
+    *status = ok ? 0 : 1;
+  }
+  // ---- weights: W_hh0 -> LDS (k-blocked), W_ih1 / W_hh1 -> VGPRs (B fragments)
+  if (BF) {
+    for (int e = tid; e < (H / 8) * RS_C; e += PNT) {
+      const int kb = e / RS_C, col = e % RS_C;
+      *reinterpret_cast<bf16x8*>(W0b + e * 8) = *reinterpret_cast<const bf16x8*>(a.W0b + (int64_t)grow(col) * H + kb * 8);
+    }
+  } else {
+    for (int e = tid; e < (H / 4) * RS_C; e += PNT) {
+      const int kb = e / RS_C, col = e % RS_C;
+      *reinterpret_cast<f32x4*>(W0 + e * 4) = *reinterpret_cast<const f32x4*>(a.W_hh0 + (int64_t)grow(col) * H + kb * 4);
+    }
+  }
+  const int kw = wave;
+  const int kbase = kw * KW + KL * (lane >> 4), kb0 = kbase / 4;
+  const int k8_0 = (kw * KW) / 8 + (lane >> 4);
+  float wi[RS_CB][BF ? 1 : KL], wh[RS_CB][BF ? 1 : KL];
+  bf16x8 wib[RS_CB][BF ? NS : 1], whb[RS_CB][BF ? NS : 1];
+#pragma unroll
+  for (int cb = 0; cb < RS_CB; ++cb) {
+    const int64_t row = (int64_t)grow(16 * cb + (lane & 15)) * H;
+    if constexpr (BF) {
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        wib[cb][st] = *reinterpret_cast<const bf16x8*>(a.Wi1b + row + 8 * (k8_0 + 4 * st));
+        whb[cb][st] = *reinterpret_cast<const bf16x8*>(a.W1b + row + 8 * (k8_0 + 4 * st));
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < KL / 4; ++g) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(a.W_ih1 + row + kbase + 4 * g);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(a.W_hh1 + row + kbase + 4 * g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          wi[cb][4 * g + q] = u[q];
+          wh[cb][4 * g + q] = v[q];
+        }
+      }
+    }
+  }
+  if (tid < 256) {                                               // c_{-1} = 0 for both layers
+    keep[tid] = 0.f;
+    keep[6 * 256 + tid] = 0.f;
+  }
+  __syncthreads();
+  if (*status != 0) {
+    fail();
+    return;
+  }
+
+  float bias1[4] = {0.f, 0.f, 0.f, 0.f};
+  if (eown)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bias1[g] = a.b_ih1[g * H + ej] + a.b_hh1[g * H + ej];
+  const int64_t BH = (int64_t)B * H;
+  float* keep_t = keep + (tid & 255);
+  auto cell_keep = [&](int layer, const float (&pre)[4]) {      // waves 0-3: returns h
+    float* k = keep_t + layer * 6 * 256;
+    const CellOut r = cell(pre, k[0]);
+    k[0] = r.c; k[256] = r.h; k[512] = r.i; k[768] = r.f; k[1024] = r.g; k[1280] = r.o;
+    return r.h;
+  };
+  auto kept = [&](int layer) {
+    const float* k = keep_t + layer * 6 * 256;
+    return CellOut{k[0], k[256], k[512], k[768], k[1024], k[1280]};
+  };
+  // outputs of layer 0 at step t0 and layer 1 at step t1 (either may be out of range)
+  auto store = [&](int t0, int t1) {
+    if (!eown) return;
+    if (t1 >= 0 && t1 < T) {
+      const int64_t o = ((int64_t)eb * T + t1) * H + ej;
+      cell_store(kept(1), a.c1 + o, a.h1 + o, a.g1 ? a.g1 + ((int64_t)eb * T + t1) * 4 * H + ej : nullptr, H);
+    }
+    if (t0 >= 0 && t0 < T) {
+      const int64_t o = ((int64_t)eb * T + t0) * H + ej;
+      cell_store(kept(0), a.c0 + o, a.h0 + (int64_t)eb * a.h0_ldb + (int64_t)t0 * a.h0_ldt + ej,
+                 a.g0 ? a.g0 + ((int64_t)eb * T + t0) * 4 * H + ej : nullptr, H);
+    }
+  };
+  auto sum = [&](int g) {
+    const float* r = red + er * RS_LD + g * RS_U + eu;
+    return ((r[0] + r[RS_SLOT]) + r[2 * RS_SLOT]) + r[3 * RS_SLOT];
+  };
+  // waves 0-3 store their tiles into slots 0-3, then waves 4-7 add into them (fixed order)
+  auto reduce_put = [&](const RsAcc& acc) {
+    if (kw < 4) rs_tile<false>(red + kw * RS_SLOT, acc, lane);
+    __syncthreads();
+    if (kw >= 4) rs_tile<true>(red + (kw - 4) * RS_SLOT, acc, lane);
+  };
+  // one product call: which of the three products run is a template choice
+  auto products = [&](int th0, int th1, bool s0, bool l0, bool s1, RsAcc& acc1, RsAcc& acc0) {
+    if constexpr (BF) {
+      const __bf16* p0 = a.hk0b + (int64_t)th0 * BH;
+      const __bf16* p1 = a.hk1b + (int64_t)th1 * BH;
+      if (s0 && l0 && s1) rs_gemm_bf<NS, true, true, true>(p0, p1, wib, whb, W0b, k8_0, B, r0, lane, acc1, acc0);
+      else if (s0 && l0) rs_gemm_bf<NS, true, true, false>(p0, p1, wib, whb, W0b, k8_0, B, r0, lane, acc1, acc0);
+      else if (s0 && s1) rs_gemm_bf<NS, true, false, true>(p0, p1, wib, whb, W0b, k8_0, B, r0, lane, acc1, acc0);
+      else if (l0 && s1) rs_gemm_bf<NS, false, true, true>(p0, p1, wib, whb, W0b, k8_0, B, r0, lane, acc1, acc0);
+      else if (s0) rs_gemm_bf<NS, true, false, false>(p0, p1, wib, whb, W0b, k8_0, B, r0, lane, acc1, acc0);
+      else if (l0) rs_gemm_bf<NS, false, true, false>(p0, p1, wib, whb, W0b, k8_0, B, r0, lane, acc1, acc0);
+      else if (s1) rs_gemm_bf<NS, false, false, true>(p0, p1, wib, whb, W0b, k8_0, B, r0, lane, acc1, acc0);
+    } else {
+      const float* p0 = a.hk0 + (int64_t)th0 * BH;
+      const float* p1 = a.hk1 + (int64_t)th1 * BH;
+      if (s0 && l0 && s1) rs_gemm<KL, true, true, true>(p0, p1, wi, wh, W0, kb0, B, r0, lane, acc1, acc0);
+      else if (s0 && l0) rs_gemm<KL, true, true, false>(p0, p1, wi, wh, W0, kb0, B, r0, lane, acc1, acc0);
+      else if (s0 && s1) rs_gemm<KL, true, false, true>(p0, p1, wi, wh, W0, kb0, B, r0, lane, acc1, acc0);
+      else if (l0 && s1) rs_gemm<KL, false, true, true>(p0, p1, wi, wh, W0, kb0, B, r0, lane, acc1, acc0);
+      else if (s0) rs_gemm<KL, true, false, false>(p0, p1, wi, wh, W0, kb0, B, r0, lane, acc1, acc0);
+      else if (l0) rs_gemm<KL, false, true, false>(p0, p1, wi, wh, W0, kb0, B, r0, lane, acc1, acc0);
+      else if (s1) rs_gemm<KL, false, false, true>(p0, p1, wi, wh, W0, kb0, B, r0, lane, acc1, acc0);
+    }
+  };
+  auto zero = [](RsAcc& acc) {
+#pragma unroll
+    for (int rb = 0; rb < RS_RB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < RS_CB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // iteration t: layer 0 at step t; layer 1 at step t - LAG (LAG = 2: its input product for
+  // step t - 1 runs between this workgroup's arrival at barrier t and the release)
+  constexpr int LAG = LAG2 ? 2 : 1;
+  const int last = T - 1 + LAG;
+  RsAcc acc1c;                                  // LAG2: layer 1's carried input product
+  zero(acc1c);
+  for (int t = 0; t <= last; ++t) {
+    const bool l0 = t < T, l1 = t >= LAG;
+    if (t >= 1) store(t - 1, t - 1 - LAG);
+    float gxv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (eown && l0) {
+      const float* g = a.gx0 + (int64_t)eb * a.gx_ldb + (int64_t)t * a.gx_ldt;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gxv[q] = g[q * H + ej];
+    }
+    RsAcc acc0, acc1;
+    zero(acc0);
+    if (LAG2) {
+#pragma unroll
+      for (int rb = 0; rb < RS_RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < RS_CB; ++cb) acc1[rb][cb] = acc1c[rb][cb];
+    } else {
+      zero(acc1);
+    }
+    // h0_{t-1} feeds layer 0 (t >= 1) and, one-step form, layer 1's input product (1 <= t <= T);
+    // h1_{t-1-LAG} feeds layer 1's recurrent product (t - 1 - LAG >= 0, layer 1 running)
+    const bool pl0 = l0 && t >= 1, ps0 = !LAG2 && l1, ps1 = l1 && t - 1 - LAG >= 0;
+    products(t >= 1 ? t - 1 : 0, t - 1 - LAG >= 0 ? t - 1 - LAG : 0, ps0, pl0, ps1, acc1, acc0);
+    if (l1) {                                                      // layer 1 at step t - LAG
+      reduce_put(acc1);
+      __syncthreads();
+      if (wave < 4) {
+        float pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pre[g] = sum(g) + bias1[g];
+        handoff<BF>(cell_keep(1, pre), a.hk1 + (int64_t)(t - LAG) * BH, a.hk1b + (int64_t)(t - LAG) * BH, B, eb, ej,
+                    lane);
+      }
+      __syncthreads();                                             // slots reused for layer 0
+    }
+    if (l0) {                                                      // layer 0 at step t
+      reduce_put(acc0);
+      __syncthreads();
+      if (wave < 4) {
+        float pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pre[g] = sum(g) + gxv[g];
+        handoff<BF>(cell_keep(0, pre), a.hk0 + (int64_t)t * BH, a.hk0b + (int64_t)t * BH, B, eb, ej, lane);
+      }
+    }
+    if (t == last) break;
+    if constexpr (LAG2) {
+      grid_arrive(a, xcc_id, xcc_wgs, xcc_n, t);
+      zero(acc1c);                                                 // under the barrier:
+      if (t >= 1 && t - 1 < T) {                                   // layer 1's input product
+        RsAcc dummy;                                               // for its step t - 1
+        products(t - 1, 0, true, false, false, acc1c, dummy);
+      }
+      if (!grid_wait(a, xcc_id, status, t)) {
+        fail();
+        return;
+      }
+    } else if (!grid_sync(a, xcc_id, xcc_wgs, xcc_n, census, status, t)) {
+      fail();
+      return;
+    }
+  }
+  store(last, last - LAG);
+}
+
 int g_cus = -1;
 
 // one workgroup of the <HH, TWO> kernel must fit on a CU, and every workgroup must be resident
@@ -702,11 +1116,43 @@ bool persist_fits() {
 // profiles/r03/ab_lstm2_lag2.txt); not under bf16, whose 8x cheaper products leave the
 // barrier nothing to hide and the second h0 read costs (10.5 -> 14.1 us).  AVC_LSTM2_LAG2=0 /
 // =1 forces it off / on for both; read per launch (one per forward), so tests compare both.
-bool lag2_on(bool bf) {
+// Under the row split (lstm2_rs_kernel, half the h fill per CU) the two-step form wins for
+// bf16 too: 8.2-8.3 -> 7.3 us per wavefront step (profiles/r04/lstm2_rs_ab.txt).
+bool lag2_on(bool bf, bool rs = false) {
   const char* e = getenv("AVC_LSTM2_LAG2");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return !bf;
+  return rs || !bf;
+}
+
+// The row-split stacked forward (lstm2_rs_kernel), the default: AVC_LSTM2_RS=0 selects
+// lstm_persist_kernel instead (read per launch); it runs only where one workgroup per CU fits
+// and B is two row halves.  fp32 15.8-15.9 -> 15.0-15.1 us per wavefront step, 14.66 -> 14.57
+// ms per training step (profiles/r04/lstm2_rs_ab.txt); bit-identical outputs.
+template <bool BF>
+bool rs_fits() {
+  static int per = -1;
+  if (per < 0) {
+    per = 1;
+    for (int lag = 0; lag < 2 && per > 0; ++lag) {
+      const void* k = lag ? reinterpret_cast<const void*>(lstm2_rs_kernel<1024, BF, true>)
+                          : reinterpret_cast<const void*>(lstm2_rs_kernel<1024, BF, false>);
+      int n = 0;
+      if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, rs_lds_bytes<1024, BF>()) != hipSuccess ||
+          (lag ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lstm2_rs_kernel<1024, BF, true>, PNT,
+                                                             rs_lds_bytes<1024, BF>())
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lstm2_rs_kernel<1024, BF, false>, PNT,
+                                                             rs_lds_bytes<1024, BF>())) != hipSuccess ||
+          n < 1)
+        per = 0;
+    }
+  }
+  return per >= 1 && 2 * 1024 / RS_U <= g_cus;
+}
+
+bool rs_on() {
+  const char* e = getenv("AVC_LSTM2_RS");
+  return !(e && e[0] == '0');
 }
 
 template <int HH, bool TWO, bool BF = false>
@@ -718,6 +1164,16 @@ void launch_persist(PArgs& a, void* workspace, hipStream_t stream) {
   a.hk1b = TWO ? a.hk0b + (int64_t)a.T * a.B * HH : nullptr;
   // 1 s of s_memrealtime (100 MHz) per wait: a safety net, never a schedule
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
+  if constexpr (TWO && HH == 1024) {
+    if (rs_on() && a.B == 2 * RS_ROWS && rs_fits<BF>()) {
+      const dim3 grid(2 * HH / RS_U);
+      if (lag2_on(BF, true))
+        hipLaunchKernelGGL((lstm2_rs_kernel<HH, BF, true>), grid, dim3(PNT), (rs_lds_bytes<HH, BF>()), stream, a);
+      else
+        hipLaunchKernelGGL((lstm2_rs_kernel<HH, BF, false>), grid, dim3(PNT), (rs_lds_bytes<HH, BF>()), stream, a);
+      return;
+    }
+  }
   if (TWO && lag2_on(BF))
     hipLaunchKernelGGL((lstm_persist_kernel<HH, TWO, BF, true>), dim3(HH / PU), dim3(PNT), (lds_bytes<HH, TWO, BF>()),
                        stream, a);
@@ -1254,7 +1710,6 @@ __global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
   // MFMAs of K = 32)
   const int g = lane >> 4, jl = lane & 15;
   const int kw = k0 + BKW * wave;
-  constexpr int NM = BF ? 2 : 16;
   // fp32: W_hh1 and W_ih1 slices in VGPRs (64 per lane), W_hh0's in LDS after the reduction
   // slots (w0s, 64 KB, [wave][cb][g][m / 4][16 lanes][4]: a lane's 4 consecutive m as one
   // conflict-free ds_read_b128); bf16: all three in VGPRs (48 per lane)

@@ -1342,7 +1342,7 @@ class DeviceFault(RuntimeError):
 
 # fault-word bits (csrc/lstm2_persist.hip) -> (kernel, what it overwrote, the switch that avoids it)
 _FAULT_BITS = (
-    (1, "lstm_persist_kernel, two layers (decoder lstm2 forward)", "h/c", "AVC_LSTM2_PERSIST=0"),
+    (1, "lstm_persist_kernel / lstm2_rs_kernel, two layers (decoder lstm2 forward)", "h/c", "AVC_LSTM2_PERSIST=0"),
     (2, "lstm_xcd_fwd_kernel (decoder lstm1 forward)", "h/c", "AVC_LSTM_XCD=0"),
     (4, "lstm_xcd_bwd_kernel (decoder lstm1 backward)", "gate gradients", "AVC_LSTM_XCD_BWD=0"),
     (8, "lstm_persist_kernel, one layer (decoder lstm1 forward)", "h/c", "AVC_LSTM_PERSIST=0"),

@@ -106,13 +106,16 @@ def lstm_roofline(solver, B, T, dev):
             xs.append(e0.elapsed_time(e1) * 1e3)
         launch_us = sorted(xs[1:])[1]
         flop_launch, bytes_launch = flop2 * T, 2 * per_layer_step * T
-        # the fp32 default is the two-step wavefront form (layer 1 two steps behind layer 0: T + 2
-        # iterations); AVC_LSTM2_LAG2=0 selects the one-step form (T + 1)
+        # the default is the row-split kernel (AVC_LSTM2_RS=0: lstm_persist_kernel) in the two-step
+        # wavefront form (layer 1 two steps behind layer 0: T + 2 iterations); AVC_LSTM2_LAG2=0
+        # selects the one-step form (T + 1)
         lag2 = os.environ.get("AVC_LSTM2_LAG2", "") != "0"
+        rs = os.environ.get("AVC_LSTM2_RS", "") != "0"
         iters = T + 2 if lag2 else T + 1
-        kernel = (f"lstm_persist_kernel<1024, true, false, {'true' if lag2 else 'false'}> (decoder lstm2 forward, "
-                  "both layers, whole sequence per launch, H=1024, B=64"
-                  + (", two-step wavefront)" if lag2 else ")"))
+        kname = (f"lstm2_rs_kernel<1024, false, {'true' if lag2 else 'false'}>" if rs else
+                 f"lstm_persist_kernel<1024, true, false, {'true' if lag2 else 'false'}>")
+        kernel = (f"{kname} (decoder lstm2 forward, both layers, whole sequence per launch, H=1024, B=64"
+                  + (", row split" if rs else "") + (", two-step wavefront)" if lag2 else ")"))
         pmc_file = "lstm2_persist_pmc.json"
     else:
         launch_us, flop_launch, bytes_launch = us2, flop2, 2 * per_layer_step

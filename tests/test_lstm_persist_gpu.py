@@ -156,6 +156,56 @@ def test_bf16_persistent_matches_bf16_per_step_launches(cuda, T, lag2):
         assert d.mean().item() < 1e-4 * max(r.abs().max().item(), 1e-30), (name, d.mean().item())
 
 
+@pytest.mark.parametrize("T", [3, 128])
+@pytest.mark.parametrize("bf16", [False, True], ids=["fp32", "bf16"])
+def test_row_split_persistent_bit_identical(cuda, T, bf16, lag2, monkeypatch):
+    """The row-split stacked forward (lstm2_rs_kernel, AVC_LSTM2_RS=1: workgroup pairs split the
+    64 batch rows, each owns 8 units) sums the same products in the same k order as
+    lstm_persist_kernel, so every output is bit-identical, in both wavefront forms."""
+    from autovc_amd import _lib
+    B, H = 64, 1024
+    if not _supported(B, H):
+        pytest.skip("persistent lstm2 needs one CU per workgroup on this device")
+    gx, W, b1, b2 = _inputs(B, T, H, cuda, seed=11)
+    if bf16:
+        W = [w.bfloat16().contiguous() for w in W]
+    name = "autovc_lstm2_fwd_persist_bf16" if bf16 else "autovc_lstm2_fwd_persist_f32"
+    ws = torch.empty(_lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), dtype=torch.uint8, device=cuda)
+    res = {}
+    for rs in ("0", "1"):
+        monkeypatch.setenv("AVC_LSTM2_RS", rs)
+        res[rs] = _run(name, B, T, H, gx, W, b1, b2, cuda, ws)
+        assert _lib.load().autovc_lstm2_persist_status(ws.data_ptr(), _lib.stream_ptr(cuda)) == 0
+    diff = {nm: (a - r).abs().max().item() for nm, a, r in zip(["h0", "c0", "gates0", "h1", "c1", "gates1"],
+                                                                 res["1"], res["0"])}
+    assert all(bool(torch.isfinite(a).all()) for a in res["1"])
+    assert all(v == 0 for v in diff.values()), diff
+
+
+def test_row_split_timeout_surfaces(cuda, monkeypatch):
+    """A row-split launch whose grid barrier times out writes NaN over what it owns and sets the
+    lstm2 forward's fault bit, like lstm_persist_kernel."""
+    from autovc_amd import _lib, functional as AF
+    B, T, H = 64, 8, 1024
+    if not _supported(B, H):
+        pytest.skip("persistent lstm2 needs one CU per workgroup on this device")
+    AF.check_device_faults(cuda)
+    monkeypatch.setenv("AVC_LSTM2_RS", "1")
+    gx, W, b1, b2 = _inputs(B, T, H, cuda)
+    ws = torch.empty(_lib.load().autovc_lstm2_persist_workspace_bytes(B, T, H), dtype=torch.uint8, device=cuda)
+    _lib.call("autovc_lstm_persist_set_timeout_ticks", 1)
+    try:
+        got = _run("autovc_lstm2_fwd_persist_f32", B, T, H, gx, W, b1, b2, cuda, ws)
+    finally:
+        _lib.call("autovc_lstm_persist_set_timeout_ticks", 0)
+    assert not bool(torch.isfinite(got[3]).all())
+    with pytest.raises(AF.DeviceFault, match="lstm_persist_kernel"):
+        AF.check_device_faults(cuda)
+    got = _run("autovc_lstm2_fwd_persist_f32", B, T, H, gx, W, b1, b2, cuda, ws)
+    assert all(bool(torch.isfinite(a).all()) for a in got)
+    AF.check_device_faults(cuda)
+
+
 def test_barrier_timeout_surfaces_as_error(cuda):
     """A persistent launch whose grid barrier times out (forced with a 1-tick spin budget)
     must not let training continue on garbage: its h / c become NaN (so the losses do) and

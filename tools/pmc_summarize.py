@@ -11,7 +11,7 @@ import sys
 
 MODE = sys.argv[3] if len(sys.argv) > 3 else "single"
 KERNEL = {"stack": "lstm2_fwd_step_kernel", "stackbwd": "lstm2_bwd_rec_kernel",
-          "persist": "lstm_persist_kernel<1024, true, false", "blstm_fwd": "blstm_fwd_kernel",
+          "persist": os.environ.get("PMC_KERNEL", "lstm2_rs_kernel<1024, false"), "blstm_fwd": "blstm_fwd_kernel",
           "blstm_bwd": "blstm_bwd_kernel", "xcd": "lstm_xcd_fwd_kernel"}.get(MODE, "lstm_fwd_step_kernel")
 
 
@@ -40,7 +40,7 @@ fa = sum(keep(f)) / max(1, len(keep(f)))
 wa = sum(keep(w)) / max(1, len(keep(w)))
 out = {"kernel": {"stack": "lstm2_fwd_step_kernel (decoder lstm2, both layers, H=1024, B=64)",
                   "stackbwd": "lstm2_bwd_rec_kernel (decoder lstm2 backward, both layers + W_ih1, H=1024, B=64)",
-                  "persist": "lstm_persist_kernel<1024, true, false, true> (decoder lstm2 forward, two-step wavefront, whole sequence, H=1024, B=64, T=128)",
+                  "persist": "lstm2_rs_kernel<1024, false, true> (decoder lstm2 forward, row split, two-step wavefront, whole sequence, H=1024, B=64, T=128)",
                   "blstm_fwd": "blstm_fwd_kernel (encoder BLSTM layer, H=32, B=64, T=128, both directions)",
                   "blstm_bwd": "blstm_bwd_kernel (encoder BLSTM layer backward, H=32, B=64, T=128)",
                   "xcd": "lstm_xcd_fwd_kernel<512, false> (decoder lstm1 forward, XCD-local, H=512, B=64, T=128)"}

@@ -9,7 +9,7 @@ import re
 import sys
 
 CATS = [
-    ("lstm2 fwd (persistent)", r"lstm_persist_kernel<1024"),
+    ("lstm2 fwd (persistent)", r"lstm_persist_kernel<1024|lstm2_rs_kernel"),
     ("lstm2 fwd (per step)", r"lstm2_fwd_step"),
     ("lstm2 bwd products", r"lstm2_bwd_rec"),
     ("lstm2 bwd pointwise", r"lstm2_bwd_pointwise"),
