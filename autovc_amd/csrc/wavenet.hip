@@ -63,6 +63,11 @@ struct WnArgs {
   float* gbuf;
   float* ptap;       // past-tap products of the next step: (2, n_layers, B, G), by step parity
   float* molp;       // MoL head partials of the head kernel's row blocks: (S / kHR, B, kMaxNO)
+  // all-CU generation (wn_grid_kernel): tagged 16-byte hand-off granules
+  float* gring;      // (n_layers, RING, B, 256) x {g_l[o], x_l[2o], x_l[2o+1], step + 1}
+  float* gsk;        // (B, 256) x {skip sum, -, -, step + 1}
+  float* gh1;        // (B, 256) x {h1, -, -, step + 1}
+  float* gpt;        // (2 parities, n_layers, B, 512) x {past-tap sum, step + 1} (8 bytes)
   int* ctr;
   const float* teacher;
   int teacher_len;
@@ -856,18 +861,27 @@ constexpr int kXR4 = 24 * 256 / 4;     // float4 of the residual / skip / head r
 constexpr int kXLd = (kXG4 + kXR4) / (64 * (kXW - kXCW));   // float4 per loader lane (34)
 static_assert(kXLd * 64 * (kXW - kXCW) == kXG4 + kXR4, "loader map");
 
+// A wave-uniform base pointer forced into SGPRs: a buffer descriptor built from a value the
+// compiler keeps in VGPRs (e.g. live across divergent code) otherwise becomes a waterfall loop
+// around every load.  A no-op for a base already in SGPRs.
+__device__ __forceinline__ float* wave_uniform(const float* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<float*>(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ f32x4 ld4_l2(const float* base, int off) {
   // an L1-bypassing (sc1) 16-byte load of data another workgroup of this XCD wrote: `base` is
   // wave-uniform (the descriptor lives in SGPRs; a per-lane base would make the compiler
   // loop over the lanes), `off` the lane's float offset
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff,
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(base), (short)0, 0x7fffffff,
                                                                      0x00020000);
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)off * 4u, 0, 16));
 }
 
 __device__ __forceinline__ f32x4 ld4_ro(const float* base, int off) {
   // a 16-byte load of read-only weights through a wave-uniform buffer descriptor
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff,
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(base), (short)0, 0x7fffffff,
                                                                      0x00020000);
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)off * 4u, 0, 0));
 }
@@ -1178,6 +1192,605 @@ __global__ __launch_bounds__(64 * kXW, 1) void wn_xcd_kernel(WnArgs a, int t0, i
   }
 }
 
+// ================================================================ all-CU weight-resident generation
+// (B <= 8, the r9y9 shapes R = 512, G = 512, S = 256, 3 taps, 8..24 layers).  ONE persistent
+// launch per autovc_wavenet_generate_f32 call; its 256 workgroups (one per CU) run the 26
+// phases of every sample step (layers 0..L-1, the last layer's skip rows, h1) as a DATAFLOW:
+// no grid barrier, every hand-off is a tagged 16-byte granule.  Workgroup o owns gate pair
+// (o, o + H), residual rows 2o, 2o + 1 (x_(l+1)) and skip row o of every layer, and head row
+// o, and publishes per phase and utterance exactly ONE granule {g_l[o], x_l[2o], x_l[2o+1],
+// tag} (x_l = layer l's input, computed in phase l from layer l-1's output) with one sc1
+// (write-through) store; the tag is the step + 1, so a consumer knows a granule is this step's
+// by reading it (16-byte sc1 stores are observed untorn on gfx950 / ROCm 7.2, MI355X_MICROARCH
+// "Valid forms").  The next phase's inputs [g_l | x_l] are exactly the 256 granules of the
+// previous phase (4 KB per utterance): chain lane o (waves 0-3) polls granule o of every
+// utterance with sc1 loads until all tags match — the store and its observation replace the
+// barrier's vmcnt drain, two atomic round trips and the release broadcast.
+//   weights: the gate rows of every layer resident in LDS ([l][o][6]: the 3 weights of gate
+//   rows o_s and o_s + H that meet granule o, 147 KB at 24 layers); the 3 residual weights a
+//   lane needs for the next phase (W_out rows 2o_s, 2o_s + 1 and W_skip row o_s at column o)
+//   and W2 are loaded into registers before the lane starts polling, so their fetch hides
+//   under the wait for the producers.
+// Lane o multiplies its granule into 5 partial sums per utterance (2 gate rows, 3 residual
+// rows); a wave butterfly and an LDS counter handshake among the 4 chain waves leave the sums
+// to wave 0, whose lanes b < B run the cell update and publish.  The past taps of the next step
+// (W_0 x_l(t+1-2d) + W_1 x_l(t+1-d): 48 MB of weights per step, too many to hold) are computed
+// by waves 4..7 of workgroup o (up to 4 16-row blocks of layer o % L) on MFMA as soon as their
+// inputs are published, into 8-byte {value, tag} granules the chain lane polls; they never
+// synchronise with the chain waves.  The sample of step t-1 is drawn by every workgroup itself
+// at the start of step t (the same Philox stream, the same value everywhere).  A wait that times
+// out (the 256 workgroups were not all resident) sets an error word every other wait checks,
+// and the call's samples are poisoned with NaN and bit 2 of autovc_wavenet_fault is set.
+constexpr int kGrW = 8;                       // waves per workgroup: 4 chain + 4 past-tap
+constexpr int kGMaxL = 24;
+constexpr int kGMaxB = 8;
+constexpr int kGFault = 2;
+constexpr int kGErrInts = 32;                 // the error word's line (ints)
+
+struct GLds {                                 // float offsets into the dynamic LDS block
+  int gw, h1, molp, mol, gum, in, part, xres, cnt, total;
+};
+__host__ __device__ inline GLds g_lds(int L, int NO) {
+  (void)NO;
+  GLds o;
+  int p = 0;
+  o.gw = p;    p += L * 256 * 6;              // gate weights [l][o][6]
+  o.h1 = p;    p += kGMaxB * 256;             // h1 of the previous step [b][o] (the MoL GEMV's input)
+  o.molp = p;  p += 4 * 32 * kGMaxB;          // per-wave MoL partials [wave][j][b]
+  o.mol = p;   p += kGMaxB * 32;              // MoL parameters [b][j]
+  o.gum = p;   p += kGMaxB * 16;              // sampling noise [b][j]
+  o.in = p;    p += kGMaxB;                   // this step's input sample per utterance
+  // per-wave partial sums of a phase [parity][wave][value] and x_(l-1)[2o_s], [2o_s + 1] per
+  // utterance [parity][b][2]: double-buffered by phase, since a chain wave may enter the next
+  // phase (its inputs come from other workgroups) while wave 0 still reads this one's
+  o.part = p;  p += 2 * 4 * 64;
+  o.xres = p;  p += 2 * kGMaxB * 2;
+  o.cnt = p;   p += 4;                        // the chain waves' LDS handshake counter
+  o.total = p;
+  return o;
+}
+
+__host__ __device__ inline int64_t g_ring_f4(const WnArgs& a) {   // granules of the tagged ring
+  return (int64_t)a.n_layers * a.RING * a.B * 256;
+}
+
+// NOTE: __float_as_int, not __builtin_bit_cast: this clang lowers a bit_cast of an ext-vector
+// ELEMENT (g[3]) as a read of element 0 (the vector's address), which made every poll compare
+// the granule's first word against the tag
+__device__ __forceinline__ int tag_of(f32x4 g) { return __float_as_int(g[3]); }
+
+// one 16-byte write-through (sc1) store {v0, v1, v2, tag} at base + off floats; `base` is
+// wave-uniform (the descriptor lives in SGPRs)
+__device__ __forceinline__ void st4_sc1(float* base, int off, float v0, float v1, float v2, int tag) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(base), (short)0, 0x7fffffff, 0x00020000);
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 w = {__float_as_int(v0), __float_as_int(v1), __float_as_int(v2), tag};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (uint32_t)off * 4u, 0, 16);
+}
+// 8-byte {value, tag} granule, write-through
+__device__ __forceinline__ void st2t_sc1(float* base, int off, float v, int tag) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(base), (short)0, 0x7fffffff, 0x00020000);
+  typedef int i32x2 __attribute__((ext_vector_type(2)));
+  const i32x2 w = {__float_as_int(v), tag};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, (uint32_t)off * 4u, 0, 16);
+}
+__device__ __forceinline__ float2 ld2_l2(const float* base, int off) {   // sc1 8-byte load
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(base), (short)0, 0x7fffffff,
+                                                                     0x00020000);
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 v = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)off * 4u, 0, 16));
+  return make_float2(v[0], v[1]);
+}
+
+// Which wait of wn_grid_kernel timed out first: {wait kind, step, phase or job, workgroup}
+// (autovc_wavenet_grid_diag reads and clears it).  Kinds: 1 layer inputs, 2 past-tap sums,
+// 3 the chain waves' LDS handshake, 4 past-tap inputs, 5 past-tap consumers, 6 skip sums, 7 h1.
+__device__ int g_wn_grid_diag[5] = {};
+
+// bounded spin state of one wave: the deadline, the device-wide error word, what it waits for
+struct Spin {
+  uint64_t t0;
+  int* err;
+  int ticks;
+  int kind, step, ph;
+  int seen = -1;                              // the tag last observed (diagnostics)
+  bool slow = false;                          // off the critical path: long sleeps, every check
+  int n = 0;
+  __device__ bool tick() {                    // false: give up (timed out, or another wave did)
+    if (!slow && (++n & 3) != 0) {            // the error word and the clock every 4th retry
+      __builtin_amdgcn_s_sleep(1);
+      return true;
+    }
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)ticks) {
+      int z = 0;
+      if (__hip_atomic_compare_exchange_strong(err, &z, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(&g_wn_grid_diag[1], step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&g_wn_grid_diag[2], ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&g_wn_grid_diag[3], (int)blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&g_wn_grid_diag[4], seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&g_wn_grid_diag[0], kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+    if (slow) __builtin_amdgcn_s_sleep(32);   // ~2k clocks: a waiting past-tap wave costs the fabric little
+    else __builtin_amdgcn_s_sleep(1);
+    return true;
+  }
+};
+
+// LDS handshake of the 4 chain waves: each wave's LDS writes are complete before its lane 0
+// adds to the counter; every wave then waits for the k-th round (4 k arrivals).  Bounded: a
+// wave that gave up elsewhere never arrives, and the device error word then ends the wait.
+__device__ __forceinline__ bool chain_sync(int* cnt, int& k, int lane, int* err, int ticks, int step, int ph) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int want = 4 * ++k;
+  Spin sp{__builtin_amdgcn_s_memrealtime(), err, ticks, 3, step, ph};
+  int n = 0;
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+    if ((++n & 255) == 0 && !sp.tick()) return false;
+  asm volatile("" ::: "memory");
+  return true;
+}
+
+// Poll the NB granules of lane o (utterance slots b: base + ((b < B ? b : 0) * 256 + o) * 4
+// floats) until every lane of the wave holds this step's tag.  false: the wait gave up.
+template <int NB>
+__device__ __forceinline__ bool poll_granules(const float* base, int o, int B, int tag, f32x4 (&g)[NB], int* err,
+                                              int ticks, int kind, int ph) {
+  Spin sp{__builtin_amdgcn_s_memrealtime(), err, ticks, kind, tag - 1, ph};
+  while (true) {
+    // every retry re-issues every load (the clobber keeps the compiler from reusing a value
+    // loaded in an earlier pass), and all of them are in flight before the first compare; a
+    // retry of only the late granules costs phi copies of all NB granules (spills at NB = 8)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < NB; ++b) g[b] = ld4_l2(base, ((b < B ? b : 0) * 256 + o) * 4);
+    int bad = 0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) bad |= tag_of(g[b]) ^ tag;
+    if (__builtin_amdgcn_ballot_w64(bad != 0) == 0) return true;
+    sp.seen = __builtin_amdgcn_readfirstlane(tag_of(g[0]));
+    if (!sp.tick()) return false;
+  }
+}
+
+// One 128-deep chunk kc (tap kc / 4, k0 = 128 (kc % 4)) of the past taps of step `job` for the
+// 16 gate rows of block blk of layer lp on v_mfma_f32_16x16x4_f32 tiles (past_taps' operand
+// map: lane l feeds weight row l % 16 / utterance column l % 16 with 4 consecutive k of group
+// l / 16).  The x inputs come from the tagged ring: x_lp(s)[k] is component 1 + (k & 1) of
+// granule k / 2; steps s < 0 are zero.  false: a wait gave up.
+__device__ __forceinline__ bool wn_grid_past_tap_chunk(const WnArgs& a, int lp, int blk, int d, int job, int kc,
+                                                       int lane, f32x4& pacc, int* err, int ticks) {
+  constexpr int R = 512, KX = 3 * 512 + 256;
+  const int m = lane & 15, q = lane >> 4;
+  const int tap = kc >> 2, k0 = (kc & 3) * 128;
+  const int s = job - (2 - tap) * d;
+  const int ub = (m & 7) < a.B ? (m & 7) : 0;
+  const float* w0 = layer_base(a, lp) + (int64_t)(blk * 16 + m) * KX + tap * R + k0 + 4 * q;
+  f32x4 acc = pacc;
+  if (s >= 0) {
+    const float* xr = a.gring + ((int64_t)lp * a.RING + (s & (a.RING - 1))) * a.B * 256 * 4;   // wave-uniform
+#pragma unroll
+    for (int h = 0; h < 8; h += 4) {          // four 16-deep steps in flight
+      f32x4 wv[4], xv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wv[i] = ld4(w0 + (h + i) * 16);
+      Spin sp{__builtin_amdgcn_s_memrealtime(), err, ticks, 4, job, kc};
+      while (true) {
+        asm volatile("" ::: "memory");       // re-issue every load on a retry (see poll_granules)
+        f32x4 ga[4], gb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int o2 = (k0 + (h + i) * 16 + 4 * q) / 2;        // granules o2, o2 + 1
+          ga[i] = ld4_l2(xr, (ub * 256 + o2) * 4);
+          gb[i] = ld4_l2(xr, (ub * 256 + o2) * 4 + 4);
+        }
+        int bad = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bad |= (tag_of(ga[i]) ^ (s + 1)) | (tag_of(gb[i]) ^ (s + 1));
+          xv[i] = f32x4{ga[i][1], ga[i][2], gb[i][1], gb[i][2]};
+        }
+        if (__builtin_amdgcn_ballot_w64(bad != 0) == 0) break;
+        sp.seen = __builtin_amdgcn_readfirstlane(tag_of(ga[0]));
+        if (!sp.tick()) return false;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i][j], xv[i][j], acc, 0, 0, 0);
+    }
+  }
+  pacc = acc;
+  return true;
+}
+
+#ifdef AVC_WN_GRID_TRACE
+// phase timeline of workgroups 0 and 137 at one steady-state step (tools/wn_grid_trace.py):
+// [wg][phase][start, inputs in, partials summed, past taps in, published], s_memrealtime
+__device__ int g_wn_grid_trace[2][kGMaxL + 2][5];
+#define WN_GT(k)                                                                                      \
+  if (trc && t == t0 + 64) g_wn_grid_trace[os == 0 ? 0 : 1][p][k] = (int)__builtin_amdgcn_s_memrealtime()
+#else
+#define WN_GT(k)
+#endif
+
+// NB: utterance slots of the launch (1, 2, 4 or 8 >= B; slots >= B compute on utterance 0
+// and are dropped), so every per-utterance loop is straight-line code
+template <int NB>
+__global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0, int t1, int* errw, int ticks) {
+  // no mul-add contraction: the NB instantiations (1, 2, 4, 8 utterance slots) must round every
+  // utterance's arithmetic the same way (batch invariance: an utterance's samples do not depend
+  // on the batch it was generated in)
+#pragma clang fp contract(off)
+  constexpr int R = 512, H = 256, S = 256, KX = 3 * 512 + 256, KT = 2 * 512;
+  constexpr int NV = 5 * NB <= 8 ? 8 : 5 * NB <= 16 ? 16 : 5 * NB <= 32 ? 32 : 64;   // partials, padded
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int L = a.n_layers, B = a.B, T = a.T, RING = a.RING, NO = a.NO;
+  const GLds lo = g_lds(L, NO);
+  float* s_gw = lds + lo.gw;
+  float* s_h1 = lds + lo.h1;
+  float* s_molp = lds + lo.molp;
+  float* s_mol = lds + lo.mol;
+  float* s_gum = lds + lo.gum;
+  float* s_in = lds + lo.in;
+  float* s_part = lds + lo.part;
+  float* s_xres = lds + lo.xres;
+  int* s_cnt = reinterpret_cast<int*>(lds + lo.cnt);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int os = blockIdx.x;                  // this workgroup's gate pair / residual pair / skip and head row
+  const float* W1 = head_base(a);
+  const float* b1 = W1 + (int64_t)S * S;
+  const float* W2 = b1 + S;
+  const float* b2 = W2 + (int64_t)NO * S;
+  const int64_t RB4 = (int64_t)B * 256 * 4;   // floats of one ring slot (all utterances)
+
+  // ---- resident gate weights: s_gw[l][o][r * 3 + {g, x0, x1}] = W(o_s + r H)[KT + o], [KT + H + 2o], [.. + 1]
+  for (int e = tid; e < L * 256; e += 64 * kGrW) {
+    const int l = e / 256, o = e % 256;
+    const float* base = layer_base(a, l) + KT;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const float* w = base + (int64_t)(os + r * H) * KX;
+      s_gw[e * 6 + 3 * r] = w[o];
+      s_gw[e * 6 + 3 * r + 1] = w[H + 2 * o];
+      s_gw[e * 6 + 3 * r + 2] = w[H + 2 * o + 1];
+    }
+  }
+  if (tid == 0) *s_cnt = 0;
+  // The polls are sc1 loads: drop any line of the hand-off region an earlier kernel's plain
+  // access left in this XCD's L2 (system-scope acquire = buffer_inv sc0 sc1) before the first.
+  if (tid < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();
+
+  if (wave >= 4) {
+    // =========================== past-tap waves: blocks of layer lp = os % L
+    const int lp = os % L, pk = os / L, pn = (int)((gridDim.x - lp + L - 1) / L);
+    constexpr int kPTB = 512 / 16;            // 16-row blocks per layer (G = 512)
+    const int pnb = pk < kPTB ? (kPTB - pk + pn - 1) / pn : 0;
+    const int pw = wave - 4;
+    if (pw >= pnb) return;
+    const int blk = pk + pn * pw, d = 1 << (lp % a.lps);
+    const int m = lane & 15, q = lane >> 4;
+    for (int job = t0 + 1; job <= t1; ++job) {
+      if (job >= T) break;                    // P(T) feeds no step
+      // wait (slowly: P(job) is needed a whole step later) until the owners of these rows
+      // (rows r and r - H -> workgroup r mod H) have published layer lp of step job - 1: they
+      // are past P(job - 2), whose parity this job overwrites, and x_lp(job - 1) — the d = 1
+      // layers' newest input — is out
+      if (job - 1 >= 0) {
+        const int owner = (blk * 16 + (lane & 15)) & (H - 1);
+        const float* xr = a.gring + ((int64_t)lp * RING + ((job - 1) & (RING - 1))) * RB4;
+        Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 5, job, lp};
+        sp.slow = true;
+        while (true) {
+          asm volatile("" ::: "memory");
+          const int tg = tag_of(ld4_l2(xr, 4 * owner));
+          if (__builtin_amdgcn_ballot_w64(tg != job) == 0) break;
+          sp.seen = __builtin_amdgcn_readfirstlane(tg);
+          if (!sp.tick()) return;
+        }
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < 8; ++kc)
+        if (!wn_grid_past_tap_chunk(a, lp, blk, d, job, kc, lane, acc, errw, ticks)) return;
+      if (m < B) {
+        float* pt = a.gpt + ((int64_t)(job & 1) * L + lp) * B * 512 * 2;      // wave-uniform
+#pragma unroll
+        for (int v = 0; v < 4; ++v) st2t_sc1(pt, m * 1024 + 2 * (blk * 16 + 4 * q + v), acc[v], job + 1);
+      }
+    }
+    return;
+  }
+
+  // =========================== chain waves 0-3: lane o = granule o
+  const int o = wave * 64 + lane;
+#ifdef AVC_WN_GRID_TRACE
+  const bool trc = (os == 0 || os == 137) && wave == 0 && lane == 0;
+#endif
+  int kx = 0;                                 // chain_sync rounds
+  int cur_t = t0, cur_p = 0;                  // (diagnostics of a timed-out wait)
+  bool ok = true;
+  // first_conv weights of channels 2o, 2o + 1 (layer 0's x inputs) and of 2 os, 2 os + 1
+  const float fw0 = a.packed[2 * o], fw1 = a.packed[2 * o + 1], fb0 = a.packed[R + 2 * o], fb1 = a.packed[R + 2 * o + 1];
+  const float fwo0 = a.packed[2 * os], fwo1 = a.packed[2 * os + 1], fbo0 = a.packed[R + 2 * os],
+              fbo1 = a.packed[R + 2 * os + 1];
+  const float w1o = W1[(int64_t)os * S + o], b1o = b1[os];
+  // residual weights of layer lr at column o: W_out rows 2 os, 2 os + 1, W_skip row os
+  float rw0 = 0.f, rw1 = 0.f, rw2 = 0.f;
+  auto fetch_res = [&](int lr) {
+    const float* pb = layer_base(a, lr) + (int64_t)a.G * KX;
+    rw0 = pb[(int64_t)(2 * os) * H + o];
+    rw1 = pb[(int64_t)(2 * os + 1) * H + o];
+    rw2 = pb[(int64_t)(R + os) * H + o];
+  };
+  // W2 for the MoL GEMV: lane (j = lane % 32, 32-deep k slice 2 wave + lane / 32)
+  const int mj = lane & 31, mks = 2 * wave + (lane >> 5);
+  f32x4 w2r[8];
+  auto fetch_w2 = [&]() {
+    const int jj = mj < NO ? mj : 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w2r[i] = ld4(W2 + (int64_t)jj * S + 32 * mks + 4 * i);
+  };
+  auto noise = [&](int tp) {                  // wave 3: lane 16 (b % 4) + j, utterances 0..3 then 4..7
+    if (wave != 3 || tp < 0) return;
+    for (int half = 0; half < 2; ++half) {
+      const int b = 4 * half + (lane >> 4), j = lane & 15;
+      if (b < B && (j < NO / 3 || j == 10)) s_gum[b * 16 + j] = mol_noise(j, tp, a.utt_base + b, a);
+    }
+  };
+  // butterfly the partial sums of this wave, park them in s_part[wave][j], then hand them to
+  // wave 0 (every chain wave joins the handshake)
+  int par = 0;                                // phase parity: s_part / s_xres buffer
+  auto reduce_park = [&](float (&acc)[NV]) {
+    if constexpr (NV == 64) {
+      // 8 utterances: the 5 partial groups one butterfly of 8 each (50 shuffles, 8 live
+      // copies instead of 64); the same pairing tree per value as the single butterfly
+#pragma unroll
+      for (int g = 0; g < 5; ++g) {
+        float cur[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cur[j] = acc[g * 8 + j];
+        butterfly<8, 32>(cur, lane);
+        if ((lane & 7) == 0) s_part[par * 256 + wave * 64 + g * 8 + (lane >> 3)] = cur[0];
+      }
+    } else {
+      const float v = wave_reduce_multi<NV>(acc, lane);
+      if ((lane & (64 / NV - 1)) == 0) s_part[par * 256 + wave * 64 + lane / (64 / NV)] = v;
+    }
+    return chain_sync(s_cnt, kx, lane, errw, ticks, cur_t, cur_p);
+  };
+  auto psum = [&](int j) {
+    const float* sp = s_part + par * 256;
+    return ((sp[j] + sp[64 + j]) + sp[128 + j]) + sp[192 + j];
+  };
+
+  noise(t0 - 1);
+  float skip_acc = 0.f;                       // epilogue lane b: the skip sum of utterance b
+  for (int t = t0; t < t1 && ok; ++t) {
+    const int ts = t & (RING - 1), prow = t % a.Tch;
+    for (int p = 0; p < L + 2 && ok; ++p, par ^= 1) {
+      cur_t = t;
+      cur_p = p;
+      WN_GT(0);
+      float acc[NV];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) acc[j] = 0.f;
+      if (p < L) {
+        const int l = p;
+        // epilogue operands of lane b (wave 0): conditioning + past taps of the gate pair, the
+        // residual biases of layer l-1
+        float pre_a = 0.f, pre_b = 0.f, bias0 = 0.f, bias1 = 0.f, bias2 = 0.f;
+        if (wave == 0 && lane < B) {
+          const float* pr = a.pre + ((int64_t)prow * B + lane) * ((int64_t)L * a.G) + (int64_t)l * a.G;
+          pre_a = pr[os];
+          pre_b = pr[os + H];
+          if (l >= 1) {
+            const float* pbias = layer_base(a, l - 1) + (int64_t)a.G * KX + (int64_t)(R + S) * H;
+            bias0 = pbias[2 * os]; bias1 = pbias[2 * os + 1]; bias2 = pbias[R + os];
+          }
+        }
+        // this phase's past-tap sums (rows o_s, o_s + H), computed a step ahead by the past-tap
+        // waves: their loads go out now, so the round trip hides under the input wait
+        const float* ptl = a.gpt + ((int64_t)(t & 1) * L + l) * B * 512 * 2;   // wave-uniform
+        float2 pva = make_float2(0.f, 0.f), pvb = make_float2(0.f, 0.f);
+        if (wave == 0 && lane < B && t > 0) {
+          pva = ld2_l2(ptl, lane * 1024 + 2 * os);
+          pvb = ld2_l2(ptl, lane * 1024 + 2 * (os + H));
+        }
+        const float* wgl = s_gw + ((int64_t)l * 256 + o) * 6;
+        if (l == 0) {
+          // ---- the MoL parameters of step t-1 from its h1, then the draw (every workgroup)
+          const int tp = t - 1;
+          if (tp >= 0) {
+            fetch_w2();                       // in flight during the h1 wait; live in this phase only
+            f32x4 gh[NB];
+            if (!poll_granules<NB>(a.gh1, o, B, tp + 1, gh, errw, ticks, 7, 0)) { ok = false; break; }
+            WN_GT(1);
+#pragma unroll
+            for (int b = 0; b < NB; ++b) s_h1[b * 256 + o] = gh[b][0];
+            if (!chain_sync(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+            float am[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+              asm volatile("" ::: "memory");  // one utterance's 8 LDS reads in flight at a time (registers)
+              am[b] = 0.f;
+              const float* hb = s_h1 + b * 256 + 32 * mks;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) am[b] = dot4(w2r[i], *reinterpret_cast<const f32x4*>(hb + 4 * i), am[b]);
+            }
+#pragma unroll
+            for (int b = 0; b < NB; ++b) am[b] += __shfl_xor(am[b], 32);
+            if (lane < 32)
+#pragma unroll
+              for (int b = 0; b < NB; ++b) s_molp[(wave * 32 + lane) * kGMaxB + b] = am[b];
+            if (!chain_sync(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+            if (o < B * 32) {                 // thread (b, j)
+              const int b = o >> 5, jj = o & 31;
+              if (jj < NO)
+                s_mol[b * 32 + jj] = b2[jj] + (((s_molp[(0 * 32 + jj) * kGMaxB + b] + s_molp[(1 * 32 + jj) * kGMaxB + b]) +
+                                                s_molp[(2 * 32 + jj) * kGMaxB + b]) +
+                                               s_molp[(3 * 32 + jj) * kGMaxB + b]);
+            }
+            if (!chain_sync(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+          }
+          if (wave < 2) {
+            // the mixture pick on 16 lanes per utterance (mol_finish's order and tie rule)
+            const int b = 4 * wave + (lane >> 4), j = lane & 15, nr = NO / 3;
+            float v = -INFINITY;
+            if (tp >= 0 && b < B && j < nr) {
+              v = s_mol[b * 32 + j] - s_gum[b * 16 + j];
+              if (!(v == v)) v = -INFINITY;
+            }
+            int bi = j;
+#pragma unroll
+            for (int mm = 8; mm >= 1; mm >>= 1) {
+              const float ov = __shfl_xor(v, mm);
+              const int oi = __shfl_xor(bi, mm);
+              if (ov > v || (ov == v && oi < bi)) { v = ov; bi = oi; }
+            }
+            if (j == 0 && b < B) {
+              float in_v = 0.f, smp = 0.f;
+              if (tp >= 0) {
+                const float mean = s_mol[b * 32 + nr + bi];
+                const float ls = fmaxf(s_mol[b * 32 + 2 * nr + bi], a.log_scale_min);
+                const float x = mean + expf(ls) * s_gum[b * 16 + 10];
+                smp = fminf(fmaxf(x, -1.0f), 1.0f);
+              }
+              if (a.teacher != nullptr && t < a.teacher_len) in_v = a.teacher[(int64_t)b * a.teacher_len + t];
+              else if (tp >= 0) in_v = smp;
+              s_in[b] = in_v;
+              if (os == 0) {
+                a.yin[(int64_t)b * T + t] = in_v;
+                if (tp >= 0) {
+                  a.y_out[(int64_t)b * T + tp] = smp;
+                  if (a.mol_out)
+                    for (int qq = 0; qq < NO; ++qq) a.mol_out[((int64_t)b * T + tp) * NO + qq] = s_mol[b * 32 + qq];
+                }
+              }
+            }
+          }
+          if (!chain_sync(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+          // x_0(t)[2o], [2o + 1] = first_conv(input): the gate's x inputs; no g block
+          const float wa1 = wgl[1], wa2 = wgl[2], wb1 = wgl[4], wb2 = wgl[5];
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const float in_v = s_in[b];
+            const float x0 = in_v * fw0 + fb0, x1 = in_v * fw1 + fb1;
+            acc[b] = wa1 * x0 + wa2 * x1;
+            acc[NB + b] = wb1 * x0 + wb2 * x1;
+          }
+        } else {
+          // ---- this step's granules of layer l-1: [g_(l-1)[o] | x_(l-1)[2o], [2o + 1]]
+          f32x4 gin[NB];
+          if (!poll_granules<NB>(a.gring + ((int64_t)(l - 1) * RING + ts) * RB4, o, B, t + 1, gin, errw, ticks, 1, l)) {
+            ok = false;
+            break;
+          }
+          WN_GT(1);
+          const float wa0 = wgl[0], wa1 = wgl[1], wa2 = wgl[2], wb0 = wgl[3], wb1 = wgl[4], wb2 = wgl[5];
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const float g = gin[b][0], x0 = gin[b][1], x1 = gin[b][2];
+            acc[b] = (wa0 * g + wa1 * x0) + wa2 * x1;
+            acc[NB + b] = (wb0 * g + wb1 * x0) + wb2 * x1;
+            acc[2 * NB + b] = rw0 * g;
+            acc[3 * NB + b] = rw1 * g;
+            acc[4 * NB + b] = rw2 * g;
+          }
+          if (o == os)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+              s_xres[par * 2 * kGMaxB + 2 * b] = gin[b][1];
+              s_xres[par * 2 * kGMaxB + 2 * b + 1] = gin[b][2];
+            }
+        }
+        // the next phase's residual weights (layer l) fetched while the epilogue and the
+        // producers run
+        fetch_res(l);
+        if (!reduce_park(acc)) { ok = false; break; }
+        WN_GT(2);
+        if (wave == 0 && lane < B) {
+          const int b = lane;
+          float pta = 0.f, ptb = 0.f;
+          if (t > 0) {                        // P(0) = 0 (every past input is zero)
+            Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 2, t, l};
+            while (__float_as_int(pva.y) != t + 1 || __float_as_int(pvb.y) != t + 1) {   // rarely: not yet out
+              if (!sp.tick()) { ok = false; break; }
+              asm volatile("" ::: "memory");
+              pva = ld2_l2(ptl, b * 1024 + 2 * os);
+              pvb = ld2_l2(ptl, b * 1024 + 2 * (os + H));
+            }
+            pta = pva.x;
+            ptb = pvb.x;
+          }
+          WN_GT(3);
+          const float za = psum(b) + (pre_a + pta), zb = psum(NB + b) + (pre_b + ptb);
+          const float gv = tanhf(za) * avc_sigmoid(zb);
+          float x0n, x1n;
+          if (l == 0) {
+            const float in_v = s_in[b];
+            x0n = in_v * fwo0 + fbo0;
+            x1n = in_v * fwo1 + fbo1;
+          } else {
+            x0n = (psum(2 * NB + b) + bias0 + s_xres[par * 2 * kGMaxB + 2 * b]) * kSqrtHalf;
+            x1n = (psum(3 * NB + b) + bias1 + s_xres[par * 2 * kGMaxB + 2 * b + 1]) * kSqrtHalf;
+            const float sv = psum(4 * NB + b) + bias2;
+            skip_acc = l - 1 == 0 ? sv : (a.legacy ? (skip_acc + sv) * kSqrtHalf : skip_acc + sv);
+          }
+          st4_sc1(a.gring + ((int64_t)l * RING + ts) * RB4, (b * 256 + os) * 4, gv, x0n, x1n, t + 1);
+          WN_GT(4);
+        }
+        ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+      } else if (p == L) {
+        // ---- tail: the last layer's skip row os; wave 3 then draws the next sample's noise
+        f32x4 gin[NB];
+        if (!poll_granules<NB>(a.gring + ((int64_t)(L - 1) * RING + ts) * RB4, o, B, t + 1, gin, errw, ticks, 1, L)) {
+          ok = false;
+          break;
+        }
+        WN_GT(1);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] = rw2 * gin[b][0];
+        if (!reduce_park(acc)) { ok = false; break; }
+        WN_GT(2);
+        if (wave == 0 && lane < B) {
+          const float* pbias = layer_base(a, L - 1) + (int64_t)a.G * KX + (int64_t)(R + S) * H;
+          const float sv = psum(lane) + pbias[R + os];
+          const float sk = L - 1 == 0 ? sv : (a.legacy ? (skip_acc + sv) * kSqrtHalf : skip_acc + sv);
+          st4_sc1(a.gsk, (lane * 256 + os) * 4, sk, 0.f, 0.f, t + 1);
+          WN_GT(4);
+        }
+        noise(t);
+      } else {
+        // ---- head: h1 row os = relu(W1[os] relu(skip) + b1[os])
+        f32x4 gs[NB];
+        if (!poll_granules<NB>(a.gsk, o, B, t + 1, gs, errw, ticks, 6, L + 1)) { ok = false; break; }
+        WN_GT(1);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] = w1o * fmaxf(gs[b][0], 0.f);
+        if (!reduce_park(acc)) { ok = false; break; }
+        WN_GT(2);
+        if (wave == 0 && lane < B) {
+          const float h = fmaxf(psum(lane) + b1o, 0.f);
+          st4_sc1(a.gh1, (lane * 256 + os) * 4, h, 0.f, 0.f, t + 1);
+          WN_GT(4);
+          a.h1[(int64_t)lane * S + os] = h;   // plain copy for the last step's sample (wn_final_sample_kernel)
+        }
+      }
+    }
+  }
+  if (!ok) {
+    if (os == 0 && wave == 0)
+      for (int i = lane; i < B * (t1 - t0); i += 64)
+        a.y_out[(int64_t)(i / (t1 - t0)) * T + t0 + i % (t1 - t0)] = __builtin_nanf("");
+    if (tid == 0) __hip_atomic_fetch_or(&g_wn_fault, kGFault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---- graph cache: a captured S-step graph depends only on WnArgs and S.
 struct GraphKey {
   WnArgs a;
@@ -1265,6 +1878,37 @@ bool xcd_eligible(int B, int n_layers, int taps, int R, int G, int S) {
   return dev_ok;
 }
 
+// All-CU weight-resident generation (wn_grid_kernel): AVC_WN_GRID=1 / autovc_wavenet_set_grid(1)
+int g_wn_grid = [] { const char* e = getenv("AVC_WN_GRID"); return e ? atoi(e) : 0; }();
+
+template <int NB>
+bool grid_attr(int bytes) {
+  int per = 0;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(wn_grid_kernel<NB>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess &&
+         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wn_grid_kernel<NB>, 64 * kGrW, bytes) == hipSuccess &&
+         per >= 1;
+}
+
+bool grid_eligible(int B, int n_layers, int taps, int R, int G, int S, int NO) {
+  if (!g_wn_grid || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
+      S != 256 || NO > kMaxNO)
+    return false;
+  static int ok = -1;
+  static int lds_ok_for = -1;
+  const int bytes = 4 * g_lds(n_layers, NO).total;
+  if (ok < 0 || lds_ok_for != bytes) {
+    ok = 0;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus == 256 &&
+        grid_attr<1>(bytes) && grid_attr<2>(bytes) && grid_attr<4>(bytes) && grid_attr<8>(bytes))
+      ok = 1;
+    lds_ok_for = bytes;
+  }
+  return ok == 1;
+}
+
 int64_t ring_frames(int n_layers, int lps, int K) {
   const int64_t dmax = (int64_t)1 << (std::min(n_layers, lps) - 1);
   const int64_t need = (K - 1) * dmax + 1;
@@ -1285,6 +1929,33 @@ int autovc_wavenet_set_xcd(int on) {
 }
 
 int autovc_wavenet_get_xcd(void) { return g_wn_xcd; }
+
+int autovc_wavenet_set_grid(int on) {
+  AVC_CHECK_ARG(on == 0 || on == 1, "autovc_wavenet_set_grid: 0 or 1");
+  g_wn_grid = on;
+  return avc::kOk;
+}
+
+int autovc_wavenet_get_grid(void) { return g_wn_grid; }
+
+#ifdef AVC_WN_GRID_TRACE
+extern "C" int autovc_wavenet_grid_trace(int* out) {   // trace builds only: 2 x 26 x 5 ints
+  AVC_HIP(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  AVC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wn_grid_trace), sizeof(int) * 2 * (kGMaxL + 2) * 5), "trace");
+  return avc::kOk;
+}
+#endif
+
+int autovc_wavenet_grid_diag(int clear, int* out5) {
+  AVC_CHECK_ARG(out5 != nullptr, "autovc_wavenet_grid_diag: null out");
+  AVC_HIP(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  AVC_HIP(hipMemcpyFromSymbol(out5, HIP_SYMBOL(g_wn_grid_diag), 5 * sizeof(int)), "hipMemcpyFromSymbol");
+  if (clear) {
+    const int zero[5] = {};
+    AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wn_grid_diag), zero, 5 * sizeof(int)), "hipMemcpyToSymbol");
+  }
+  return avc::kOk;
+}
 
 int autovc_wavenet_set_timeout_ticks(int ticks) {
   AVC_CHECK_ARG(ticks >= 0, "autovc_wavenet_set_timeout_ticks: ticks >= 0");
@@ -1321,7 +1992,9 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
   const int64_t ring = (int64_t)(n_layers + 1) * ring_frames(n_layers, layers_per_stack, taps) * B * R;
   const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + 2 * (int64_t)B * (G / 2) +
                          2 * (int64_t)n_layers * B * G + (int64_t)(S / kHR) * B * kMaxNO + 7 * 64;
-  return floats * 4 + kCtrSlots * 4 + (int64_t)kXBarLines * kXLn * 4 + 256;
+  const int64_t grid = 16 * ((int64_t)n_layers * ring_frames(n_layers, layers_per_stack, taps) * B * 256 + 2 * (int64_t)B * 256) +
+                       8 * 2 * (int64_t)n_layers * B * 512;   // wn_grid_kernel's tagged granules
+  return floats * 4 + kCtrSlots * 4 + (int64_t)kXBarLines * kXLn * 4 + kGErrInts * 4 + grid + 1024;
 }
 
 int autovc_wavenet_upsample_f32(int B, int Tc, int C, int n_stages, const int* scales, const float* c,
@@ -1388,15 +2061,38 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   a.molp = ws;                 ws += round64((int64_t)(S / kHR) * B * kMaxNO);
   a.ctr = reinterpret_cast<int*>(ws);
   int* xbar = a.ctr + kCtrSlots;   // the XCD-local generation's census / phase counters
+  int* gerr = xbar + kXBarLines * kXLn;   // the all-CU generation's error word (one line)
+  {
+    float* g = reinterpret_cast<float*>(gerr + kGErrInts);
+    a.gring = g;  g += 4 * (int64_t)n_layers * RING * B * 256;
+    a.gsk = g;    g += 4 * (int64_t)B * 256;
+    a.gh1 = g;    g += 4 * (int64_t)B * 256;
+    a.gpt = g;    g += 2 * 2 * (int64_t)n_layers * B * 512;
+  }
   a.teacher = teacher; a.teacher_len = teacher ? teacher_len : 0;
   a.y_out = y_out; a.mol_out = mol_out;
   a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32);
   a.utt_base = utt_base; a.log_scale_min = log_scale_min;
-  const int64_t used = reinterpret_cast<char*>(xbar + kXBarLines * kXLn) - static_cast<char*>(workspace);
+  const int64_t used = reinterpret_cast<char*>(a.gpt + 2 * 2 * (int64_t)n_layers * B * 512) - static_cast<char*>(workspace);
   AVC_CHECK_ARG(used <= autovc_wavenet_workspace_bytes(B, T, n_layers, layers_per_stack, taps, R, G, S),
                 "%s: workspace layout overflow", fn);
 
   if (t0 == 0) AVC_HIP(avc::zero_async(workspace, (size_t)used, stream), "zero_async");
+  if (grid_eligible(B, n_layers, taps, R, G, S, n_out)) {
+    // one persistent launch for the whole call, every gate weight of the chain on chip (wn_grid_kernel)
+    AVC_HIP(avc::zero_async(gerr, (size_t)kGErrInts * 4, stream), "zero_async");
+    const int lds = 4 * g_lds(n_layers, n_out).total;
+    if (B == 1) hipLaunchKernelGGL(wn_grid_kernel<1>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else if (B == 2) hipLaunchKernelGGL(wn_grid_kernel<2>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else if (B <= 4) hipLaunchKernelGGL(wn_grid_kernel<4>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else hipLaunchKernelGGL(wn_grid_kernel<8>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    AVC_CHECK_LAUNCH(fn);
+    if (t1 == T) {
+      hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);
+      AVC_CHECK_LAUNCH(fn);
+    }
+    return avc::kOk;
+  }
   if (xcd_eligible(B, n_layers, taps, R, G, S)) {
     // one persistent launch for the whole call: utterance x on XCD x (see wn_xcd_kernel)
     AVC_HIP(avc::zero_async(xbar, (size_t)kXBarLines * kXLn * 4, stream), "zero_async");

@@ -335,8 +335,15 @@ class WaveNet(nn.Module):
         # wait timed out (its 32 workgroups per XCD were not all resident): surface it here.
         # Reading the word synchronises the device, so only that mode pays for it.
         fault = ctypes.c_int(0)
-        if lib.autovc_wavenet_get_xcd():
+        if lib.autovc_wavenet_get_xcd() or lib.autovc_wavenet_get_grid():
             _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(fault))
+        if fault.value & 2:
+            diag = (ctypes.c_int * 5)()
+            _lib.call("autovc_wavenet_grid_diag", 1, ctypes.addressof(diag))
+            raise RuntimeError("wn_grid_kernel (all-CU WaveNet generation): a hand-off wait timed out "
+                               f"(kind, step, phase, workgroup, tag seen = {tuple(diag)}) — its 256 workgroups were not all "
+                               "resident (another process on this GPU?); outputs are NaN. Set AVC_WN_GRID=0 to use "
+                               "the per-layer launches.")
         if fault.value:
             raise RuntimeError("wn_xcd_kernel (XCD-local WaveNet generation): a per-XCD phase wait timed out — "
                                "its workgroups were not all resident (another process on this GPU?); outputs are NaN. "

@@ -536,6 +536,20 @@ int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, 
  * (synchronising; clear != 0 resets it). */
 int autovc_wavenet_set_xcd(int on);
 int autovc_wavenet_get_xcd(void);
+/* All-CU weight-resident generation (B <= 8, R = 512, G = 512, S = 256, 3 taps, 8..24 layers, a
+ * 256-CU device): ONE persistent launch per autovc_wavenet_generate_f32 call whose 256
+ * workgroups keep every gate weight of the sample chain on chip and hand each phase's outputs
+ * to the next through tagged 16-byte granules (dataflow, no grid barrier).  Same
+ * arguments and outputs; a hand-off wait that times out poisons the call's samples with NaN and
+ * sets bit 2 of the autovc_wavenet_fault word.
+ * AVC_WN_GRID=1 or autovc_wavenet_set_grid(1) selects it; takes precedence over the XCD form. */
+int autovc_wavenet_set_grid(int on);
+int autovc_wavenet_get_grid(void);
+/* The first wait of the all-CU generation that timed out since the last clear: out5 = {kind
+ * (0 none, 1 layer inputs, 2 past-tap sums, 3 LDS handshake, 4 past-tap inputs, 5 past-tap
+ * consumers, 6 skip sums, 7 h1), step, phase (or job), workgroup, last tag seen (-1 if not
+ * recorded)}; synchronises the device. */
+int autovc_wavenet_grid_diag(int clear, int* out5);
 int autovc_wavenet_set_timeout_ticks(int ticks);
 int autovc_wavenet_fault(int clear, int* out);
 int64_t autovc_wavenet_ring_frames(int n_layers, int layers_per_stack, int taps);

@@ -36,15 +36,19 @@ def _cond(B, Tc, seed=4321):
     return torch.from_numpy(np.clip(rs.normal(0.43, 0.18, (B, 80, Tc)), 0, 1).astype(np.float32))
 
 
-@pytest.fixture(params=[0, 1], ids=["launches", "xcd"])
+@pytest.fixture(params=[0, 1, 2], ids=["launches", "xcd", "grid"])
 def xcd(request):
-    """Run a test with the per-layer launches and with the XCD-local persistent generation
-    (wn_xcd_kernel: B <= 8 on 8 XCDs x 32 CUs; larger batches use the launches either way)."""
+    """Run a test with the per-layer launches, with the XCD-local persistent generation
+    (wn_xcd_kernel: B <= 8 on 8 XCDs x 32 CUs) and with the all-CU weight-resident generation
+    (wn_grid_kernel: B <= 8, 8..24 layers, 256 CUs); other shapes use the launches either way."""
     from autovc_amd import _lib
-    prev = _lib.load().autovc_wavenet_get_xcd()
-    _lib.call("autovc_wavenet_set_xcd", request.param)
+    lib = _lib.load()
+    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
+    _lib.call("autovc_wavenet_set_xcd", int(request.param == 1))
+    _lib.call("autovc_wavenet_set_grid", int(request.param == 2))
     yield request.param
-    _lib.call("autovc_wavenet_set_xcd", prev)
+    _lib.call("autovc_wavenet_set_xcd", prev[0])
+    _lib.call("autovc_wavenet_set_grid", prev[1])
 
 
 def rel(a, b):
@@ -227,3 +231,70 @@ def test_xcd_generation_timeout_surfaces(cuda):
         _lib.call("autovc_wavenet_set_xcd", prev)
     y = m.generate(c, seed=1, log_scale_min=LSM)          # the next call runs clean
     assert torch.isfinite(y).all()
+
+
+def _set_modes(xcd, grid):
+    from autovc_amd import _lib
+    _lib.call("autovc_wavenet_set_xcd", xcd)
+    _lib.call("autovc_wavenet_set_grid", grid)
+
+
+@pytest.mark.parametrize("B", [8, 1])
+def test_grid_generation_matches_launches(cuda, B):
+    """The all-CU weight-resident generation (wn_grid_kernel: every chain weight on chip, a
+    grid barrier per layer, the past taps streamed in the barrier windows) against the
+    per-layer launches: 24 layers, 2,048 free-running samples (16 ring wraps, 16 conditioning
+    chunks = 16 persistent launches, so the past taps cross launch seams), within fp32
+    summation-order noise, the MoL parameters of a teacher-forced run within 1e-5; B = 8 and
+    the reference's wavegen batch of one; no fault recorded."""
+    import ctypes
+    from autovc_amd import _lib
+    lib = _lib.load()
+    if lib.autovc_lstm_xcd_supported(64, 512) == 0:
+        pytest.skip("needs 8 XCDs x 32 CUs")
+    hp = ow.HPARAMS
+    m, _ = _model(hp, cuda)
+    c = _cond(B, 8, seed=31).to(cuda)
+    rs = np.random.RandomState(6)
+    teacher = torch.from_numpy(rs.uniform(-0.9, 0.9, (B, 2048)).astype(np.float32)).to(cuda)
+    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
+    out = {}
+    try:
+        for mode in (0, 1):
+            _set_modes(0, mode)
+            y = m.generate(c, seed=17, log_scale_min=LSM)
+            _, mol = m.generate(c, seed=17, log_scale_min=LSM, teacher=teacher, return_mol=True)
+            out[mode] = (y, mol)
+    finally:
+        _set_modes(*prev)
+    (y0, m0), (y1, m1) = out[0], out[1]
+    assert torch.isfinite(y1).all() and torch.isfinite(m1).all()
+    assert rel(m1, m0) < 1e-5
+    assert (y1 - y0).abs().max().item() < 1e-4
+    f = ctypes.c_int(0)
+    _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(f))
+    assert f.value == 0
+
+
+def test_grid_generation_timeout_surfaces(cuda):
+    """A grid-barrier wait that gives up (forced: a 1-tick timeout) poisons the outputs and
+    raises; the next call runs clean."""
+    from autovc_amd import _lib
+    lib = _lib.load()
+    if lib.autovc_lstm_xcd_supported(64, 512) == 0:
+        pytest.skip("needs 8 XCDs x 32 CUs")
+    hp = ow.small_hparams(layers=8, stacks=2)
+    m, _ = _model(hp, cuda)
+    c = _cond(2, 1).to(cuda)
+    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
+    try:
+        _set_modes(0, 1)
+        _lib.call("autovc_wavenet_set_timeout_ticks", 1)
+        with pytest.raises(RuntimeError, match="wn_grid_kernel"):
+            m.generate(c, seed=1, log_scale_min=LSM)
+        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
+        y = m.generate(c, seed=1, log_scale_min=LSM)      # the next call runs clean
+        assert torch.isfinite(y).all()
+    finally:
+        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
+        _set_modes(*prev)
