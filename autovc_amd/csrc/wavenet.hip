@@ -1341,6 +1341,18 @@ template <int NB>
 __device__ __forceinline__ bool poll_granules(const float* base, int o, int B, int tag, f32x4 (&g)[NB], int* err,
                                               int ticks, int kind, int ph) {
   Spin sp{__builtin_amdgcn_s_memrealtime(), err, ticks, kind, tag - 1, ph};
+  if constexpr (NB > 1) {
+    // poll utterance 0's granule alone: the producer lane group publishes every utterance's
+    // granule with one store instruction, so the rest are out (almost always) once it is, and
+    // the waiting costs the fabric one 16-byte load per lane per retry instead of NB
+    while (true) {
+      asm volatile("" ::: "memory");
+      g[0] = ld4_l2(base, o * 4);
+      if (__builtin_amdgcn_ballot_w64(tag_of(g[0]) != tag) == 0) break;
+      sp.seen = __builtin_amdgcn_readfirstlane(tag_of(g[0]));
+      if (!sp.tick()) return false;
+    }
+  }
   while (true) {
     // every retry re-issues every load (the clobber keeps the compiler from reusing a value
     // loaded in an earlier pass), and all of them are in flight before the first compare; a
@@ -1878,8 +1890,10 @@ bool xcd_eligible(int B, int n_layers, int taps, int R, int G, int S) {
   return dev_ok;
 }
 
-// All-CU weight-resident generation (wn_grid_kernel): AVC_WN_GRID=1 / autovc_wavenet_set_grid(1)
-int g_wn_grid = [] { const char* e = getenv("AVC_WN_GRID"); return e ? atoi(e) : 0; }();
+// All-CU weight-resident generation (wn_grid_kernel): 0 never, 1 every eligible batch, 2 (the
+// default) one utterance only — the measured crossover: B = 1 94.2 vs 109.1 us per sample step
+// for the launches, B = 2 118.8 vs 109.4 (profiles/r04/wn_grid_ab.txt).  AVC_WN_GRID / set_grid.
+int g_wn_grid = [] { const char* e = getenv("AVC_WN_GRID"); return e ? atoi(e) : 2; }();
 
 template <int NB>
 bool grid_attr(int bytes) {
@@ -1891,7 +1905,7 @@ bool grid_attr(int bytes) {
 }
 
 bool grid_eligible(int B, int n_layers, int taps, int R, int G, int S, int NO) {
-  if (!g_wn_grid || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
+  if (!g_wn_grid || (g_wn_grid == 2 && B != 1) || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
       S != 256 || NO > kMaxNO)
     return false;
   static int ok = -1;
@@ -1931,7 +1945,7 @@ int autovc_wavenet_set_xcd(int on) {
 int autovc_wavenet_get_xcd(void) { return g_wn_xcd; }
 
 int autovc_wavenet_set_grid(int on) {
-  AVC_CHECK_ARG(on == 0 || on == 1, "autovc_wavenet_set_grid: 0 or 1");
+  AVC_CHECK_ARG(on == 0 || on == 1 || on == 2, "autovc_wavenet_set_grid: 0 (off), 1 (B <= 8) or 2 (B = 1)");
   g_wn_grid = on;
   return avc::kOk;
 }

@@ -241,9 +241,9 @@ def _set_modes(xcd, grid):
 
 @pytest.mark.parametrize("B", [8, 1])
 def test_grid_generation_matches_launches(cuda, B):
-    """The all-CU weight-resident generation (wn_grid_kernel: every chain weight on chip, a
-    grid barrier per layer, the past taps streamed in the barrier windows) against the
-    per-layer launches: 24 layers, 2,048 free-running samples (16 ring wraps, 16 conditioning
+    """The all-CU weight-resident generation (wn_grid_kernel: every gate weight of the chain
+    on chip, each phase's outputs handed on in tagged granules, the past taps computed a step
+    ahead by the same workgroups) against the per-layer launches: 24 layers, 2,048 free-running samples (16 ring wraps, 16 conditioning
     chunks = 16 persistent launches, so the past taps cross launch seams), within fp32
     summation-order noise, the MoL parameters of a teacher-forced run within 1e-5; B = 8 and
     the reference's wavegen batch of one; no fault recorded."""
@@ -277,8 +277,8 @@ def test_grid_generation_matches_launches(cuda, B):
 
 
 def test_grid_generation_timeout_surfaces(cuda):
-    """A grid-barrier wait that gives up (forced: a 1-tick timeout) poisons the outputs and
-    raises; the next call runs clean."""
+    """A hand-off wait that gives up (forced: a 1-tick timeout) with the all-CU form requested
+    (mode 1) poisons the outputs and raises; the next call runs clean."""
     from autovc_amd import _lib
     lib = _lib.load()
     if lib.autovc_lstm_xcd_supported(64, 512) == 0:
@@ -295,6 +295,35 @@ def test_grid_generation_timeout_surfaces(cuda):
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
         y = m.generate(c, seed=1, log_scale_min=LSM)      # the next call runs clean
         assert torch.isfinite(y).all()
+    finally:
+        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
+        _set_modes(*prev)
+
+
+def test_grid_default_mode_batch_of_one(cuda):
+    """Mode 2 (the default) runs the all-CU form for one utterance only: B = 1 equals mode 1
+    bit for bit, B = 2 equals the launches bit for bit.  If its wait gives up (forced: a 1-tick
+    timeout) it warns, keeps to the launches in this process and returns the launches' samples."""
+    from autovc_amd import _lib
+    lib = _lib.load()
+    if lib.autovc_lstm_xcd_supported(64, 512) == 0:
+        pytest.skip("needs 8 XCDs x 32 CUs")
+    hp = ow.small_hparams(layers=8, stacks=2)
+    m, _ = _model(hp, cuda)
+    c1, c2 = _cond(1, 2, seed=3).to(cuda), _cond(2, 2, seed=4).to(cuda)
+    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
+    try:
+        out = {}
+        for mode in (0, 1, 2):
+            _set_modes(0, mode)
+            out[mode] = (m.generate(c1, seed=5, log_scale_min=LSM), m.generate(c2, seed=5, log_scale_min=LSM))
+        assert torch.equal(out[2][0], out[1][0]) and torch.equal(out[2][1], out[0][1])
+        _set_modes(0, 2)
+        _lib.call("autovc_wavenet_set_timeout_ticks", 1)
+        with pytest.warns(RuntimeWarning, match="wn_grid_kernel"):
+            y = m.generate(c1, seed=5, log_scale_min=LSM)
+        assert lib.autovc_wavenet_get_grid() == 0
+        assert torch.equal(y, out[0][0])
     finally:
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
         _set_modes(*prev)
