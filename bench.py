@@ -298,7 +298,9 @@ def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=
     assert y1.shape == (1, n1) and bool(torch.isfinite(y1).all())
     out["b1"] = {"workload": f"1 utterance x {n1} samples (wavegen's batch of one)",
                  "us_per_sample_step": round(d1 / n1 * 1e6, 2), "samples_per_s": round(n1 / d1, 1),
-                 "rtf": round(n1 / 16000.0 / d1, 3)}
+                 "rtf": round(n1 / 16000.0 / d1, 3),
+                 "path": ("wn_grid_kernel (all-CU weight-resident dataflow, one launch per call)"
+                          if _lib.load().autovc_wavenet_get_grid() in (1, 2) else "per-layer launches")}
     if cpu:
         out["cpu_baseline"] = wavenet_cpu_baseline(n_utt, seconds_cpu)
         out["vs_cpu_baseline"] = round(out["samples_per_s"] / out["cpu_baseline"]["value"], 1)
