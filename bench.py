@@ -579,7 +579,8 @@ def main():
     # each hold part of the chip, so ranks sharing a device use the per-step launches.
     share = os.environ.get("AVC_BENCH_SHARE_DEVICE") == "1"
     if share:
-        for k in ("AVC_LSTM2_PERSIST", "AVC_LSTM_XCD", "AVC_LSTM_XCD_BWD", "AVC_LSTM_PERSIST"):
+        for k in ("AVC_LSTM2_PERSIST", "AVC_LSTM_XCD", "AVC_LSTM_XCD_BWD", "AVC_LSTM_PERSIST", "AVC_WN_GRID",
+                  "AVC_WN_XCD"):
             os.environ[k] = "0"
     from autovc_amd import ddp
     rank, world = ddp.init_from_env(backend="gloo" if share else None)

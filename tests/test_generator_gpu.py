@@ -404,3 +404,51 @@ def test_conversion_caller_flow(cuda):
                                          torch.from_numpy(G["emb"][1:2]))
     assert out.shape == (150, 80)
     assert rel(out, ref_psnt[0, 0, :-len_pad, :]) < FWD_TOL
+
+
+def _colsum_order(X, out0=None):
+    """numpy restatement of autovc_colsum_f32's fixed summation order (float32): RS row blocks
+    of 4 row-strided sums added in wave order, then 16 row groups of partials, groups in order."""
+    M, N = X.shape
+    RS = min(128, M)
+    part = np.zeros((RS, N), np.float32)
+    for rs in range(RS):
+        r0, r1 = M * rs // RS, M * (rs + 1) // RS
+        ws = []
+        for w in range(4):
+            s = np.zeros(N, np.float32)
+            for r in range(r0 + w, r1, 4):
+                s = s + X[r]
+            ws.append(s)
+        part[rs] = ((ws[0] + ws[1]) + ws[2]) + ws[3]
+    groups = []
+    for g in range(16):
+        t = np.zeros(N, np.float32)
+        for q in range(g, RS, 16):
+            t = t + part[q]
+        groups.append(t)
+    tot = np.zeros(N, np.float32)
+    for t in groups:
+        tot = tot + t
+    return tot if out0 is None else out0 + tot
+
+
+@pytest.mark.parametrize("M,N", [(8192, 300), (37, 64), (5, 1000), (1000, 4096)])
+def test_colsum_bit_exact(cuda, M, N):
+    """autovc_colsum_f32 (the bias gradients' column sums: partial rows, then a fixed-order
+    finalize) equals the numpy restatement of its summation order bit for bit, with
+    accumulate and the second output, at ragged widths and row counts below the 128 splits."""
+    from autovc_amd import functional as Fh
+    rs = np.random.RandomState(M + N)
+    X = rs.standard_normal((M, N)).astype(np.float32)
+    base = rs.standard_normal(N).astype(np.float32)
+    xd = torch.from_numpy(X).to(cuda)
+    out = torch.from_numpy(base.copy()).to(cuda)
+    out2 = torch.from_numpy(base.copy()).to(cuda)
+    Fh.colsum(xd, out, out2, accumulate=True)
+    want = _colsum_order(X, base)
+    assert np.array_equal(out.cpu().numpy(), want) and np.array_equal(out2.cpu().numpy(), want)
+    n3 = max(1, N // 3)
+    o3 = torch.empty(n3, device=cuda)
+    Fh.colsum(xd[:, :n3], o3)
+    assert np.array_equal(o3.cpu().numpy(), _colsum_order(X[:, :n3]))
