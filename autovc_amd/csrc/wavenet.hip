@@ -181,6 +181,65 @@ __device__ inline void butterfly(float* cur, int lane) {
   }
 }
 
+// The same halving reduction on gfx950's cross-lane hardware instead of ds_bpermute (an LDS
+// round trip per shuffle): level 0 pairs lanes l, l ^ 32 with v_permlane32_swap, level 1 l,
+// l ^ 16 with v_permlane16_swap (one swap moves two values: the kept half of one lane group
+// and the sent half of the other), level 2 l, l ^ 15 (DPP row_mirror), level 3 l, l ^ 7
+// (row_half_mirror), levels 4 / 5 l ^ 2, l ^ 1 (quad_perm).  The pairings generate every
+// lane, so lane L with (L & (64/NV - 1)) == 0 ends with the full sum of value L / (64/NV), as
+// wave_reduce_multi; the pairing tree is fixed, so every NV rounds each value alike.
+template <int LVL>
+__device__ __forceinline__ float dpp_partner(float v) {
+  constexpr int ctrl = LVL == 2 ? 0x140 : LVL == 3 ? 0x141 : LVL == 4 ? 0x4E : 0xB1;
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xf, 0xf, false));
+}
+template <int N, int LVL>
+__device__ __forceinline__ void butterfly_hw(float* cur, int lane) {
+  if constexpr (LVL < 6) {
+    constexpr int bit = LVL == 0 ? 32 : LVL == 1 ? 16 : LVL == 2 ? 8 : LVL == 3 ? 4 : LVL == 4 ? 2 : 1;
+    if constexpr (LVL < 2) {
+      if constexpr (N > 1) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+          const auto r = LVL == 0 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(cur[j]), __float_as_uint(cur[j + N / 2]), false, false)
+                                  : __builtin_amdgcn_permlane16_swap(__float_as_uint(cur[j]), __float_as_uint(cur[j + N / 2]), false, false);
+          cur[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+        }
+        butterfly_hw<N / 2, LVL + 1>(cur, lane);
+      } else {
+        const auto r = LVL == 0 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(cur[0]), __float_as_uint(cur[0]), false, false)
+                                : __builtin_amdgcn_permlane16_swap(__float_as_uint(cur[0]), __float_as_uint(cur[0]), false, false);
+        cur[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+        butterfly_hw<1, LVL + 1>(cur, lane);
+      }
+    } else {
+      if constexpr (N > 1) {
+        const bool up = (lane & bit) != 0;
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+          const float keep = up ? cur[j + N / 2] : cur[j];
+          const float send = up ? cur[j] : cur[j + N / 2];
+          cur[j] = keep + dpp_partner<LVL>(send);
+        }
+        butterfly_hw<N / 2, LVL + 1>(cur, lane);
+      } else {
+        cur[0] += dpp_partner<LVL>(cur[0]);
+        butterfly_hw<1, LVL + 1>(cur, lane);
+      }
+    }
+  }
+}
+
+template <int NV>
+__device__ inline float wave_reduce_hw(float (&v)[NV], int lane) {
+  static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "power-of-two value count");
+  float cur[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) cur[j] = v[j];
+  butterfly_hw<NV, 0>(cur, lane);
+  return cur[0];
+}
+
 template <int NV>
 __device__ inline float wave_reduce_multi(float (&v)[NV], int lane) {
   static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "power-of-two value count");
@@ -1287,6 +1346,9 @@ __device__ __forceinline__ float2 ld2_l2(const float* base, int off) {   // sc1 
 // 3 the chain waves' LDS handshake, 4 past-tap inputs, 5 past-tap consumers, 6 skip sums, 7 h1.
 __device__ int g_wn_grid_diag[5] = {};
 
+#ifndef AVC_WN_SPIN_SLEEP
+#define AVC_WN_SPIN_SLEEP 1                   // a chain wave's retry pause (tools/build_variant.sh A/B)
+#endif
 // bounded spin state of one wave: the deadline, the device-wide error word, what it waits for
 struct Spin {
   uint64_t t0;
@@ -1298,7 +1360,7 @@ struct Spin {
   int n = 0;
   __device__ bool tick() {                    // false: give up (timed out, or another wave did)
     if (!slow && (++n & 3) != 0) {            // the error word and the clock every 4th retry
-      __builtin_amdgcn_s_sleep(1);
+      if (AVC_WN_SPIN_SLEEP) __builtin_amdgcn_s_sleep(1);
       return true;
     }
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
@@ -1531,6 +1593,8 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
   const float fwo0 = a.packed[2 * os], fwo1 = a.packed[2 * os + 1], fbo0 = a.packed[R + 2 * os],
               fbo1 = a.packed[R + 2 * os + 1];
   const float w1o = W1[(int64_t)os * S + o], b1o = b1[os];
+  // the last layer's skip bias of row os (the tail's epilogue: loaded once, off the chain)
+  const float bsk_last = (layer_base(a, L - 1) + (int64_t)a.G * KX + (int64_t)(R + S) * H)[R + os];
   // residual weights of layer lr at column o: W_out rows 2 os, 2 os + 1, W_skip row os
   float rw0 = 0.f, rw1 = 0.f, rw2 = 0.f;
   auto fetch_res = [&](int lr) {
@@ -1566,11 +1630,11 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
         float cur[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) cur[j] = acc[g * 8 + j];
-        butterfly<8, 32>(cur, lane);
+        butterfly_hw<8, 0>(cur, lane);
         if ((lane & 7) == 0) s_part[par * 256 + wave * 64 + g * 8 + (lane >> 3)] = cur[0];
       }
     } else {
-      const float v = wave_reduce_multi<NV>(acc, lane);
+      const float v = wave_reduce_hw<NV>(acc, lane);
       if ((lane & (64 / NV - 1)) == 0) s_part[par * 256 + wave * 64 + lane / (64 / NV)] = v;
     }
     return chain_sync(s_cnt, kx, lane, errw, ticks, cur_t, cur_p);
@@ -1635,7 +1699,10 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
               for (int i = 0; i < 8; ++i) am[b] = dot4(w2r[i], *reinterpret_cast<const f32x4*>(hb + 4 * i), am[b]);
             }
 #pragma unroll
-            for (int b = 0; b < NB; ++b) am[b] += __shfl_xor(am[b], 32);
+            for (int b = 0; b < NB; ++b) {   // + lane l ^ 32 (v_permlane32_swap, no LDS round trip)
+              const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(am[b]), __float_as_uint(am[b]), false, false);
+              am[b] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+            }
             if (lane < 32)
 #pragma unroll
               for (int b = 0; b < NB; ++b) s_molp[(wave * 32 + lane) * kGMaxB + b] = am[b];
@@ -1770,8 +1837,7 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
         if (!reduce_park(acc)) { ok = false; break; }
         WN_GT(2);
         if (wave == 0 && lane < B) {
-          const float* pbias = layer_base(a, L - 1) + (int64_t)a.G * KX + (int64_t)(R + S) * H;
-          const float sv = psum(lane) + pbias[R + os];
+          const float sv = psum(lane) + bsk_last;
           const float sk = L - 1 == 0 ? sv : (a.legacy ? (skip_acc + sv) * kSqrtHalf : skip_acc + sv);
           st4_sc1(a.gsk, (lane * 256 + os) * 4, sk, 0.f, 0.f, t + 1);
           WN_GT(4);
@@ -1891,8 +1957,8 @@ bool xcd_eligible(int B, int n_layers, int taps, int R, int G, int S) {
 }
 
 // All-CU weight-resident generation (wn_grid_kernel): 0 never, 1 every eligible batch, 2 (the
-// default) one utterance only — the measured crossover: B = 1 94.2 vs 109.1 us per sample step
-// for the launches, B = 2 118.8 vs 109.4 (profiles/r04/wn_grid_ab.txt).  AVC_WN_GRID / set_grid.
+// default) up to two utterances — the measured crossover: B = 1 86.5, B = 2 100.9 us per sample
+// step against 109.8 / 110.5 for the launches, B = 4 even (profiles/r04/wn_grid_ab.txt).
 int g_wn_grid = [] { const char* e = getenv("AVC_WN_GRID"); return e ? atoi(e) : 2; }();
 
 template <int NB>
@@ -1905,7 +1971,7 @@ bool grid_attr(int bytes) {
 }
 
 bool grid_eligible(int B, int n_layers, int taps, int R, int G, int S, int NO) {
-  if (!g_wn_grid || (g_wn_grid == 2 && B != 1) || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
+  if (!g_wn_grid || (g_wn_grid == 2 && B > 2) || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
       S != 256 || NO > kMaxNO)
     return false;
   static int ok = -1;
@@ -1945,7 +2011,7 @@ int autovc_wavenet_set_xcd(int on) {
 int autovc_wavenet_get_xcd(void) { return g_wn_xcd; }
 
 int autovc_wavenet_set_grid(int on) {
-  AVC_CHECK_ARG(on == 0 || on == 1 || on == 2, "autovc_wavenet_set_grid: 0 (off), 1 (B <= 8) or 2 (B = 1)");
+  AVC_CHECK_ARG(on == 0 || on == 1 || on == 2, "autovc_wavenet_set_grid: 0 (off), 1 (B <= 8) or 2 (B <= 2)");
   g_wn_grid = on;
   return avc::kOk;
 }

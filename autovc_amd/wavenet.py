@@ -336,13 +336,13 @@ class WaveNet(nn.Module):
         # the word synchronises the device, so only those modes pay for it.
         fault = ctypes.c_int(0)
         grid_mode = lib.autovc_wavenet_get_grid()
-        if lib.autovc_wavenet_get_xcd() or (grid_mode == 1 or (grid_mode == 2 and B == 1)):
+        if lib.autovc_wavenet_get_xcd() or (grid_mode == 1 or (grid_mode == 2 and B <= 2)):
             _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(fault))
         if fault.value & 2:
             diag = (ctypes.c_int * 5)()
             _lib.call("autovc_wavenet_grid_diag", 1, ctypes.addressof(diag))
             if grid_mode == 2:
-                # the default (B = 1) choice, not a request: warn, keep to the per-layer launches
+                # the default (B <= 2) choice, not a request: warn, keep to the per-layer launches
                 # in this process, and generate again
                 warnings.warn("wn_grid_kernel (all-CU WaveNet generation) could not keep its 256 workgroups "
                               f"resident (wait {tuple(diag)} timed out; another process on this GPU?): "

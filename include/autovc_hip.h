@@ -543,8 +543,8 @@ int autovc_wavenet_get_xcd(void);
  * arguments and outputs; a hand-off wait that times out poisons the call's samples with NaN and
  * sets bit 2 of the autovc_wavenet_fault word.
  * Mode (AVC_WN_GRID or autovc_wavenet_set_grid): 0 never, 1 for every eligible batch, 2 (the
- * default) for one utterance only (B = 1, where it beats the launches); it takes
- * precedence over the XCD form. */
+ * default) for B <= 2, where it beats the launches; it takes precedence
+ * over the XCD form. */
 int autovc_wavenet_set_grid(int on);
 int autovc_wavenet_get_grid(void);
 /* The first wait of the all-CU generation that timed out since the last clear: out5 = {kind

@@ -300,9 +300,9 @@ def test_grid_generation_timeout_surfaces(cuda):
         _set_modes(*prev)
 
 
-def test_grid_default_mode_batch_of_one(cuda):
-    """Mode 2 (the default) runs the all-CU form for one utterance only: B = 1 equals mode 1
-    bit for bit, B = 2 equals the launches bit for bit.  If its wait gives up (forced: a 1-tick
+def test_grid_default_mode_small_batches(cuda):
+    """Mode 2 (the default) runs the all-CU form for up to two utterances: B = 1 and B = 2
+    equal mode 1 bit for bit, B = 3 equals the launches bit for bit.  If its wait gives up (forced: a 1-tick
     timeout) it warns, keeps to the launches in this process and returns the launches' samples."""
     from autovc_amd import _lib
     lib = _lib.load()
@@ -310,14 +310,15 @@ def test_grid_default_mode_batch_of_one(cuda):
         pytest.skip("needs 8 XCDs x 32 CUs")
     hp = ow.small_hparams(layers=8, stacks=2)
     m, _ = _model(hp, cuda)
-    c1, c2 = _cond(1, 2, seed=3).to(cuda), _cond(2, 2, seed=4).to(cuda)
+    c1, c2, c3 = _cond(1, 2, seed=3).to(cuda), _cond(2, 2, seed=4).to(cuda), _cond(3, 2, seed=5).to(cuda)
     prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
     try:
         out = {}
         for mode in (0, 1, 2):
             _set_modes(0, mode)
-            out[mode] = (m.generate(c1, seed=5, log_scale_min=LSM), m.generate(c2, seed=5, log_scale_min=LSM))
-        assert torch.equal(out[2][0], out[1][0]) and torch.equal(out[2][1], out[0][1])
+            out[mode] = tuple(m.generate(c, seed=5, log_scale_min=LSM) for c in (c1, c2, c3))
+        assert torch.equal(out[2][0], out[1][0]) and torch.equal(out[2][1], out[1][1])
+        assert torch.equal(out[2][2], out[0][2])
         _set_modes(0, 2)
         _lib.call("autovc_wavenet_set_timeout_ticks", 1)
         with pytest.warns(RuntimeWarning, match="wn_grid_kernel"):
