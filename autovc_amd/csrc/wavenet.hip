@@ -240,13 +240,17 @@ __device__ inline float wave_reduce_hw(float (&v)[NV], int lane) {
   return cur[0];
 }
 
+#ifndef AVC_WN_HW_REDUCE
+#define AVC_WN_HW_REDUCE 1                    // 0: the ds_bpermute butterfly (tools/build_variant.sh A/B)
+#endif
 template <int NV>
 __device__ inline float wave_reduce_multi(float (&v)[NV], int lane) {
   static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "power-of-two value count");
   float cur[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) cur[j] = v[j];
-  butterfly<NV, 32>(cur, lane);
+  if constexpr (AVC_WN_HW_REDUCE) butterfly_hw<NV, 0>(cur, lane);
+  else butterfly<NV, 32>(cur, lane);
   return cur[0];
 }
 
