@@ -17,6 +17,7 @@ update: those buffers are snapshotted and restored around it.
 from __future__ import annotations
 
 import collections
+import gc
 import os
 
 import torch
@@ -51,8 +52,18 @@ class StepGraphs:
         graph = torch.cuda.CUDAGraph()
         if self.debug_dot:
             graph.enable_debug_mode()
-        with torch.cuda.graph(graph):
-            out = self.fn(*static)
+        # No garbage collection inside the capture: a collection there can finalise an
+        # unreachable object that owns device state (an earlier Solver's captured graphs and
+        # their private memory pool), and freeing it calls HIP APIs a capturing process must
+        # not call — the process aborts (seen once: a previous test's Solver collected during
+        # the next test's bf16 capture).  Collect first, then keep the collector off.
+        gc.collect()
+        gc.disable()
+        try:
+            with torch.cuda.graph(graph):
+                out = self.fn(*static)
+        finally:
+            gc.enable()
         if self.debug_dot:
             graph.debug_dump(self.debug_dot)
         with torch.no_grad():
