@@ -84,6 +84,8 @@ def _ws(device, nbytes, slot="main"):
 # make the main stream wait before the gradients are read.  AVC_GRAD_STREAM=0 disables.
 _GRAD_STREAM_ON = os.environ.get("AVC_GRAD_STREAM", "1") != "0"
 _GRAD_STREAM_ACTIVE = [False]
+# the side stream's priority (torch: lower = higher priority; 0 = default): AVC_GRAD_PRIORITY
+_GRAD_PRIORITY = int(os.environ.get("AVC_GRAD_PRIORITY", "0"))
 _GRAD_STREAMS: dict = {}
 # LDS left free per CU for the recurrence's step workgroup (37 KB) while side GEMMs run;
 # measured per precision (bench.py, same box, alternating): fp32 21.1 ms/step with room
@@ -95,7 +97,7 @@ def _grad_stream(dev):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     st = _GRAD_STREAMS.get(idx)
     if st is None:
-        st = torch.cuda.Stream(torch.device("cuda", idx))
+        st = torch.cuda.Stream(torch.device("cuda", idx), priority=_GRAD_PRIORITY)
         _GRAD_STREAMS[idx] = st
     return st
 
