@@ -13,6 +13,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "bn_finalize.h"
 #include "../../include/autovc_hip.h"
 
 namespace {
@@ -232,21 +233,7 @@ __global__ __launch_bounds__(256) void stats_finalize_raw_kernel(int64_t M, int 
   const bool own = sum_partials(part, RS, C, c, a, b);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   if (!own) return;
-  const double n = (double)M;
-  const double mu = a / n;
-  double v = b / n - mu * mu;
-  if (v < 0.0) v = 0.0;
-  const float muf = (float)mu, vf = (float)v;
-  mean[c] = muf;
-  var[c] = vf;
-  const float invstd = 1.0f / sqrtf(vf + eps);
-  const float alpha = invstd * (gamma ? gamma[c] : 1.f);
-  coef[c] = alpha;
-  coef[C + c] = (beta ? beta[c] : 0.f) - muf * alpha;
-  coef[2 * C + c] = muf;
-  coef[3 * C + c] = invstd;
-  if (run_mean) run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mu);
-  if (run_var) run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * v * n / (n > 1.0 ? n - 1.0 : 1.0));
+  avc::bn_finalize_channel(M, C, c, a, b, gamma, beta, eps, mean, var, coef, run_mean, run_var, momentum);
 }
 
 // eval mode: the same coefficients from the running statistics

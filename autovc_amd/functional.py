@@ -700,6 +700,11 @@ def conv_bn_act(x, conv, bn, act, residual=None):
 _CHAIN_ON = os.environ.get("AVC_CONV_CHAIN", "1") != "0"
 
 
+# the fp32 stacks' BatchNorm statistics finalized inside the output transform's launch
+# (autovc_wino5_output_bnstats_f32, bit-identical); AVC_BN_FUSED_STATS=0 keeps two launches
+_BN_FUSED_STATS = os.environ.get("AVC_BN_FUSED_STATS", "0") != "0"
+
+
 def _chain_ok(x, layers, training):
     if not (_CHAIN_ON and _WINOGRAD and _PRECISION[0] == "fp32" and x.is_cuda and x.dim() == 3
             and x.dtype == torch.float32):
@@ -768,12 +773,20 @@ class ConvBNChainFn(torch.autograd.Function):
             y = torch.empty((B, T, Co), device=dev, dtype=torch.float32)
             coef = torch.empty((4, Co), device=dev, dtype=torch.float32)
             if training:
-                part = _ws(dev, RS * Co * 16, "chain_fwd")
-                _lib.call("autovc_wino5_output_stats_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, part, _s())
                 mean = torch.empty(Co, device=dev, dtype=torch.float32)
                 var = torch.empty(Co, device=dev, dtype=torch.float32)
-                _lib.call("autovc_bn_finalize_f32", RS, M, Co, part, _p(g), _p(be), float(epss[l]), mean.data_ptr(),
-                          var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt), _s())
+                if _BN_FUSED_STATS:   # output transform + statistics + finalize in one launch
+                    ws = _ws(dev, lib.autovc_wino5_bnstats_workspace_bytes(B, T, Co), "chain_fwd_fused")
+                    _lib.call("autovc_wino5_output_bnstats_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co,
+                              _p(g), _p(be), float(epss[l]), mean.data_ptr(), var.data_ptr(), coef.data_ptr(), _p(rm),
+                              _p(rv), float(moms[l]), _p(nbt), ws, _s())
+                else:
+                    part = _ws(dev, RS * Co * 16, "chain_fwd")
+                    _lib.call("autovc_wino5_output_stats_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, part,
+                              _s())
+                    _lib.call("autovc_bn_finalize_f32", RS, M, Co, part, _p(g), _p(be), float(epss[l]),
+                              mean.data_ptr(), var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt),
+                              _s())
             else:
                 _lib.call("autovc_wino5_output_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, _s())
                 mean, var = rm, rv

@@ -206,6 +206,15 @@ int autovc_wino5_input_bn_f32(int B, int T, int C, const float* y, int64_t ldy, 
                               float* out, hipStream_t stream);
 int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
                                   int64_t ldy, double* part, hipStream_t stream);
+/* output_stats + autovc_bn_finalize_f32 in ONE launch (the block completing the statistics
+ * finalizes; bit-identical): mean, var, coef, running stats, num_batches_tracked as
+ * autovc_bn_finalize_f32 with M = B*T.  workspace: autovc_wino5_bnstats_workspace_bytes bytes,
+ * ZEROED before its first use and left zeroed (its first 4 KB are tickets); C <= 8192. */
+int64_t autovc_wino5_bnstats_workspace_bytes(int B, int T, int C);
+int autovc_wino5_output_bnstats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
+                                    int64_t ldy, const float* gamma, const float* beta, float eps, float* mean,
+                                    float* var, float* coef, float* run_mean, float* run_var, float momentum,
+                                    int64_t* nbt, void* workspace, hipStream_t stream);
 int autovc_wino5_output_bnbwd_f32(int B, int T, int C, const float* Yt, const float* yprev, int64_t ldy,
                                   const float* coef, int act, float* dz, int64_t lddz, double* part,
                                   hipStream_t stream);
