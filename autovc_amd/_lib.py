@@ -29,7 +29,7 @@ _RESTYPES = {"autovc_last_error": ctypes.c_char_p,
              "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_lstm2_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
              "autovc_colsum_workspace_floats": c_i64, "autovc_wavenet_packed_floats": c_i64, "autovc_wavenet_ring_frames": c_i64,
              "autovc_wavenet_workspace_bytes": c_i64, "autovc_lstm2_persist_workspace_bytes": c_i64,
-             "autovc_lstm_persist_workspace_bytes": c_i64, "autovc_lstm2_bwd_persist_workspace_bytes": c_i64, "autovc_wino5_rows": c_i64, "autovc_wino5_bnstats_workspace_bytes": c_i64, "autovc_bnconv_workspace_floats": c_i64, "autovc_lstm_xcd_workspace_bytes": c_i64}
+             "autovc_lstm_persist_workspace_bytes": c_i64, "autovc_lstm2_bwd_persist_workspace_bytes": c_i64, "autovc_wino5_rows": c_i64, "autovc_wino5_bnstats_workspace_bytes": c_i64, "autovc_bnconv_bnstats_workspace_bytes": c_i64, "autovc_bnconv_workspace_floats": c_i64, "autovc_lstm_xcd_workspace_bytes": c_i64}
 
 
 def sig(name: str, *argtypes):
@@ -60,6 +60,9 @@ sig("autovc_bnconv_stats_rows", c_i64)
 sig("autovc_bnconv_workspace_floats", c_int, c_int, c_int, c_int)
 sig("autovc_bnconv_fwd_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int,
     c_ptr, c_ptr)
+sig("autovc_bnconv_bnstats_workspace_bytes", c_i64, c_int)
+sig("autovc_bnconv_fwd_bnstats_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_bnconv_dx_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int,
     c_ptr, c_ptr)
 sig("autovc_bnconv_dw_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int, c_ptr, c_ptr)

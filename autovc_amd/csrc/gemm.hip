@@ -30,6 +30,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "bn_finalize.h"
 #include "../../include/autovc_hip.h"
 
 namespace {
@@ -761,12 +762,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int64_t M, int64_t N
 // Block = 64 columns x 4 waves; wave w takes rows r0 + w, r0 + w + 4, ... of the block's
 // range (the loads of 4 rows in flight per thread), the 4 waves' sums are added in wave
 // order through LDS (deterministic).
-template <int MODE, int ACTP>
+// FUSE (MODE 1 only): the statistics finalized in this launch (avc::bn_stats_complete:
+// tickets tk, group partials gpart, outputs f), bit-identical to stats_finalize_raw_kernel
+template <int MODE, int ACTP, bool FUSE = false>
 __global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N, int splits,
                                                           const float* __restrict__ slab, float* __restrict__ C,
                                                           int64_t ldc, const float* __restrict__ bias,
                                                           const float* __restrict__ yp, const float* __restrict__ coefp,
-                                                          double* __restrict__ part) {
+                                                          double* __restrict__ part, int* __restrict__ tk = nullptr,
+                                                          double* __restrict__ gpart = nullptr,
+                                                          avc::BnFin f = avc::BnFin{}) {
   __shared__ double red[4][64][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 64 + lane;
@@ -802,8 +807,19 @@ __global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N,
   red[w][lane][1] = s2;
   __syncthreads();
   if (w == 0 && n < N) {
-    part[((int64_t)blockIdx.y * N + n) * 2 + 0] = ((red[0][lane][0] + red[1][lane][0]) + red[2][lane][0]) + red[3][lane][0];
-    part[((int64_t)blockIdx.y * N + n) * 2 + 1] = ((red[0][lane][1] + red[1][lane][1]) + red[2][lane][1]) + red[3][lane][1];
+    const double a = ((red[0][lane][0] + red[1][lane][0]) + red[2][lane][0]) + red[3][lane][0];
+    const double b = ((red[0][lane][1] + red[1][lane][1]) + red[2][lane][1]) + red[3][lane][1];
+    if constexpr (FUSE) {
+      avc::st_f64x2_sc1(part, ((int64_t)blockIdx.y * N + n) * 2, a, b);
+    } else {
+      part[((int64_t)blockIdx.y * N + n) * 2 + 0] = a;
+      part[((int64_t)blockIdx.y * N + n) * 2 + 1] = b;
+    }
+  }
+  if constexpr (FUSE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    avc::bn_stats_complete(tk, part, gpart, (int)N, blockIdx.x * 64, 64, blockIdx.y, gridDim.y, blockIdx.x, f);
   }
 }
 
@@ -1173,7 +1189,7 @@ constexpr int kStatsRows = 256;
 // (+ bias), 1 / 2: splitk_stats_kernel<mode> into part
 int bn_gemm(int bnop, int src, int a_trans, int b_trans, int M, int N, int K, Opnd oa, Opnd ob, float* C,
             const float* bias, int mode, const float* yp, const float* coefp, int actp, double* part, float* ws,
-            hipStream_t st) {
+            hipStream_t st, const avc::BnFin* fin = nullptr, int* tk = nullptr, double* gpart = nullptr) {
   const BnPlan pl = plan_bn(M, N, K);
   const dim3 grid((N + pl.cfg.bn - 1) / pl.cfg.bn, (M + pl.cfg.bm - 1) / pl.cfg.bm, pl.splits);
   g_batch = Batch{0, 0, 0, nullptr};
@@ -1202,7 +1218,10 @@ int bn_gemm(int bnop, int src, int a_trans, int b_trans, int M, int N, int K, Op
     const dim3 g2((N + 63) / 64, (unsigned)std::min<int64_t>(kStatsRows, M));
 #define AVC_STATS(MODE, ACT) hipLaunchKernelGGL((splitk_stats_kernel<MODE, ACT>), g2, dim3(256), 0, st, (int64_t)M, \
                                                (int64_t)N, pl.splits, ws, C, (int64_t)N, bias, yp, coefp, part)
-    if (mode == 1) AVC_STATS(1, 0);
+    if (mode == 1 && fin)
+      hipLaunchKernelGGL((splitk_stats_kernel<1, 0, true>), g2, dim3(256), 0, st, (int64_t)M, (int64_t)N, pl.splits, ws, C,
+                         (int64_t)N, bias, yp, coefp, part, tk, gpart, *fin);
+    else if (mode == 1) AVC_STATS(1, 0);
     else if (actp == 1) AVC_STATS(2, 1);
     else if (actp == 2) AVC_STATS(2, 2);
     else AVC_STATS(2, 0);
@@ -1244,6 +1263,36 @@ extern "C" int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const vo
   const Opnd ob{(const float*)Wf, 5 * Ci, 0, 0, 0, nullptr, 0};
   return bn_gemm(x_coef ? 1 : 0, src, 0, 0, M, Co, 5 * Ci, oa, ob, y, bias, 1, nullptr, nullptr, 0, part, workspace,
                  stream);
+}
+
+extern "C" int64_t autovc_bnconv_bnstats_workspace_bytes(int64_t M, int N) {
+  if (M <= 0 || N <= 0) return -1;
+  return (int64_t)avc::kBnTickets * 4 + (std::min<int64_t>(kStatsRows, M) + 16) * (int64_t)N * 16;
+}
+
+extern "C" int autovc_bnconv_fwd_bnstats_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef,
+                                                  int x_act, const void* Wf, const float* bias, float* y,
+                                                  const float* gamma, const float* beta, float eps, float* mean,
+                                                  float* var, float* coef, float* run_mean, float* run_var,
+                                                  float momentum, int64_t* nbt, void* stats_ws, int src,
+                                                  float* workspace, hipStream_t stream) {
+  static const char* fn = "autovc_bnconv_fwd_bnstats_bf16_f32";
+  AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && x && Wf && y && mean && var && coef && stats_ws && workspace,
+                "%s: bad args", fn);
+  AVC_CHECK_ARG(x_act >= 0 && x_act <= 2 && AVC_ALIGNED16(x) && AVC_ALIGNED16(Wf) && (!x_coef || AVC_ALIGNED16(x_coef)) &&
+                    AVC_ALIGNED16(stats_ws), "%s: activation / alignment", fn);
+  AVC_CHECK_ARG(bn_src_ok(src, Ci, Co) && !(x_coef && (src & 1)), "%s: bad src %d", fn, src);
+  AVC_CHECK_ARG(!x_coef || Ci <= kBnMaxC, "%s: BatchNorm input channels > %d", fn, kBnMaxC);
+  AVC_CHECK_ARG((Co + 63) / 64 <= avc::kBnTickets / 32, "%s: Co = %d above %d", fn, Co, 64 * avc::kBnTickets / 32);
+  const int M = B * T;
+  const Opnd oa{(const float*)x, Ci, T, Ci, -2, x_coef, x_act};
+  const Opnd ob{(const float*)Wf, 5 * Ci, 0, 0, 0, nullptr, 0};
+  int* tk = static_cast<int*>(stats_ws);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(stats_ws) + avc::kBnTickets * 4);
+  double* gpart = part + std::min<int64_t>(kStatsRows, M) * (int64_t)Co * 2;
+  const avc::BnFin f{gamma, beta, eps, mean, var, coef, run_mean, run_var, momentum, nbt, (int64_t)M};
+  return bn_gemm(x_coef ? 1 : 0, src, 0, 0, M, Co, 5 * Ci, oa, ob, y, bias, 1, nullptr, nullptr, 0, part, workspace,
+                 stream, &f, tk, gpart);
 }
 
 extern "C" int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* Wd, float* dz,

@@ -415,37 +415,8 @@ __global__ __launch_bounds__(kThreads) void wino_output_stats_kernel(int T, int 
 // arrivals per counter (a counter every block hits serialises: measured on the colsum).
 // Workspace (autovc_wino5_bnstats_workspace_bytes): tickets (zeroed once, left zeroed), RS
 // partial rows, 16 group partials.
-struct BnFin {
-  const float* gamma;
-  const float* beta;
-  float eps;
-  float* mean;
-  float* var;
-  float* coef;
-  float* run_mean;
-  float* run_var;
-  float momentum;
-  int64_t* nbt;
-  int64_t M;
-};
-
-constexpr int kBnTickets = 1024;              // ints: 16 per column block + 1 per column block
-
-__device__ __forceinline__ void st_f64x2_sc1(double* base, int64_t idx, double x, double y) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 w = {(unsigned)__double_as_longlong(x), (unsigned)((unsigned long long)__double_as_longlong(x) >> 32),
-                   (unsigned)__double_as_longlong(y), (unsigned)((unsigned long long)__double_as_longlong(y) >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, (uint32_t)(idx * 8), 0, 16);
-}
-__device__ __forceinline__ double2 ld_f64x2_sc1(const double* base, int64_t idx) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, 0x7fffffff,
-                                                                     0x00020000);
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(idx * 8), 0, 16));
-  return make_double2(__longlong_as_double((long long)(((unsigned long long)w[1] << 32) | w[0])),
-                      __longlong_as_double((long long)(((unsigned long long)w[3] << 32) | w[2])));
-}
+using avc::BnFin;
+using avc::kBnTickets;
 
 __global__ __launch_bounds__(kThreads) void wino_output_bnstats_kernel(int T, int C, const float* __restrict__ Yt,
                                                                   const float* __restrict__ bias, float* __restrict__ y,
@@ -480,7 +451,6 @@ __global__ __launch_bounds__(kThreads) void wino_output_bnstats_kernel(int T, in
   }
   // the block's partial row (block_pairs' fixed wave order), written through
   __shared__ double red[kWaves][64][8];
-  __shared__ int s_last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -499,57 +469,11 @@ __global__ __launch_bounds__(kThreads) void wino_output_bnstats_kernel(int T, in
       a8[e] = a;
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) st_f64x2_sc1(part, ((int64_t)rs * C + c + e) * 2, a8[2 * e], a8[2 * e + 1]);
+    for (int e = 0; e < 4; ++e) avc::st_f64x2_sc1(part, ((int64_t)rs * C + c + e) * 2, a8[2 * e], a8[2 * e + 1]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int g = rs & 15, ng = RS < 16 ? RS : 16;
-  if (threadIdx.x == 0) {
-    const int n_in = (RS - g + 15) / 16;
-    int* t1 = tk + cb * 16 + g;
-    const int old = __hip_atomic_fetch_add(t1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == n_in - 1;
-    if (s_last) __hip_atomic_store(t1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // row group g of this column block's 256 channels: thread t < 256 -> channel c0 + t
-  const int c0 = cb * 256, ch = c0 + (int)threadIdx.x;
-  if (threadIdx.x < 256 && ch < C) {
-    double a = 0.0, b = 0.0;
-    for (int q = g; q < RS; q += 16) {
-      const double2 v = ld_f64x2_sc1(part, ((int64_t)q * C + ch) * 2);
-      a += v.x;
-      b += v.y;
-    }
-    st_f64x2_sc1(gpart, ((int64_t)g * C + ch) * 2, a, b);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int* t2 = tk + kBnTickets / 2 + cb;
-    const int old = __hip_atomic_fetch_add(t2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == ng - 1;
-    if (s_last) __hip_atomic_store(t2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (cb == 0 && threadIdx.x == 0 && f.nbt) *f.nbt += 1;
-  if (threadIdx.x < 256 && ch < C) {
-    double a = 0.0, b = 0.0;
-    for (int q = 0; q < 16; ++q) {             // groups >= RS hold nothing: sum_partials adds 0.0 for them
-      if (q < ng) {
-        const double2 v = ld_f64x2_sc1(gpart, ((int64_t)q * C + ch) * 2);
-        a += v.x;
-        b += v.y;
-      } else {
-        a += 0.0;
-        b += 0.0;
-      }
-    }
-    avc::bn_finalize_channel(f.M, C, ch, a, b, f.gamma, f.beta, f.eps, f.mean, f.var, f.coef, f.run_mean, f.run_var,
-                             f.momentum);
-  }
+  avc::bn_stats_complete(tk, part, gpart, C, cb * 256, 256, rs, RS, cb, f);
 }
 
 // Input gradient of a conv whose input is the previous layer's BN + activation output:

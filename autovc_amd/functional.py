@@ -700,8 +700,9 @@ def conv_bn_act(x, conv, bn, act, residual=None):
 _CHAIN_ON = os.environ.get("AVC_CONV_CHAIN", "1") != "0"
 
 
-# the fp32 stacks' BatchNorm statistics finalized inside the output transform's launch
-# (autovc_wino5_output_bnstats_f32, bit-identical); AVC_BN_FUSED_STATS=0 keeps two launches
+# the stacks' BatchNorm statistics finalized inside the launch that reduces them (fp32:
+# autovc_wino5_output_bnstats_f32, bf16: autovc_bnconv_fwd_bnstats_bf16_f32; bit-identical);
+# AVC_BN_FUSED_STATS=0 keeps the separate finalize launch
 _BN_FUSED_STATS = os.environ.get("AVC_BN_FUSED_STATS", "0") != "0"
 
 
@@ -968,15 +969,23 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                 xin, xcoef, xact, src = zbs[-1], None, 0, 3
             else:
                 xin, xcoef, xact, src = ys[-1], coefs[-1], ACT[acts[l - 1]], 0
-            _lib.call("autovc_bnconv_fwd_bf16_f32", B, T, Ci, Co, xin.data_ptr(), _p(xcoef), xact, Wf.data_ptr(),
-                      _p(b), y.data_ptr(), part, src, ws, _s())
             coef = torch.empty((4, Co), device=dev, dtype=torch.float32)
-            if training:
+            if training and _BN_FUSED_STATS:   # the statistics finalized inside the reduce launch
+                mean = torch.empty(Co, device=dev, dtype=torch.float32)
+                var = torch.empty(Co, device=dev, dtype=torch.float32)
+                sws = _ws(dev, lib.autovc_bnconv_bnstats_workspace_bytes(M, Co), "chain_fwd_fused")
+                _lib.call("autovc_bnconv_fwd_bnstats_bf16_f32", B, T, Ci, Co, xin.data_ptr(), _p(xcoef), xact,
+                          Wf.data_ptr(), _p(b), y.data_ptr(), _p(g), _p(be), float(epss[l]), mean.data_ptr(),
+                          var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt), sws, src, ws, _s())
+            else:
+                _lib.call("autovc_bnconv_fwd_bf16_f32", B, T, Ci, Co, xin.data_ptr(), _p(xcoef), xact, Wf.data_ptr(),
+                          _p(b), y.data_ptr(), part, src, ws, _s())
+            if training and not _BN_FUSED_STATS:
                 mean = torch.empty(Co, device=dev, dtype=torch.float32)
                 var = torch.empty(Co, device=dev, dtype=torch.float32)
                 _lib.call("autovc_bn_finalize_f32", RS, M, Co, part, _p(g), _p(be), float(epss[l]), mean.data_ptr(),
                           var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt), _s())
-            else:
+            elif not training:
                 mean, var = rm, rv
                 _lib.call("autovc_bn_coef_f32", Co, rm.data_ptr(), rv.data_ptr(), _p(g), _p(be), float(epss[l]),
                           coef.data_ptr(), _s())

@@ -267,6 +267,15 @@ int64_t autovc_bnconv_workspace_floats(int B, int T, int Ci, int Co);
 int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef, int x_act,
                                const void* Wf, const float* bias, float* y, double* part, int src, float* workspace,
                                hipStream_t stream);
+/* autovc_bnconv_fwd_bf16_f32 + autovc_bn_finalize_f32 (train statistics), the finalize inside
+ * the reduce launch (bit-identical).  stats_ws: autovc_bnconv_bnstats_workspace_bytes(B*T, Co)
+ * bytes, ZEROED before its first use and left zeroed (its first 4 KB are tickets). */
+int64_t autovc_bnconv_bnstats_workspace_bytes(int64_t M, int N);
+int autovc_bnconv_fwd_bnstats_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef, int x_act,
+                                       const void* Wf, const float* bias, float* y, const float* gamma,
+                                       const float* beta, float eps, float* mean, float* var, float* coef,
+                                       float* run_mean, float* run_var, float momentum, int64_t* nbt, void* stats_ws,
+                                       int src, float* workspace, hipStream_t stream);
 int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* Wd, float* dz,
                               const float* y_prev, const float* coef_prev, int act_prev, double* part, int src,
                               float* workspace, hipStream_t stream);
