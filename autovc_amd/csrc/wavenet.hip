@@ -1961,8 +1961,8 @@ bool xcd_eligible(int B, int n_layers, int taps, int R, int G, int S) {
 }
 
 // All-CU weight-resident generation (wn_grid_kernel): 0 never, 1 every eligible batch, 2 (the
-// default) up to two utterances — the measured crossover: B = 1 86.5, B = 2 100.9 us per sample
-// step against 109.8 / 110.5 for the launches, B = 4 even (profiles/r04/wn_grid_ab.txt).
+// default) up to two utterances — the measured crossover: B = 1 86.5, B = 2 101.1 us per sample
+// step against 103.8 / 104.6 for the launches, B = 4 and up slower (profiles/r04/wn_grid_ab.txt).
 int g_wn_grid = [] { const char* e = getenv("AVC_WN_GRID"); return e ? atoi(e) : 2; }();
 
 template <int NB>
