@@ -51,6 +51,7 @@ sig("autovc_event_create", c_ptr)
 sig("autovc_event_destroy", c_ptr)
 sig("autovc_event_record_any", c_ptr, c_ptr)
 sig("autovc_stream_wait_event", c_ptr, c_ptr)
+sig("autovc_stamp", c_ptr, c_ptr)
 sig("autovc_gemm_bf16_splits", c_int, c_int, c_int, c_int)
 sig("autovc_gemm_batched_f32", c_int, c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_int, c_ptr, c_i64, c_i64, c_int,
     c_ptr, c_i64, c_i64, c_int, c_ptr)
@@ -115,6 +116,7 @@ sig("autovc_lstm2_fwd_timed_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_pt
 sig("autovc_lstm_fwd_timed_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64,
     c_ptr, c_ptr, c_ptr, ctypes.POINTER(c_f32))
 sig("autovc_lstm_bwd_workspace_floats", c_int, c_int, c_int)
+sig("autovc_lstm_bwd_set_fused", c_int)
 sig("autovc_lstm_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
     c_int, c_int, c_ptr, c_ptr)
 sig("autovc_lstm2_bwd_workspace_floats", c_int, c_int, c_int)

@@ -84,3 +84,20 @@ int autovc_stream_wait_event(hipStream_t stream, hipEvent_t ev) {
 }
 
 }  // extern "C"
+
+// ---- measurement: a one-thread kernel that stores the chip's 100 MHz clock when the stream
+// reaches it.  Unlike an event it is an ordinary kernel node inside a captured graph, so an
+// unprofiled replay can be time-stamped on several streams at once (tools/side_timeline.py).
+namespace {
+__global__ void stamp_kernel(unsigned long long* dst) {
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) dst[0] = t;
+}
+}  // namespace
+
+extern "C" int autovc_stamp(uint64_t* dst, hipStream_t stream) {
+  AVC_CHECK_ARG(dst != nullptr, "autovc_stamp: null destination");
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<unsigned long long*>(dst));
+  AVC_CHECK_LAUNCH("autovc_stamp");
+  return avc::kOk;
+}

@@ -22,6 +22,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "../../include/autovc_hip.h"
@@ -325,12 +326,25 @@ struct BwdArgs {
 // hipcc wait vmcnt(0) per load, serialising a dozen HBM round trips.
 // Thread = 4 consecutive units of one batch row (float4 loads / stores), grid (H/256, B)
 // of 64-thread blocks: no 64-bit index division, and the bf16 dG copy comes from registers.
-template <int S, bool FIRST, bool HAS_DH>
-__device__ __forceinline__ void bwd_pointwise_body(const BwdArgs& a, int t, int tp) {
+// 16-byte load through L2 only (sc1: the vector L1 is bypassed) — the partial slabs of the
+// fused backward below, written by other workgroups of the same launch with sc1 stores
+// (cdna_hip_programming.md §6 Guideline 16, the write-through counter form)
+__device__ __forceinline__ f32x4 ld4_sc1(const float* base, int64_t off) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(off * 4), 0, 16));
+}
+__device__ __forceinline__ void st4_sc1(float* base, int64_t off, f32x4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
+                                         (uint32_t)(off * 4), 0, 16);
+}
+
+// The pointwise pass of 4 consecutive units (b, j..j+3).  SC1: the partials were stored
+// write-through by other workgroups of the running launch and are read through L2.
+template <int S, bool FIRST, bool HAS_DH, bool SC1 = false>
+__device__ __forceinline__ void bwd_pointwise_elem(const BwdArgs& a, int t, int tp, int b, int j) {
   const int H = a.H;
-  const int j = 4 * (blockIdx.x * 64 + threadIdx.x);
-  if (j >= H) return;
-  const int b = blockIdx.y;
   const int64_t BH = (int64_t)a.B * H, bj = (int64_t)b * H + j;
   auto ld4 = [](const float* p) { return *reinterpret_cast<const f32x4*>(p); };
   const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H + j;
@@ -343,7 +357,7 @@ __device__ __forceinline__ void bwd_pointwise_body(const BwdArgs& a, int t, int 
   if (!FIRST) {
     dcs = ld4(a.dc_state + bj);
 #pragma unroll
-    for (int s = 0; s < S; ++s) p[s] = ld4(a.P + (int64_t)s * BH + bj);
+    for (int s = 0; s < S; ++s) p[s] = SC1 ? ld4_sc1(a.P, (int64_t)s * BH + bj) : ld4(a.P + (int64_t)s * BH + bj);
 #pragma unroll
     for (int s = 0; s < S; ++s) dh += p[s];
   }
@@ -373,6 +387,13 @@ __device__ __forceinline__ void bwd_pointwise_body(const BwdArgs& a, int t, int 
     *reinterpret_cast<bf16x4*>(db + 3 * H) = cv(dO);
   }
   *reinterpret_cast<f32x4*>(a.dc_state + bj) = dcn;
+}
+
+template <int S, bool FIRST, bool HAS_DH>
+__device__ __forceinline__ void bwd_pointwise_body(const BwdArgs& a, int t, int tp) {
+  const int j = 4 * (blockIdx.x * 64 + threadIdx.x);
+  if (j >= a.H) return;
+  bwd_pointwise_elem<S, FIRST, HAS_DH>(a, t, tp, blockIdx.y, j);
 }
 
 template <int S, bool FIRST, bool HAS_DH>
@@ -473,6 +494,126 @@ __global__ __launch_bounds__(64 * NW_) void lstm2_bwd_rec_kernel(int B, int T, i
   } else {
     if (t0 >= T) return;
     bwd_rec_body<KCH_, NW_, D_, BF>(B, T, H, dG0, t0, WT0, PQ0, j0);
+  }
+}
+
+// ---------------------------------------------------------------- fused backward step
+// One launch per backward step instead of a product launch + a pointwise launch: every
+// split-K job of an output tile (32 batch rows x 32 units) stores its partial write-through
+// (sc1), waits for its stores (vmcnt(0)), and one lane draws a ticket on the tile's counter
+// (relaxed agent-scope fetch_add); the job that draws the last ticket reads every partial of
+// the tile through L2 (sc1 loads) in slab order and runs the pointwise pass of the tile's
+// 32 x 32 (b, j) — the placement-independent counter hand-off of cdna_hip_programming.md
+// §6 Guideline 16 (its write-through form: no release or acquire fence).  The products, the
+// partial values, the order of the sums and the pointwise arithmetic are those of the
+// two-launch path, so dG is bit-identical to it (tests/test_lstm_bwd_fused_gpu.py).  The
+// grid keeps the product kernels' (x = column tile, y = row tile, z = split) layout with x
+// a multiple of 8, so a tile's jobs share blockIdx % 8 (one XCD under the observed
+// round-robin placement: speed only).  The counter is reset by the last arriver; the call
+// zeroes it once.
+struct FusedTile {
+  int* cnt;            // arrival counters, one per output tile (layer-1 tiles, then layer 0)
+};
+
+// the job's half of the hand-off: its 32 x 32 partial (waves 0..3 hold it after tile_gemm),
+// transposed through LDS so that each of 256 threads stores one 16-byte row piece
+// P[b][j0 + 4q .. +3] write-through; returns true in every thread of the last-arriving job
+__device__ __forceinline__ bool fused_arrive(float* smem, const f32x4& acc, bool zero, float* P, int B, int H,
+                                             int b0, int j0, int* cnt, int njobs) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __syncthreads();                                          // tile_gemm's LDS buffers are free
+  float* tile = smem;                                       // [32][33]
+  if (w < 4) {
+    const int wi = w >> 1, wn = w & 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      tile[(wi * 16 + 4 * (lane >> 4) + r) * (TN + 1) + wn * 16 + (lane & 15)] = zero ? 0.f : acc[r];
+  }
+  __syncthreads();
+  if (tid < 256) {
+    const int row = tid >> 3, q = tid & 7, b = b0 + row;
+    if (b < B) {
+      const float* src = tile + row * (TN + 1) + 4 * q;
+      const f32x4 v = {src[0], src[1], src[2], src[3]};
+      st4_sc1(P, (int64_t)b * H + j0 + 4 * q, v);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // this wave's partial is written through
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem + TB * (TN + 1));  // one LDS array only (no second __shared__)
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == njobs - 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next launch
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// the last arriver's pointwise pass: 256 threads x 4 units = the tile's 32 rows x 32 units
+template <int NP, bool HAS_DH>
+__device__ __forceinline__ void fused_pointwise(const BwdArgs& a, int t, int tp, int b0, int j0) {
+  const int tid = threadIdx.x;
+  if (tid >= 256) return;
+  const int b = b0 + (tid >> 3), j = j0 + 4 * (tid & 7);
+  if (b < a.B) bwd_pointwise_elem<NP, false, HAS_DH, true>(a, t, tp, b, j);
+}
+
+// single layer (decoder lstm1): grid (H/32, ceil(B/32), S); launch for processed step t
+// (products dG_t W_hh -> partials of step tn) runs the pointwise pass of step tn (previous
+// cell at tnp, -1 = none)
+template <int KCH_, int NW_, int D_, bool BF, int S, bool HAS_DH>
+__global__ __launch_bounds__(64 * NW_) void lstm_bwd_fused_kernel(BwdArgs a, const float* dG, int t, int tn, int tnp,
+                                                                 const float* WT, FusedTile f) {
+  using C = Tile<KCH_, NW_, D_>;
+  __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
+  const int B = a.B, T = a.T, H = a.H;
+  const int j0 = blockIdx.x * TN, b0 = blockIdx.y * TB, s = blockIdx.z;
+  const int K4 = BF ? 2 * H : 4 * H, ks = K4 / S, kb = s * ks;
+  auto arow_of = [&](int r) { return dG + ((int64_t)min(b0 + r, B - 1) * T + t) * K4 + kb; };
+  auto brow_of = [&](int r) { return WT + (int64_t)(j0 + r) * K4 + kb; };
+  const f32x4 acc = tile_gemm<KCH_, NW_, D_, BF>(smem, arow_of, brow_of, ks);
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (fused_arrive(smem, acc, false, a.P + (int64_t)s * B * H, B, H, b0, j0, f.cnt + tile, S))
+    fused_pointwise<S, HAS_DH>(a, tn, tnp, b0, j0);
+}
+
+// stacked pair (decoder lstm2): grid (3 H/32, ceil(B/32), S) as lstm2_bwd_rec_kernel's.
+// Launch for (t1, t0 = t1 + 1): layer-1 tiles (product 0, S jobs) finish layer 1's step
+// t1 - 1; layer-0 tiles (products 2 and 1: 2S jobs, slab order = the two-launch path's) finish
+// layer 0's step t1.  t0 = T: product 2 has no step and contributes zero slabs; t1 = 0: the
+// layer-1 jobs have nothing left to finish and exit.
+template <int KCH_, int NW_, int D_, bool BF, int S>
+__global__ __launch_bounds__(64 * NW_) void lstm2_bwd_fused_kernel(BwdArgs a1, BwdArgs a0, const float* dG1,
+                                                                  const float* dG0, int t1, int t0,
+                                                                  const float* WT1, const float* WIT1,
+                                                                  const float* WT0, FusedTile f) {
+  using C = Tile<KCH_, NW_, D_>;
+  __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
+  const int B = a1.B, T = a1.T, H = a1.H;
+  const int nt = H / TN, prod = blockIdx.x / nt, ct = blockIdx.x % nt, j0 = ct * TN;
+  const int b0 = blockIdx.y * TB, s = blockIdx.z;
+  if (prod == 0 && t1 == 0) return;
+  const int K4 = BF ? 2 * H : 4 * H, ks = K4 / S, kb = s * ks;
+  const float* dG = prod == 2 ? dG0 : dG1;
+  const int t = prod == 2 ? t0 : t1;
+  const float* WT = prod == 0 ? WT1 : (prod == 1 ? WIT1 : WT0);
+  const bool none = t >= T;                                  // product 2 of the first launch
+  auto arow_of = [&](int r) { return dG + ((int64_t)min(b0 + r, B - 1) * T + min(t, T - 1)) * K4 + kb; };
+  auto brow_of = [&](int r) { return WT + (int64_t)(j0 + r) * K4 + kb; };
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (!none) acc = tile_gemm<KCH_, NW_, D_, BF>(smem, arow_of, brow_of, ks);
+  const int64_t slab = (int64_t)B * H;
+  const int ntile = gridDim.y * nt, tile = blockIdx.y * nt + ct;
+  if (prod == 0) {
+    if (fused_arrive(smem, acc, false, a1.P + s * slab, B, H, b0, j0, f.cnt + tile, S))
+      fused_pointwise<S, true>(a1, t1 - 1, t1 - 2, b0, j0);
+  } else {
+    // layer 0's slabs: [S of its own recurrence (product 2) | S of dG1 W_ih1 (product 1)]
+    float* P = a0.P + (prod == 2 ? s : S + s) * slab;
+    if (fused_arrive(smem, acc, none, P, B, H, b0, j0, f.cnt + ntile + tile, 2 * S))
+      fused_pointwise<2 * S, false>(a0, t1, t1 - 1, b0, j0);
   }
 }
 
@@ -770,6 +911,57 @@ __global__ __launch_bounds__(kThreads) void blstm_bwd_kernel(int B, int T, const
 
 bool lstm_shape_ok(int B, int H) { return B > 0 && H > 0 && H % 64 == 0; }
 
+// the fused backward step (one launch per step) is the default; AVC_LSTM_BWD_FUSED=0 or
+// autovc_lstm_bwd_set_fused(0) selects the product + pointwise launch pair (A/B and the
+// bit-identity test); set_fused(-1) returns to the environment's choice
+int g_bwd_fused = -1;
+bool bwd_fused() {
+  static const bool env = [] {
+    const char* e = getenv("AVC_LSTM_BWD_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return g_bwd_fused < 0 ? env : g_bwd_fused != 0;
+}
+
+int64_t ceil4(int64_t n) { return (n + 3) / 4 * 4; }
+int64_t bwd_tiles(int B, int H) { return (int64_t)((B + TB - 1) / TB) * (H / TN); }
+
+template <bool BF, int S>
+void launch_lstm_fused_s(hipStream_t st, const BwdArgs& a, const float* dG, int t, int tn, int tnp, const float* WT,
+                         FusedTile f) {
+  const dim3 grid(a.H / TN, (a.B + TB - 1) / TB, S);
+  if (a.dh_out)
+    hipLaunchKernelGGL((lstm_bwd_fused_kernel<KCH, NWV, DPF, BF, S, true>), grid, dim3(64 * NWV), 0, st, a, dG, t, tn,
+                       tnp, WT, f);
+  else
+    hipLaunchKernelGGL((lstm_bwd_fused_kernel<KCH, NWV, DPF, BF, S, false>), grid, dim3(64 * NWV), 0, st, a, dG, t, tn,
+                       tnp, WT, f);
+}
+
+template <bool BF>
+void launch_lstm_fused(hipStream_t st, const BwdArgs& a, const float* dG, int t, int tn, int tnp, const float* WT,
+                       FusedTile f) {
+  switch (a.S) {
+    case 1: launch_lstm_fused_s<BF, 1>(st, a, dG, t, tn, tnp, WT, f); break;
+    case 2: launch_lstm_fused_s<BF, 2>(st, a, dG, t, tn, tnp, WT, f); break;
+    case 4: launch_lstm_fused_s<BF, 4>(st, a, dG, t, tn, tnp, WT, f); break;
+    default: launch_lstm_fused_s<BF, 8>(st, a, dG, t, tn, tnp, WT, f); break;
+  }
+}
+
+template <bool BF>
+void launch_lstm2_fused(hipStream_t st, int S, const BwdArgs& a1, const BwdArgs& a0, const float* dG1,
+                        const float* dG0, int t1, int t0, const float* w1, const float* wi, const float* w0,
+                        FusedTile f) {
+  const dim3 grid(3 * a1.H / TN, (a1.B + TB - 1) / TB, S);
+  if (S == 4)
+    hipLaunchKernelGGL((lstm2_bwd_fused_kernel<KCH, NWV, DPF, BF, 4>), grid, dim3(64 * NWV), 0, st, a1, a0, dG1, dG0,
+                       t1, t0, w1, wi, w0, f);
+  else
+    hipLaunchKernelGGL((lstm2_bwd_fused_kernel<KCH, NWV, DPF, BF, 2>), grid, dim3(64 * NWV), 0, st, a1, a0, dG1, dG0,
+                       t1, t0, w1, wi, w0, f);
+}
+
 // k-chunk of the tile GEMM: the tuned KCH when it divides K, else 64
 template <int ABL = 0>
 void launch_fwd_step(dim3 grid, hipStream_t st, const StepArgs& a, int t, int tp) {
@@ -819,9 +1011,46 @@ extern "C" int autovc_lstm2_fwd_f32(int B, int T, int H, const float* gx0, int64
   return avc::kOk;
 }
 
+// [S partial slabs | dc carry | fused-step tile counters]
 extern "C" int64_t autovc_lstm_bwd_workspace_floats(int B, int H, int splits) {
-  return (int64_t)splits * B * H + (int64_t)B * H;
+  return (int64_t)splits * B * H + (int64_t)B * H + ceil4(bwd_tiles(B, H));
 }
+
+extern "C" int autovc_lstm_bwd_set_fused(int on) {
+  AVC_CHECK_ARG(on >= -1 && on <= 1, "autovc_lstm_bwd_set_fused: -1, 0 or 1");
+  g_bwd_fused = on;
+  return avc::kOk;
+}
+
+namespace {
+// the backward steps of one large-H layer in processing order: the first pointwise pass, then
+// per step either one fused launch or the product + pointwise pair
+template <bool BF>
+int lstm_bwd_steps(const BwdArgs& a, int reverse, const float* dGsrc, const float* WT, float* workspace,
+                   hipStream_t stream, const char* fn) {
+  const int B = a.B, T = a.T, H = a.H;
+  const bool fused = bwd_fused();
+  FusedTile f{reinterpret_cast<int*>(workspace + (int64_t)(a.S + 1) * B * H)};
+  if (fused && T > 1) AVC_HIP(avc::zero_async(f.cnt, 4 * ceil4(bwd_tiles(B, H)), stream), fn);
+  const int64_t BH = (int64_t)B * H;
+  const int pw_blocks = (int)((BH + 255) / 256);
+  const dim3 rgrid(H / TN, (B + TB - 1) / TB, a.S);
+  auto step_t = [&](int s) { return reverse ? T - 1 - s : s; };
+  auto step_tp = [&](int s) { return s == 0 ? -1 : (reverse ? step_t(s) + 1 : step_t(s) - 1); };
+  for (int s = T - 1; s >= 0; --s) {
+    const int t = step_t(s);
+    if (!fused || s == T - 1) launch_pointwise_any(pw_blocks, stream, a, t, step_tp(s), s == T - 1);
+    if (s == 0) continue;
+    if (fused)
+      launch_lstm_fused<BF>(stream, a, dGsrc, t, step_t(s - 1), step_tp(s - 1), WT, f);
+    else
+      hipLaunchKernelGGL((lstm_bwd_rec_kernel<KCH, NWV, DPF, BF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H, dGsrc,
+                         t, WT, a.P);
+  }
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+}  // namespace
 
 extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
                                    const float* gates, const float* c_all, const float* W_hh_T, float* dG,
@@ -836,29 +1065,59 @@ extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int
   float* P = workspace;
   float* dcs = workspace + (int64_t)splits * B * H;
   BwdArgs a{B, T, H, dh_out, d_ldb, d_ldt, gates, c_all, dG, dcs, P, splits};
-  const int64_t BH = (int64_t)B * H;
-  const int pw_blocks = (int)((BH + 255) / 256);
-  const dim3 rgrid(H / TN, (B + TB - 1) / TB, splits);
-  for (int s = T - 1; s >= 0; --s) {
-    const int t = reverse ? T - 1 - s : s;
-    const int tp = s == 0 ? -1 : (reverse ? t + 1 : t - 1);
-    const int first = s == T - 1;
-    launch_pointwise_any(pw_blocks, stream, a, t, tp, first);
-    if (s == 0) continue;
-    if ((4 * H / splits) % KCH == 0)
-      hipLaunchKernelGGL((lstm_bwd_rec_kernel<KCH, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
-                         (const float*)dG, t, W_hh_T, P);
-    else
-      hipLaunchKernelGGL((lstm_bwd_rec_kernel<64, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
-                         (const float*)dG, t, W_hh_T, P);
-  }
-  AVC_CHECK_LAUNCH("autovc_lstm_bwd_f32");
-  return avc::kOk;
+  return lstm_bwd_steps<false>(a, reverse, dG, W_hh_T, workspace, stream, "autovc_lstm_bwd_f32");
 }
 
+// [P1: S slabs | PQ0: 2S slabs | dc carry layer 1 | dc carry layer 0 | fused-step tile counters]
 extern "C" int64_t autovc_lstm2_bwd_workspace_floats(int B, int H, int splits) {
-  return (int64_t)(3 * splits + 2) * B * H;
+  return (int64_t)(3 * splits + 2) * B * H + ceil4(2 * bwd_tiles(B, H));
 }
+
+namespace {
+// the stacked backward wavefront: launch pair s = 0..T of autovc_lstm2_bwd_f32, or (fused)
+// the first pointwise pass and T fused launches
+template <bool BF>
+int lstm2_bwd_steps(const BwdArgs& a1, const BwdArgs& a0, int splits, const float* d1, const float* d0,
+                    const float* w1, const float* wi, const float* w0, float* workspace, hipStream_t stream,
+                    const char* fn) {
+  const int B = a1.B, T = a1.T, H = a1.H;
+  const int64_t BH = (int64_t)B * H;
+  const bool wide = splits == 8;
+  const bool fused = bwd_fused() && !wide;
+  float* dcs0 = workspace + (int64_t)(3 * splits + 1) * BH;
+  FusedTile f{reinterpret_cast<int*>(workspace + (int64_t)(3 * splits + 2) * BH)};
+  if (fused) {
+    // layer 0's carried cell gradient and the tile counters (contiguous); product 2 of the
+    // first launch writes zero slabs itself
+    AVC_HIP(avc::zero_async(dcs0, 4 * (BH + ceil4(2 * bwd_tiles(B, H))), stream), fn);
+  } else {
+    // layer 0's first processed step has no recurrent partials and no carried cell gradient
+    AVC_HIP(avc::zero_async(a0.P, sizeof(float) * splits * BH, stream), fn);
+    AVC_HIP(avc::zero_async(dcs0, sizeof(float) * BH, stream), fn);
+  }
+  const dim3 pgrid((H / 4 + 63) / 64, B, 2);
+  const dim3 rgrid = wide ? dim3(3 * H / TNW, (B + TBW - 1) / TBW, splits) : dim3(3 * H / TN, (B + TB - 1) / TB, splits);
+  for (int s = 0; s <= T; ++s) {
+    const int t1 = T - 1 - s, t0 = T - s;
+    if (!fused || s == 0) {
+      if (splits == 8) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<8>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+      else if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+      else hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<2>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
+    }
+    if (s == T) break;
+    if (fused)
+      launch_lstm2_fused<BF>(stream, splits, a1, a0, d1, d0, t1, t0, w1, wi, w0, f);
+    else if (wide)
+      hipLaunchKernelGGL((lstm2_bwd_rec_wide_kernel<KCH, DPF, BF>), rgrid, dim3(512), 0, stream, B, T, H, d1, d0, t1,
+                         t0, w1, wi, w0, a1.P, a0.P);
+    else
+      hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF, BF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H, d1, d0,
+                         t1, t0, w1, wi, w0, a1.P, a0.P);
+  }
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+}  // namespace
 
 // Backward of two stacked layers (decoder lstm2) as a one-step-lagged wavefront, the
 // mirror of autovc_lstm2_fwd_f32: launch pair s = 0..T runs layer 1 at t1 = T-1-s and
@@ -884,30 +1143,11 @@ extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, i
   float* PQ0 = P1 + splits * BH;            // [S slabs of layer 0's recurrence | S slabs of dG1 W_ih1]
   float* dcs1 = PQ0 + 2 * splits * BH;
   float* dcs0 = dcs1 + BH;
-  // layer 0's first processed step has no recurrent partials and no carried cell gradient
-  AVC_HIP(avc::zero_async(PQ0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_f32");
-  AVC_HIP(avc::zero_async(dcs0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_f32");
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits};
-  const dim3 pgrid((H / 4 + 63) / 64, B, 2);
-  // splits 8: the wide-tile products (64 x 64 per workgroup); 2 / 4: 32 x 32 tiles
-  const bool wide = splits == 8;
-  const dim3 rgrid = wide ? dim3(3 * H / TNW, (B + TBW - 1) / TBW, splits) : dim3(3 * H / TN, (B + TB - 1) / TB, splits);
-  for (int s = 0; s <= T; ++s) {
-    const int t1 = T - 1 - s, t0 = T - s;
-    if (splits == 8) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<8>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
-    else if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
-    else hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<2>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
-    if (s == T) break;
-    if (wide)
-      hipLaunchKernelGGL((lstm2_bwd_rec_wide_kernel<KCH, DPF>), rgrid, dim3(512), 0, stream, B, T, H,
-                         (const float*)dG1, (const float*)dG0, t1, t0, W_hh1_T, W_ih1_T, W_hh0_T, P1, PQ0);
-    else
-      hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
-                         (const float*)dG1, (const float*)dG0, t1, t0, W_hh1_T, W_ih1_T, W_hh0_T, P1, PQ0);
-  }
-  AVC_CHECK_LAUNCH("autovc_lstm2_bwd_f32");
-  return avc::kOk;
+  // splits 8: the wide-tile products (64 x 64 per workgroup, never fused); 2 / 4: 32 x 32 tiles
+  return lstm2_bwd_steps<false>(a1, a0, splits, dG1, dG0, W_hh1_T, W_ih1_T, W_hh0_T, workspace, stream,
+                                "autovc_lstm2_bwd_f32");
 }
 
 extern "C" int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
@@ -1038,19 +1278,8 @@ extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, in
   float* P = workspace;
   float* dcs = workspace + (int64_t)splits * B * H;
   BwdArgs a{B, T, H, dh_out, d_ldb, d_ldt, gates, c_all, dG, dcs, P, splits, reinterpret_cast<__bf16*>(dG_b)};
-  const int64_t BH = (int64_t)B * H;
-  const int pw_blocks = (int)((BH + 255) / 256);
-  const dim3 rgrid(H / TN, (B + TB - 1) / TB, splits);
-  for (int s = T - 1; s >= 0; --s) {
-    const int t = reverse ? T - 1 - s : s;
-    const int tp = s == 0 ? -1 : (reverse ? t + 1 : t - 1);
-    launch_pointwise_any(pw_blocks, stream, a, t, tp, s == T - 1);
-    if (s == 0) continue;
-    hipLaunchKernelGGL((lstm_bwd_rec_kernel<KCH, NWV, DPF, true>), rgrid, dim3(64 * NWV), 0, stream, B, T, H,
-                       reinterpret_cast<const float*>(dG_b), t, reinterpret_cast<const float*>(W_hh_T_b), P);
-  }
-  AVC_CHECK_LAUNCH("autovc_lstm_bwd_bf16");
-  return avc::kOk;
+  return lstm_bwd_steps<true>(a, reverse, reinterpret_cast<const float*>(dG_b), reinterpret_cast<const float*>(W_hh_T_b),
+                              workspace, stream, "autovc_lstm_bwd_bf16");
 }
 
 // autovc_lstm2_bwd_f32 with the recurrent products on bf16 copies (precision "bf16"): the
@@ -1075,33 +1304,12 @@ extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, 
   float* PQ0 = P1 + splits * BH;
   float* dcs1 = PQ0 + 2 * splits * BH;
   float* dcs0 = dcs1 + BH;
-  AVC_HIP(avc::zero_async(PQ0, sizeof(float) * splits * BH, stream), "autovc_lstm2_bwd_bf16");
-  AVC_HIP(avc::zero_async(dcs0, sizeof(float) * BH, stream), "autovc_lstm2_bwd_bf16");
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits, reinterpret_cast<__bf16*>(dG1_b)};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits, reinterpret_cast<__bf16*>(dG0_b)};
-  const dim3 pgrid((H / 4 + 63) / 64, B, 2);
-  const bool wide = splits == 8;
-  const dim3 rgrid = wide ? dim3(3 * H / TNW, (B + TBW - 1) / TBW, splits) : dim3(3 * H / TN, (B + TB - 1) / TB, splits);
-  const float* d1 = reinterpret_cast<const float*>(dG1_b);
-  const float* d0 = reinterpret_cast<const float*>(dG0_b);
-  const float* w1 = reinterpret_cast<const float*>(W_hh1_T_b);
-  const float* wi = reinterpret_cast<const float*>(W_ih1_T_b);
-  const float* w0 = reinterpret_cast<const float*>(W_hh0_T_b);
-  for (int s = 0; s <= T; ++s) {
-    const int t1 = T - 1 - s, t0 = T - s;
-    if (splits == 8) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<8>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
-    else if (splits == 4) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<4>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
-    else hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<2>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
-    if (s == T) break;
-    if (wide)
-      hipLaunchKernelGGL((lstm2_bwd_rec_wide_kernel<KCH, DPF, true>), rgrid, dim3(512), 0, stream, B, T, H, d1, d0,
-                         t1, t0, w1, wi, w0, P1, PQ0);
-    else
-      hipLaunchKernelGGL((lstm2_bwd_rec_kernel<KCH, NWV, DPF, true>), rgrid, dim3(64 * NWV), 0, stream, B, T, H, d1,
-                         d0, t1, t0, w1, wi, w0, P1, PQ0);
-  }
-  AVC_CHECK_LAUNCH("autovc_lstm2_bwd_bf16");
-  return avc::kOk;
+  return lstm2_bwd_steps<true>(a1, a0, splits, reinterpret_cast<const float*>(dG1_b),
+                               reinterpret_cast<const float*>(dG0_b), reinterpret_cast<const float*>(W_hh1_T_b),
+                               reinterpret_cast<const float*>(W_ih1_T_b), reinterpret_cast<const float*>(W_hh0_T_b),
+                               workspace, stream, "autovc_lstm2_bwd_bf16");
 }
 
 // The product's decoder-lstm2 launch (autovc_lstm2_fwd_f32's two-layer wavefront) with every

@@ -114,6 +114,11 @@ int autovc_event_create(hipEvent_t* out);
 int autovc_event_destroy(hipEvent_t ev);
 int autovc_event_record_any(hipEvent_t ev, hipStream_t stream);
 int autovc_stream_wait_event(hipStream_t stream, hipEvent_t ev);
+/* Measurement only (no reference counterpart): a one-thread kernel that stores the chip's
+ * 100 MHz s_memrealtime clock into *dst when `stream` reaches it — a kernel node inside a
+ * captured graph, so a replay's streams can be time-stamped without a tracer (which
+ * serialises them). */
+int autovc_stamp(uint64_t* dst, hipStream_t stream);
 /* Same contract, bf16 compute (BASELINE config 3, "bf16 with fp32 master"): the fp32
  * operands are rounded to bf16 (RNE) as they are staged, v_mfma_f32_32x32x16_bf16
  * accumulates in fp32, C / bias / accumulate stay fp32 — the numerics of a torch.autocast
@@ -421,6 +426,13 @@ int autovc_lstm_fwd_timed_f32(int B, int T, int H, const float* gx, int64_t gx_l
                               int64_t h_ldt, float* c_all, float* gates, hipStream_t stream,
                               float* avg_us);
 int64_t autovc_lstm_bwd_workspace_floats(int B, int H, int splits);
+/* The large-H backward steps (autovc_lstm_bwd_f32 / _bf16, autovc_lstm2_bwd_f32 / _bf16 at
+ * splits 2 / 4) run ONE launch per step by default: the split-K product jobs of each
+ * 32 x 32 output tile hand their partials over write-through and the last to arrive runs
+ * the tile's pointwise cell backward (bit-identical to the product + pointwise launch
+ * pair).  on = 0 selects the launch pair, 1 the fused step, -1 the environment's choice
+ * (AVC_LSTM_BWD_FUSED=0: the pair).  A/B and test hook; no reference counterpart. */
+int autovc_lstm_bwd_set_fused(int on);
 int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
                         const float* gates, const float* c_all, const float* W_hh_T, float* dG,
                         int reverse, int splits, float* workspace, hipStream_t stream);
