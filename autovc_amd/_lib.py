@@ -29,7 +29,7 @@ _RESTYPES = {"autovc_last_error": ctypes.c_char_p,
              "autovc_lstm_bwd_workspace_floats": c_i64, "autovc_lstm2_bwd_workspace_floats": c_i64, "autovc_loss_workspace_bytes": c_i64,
              "autovc_colsum_workspace_floats": c_i64, "autovc_wavenet_packed_floats": c_i64, "autovc_wavenet_ring_frames": c_i64,
              "autovc_wavenet_workspace_bytes": c_i64, "autovc_lstm2_persist_workspace_bytes": c_i64,
-             "autovc_lstm_persist_workspace_bytes": c_i64, "autovc_lstm2_bwd_persist_workspace_bytes": c_i64, "autovc_wino5_rows": c_i64, "autovc_wino5_bnstats_workspace_bytes": c_i64, "autovc_bnconv_bnstats_workspace_bytes": c_i64, "autovc_bnconv_workspace_floats": c_i64, "autovc_lstm_xcd_workspace_bytes": c_i64}
+             "autovc_lstm_persist_workspace_bytes": c_i64, "autovc_wino5_rows": c_i64, "autovc_bnconv_workspace_floats": c_i64, "autovc_lstm_xcd_workspace_bytes": c_i64}
 
 
 def sig(name: str, *argtypes):
@@ -61,9 +61,6 @@ sig("autovc_bnconv_stats_rows", c_i64)
 sig("autovc_bnconv_workspace_floats", c_int, c_int, c_int, c_int)
 sig("autovc_bnconv_fwd_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int,
     c_ptr, c_ptr)
-sig("autovc_bnconv_bnstats_workspace_bytes", c_i64, c_int)
-sig("autovc_bnconv_fwd_bnstats_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
-    c_ptr, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_bnconv_dx_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int,
     c_ptr, c_ptr)
 sig("autovc_bnconv_dw_bf16_f32", c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int, c_ptr, c_ptr)
@@ -76,9 +73,6 @@ sig("autovc_wino5_wgrad_f32", c_int, c_int, c_ptr, c_ptr, c_int, c_ptr)
 sig("autovc_wino5_rows", c_int, c_int)
 sig("autovc_wino5_input_bn_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_wino5_output_stats_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr)
-sig("autovc_wino5_bnstats_workspace_bytes", c_int, c_int, c_int)
-sig("autovc_wino5_output_bnstats_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_f32, c_ptr,
-    c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_ptr, c_ptr, c_ptr)
 sig("autovc_wino5_output_bnbwd_f32", c_int, c_int, c_int, c_ptr, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_i64, c_ptr,
     c_ptr)
 sig("autovc_wino5_bnbwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
@@ -122,6 +116,14 @@ sig("autovc_lstm_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_pt
 sig("autovc_lstm2_bwd_workspace_floats", c_int, c_int, c_int)
 sig("autovc_lstm2_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
+sig("autovc_lstm2_bwd_range_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr, c_ptr, c_ptr, c_int, c_int, c_int, c_ptr, c_ptr)
+sig("autovc_lstm2_bwd_range_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int, c_int, c_ptr, c_ptr)
+sig("autovc_gemm_tchunk_f32", c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_int, c_ptr, c_i64,
+    c_int, c_int, c_ptr, c_ptr)
+sig("autovc_gemm_tchunk_bf16_f32", c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_int, c_ptr,
+    c_i64, c_int, c_int, c_ptr, c_ptr)
 sig("autovc_lstm2_persist_workspace_bytes", c_int, c_int, c_int)
 sig("autovc_lstm2_persist_supported", c_int, c_int)
 sig("autovc_lstm2_fwd_persist_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
@@ -131,7 +133,6 @@ sig("autovc_fault_status", c_ptr, c_int, c_ptr)
 sig("autovc_lstm_persist_set_timeout_ticks", c_int)
 sig("autovc_lstm_xcd_supported", c_int, c_int)
 sig("autovc_lstm_xcd_workspace_bytes")
-sig("autovc_lstm_bwd_xcd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_lstm_fwd_xcd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_ptr,
     c_ptr, c_ptr)
 sig("autovc_lstm_fwd_xcd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr,
@@ -139,12 +140,6 @@ sig("autovc_lstm_fwd_xcd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, 
 sig("autovc_lstm2_fwd_persist_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_lstm_persist_workspace_bytes", c_int, c_int, c_int)
-sig("autovc_lstm2_bwd_persist_supported", c_int, c_int)
-sig("autovc_lstm2_bwd_persist_workspace_bytes", c_int, c_int, c_int)
-sig("autovc_lstm2_bwd_persist_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-    c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
-sig("autovc_lstm2_bwd_persist_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-    c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_lstm_persist_supported", c_int, c_int)
 sig("autovc_lstm_fwd_persist_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_ptr,
     c_ptr, c_ptr)
@@ -177,10 +172,9 @@ sig("autovc_l2norm_rows_f32", c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_ptr)
 sig("autovc_colsum_workspace_floats", c_int)
 sig("autovc_colsum_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
 sig("autovc_wavenet_packed_floats", c_int, c_int, c_int, c_int, c_int, c_int)
-sig("autovc_wavenet_set_xcd", c_int)
-sig("autovc_wavenet_get_xcd")
 sig("autovc_wavenet_set_grid", c_int)
 sig("autovc_wavenet_get_grid")
+sig("autovc_wavenet_last_path")
 sig("autovc_wavenet_grid_diag", c_int, c_ptr)
 sig("autovc_wavenet_set_timeout_ticks", c_int)
 sig("autovc_wavenet_fault", c_int, c_ptr)

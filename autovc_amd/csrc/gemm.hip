@@ -30,7 +30,6 @@
 #include <cstdlib>
 
 #include "common.h"
-#include "bn_finalize.h"
 #include "../../include/autovc_hip.h"
 
 namespace {
@@ -43,6 +42,12 @@ struct Opnd {
   // element = act(coef[c] x + coef[C + c]) for a frame inside its sequence, else 0
   const float* coef;
   int act;
+  // time-chunked K (CK operands only, seg_len > 0): the K rows are (sequence b, step t) pairs of
+  // an NTC activation with seg_T steps per sequence, restricted to steps [seg_t0, seg_t0 +
+  // seg_len) of every sequence — logical row k is memory row (k / seg_len) * seg_T +
+  // seg_t0 + k % seg_len; a conv mask then sees step seg_t0 + k % seg_len.  The weight
+  // gradient of one time chunk of an LSTM layer.
+  int seg_len = 0, seg_T = 0, seg_t0 = 0;
 };
 
 // the fused Conv-BN stacks' transform of a stored pre-BN value (bn.hip apply_kernel's fmaf).
@@ -162,6 +167,7 @@ struct OpTile {
   bool rok[PER];            // RK: row inside the operand
   int tpos[PER];            // conv: frame position in its sequence (RK: fixed; CK: advancing)
   int kpos[PER];            // CK: frame index of the slot
+  int tseg[PER];            // CK, time-chunked K: the slot's step inside its chunk
   int kk;                   // RK: k of the thread's slots
   int tap, kmod;            // conv: RK: k / C, k % C (advancing); CK: q / C (fixed)
   int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
@@ -196,8 +202,14 @@ struct OpTile {
         }
       } else {
         kpos[i] = (int)k;
-        off[i] = (uint32_t)((((k + shift) * o.ld) + r) * EB);
-        if (o.conv_T > 0) tpos[i] = (int)(k % o.conv_T);
+        int64_t row = k;
+        if (o.seg_len > 0) {
+          const int64_t sb = k / o.seg_len;
+          tseg[i] = (int)(k - sb * o.seg_len);
+          row = sb * o.seg_T + o.seg_t0 + tseg[i];
+        }
+        off[i] = (uint32_t)((((row + shift) * o.ld) + r) * EB);
+        if (o.conv_T > 0) tpos[i] = o.seg_len > 0 ? o.seg_t0 + tseg[i] : (int)(k % o.conv_T);
         if (i == 0) {
           rowok = r < R;
           if (o.conv_T > 0) tap = (int)(r / o.conv_C);
@@ -257,7 +269,14 @@ struct OpTile {
         dst[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
         off[i] += (uint32_t)(BK * o.ld * EB);
         kpos[i] += BK;
-        if (o.conv_T > 0) {   // (frame + BK) % T with the uniform BK % T
+        if (o.seg_len > 0) {  // time-chunked K: skip the steps outside the chunk
+          tseg[i] += BK;
+          while (tseg[i] >= o.seg_len) {
+            tseg[i] -= o.seg_len;
+            off[i] += (uint32_t)((int64_t)(o.seg_T - o.seg_len) * o.ld * EB);
+          }
+          if (o.conv_T > 0) tpos[i] = o.seg_t0 + tseg[i];
+        } else if (o.conv_T > 0) {   // (frame + BK) % T with the uniform BK % T
           tpos[i] += step_r;
           if (tpos[i] >= o.conv_T) tpos[i] -= o.conv_T;
         }
@@ -762,16 +781,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int64_t M, int64_t N
 // Block = 64 columns x 4 waves; wave w takes rows r0 + w, r0 + w + 4, ... of the block's
 // range (the loads of 4 rows in flight per thread), the 4 waves' sums are added in wave
 // order through LDS (deterministic).
-// FUSE (MODE 1 only): the statistics finalized in this launch (avc::bn_stats_complete:
-// tickets tk, group partials gpart, outputs f), bit-identical to stats_finalize_raw_kernel
-template <int MODE, int ACTP, bool FUSE = false>
+template <int MODE, int ACTP>
 __global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N, int splits,
                                                           const float* __restrict__ slab, float* __restrict__ C,
                                                           int64_t ldc, const float* __restrict__ bias,
                                                           const float* __restrict__ yp, const float* __restrict__ coefp,
-                                                          double* __restrict__ part, int* __restrict__ tk = nullptr,
-                                                          double* __restrict__ gpart = nullptr,
-                                                          avc::BnFin f = avc::BnFin{}) {
+                                                          double* __restrict__ part) {
   __shared__ double red[4][64][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 64 + lane;
@@ -809,17 +824,8 @@ __global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N,
   if (w == 0 && n < N) {
     const double a = ((red[0][lane][0] + red[1][lane][0]) + red[2][lane][0]) + red[3][lane][0];
     const double b = ((red[0][lane][1] + red[1][lane][1]) + red[2][lane][1]) + red[3][lane][1];
-    if constexpr (FUSE) {
-      avc::st_f64x2_sc1(part, ((int64_t)blockIdx.y * N + n) * 2, a, b);
-    } else {
-      part[((int64_t)blockIdx.y * N + n) * 2 + 0] = a;
-      part[((int64_t)blockIdx.y * N + n) * 2 + 1] = b;
-    }
-  }
-  if constexpr (FUSE) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    avc::bn_stats_complete(tk, part, gpart, (int)N, blockIdx.x * 64, 64, blockIdx.y, gridDim.y, blockIdx.x, f);
+    part[((int64_t)blockIdx.y * N + n) * 2 + 0] = a;
+    part[((int64_t)blockIdx.y * N + n) * 2 + 1] = b;
   }
 }
 
@@ -1051,11 +1057,13 @@ extern "C" int64_t autovc_gemm_workspace_floats(int M, int N, int splits) {
   return splits > 1 ? kTickets + (int64_t)splits * ((M + 255) / 256 * 256) * ((N + 255) / 256 * 256) : 0;
 }
 
+// seg (seg_len > 0): time-chunked K for both operands (CK, Opnd::seg_len)
 static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c_bs, int M, int N, int K,
                                const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
                                const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                float* C, int64_t ldc, const float* bias1, const float* bias2,
-                               int accumulate, int splits, float* workspace, hipStream_t stream) {
+                               int accumulate, int splits, float* workspace, hipStream_t stream,
+                               int seg_len = 0, int seg_T = 0, int seg_t0 = 0) {
   AVC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "autovc_gemm: negative dims");
   if (M == 0 || N == 0) return avc::kOk;
   AVC_CHECK_ARG(A && B && C, "autovc_gemm: null operand");
@@ -1108,8 +1116,8 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   splits = (int)((K + kps - 1) / kps);
   if (splits < 1) splits = 1;
   AVC_CHECK_ARG(splits == 1 || workspace, "autovc_gemm_f32: split-K needs a workspace");
-  Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0};
-  Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0};
+  Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0, nullptr, 0, seg_len, seg_T, seg_t0};
+  Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0, nullptr, 0, seg_len, seg_T, seg_t0};
   const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, batch > 1 ? batch : splits);
   const bool fixup = splits > 1 && g_fixup && (int64_t)grid.x * grid.y <= kTickets;
   float* slab = splits > 1 ? workspace + kTickets : nullptr;
@@ -1148,6 +1156,34 @@ extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
                                     int accumulate, int splits, float* workspace, hipStream_t stream) {
   return gemm_impl(true, 1, 0, 0, 0, M, N, K, A, lda, a_trans, a_conv_T, a_conv_C, a_tap0, B, ldb, b_trans, b_conv_T,
                    b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
+}
+
+// Weight gradient of one time chunk (steps [t0, t0 + Tc) of each of B sequences of T steps):
+//   C[M,N] (+)= sum_b sum_t A[(b T + t) lda + m] * Bm[(b T + t + b_tap0) ldb + n]
+// (the Bm term is zero where t + b_tap0 < 0; b_tap0 = -1: the previous step's h).  Both
+// operands K-strided (CK), K = B * Tc; splits / workspace as autovc_gemm_f32.
+static int gemm_tchunk(bool bf16, int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
+                       const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate, int splits,
+                       float* workspace, hipStream_t stream) {
+  AVC_CHECK_ARG(B > 0 && T > 0 && Tc > 0 && t0 >= 0 && t0 + Tc <= T && (b_tap0 == 0 || b_tap0 == -1),
+                "autovc_gemm_tchunk: bad chunk B=%d T=%d t0=%d Tc=%d tap0=%d", B, T, t0, Tc, b_tap0);
+  AVC_CHECK_ARG(A && Bm, "autovc_gemm_tchunk: null operand");
+  AVC_CHECK_ARG(4 * ((int64_t)B * T + 2) * std::max(lda, ldb) < (int64_t)kOOB, "autovc_gemm_tchunk: operands >= 2 GiB");
+  return gemm_impl(bf16, 1, 0, 0, 0, M, N, B * Tc, A, lda, 1, 0, 0, 0, Bm, ldb,
+                   1, b_tap0 ? T : 0, b_tap0 ? N : 0, b_tap0, C, ldc, nullptr, nullptr, accumulate, splits, workspace,
+                   stream, Tc, T, t0);
+}
+
+extern "C" int autovc_gemm_tchunk_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
+                                      const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate,
+                                      int splits, float* workspace, hipStream_t stream) {
+  return gemm_tchunk(false, M, N, B, T, t0, Tc, A, lda, Bm, ldb, b_tap0, C, ldc, accumulate, splits, workspace, stream);
+}
+
+extern "C" int autovc_gemm_tchunk_bf16_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
+                                           const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc,
+                                           int accumulate, int splits, float* workspace, hipStream_t stream) {
+  return gemm_tchunk(true, M, N, B, T, t0, Tc, A, lda, Bm, ldb, b_tap0, C, ldc, accumulate, splits, workspace, stream);
 }
 
 extern "C" int autovc_gemm_bf16_splits(int M, int N, int K, int requested) {
@@ -1189,7 +1225,7 @@ constexpr int kStatsRows = 256;
 // (+ bias), 1 / 2: splitk_stats_kernel<mode> into part
 int bn_gemm(int bnop, int src, int a_trans, int b_trans, int M, int N, int K, Opnd oa, Opnd ob, float* C,
             const float* bias, int mode, const float* yp, const float* coefp, int actp, double* part, float* ws,
-            hipStream_t st, const avc::BnFin* fin = nullptr, int* tk = nullptr, double* gpart = nullptr) {
+            hipStream_t st) {
   const BnPlan pl = plan_bn(M, N, K);
   const dim3 grid((N + pl.cfg.bn - 1) / pl.cfg.bn, (M + pl.cfg.bm - 1) / pl.cfg.bm, pl.splits);
   g_batch = Batch{0, 0, 0, nullptr};
@@ -1218,10 +1254,7 @@ int bn_gemm(int bnop, int src, int a_trans, int b_trans, int M, int N, int K, Op
     const dim3 g2((N + 63) / 64, (unsigned)std::min<int64_t>(kStatsRows, M));
 #define AVC_STATS(MODE, ACT) hipLaunchKernelGGL((splitk_stats_kernel<MODE, ACT>), g2, dim3(256), 0, st, (int64_t)M, \
                                                (int64_t)N, pl.splits, ws, C, (int64_t)N, bias, yp, coefp, part)
-    if (mode == 1 && fin)
-      hipLaunchKernelGGL((splitk_stats_kernel<1, 0, true>), g2, dim3(256), 0, st, (int64_t)M, (int64_t)N, pl.splits, ws, C,
-                         (int64_t)N, bias, yp, coefp, part, tk, gpart, *fin);
-    else if (mode == 1) AVC_STATS(1, 0);
+    if (mode == 1) AVC_STATS(1, 0);
     else if (actp == 1) AVC_STATS(2, 1);
     else if (actp == 2) AVC_STATS(2, 2);
     else AVC_STATS(2, 0);
@@ -1263,36 +1296,6 @@ extern "C" int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const vo
   const Opnd ob{(const float*)Wf, 5 * Ci, 0, 0, 0, nullptr, 0};
   return bn_gemm(x_coef ? 1 : 0, src, 0, 0, M, Co, 5 * Ci, oa, ob, y, bias, 1, nullptr, nullptr, 0, part, workspace,
                  stream);
-}
-
-extern "C" int64_t autovc_bnconv_bnstats_workspace_bytes(int64_t M, int N) {
-  if (M <= 0 || N <= 0) return -1;
-  return (int64_t)avc::kBnTickets * 4 + (std::min<int64_t>(kStatsRows, M) + 16) * (int64_t)N * 16;
-}
-
-extern "C" int autovc_bnconv_fwd_bnstats_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef,
-                                                  int x_act, const void* Wf, const float* bias, float* y,
-                                                  const float* gamma, const float* beta, float eps, float* mean,
-                                                  float* var, float* coef, float* run_mean, float* run_var,
-                                                  float momentum, int64_t* nbt, void* stats_ws, int src,
-                                                  float* workspace, hipStream_t stream) {
-  static const char* fn = "autovc_bnconv_fwd_bnstats_bf16_f32";
-  AVC_CHECK_ARG(bn_dims_ok(B, T, Ci, Co) && x && Wf && y && mean && var && coef && stats_ws && workspace,
-                "%s: bad args", fn);
-  AVC_CHECK_ARG(x_act >= 0 && x_act <= 2 && AVC_ALIGNED16(x) && AVC_ALIGNED16(Wf) && (!x_coef || AVC_ALIGNED16(x_coef)) &&
-                    AVC_ALIGNED16(stats_ws), "%s: activation / alignment", fn);
-  AVC_CHECK_ARG(bn_src_ok(src, Ci, Co) && !(x_coef && (src & 1)), "%s: bad src %d", fn, src);
-  AVC_CHECK_ARG(!x_coef || Ci <= kBnMaxC, "%s: BatchNorm input channels > %d", fn, kBnMaxC);
-  AVC_CHECK_ARG((Co + 63) / 64 <= avc::kBnTickets / 32, "%s: Co = %d above %d", fn, Co, 64 * avc::kBnTickets / 32);
-  const int M = B * T;
-  const Opnd oa{(const float*)x, Ci, T, Ci, -2, x_coef, x_act};
-  const Opnd ob{(const float*)Wf, 5 * Ci, 0, 0, 0, nullptr, 0};
-  int* tk = static_cast<int*>(stats_ws);
-  double* part = reinterpret_cast<double*>(static_cast<char*>(stats_ws) + avc::kBnTickets * 4);
-  double* gpart = part + std::min<int64_t>(kStatsRows, M) * (int64_t)Co * 2;
-  const avc::BnFin f{gamma, beta, eps, mean, var, coef, run_mean, run_var, momentum, nbt, (int64_t)M};
-  return bn_gemm(x_coef ? 1 : 0, src, 0, 0, M, Co, 5 * Ci, oa, ob, y, bias, 1, nullptr, nullptr, 0, part, workspace,
-                 stream, &f, tk, gpart);
 }
 
 extern "C" int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* Wd, float* dz,

@@ -340,22 +340,45 @@ __device__ __forceinline__ void st4_sc1(float* base, int64_t off, f32x4 v) {
                                          (uint32_t)(off * 4), 0, 16);
 }
 
-// The pointwise pass of 4 consecutive units (b, j..j+3).  SC1: the partials were stored
-// write-through by other workgroups of the running launch and are read through L2.
-template <int S, bool FIRST, bool HAS_DH, bool SC1 = false>
-__device__ __forceinline__ void bwd_pointwise_elem(const BwdArgs& a, int t, int tp, int b, int j) {
+// The pointwise pass of 4 consecutive units (b, j..j+3), in two halves: pw_load issues the
+// loads that do not depend on this step's partials (saved gates and cells, dh from above, the
+// carried cell gradient), pw_finish reads the S partials, sums them after dh in slab order and
+// writes dG (and its bf16 copy) and the new carry.  SC1: the partials were stored write-through
+// by other workgroups of the running launch and are read through L2.
+struct PwIn {
+  f32x4 i, f, g, o, cc, cpr, dh, dcs;
+};
+
+template <bool FIRST, bool HAS_DH>
+__device__ __forceinline__ PwIn pw_load(const BwdArgs& a, int t, int tp, int b, int j) {
+  const int H = a.H;
+  auto ld4 = [](const float* p) { return *reinterpret_cast<const f32x4*>(p); };
+  const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H + j;
+  PwIn in;
+  in.i = ld4(gs); in.f = ld4(gs + H); in.g = ld4(gs + 2 * H); in.o = ld4(gs + 3 * H);
+  in.cc = ld4(a.c + ((int64_t)b * a.T + t) * H + j);
+  in.cpr = ld4(a.c + ((int64_t)b * a.T + (tp >= 0 ? tp : t)) * H + j);
+  in.dh = f32x4{0.f, 0.f, 0.f, 0.f};
+  in.dcs = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (HAS_DH) in.dh = ld4(a.dh_out + (int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j);
+  if (!FIRST) in.dcs = ld4(a.dc_state + (int64_t)b * H + j);
+  return in;
+}
+
+// Contraction off: the fused step and the launch pair inline this into different code, and
+// with mul-add fusion left to the compiler they rounded layer 0's cell gradient differently
+// (1 ulp); spelled out, both paths are bit-identical.
+template <int S, bool FIRST, bool SC1>
+__device__ __forceinline__ void pw_finish(const BwdArgs& a, const PwIn& in, int t, int tp, int b, int j) {
+#pragma clang fp contract(off)
   const int H = a.H;
   const int64_t BH = (int64_t)a.B * H, bj = (int64_t)b * H + j;
   auto ld4 = [](const float* p) { return *reinterpret_cast<const f32x4*>(p); };
-  const float* gs = a.gates + ((int64_t)b * a.T + t) * 4 * H + j;
-  const f32x4 i_ = ld4(gs), f_ = ld4(gs + H), g_ = ld4(gs + 2 * H), o_ = ld4(gs + 3 * H);
-  const f32x4 cc = ld4(a.c + ((int64_t)b * a.T + t) * H + j);
-  const f32x4 cpr = ld4(a.c + ((int64_t)b * a.T + (tp >= 0 ? tp : t)) * H + j);
-  f32x4 dh = {0.f, 0.f, 0.f, 0.f}, dcs = {0.f, 0.f, 0.f, 0.f};
-  if (HAS_DH) dh = ld4(a.dh_out + (int64_t)b * a.d_ldb + (int64_t)t * a.d_ldt + j);
+  f32x4 dh = in.dh;
+  const f32x4 dcs = in.dcs;
+  const f32x4 i_ = in.i, f_ = in.f, g_ = in.g, o_ = in.o, cc = in.cc, cpr = in.cpr;
   f32x4 p[S];
   if (!FIRST) {
-    dcs = ld4(a.dc_state + bj);
 #pragma unroll
     for (int s = 0; s < S; ++s) p[s] = SC1 ? ld4_sc1(a.P, (int64_t)s * BH + bj) : ld4(a.P + (int64_t)s * BH + bj);
 #pragma unroll
@@ -387,6 +410,12 @@ __device__ __forceinline__ void bwd_pointwise_elem(const BwdArgs& a, int t, int 
     *reinterpret_cast<bf16x4*>(db + 3 * H) = cv(dO);
   }
   *reinterpret_cast<f32x4*>(a.dc_state + bj) = dcn;
+}
+
+template <int S, bool FIRST, bool HAS_DH, bool SC1 = false>
+__device__ __forceinline__ void bwd_pointwise_elem(const BwdArgs& a, int t, int tp, int b, int j) {
+  const PwIn in = pw_load<FIRST, HAS_DH>(a, t, tp, b, j);
+  pw_finish<S, FIRST, SC1>(a, in, t, tp, b, j);
 }
 
 template <int S, bool FIRST, bool HAS_DH>
@@ -551,7 +580,10 @@ __device__ __forceinline__ bool fused_arrive(float* smem, const f32x4& acc, bool
   return *flag != 0;
 }
 
-// the last arriver's pointwise pass: 256 threads x 4 units = the tile's 32 rows x 32 units
+// the last arriver's pointwise pass: 256 threads x 4 units = the tile's 32 rows x 32 units.
+// (Issuing the partial-independent loads in every job before its hand-off, so that they
+// arrive under the write-through and the ticket, measured slower: the non-last jobs' extra
+// fill cost more than the tail it hid — lstm2 23.07 vs 22.36 us per step, lstm1 8.13 vs 7.52.)
 template <int NP, bool HAS_DH>
 __device__ __forceinline__ void fused_pointwise(const BwdArgs& a, int t, int tp, int b0, int j0) {
   const int tid = threadIdx.x;
@@ -1076,17 +1108,24 @@ extern "C" int64_t autovc_lstm2_bwd_workspace_floats(int B, int H, int splits) {
 namespace {
 // the stacked backward wavefront: launch pair s = 0..T of autovc_lstm2_bwd_f32, or (fused)
 // the first pointwise pass and T fused launches
+// s_begin / s_end: the wavefront iterations s (0..T) to issue — a call split into ranges runs
+// the same launches as one call (autovc_lstm2_bwd_range_*: the weight gradients of each
+// finished time chunk can start between them)
 template <bool BF>
 int lstm2_bwd_steps(const BwdArgs& a1, const BwdArgs& a0, int splits, const float* d1, const float* d0,
                     const float* w1, const float* wi, const float* w0, float* workspace, hipStream_t stream,
-                    const char* fn) {
+                    const char* fn, int s_begin = 0, int s_end = -1) {
   const int B = a1.B, T = a1.T, H = a1.H;
+  if (s_end < 0) s_end = T + 1;
+  AVC_CHECK_ARG(0 <= s_begin && s_begin <= s_end && s_end <= T + 1, "%s: bad step range [%d, %d) for T=%d", fn,
+                s_begin, s_end, T);
   const int64_t BH = (int64_t)B * H;
   const bool wide = splits == 8;
   const bool fused = bwd_fused() && !wide;
   float* dcs0 = workspace + (int64_t)(3 * splits + 1) * BH;
   FusedTile f{reinterpret_cast<int*>(workspace + (int64_t)(3 * splits + 2) * BH)};
-  if (fused) {
+  if (s_begin > 0) {
+  } else if (fused) {
     // layer 0's carried cell gradient and the tile counters (contiguous); product 2 of the
     // first launch writes zero slabs itself
     AVC_HIP(avc::zero_async(dcs0, 4 * (BH + ceil4(2 * bwd_tiles(B, H))), stream), fn);
@@ -1097,7 +1136,7 @@ int lstm2_bwd_steps(const BwdArgs& a1, const BwdArgs& a0, int splits, const floa
   }
   const dim3 pgrid((H / 4 + 63) / 64, B, 2);
   const dim3 rgrid = wide ? dim3(3 * H / TNW, (B + TBW - 1) / TBW, splits) : dim3(3 * H / TN, (B + TB - 1) / TB, splits);
-  for (int s = 0; s <= T; ++s) {
+  for (int s = s_begin; s < s_end; ++s) {
     const int t1 = T - 1 - s, t0 = T - s;
     if (!fused || s == 0) {
       if (splits == 8) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<8>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
@@ -1125,10 +1164,11 @@ int lstm2_bwd_steps(const BwdArgs& a1, const BwdArgs& a0, int splits, const floa
 // product of the recurrent launch instead of a GEMM over all frames after layer 1 ends,
 // and layer 0 starts one step behind layer 1 instead of T steps.  Same per-element sums
 // as the unstacked path except that layer 0's dh_t adds its 2S partials in one order.
-extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                    const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                    const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
-                                    float* dG0, int splits, float* workspace, hipStream_t stream) {
+extern "C" int autovc_lstm2_bwd_range_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                          const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                          const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T,
+                                          float* dG1, float* dG0, int splits, int s_begin, int s_end,
+                                          float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H), "autovc_lstm2_bwd_f32: bad dims");
   AVC_CHECK_ARG((splits == 2 || splits == 4 || splits == 8) && (4 * H) % (KCH * splits) == 0 &&
                     (splits < 8 || H % TNW == 0),
@@ -1147,7 +1187,15 @@ extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, i
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits};
   // splits 8: the wide-tile products (64 x 64 per workgroup, never fused); 2 / 4: 32 x 32 tiles
   return lstm2_bwd_steps<false>(a1, a0, splits, dG1, dG0, W_hh1_T, W_ih1_T, W_hh0_T, workspace, stream,
-                                "autovc_lstm2_bwd_f32");
+                                "autovc_lstm2_bwd_f32", s_begin, s_end);
+}
+
+extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                    const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                    const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
+                                    float* dG0, int splits, float* workspace, hipStream_t stream) {
+  return autovc_lstm2_bwd_range_f32(B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, gates0, c0, W_hh1_T, W_ih1_T, W_hh0_T,
+                                    dG1, dG0, splits, 0, T + 1, workspace, stream);
 }
 
 extern "C" int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
@@ -1285,11 +1333,12 @@ extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, in
 // autovc_lstm2_bwd_f32 with the recurrent products on bf16 copies (precision "bf16"): the
 // pointwise passes also write dG1_b / dG0_b, which the next launch's products read; W*T_b are
 // RNE bf16 copies of the (H, 4H) transposes.  Cell backward, dG, partials fp32.
-extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                     const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                     const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
-                                     float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits,
-                                     float* workspace, hipStream_t stream) {
+extern "C" int autovc_lstm2_bwd_range_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                           const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                           const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b,
+                                           const uint16_t* W_hh0_T_b, float* dG1, uint16_t* dG1_b, float* dG0,
+                                           uint16_t* dG0_b, int splits, int s_begin, int s_end, float* workspace,
+                                           hipStream_t stream) {
   AVC_CHECK_ARG(T > 0 && bf16_shape_ok(B, H), "autovc_lstm2_bwd_bf16: bad dims");
   AVC_CHECK_ARG((splits == 2 || splits == 4 || splits == 8) && (2 * H) % (KCH * splits) == 0 &&
                     (splits < 8 || H % TNW == 0),
@@ -1309,7 +1358,16 @@ extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, 
   return lstm2_bwd_steps<true>(a1, a0, splits, reinterpret_cast<const float*>(dG1_b),
                                reinterpret_cast<const float*>(dG0_b), reinterpret_cast<const float*>(W_hh1_T_b),
                                reinterpret_cast<const float*>(W_ih1_T_b), reinterpret_cast<const float*>(W_hh0_T_b),
-                               workspace, stream, "autovc_lstm2_bwd_bf16");
+                               workspace, stream, "autovc_lstm2_bwd_bf16", s_begin, s_end);
+}
+
+extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                     const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                     const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
+                                     float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits,
+                                     float* workspace, hipStream_t stream) {
+  return autovc_lstm2_bwd_range_bf16(B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, gates0, c0, W_hh1_T_b, W_ih1_T_b,
+                                     W_hh0_T_b, dG1, dG1_b, dG0, dG0_b, splits, 0, T + 1, workspace, stream);
 }
 
 // The product's decoder-lstm2 launch (autovc_lstm2_fwd_f32's two-layer wavefront) with every

@@ -188,7 +188,6 @@ __device__ __forceinline__ bool grid_wait(const PArgs& a, int xcc, int* status, 
 __device__ int g_avc_fault = 0;
 constexpr int kFaultLstm2Persist = 1;    // lstm_persist_kernel, two layers (decoder lstm2 forward)
 constexpr int kFaultLstmXcdFwd = 2;      // lstm_xcd_fwd_kernel (decoder lstm1 forward)
-constexpr int kFaultLstmXcdBwd = 4;      // lstm_xcd_bwd_kernel (decoder lstm1 backward, opt-in)
 constexpr int kFaultLstm1Persist = 8;    // lstm_persist_kernel, one layer (opt-in)
 int g_timeout_ticks = 0;             // 0 = the default 1 s; tests force a timeout with a tiny value
 
@@ -1404,174 +1403,6 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
   }
 }
 
-// Backward of the same layer (BPTT, reverse time), same XCD split: slot s owns units
-// 16s .. 16s+15 of the group's 8 rows — the cells whose dG it writes and the columns of the
-// recurrent product dh_rec(t) = dG_{t+1} W_hh (K = 4H = 2048) it reduces.  W_hh's 16 columns
-// stay in registers (A fragments: 16 units x 4 k); each wave takes a quarter of K and streams
-// its B fragments (dG_{t+1} rows of the group, written by the 32 slots of the XCD) straight
-// from L2 with sc1 loads, one chunk ahead of its MFMAs; the 4 partial tiles are summed in LDS
-// in fixed order, then the pointwise pass (lstm.hip bwd_pointwise_body's arithmetic).
-struct XBArgs {
-  int B, T;
-  const float* dh;           // dh_out (b*d_ldb + t*d_ldt), may be null
-  int64_t d_ldb, d_ldt;
-  const float* gates;        // (B,T,4H) i, f, g, o
-  const float* c;            // (B,T,H)
-  const float* W;            // W_hh (4H, H)
-  float* dG;                 // (B,T,4H)
-  int* bar;
-  int timeout_ticks;
-};
-
-template <int HH>
-__global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
-  constexpr int U = HH / XSL;            // units per slot (16)
-  constexpr int K4 = 4 * HH;             // recurrent K
-  constexpr int KW = K4 / 4;             // k per wave
-  constexpr int KG = KW / 4;             // k per MFMA lane group (consecutive)
-  static_assert(U == 16, "tile shape");
-  static_assert(4 * U * (XRB + 1) * 4 + 4 * (XRB + 1) * (KW + 4) * 4 <= XC_PAD_LDS, "LDS budget");
-  constexpr int SS = KW + 4;             // LDS row stride of a wave's slab (bank spread)
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* part = lds;                      // [4 waves][U][XRB + 1]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* slab = lds + 4 * U * (XRB + 1) + wave * (XRB + 1) * SS;   // this wave's [XRB + 1][SS], row XRB = 0
-  __shared__ int s_info[3];
-  const int T = a.T;
-  if (tid == 0) {
-    unsigned x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    const int xcc = (int)(x & 15);
-    const int slot = add_rlx(a.bar + (XC_CENSUS + xcc) * L, 1);
-    s_info[0] = xcc;
-    s_info[1] = slot;
-    s_info[2] = (xcc < XNX && slot < XSL) ? 0 : 1;
-    if (s_info[2]) st_rlx(a.bar + XC_ERR * L, 1);
-  }
-  for (int i = lane; i < SS; i += 64) slab[XRB * SS + i] = 0.f;
-  __syncthreads();
-  const int xcc = s_info[0] < XNX ? s_info[0] : 0, slot = s_info[1] < XSL ? s_info[1] : 0;
-  const int r0 = XRB * xcc, u0 = U * slot;
-  const int cb = tid >> 4, cu = tid & 15;
-  const bool cown = tid < XRB * U;
-  const int64_t cell0 = (int64_t)(r0 + cb) * T;     // (b, t) row base of this cell's batch row
-  auto fail = [&]() {
-    const float nan = __builtin_nanf("");
-    if (cown)
-      for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a.dG[(cell0 + t) * K4 + q * HH + u0 + cu] = nan;
-    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdBwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  if (s_info[2]) {
-    if (s_info[0] < XNX && s_info[1] < XSL) fail();
-    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdBwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // A fragments: lane -> unit u0 + lane % 16, k = KW wave + KG (lane / 16) + q: W_hh[k][unit]
-  const int kbase = KW * wave + KG * (lane >> 4);
-  float wf[KG];
-#pragma unroll
-  for (int q = 0; q < KG; ++q) wf[q] = a.W[(int64_t)(kbase + q) * HH + u0 + (lane & 15)];
-  const bool bvalid = (lane & 15) < XRB;
-  const float* brow_lds = slab + (bvalid ? (lane & 15) : XRB) * SS + KG * (lane >> 4);
-  // pointwise operands of step t (prefetched one step ahead)
-  f32x4 gt = {0.f, 0.f, 0.f, 0.f};
-  float cc = 0.f, cpv = 0.f, dho = 0.f, dcs = 0.f;
-  auto load_pw = [&](int t) {
-    const float* g = a.gates + (cell0 + t) * K4 + u0 + cu;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) gt[q] = g[q * HH];
-    cc = a.c[(cell0 + t) * HH + u0 + cu];
-    cpv = t > 0 ? a.c[(cell0 + t - 1) * HH + u0 + cu] : 0.f;
-    dho = a.dh ? a.dh[(int64_t)(r0 + cb) * a.d_ldb + (int64_t)t * a.d_ldt + u0 + cu] : 0.f;
-  };
-  if (cown) load_pw(T - 1);
-  int* step_ctr = a.bar + (XC_STEP + xcc) * L;
-  for (int s = 0; s < T; ++s) {
-    const int t = T - 1 - s;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (s > 0) {
-      // ---- XCD barrier: all 32 slots stored dG_{t+1}
-      if (tid == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        int ok = 1;
-        while (ld_rlx(step_ctr) < XSL * s) {
-          __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout_ticks || ld_rlx(a.bar + XC_ERR * L)) {
-            st_rlx(a.bar + XC_ERR * L, 1);
-            ok = 0;
-            break;
-          }
-        }
-        s_info[2] = ok ? 0 : 1;
-      }
-      __syncthreads();
-      if (s_info[2]) {
-        fail();
-        return;
-      }
-      // ---- this wave's K quarter of the group's dG_{t+1} rows -> its LDS slab: coalesced sc1
-      // loads (whole lines: L1 is bypassed, so scattered 16-B B-fragment loads would re-fetch
-      // every line 4-8 times), then the products dh_rec = dG_{t+1} W_hh from LDS
-      {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            a.dG + ((int64_t)r0 * T + t + 1) * K4 + KW * wave, (short)0, 0x7fffffff, 0x00020000);
-        constexpr int NL = XRB * KW / 4 / 64;            // b128 loads per lane (16)
-        f32x4 v[NL];
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-          const int ci = i * 64 + lane, row = ci / (KW / 4), k4 = ci % (KW / 4);
-          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               r, (uint32_t)(((int64_t)row * T * K4 + 4 * k4) * 4), 0, 16));
-        }
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-          const int ci = i * 64 + lane, row = ci / (KW / 4), k4 = ci % (KW / 4);
-          *reinterpret_cast<f32x4*>(slab + row * SS + 4 * k4) = v[i];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-      }
-#pragma unroll
-      for (int q = 0; q < KG; q += 4) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(brow_lds + q);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q], bv[0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 1], bv[1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 2], bv[2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 3], bv[3], acc, 0, 0, 0);
-      }
-    }
-    // C[unit 4 (lane / 16) + r][batch lane % 16]: the 4 waves' K quarters, summed in order
-    if (bvalid)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) part[(wave * U + 4 * (lane >> 4) + r) * (XRB + 1) + (lane & 15)] = acc[r];
-    __syncthreads();
-    float dgo[4];
-    if (cown) {
-      const float dh = dho + (((part[(0 * U + cu) * (XRB + 1) + cb] + part[(1 * U + cu) * (XRB + 1) + cb]) +
-                               part[(2 * U + cu) * (XRB + 1) + cb]) + part[(3 * U + cu) * (XRB + 1) + cb]);
-      const float i_ = gt[0], f_ = gt[1], g_ = gt[2], o_ = gt[3];
-      const float tc = tanhf(cc);
-      const float dc = dcs + dh * o_ * (1.f - tc * tc);
-      dgo[0] = dc * g_ * i_ * (1.f - i_);
-      dgo[1] = dc * cpv * f_ * (1.f - f_);
-      dgo[2] = dc * i_ * (1.f - g_ * g_);
-      dgo[3] = dh * tc * o_ * (1.f - o_);
-      dcs = dc * f_;
-      float* d = a.dG + (cell0 + t) * K4 + u0 + cu;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) d[q * HH] = dgo[q];
-    }
-    if (s + 1 < T) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) add_l2(step_ctr, 1);
-      if (cown) load_pw(t - 1);
-    }
-  }
-}
-
 int g_xcd_ok = -1;
 
 bool xcd_fits() {
@@ -1586,390 +1417,11 @@ bool xcd_fits() {
                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_fwd_kernel<512, false>, XNT, lb) == hipSuccess &&
                per >= 1 &&
                hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_fwd_kernel<512, true>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_bwd_kernel<512>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
-               hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_bwd_kernel<512>, XNT, lb) == hipSuccess &&
-               per >= 1;
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess;
   }
   return g_xcd_ok == 1;
 }
 
-
-// ---------------------------------------------------------------------------------------
-// Decoder lstm2 BACKWARD (BPTT of nn.LSTM(512, 1024, 2), model_vc_mel.py:104,118) as ONE
-// persistent, weight-stationary launch: the mirror of lstm_persist_kernel for the stacked
-// backward wavefront of autovc_lstm2_bwd_f32 (iteration s = 0..T: layer 1 at t1 = T-1-s,
-// layer 0 at t0 = T-s).  Per iteration three products contract over K = 4H gate rows:
-//   P1 = dG1_{t1+1} W_hh1  (layer 1's recurrent dh),  Q = dG1_{t0} W_ih1  (layer 0's dh from
-//   above),  P0 = dG0_{t0+1} W_hh0  (layer 0's recurrent dh)        [dG1_{t1+1} = dG1_{t0}]
-// The per-step launches re-stream the three (4H x H) weights (48 MB fp32) every step; here
-// the 256 workgroups (one per CU) split (units x K): XCD x holds unit groups jb = 4x .. 4x+3
-// (32 units each) and each group's 8 workgroups own one K slice kb of 512 gate rows, so a
-// workgroup keeps its 3 x (512 x 32) weight slices in VGPRs for the whole sequence and per
-// iteration reads only its K slice of the two dG rows (64 x 512 each).  Its 8 waves each
-// take 64 of the 512 k (v_mfma_f32_16x16x4_f32, or 16x16x32 bf16 on the bf16 copies), their
-// partial tiles summed through LDS in wave order; the 8 K-slice partials of a group are then
-// summed, in kb order, by the owner of each cell: workgroup (jb, kb) owns units
-// 32 jb + 4 kb .. +3 of both layers for all 64 rows, runs their cell backward (the cell
-// gradient carried in registers) and writes dG — the only bytes handed across XCDs.
-// Synchronisation per iteration: the group's partials are exchanged inside the XCD's L2
-// (plain stores, sc1 loads, a per-group counter: lstm_xcd_fwd_kernel's form), the dG rows
-// across the chip by the hierarchical grid barrier of the forward kernel (write-through
-// stores, sc1 loads).  Workgroups take their (jb, kb) role from their XCC id and a per-XCC
-// census; anything but 8 XCCs x 32 workgroups (or a timed-out wait) takes the fault path.
-constexpr int BJ = 32;             // units per group
-constexpr int BKB = 8;             // K slices per group (workgroups per group)
-constexpr int BKS = 512;           // gate rows per K slice (4H / BKB, H = 1024)
-constexpr int BKW = BKS / 8;       // gate rows per wave (64)
-constexpr int BNT = 512;           // 8 waves
-constexpr int BROW = 64;           // batch rows (all of them)
-constexpr int BPLD = BJ + 1;       // padded LDS row of a 64 x 32 partial tile
-constexpr int BSLOTS = 8 * BROW * BPLD;        // floats of the 8 waves' partial-tile slots
-constexpr int BB_GROUP = BAR_LINES;          // 32 lines: per-group partial counters
-constexpr int BB_LINES = BAR_LINES + 32;
-constexpr int64_t BB_BYTES = BB_LINES * L * 4;
-constexpr int kFaultLstm2BwdPersist = 16;    // lstm2_bwd_persist_kernel (decoder lstm2 backward)
-
-struct BArgs {
-  int B, T;
-  const float* dh1;                 // dL/dh of layer 1 (b * d_ldb + t * d_ldt)
-  int64_t d_ldb, d_ldt;
-  const float *g1, *c1, *g0, *c0;   // gates (B,T,4H) [i f g o], cells (B,T,H)
-  const float *W1, *Wi1, *W0;       // W_hh1, W_ih1, W_hh0 (4H, H), fp32
-  const __bf16 *W1b, *Wi1b, *W0b;   // their bf16 copies (BF)
-  float *dG1, *dG0;                 // (B,T,4H) out
-  __bf16 *dG1b, *dG0b;              // bf16 copies (BF: the products' operands)
-  float* part;                      // group partials [32 jb][8 kb][3][64][32]
-  int* bar;
-  int timeout_ticks;
-};
-
-// write-through store of one gate gradient (read by other XCDs after the grid barrier)
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool BF>
-__global__ __launch_bounds__(BNT, 1) void lstm2_bwd_persist_kernel(BArgs a) {
-  constexpr int H = 1024, G4 = 4 * H;
-  extern __shared__ __attribute__((aligned(16))) float lds[];   // [8 waves][64][BPLD] slots + fp32 W_hh0 slice
-  __shared__ int s_info[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = a.T;
-  int census[16] = {};
-  int xcc_id = 0, xcc_wgs = 0, xcc_n = 0;
-  int* status = &s_info[3];
-  PArgs pa = {};                   // the forward's barrier helpers read bar / timeout_ticks only
-  pa.bar = a.bar;
-  pa.timeout_ticks = a.timeout_ticks;
-  if (tid == 0) {
-    unsigned x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    const int xcc = (int)(x & 15);
-    const int slot = add_rlx(a.bar + (BAR_CENSUS + xcc) * L, 1);
-    add_rlx(a.bar + BAR_START * L, 1);
-    bool ok = wait_ge(a.bar + BAR_START * L, gridDim.x, a.bar + BAR_ERR * L, a.timeout_ticks);
-    int nx = 0;
-    for (int i = 0; i < 16; ++i) {
-      census[i] = ld_rlx(a.bar + (BAR_CENSUS + i) * L);
-      nx += census[i] > 0;
-      if (i < 8 && census[i] != 32) ok = false;   // 8 XCCs x 32 workgroups, or no run
-    }
-    ok = ok && xcc < 8 && slot < 32;
-    xcc_id = xcc;
-    xcc_wgs = census[xcc];
-    xcc_n = nx;
-    s_info[0] = xcc < 8 ? xcc : 0;
-    s_info[1] = slot < 32 ? slot : 0;
-    *status = ok ? 0 : 1;
-  }
-  __syncthreads();
-  const int jb = 4 * s_info[0] + s_info[1] / BKB, kb = s_info[1] % BKB;
-  const int j0 = jb * BJ, k0 = kb * BKS;
-  // cell ownership: thread e < 256 -> layer 1, >= 256 -> layer 0; row e / 4 % 64, unit u
-  const int ce = tid & 255, cb_ = ce >> 2, cu = j0 + kb * 4 + (ce & 3);
-  const bool l1cell = tid < 256;
-  auto fail = [&]() {
-    const float nan = __builtin_nanf("");
-    float* dG = l1cell ? a.dG1 : a.dG0;
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dG[((int64_t)cb_ * T + t) * G4 + q * H + cu] = nan;
-    if (tid == 0)
-      __hip_atomic_fetch_or(&g_avc_fault, kFaultLstm2BwdPersist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  if (*status != 0) {
-    if (tid == 0) st_rlx(a.bar + BAR_ERR * L, 1);
-    fail();
-    return;
-  }
-  // ---- weight slices -> VGPRs.  Wave w takes gate rows kw = k0 + 64 w .. +63; lane l (group
-  // g = l >> 4) supplies, for column block cb and MFMA m, W[kw + 16 g + m][j0 + 16 cb + (l & 15)]
-  // (fp32, 16 MFMAs of K = 4 per 64 rows), or the 8 bf16 W[kw + 32 m + 8 g + e][...] (bf16, 2
-  // MFMAs of K = 32)
-  const int g = lane >> 4, jl = lane & 15;
-  const int kw = k0 + BKW * wave;
-  // fp32: W_hh1 and W_ih1 slices in VGPRs (64 per lane), W_hh0's in LDS after the reduction
-  // slots (w0s, 64 KB, [wave][cb][g][m / 4][16 lanes][4]: a lane's 4 consecutive m as one
-  // conflict-free ds_read_b128); bf16: all three in VGPRs (48 per lane)
-  float wf[2][2][BF ? 1 : 16];
-  bf16x8 wb[3][2][BF ? 2 : 1];
-  float* w0s = lds + BSLOTS;
-  {
-    const float* Ws[3] = {a.W1, a.Wi1, a.W0};
-    const __bf16* Wbs[3] = {a.W1b, a.Wi1b, a.W0b};
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int col = j0 + 16 * cb + jl;
-        if constexpr (BF) {
-#pragma unroll
-          for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) wb[p][cb][m][e] = Wbs[p][(int64_t)(kw + 32 * m + 8 * g + e) * H + col];
-        } else if (p < 2) {
-#pragma unroll
-          for (int m = 0; m < 16; ++m) wf[p][cb][m] = Ws[p][(int64_t)(kw + 16 * g + m) * H + col];
-        } else {
-#pragma unroll
-          for (int m = 0; m < 16; ++m)
-            w0s[((((wave * 2 + cb) * 4 + g) * 4 + (m >> 2)) * 16 + jl) * 4 + (m & 3)] =
-                Ws[p][(int64_t)(kw + 16 * g + m) * H + col];
-        }
-      }
-  }
-  __syncthreads();
-  // ---- cell operands of the next cell update, prefetched (they do not depend on the recurrence)
-  const float* gsrc = l1cell ? a.g1 : a.g0;
-  const float* csrc = l1cell ? a.c1 : a.c0;
-  float gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f, cc = 0.f, cp = 0.f, dho = 0.f, dcs = 0.f;
-  auto load_cell = [&](int t) {
-    const float* gr = gsrc + ((int64_t)cb_ * T + t) * G4 + cu;
-    gi = gr[0]; gf = gr[H]; gg = gr[2 * H]; go = gr[3 * H];
-    cc = csrc[((int64_t)cb_ * T + t) * H + cu];
-    cp = t > 0 ? csrc[((int64_t)cb_ * T + t - 1) * H + cu] : 0.f;
-    dho = l1cell ? a.dh1[(int64_t)cb_ * a.d_ldb + (int64_t)t * a.d_ldt + cu] : 0.f;
-  };
-  float* slots = lds;                                 // [wave][64][BPLD]
-  constexpr int SLOT = BROW * BPLD;
-  float* mypart = a.part + (int64_t)(jb * BKB + kb) * 3 * BROW * BJ;
-  int* grp = a.bar + (BB_GROUP + jb) * L;
-  // ---- the products.  A = this wave's 64 rows x 64 k of a dG row block (sc1 buffer loads
-  // from a wave-uniform base), B = the weight registers.  All of a tensor's A fragments are
-  // issued at once (fp32: 16 x 16 B per lane, bf16: 8), and as each 16-row block of dG1 has
-  // fed its P1 / Q MFMAs its registers are refilled with dG0's block for P0, so the dG0
-  // loads are in flight under the P1 / Q MFMAs.
-  constexpr int NA = BF ? 2 : 4;                       // 16-B A loads per row block per lane
-  f32x4 A[4][NA];
-  auto issue = [&](const void* dGrow0, int rb) {       // dGrow0: element (b = 0, t, k = 0)
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(dGrow0), (short)0,
-                                                                       0x7fffffff, 0x00020000);
-    const uint32_t off = BF ? (uint32_t)((((int64_t)(16 * rb + jl) * T) * G4 + kw + 8 * g) * 2)
-                            : (uint32_t)((((int64_t)(16 * rb + jl) * T) * G4 + kw + 16 * g) * 4);
-#pragma unroll
-    for (int i = 0; i < NA; ++i)
-      A[rb][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off + (BF ? 64 : 16) * i, 0, 16));
-  };
-  // acc[i][rb][cb] += A[rb] x W[p + i] over this wave's 64 k (NP products, first P)
-  auto mfma_rb = [&](auto np_tag, auto p_tag, int rb, f32x4 (&acc)[2][4][2]) {
-    constexpr int NP = decltype(np_tag)::value, P = decltype(p_tag)::value;
-    if constexpr (BF) {
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int i = 0; i < NP; ++i)
-            acc[i][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, A[rb][m]),
-                                                                     wb[P + i][cb][m], acc[i][rb][cb], 0, 0, 0);
-    } else if constexpr (P == 2) {
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        f32x4 bw[2];
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          bw[cb] = *reinterpret_cast<const f32x4*>(w0s + ((((wave * 2 + cb) * 4 + g) * 4 + mq) * 16 + jl) * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-            acc[0][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[rb][mq][e], bw[cb][e], acc[0][rb][cb], 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int m = 0; m < 16; ++m)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int i = 0; i < NP; ++i)
-            acc[i][rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[rb][m >> 2][m & 3], wf[P + i][cb][m],
-                                                                  acc[i][rb][cb], 0, 0, 0);
-    }
-  };
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I0 = std::integral_constant<int, 0>;
-  // this wave's partial tiles -> LDS slots, then every thread sums the 8 waves' slots in wave
-  // order for (np) products and stores the workgroup's partial tiles (plain stores: the group
-  // reads them from this XCD's L2)
-  auto reduce_store = [&](f32x4 (&acc)[2][4][2], int np, int p_first) {
-    for (int i = 0; i < np; ++i) {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            slots[wave * SLOT + (16 * rb + 4 * g + r) * BPLD + 16 * cb + jl] = acc[i][rb][cb][r];
-      __syncthreads();
-      for (int e = tid; e < BROW * BJ; e += BNT) {
-        const int row = e / BJ, col = e % BJ;
-        float sum = 0.f;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) sum += slots[w * SLOT + row * BPLD + col];
-        mypart[(int64_t)(p_first + i) * BROW * BJ + e] = sum;
-      }
-      __syncthreads();
-    }
-  };
-  for (int s = 0; s <= T; ++s) {
-    const int t1 = T - 1 - s, t0 = T - s;
-    const bool act1 = t1 >= 0, act0 = s >= 1, doP1Q = s >= 1, doP0 = s >= 2;
-    // this iteration's cell operands (independent of the recurrence): issued first, they land
-    // under the products (issued before the grid barrier they only lengthened its wait)
-    if (l1cell ? act1 : act0) load_cell(l1cell ? t1 : t0);
-    // ---- products over this workgroup's K slice
-    if (doP1Q) {
-      const void* d1 = BF ? (const void*)(a.dG1b + (int64_t)t0 * G4) : (const void*)(a.dG1 + (int64_t)t0 * G4);
-      const void* d0 = BF ? (const void*)(a.dG0b + (int64_t)(t0 + 1) * G4)
-                          : (const void*)(a.dG0 + (int64_t)(t0 + 1) * G4);
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) issue(d1, rb);
-      f32x4 acc[2][4][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[i][rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        mfma_rb(I2{}, I0{}, rb, acc);                      // P1 (W_hh1) and Q (W_ih1) on dG1
-        if (doP0) issue(d0, rb);
-      }
-      reduce_store(acc, 2, 0);
-      if (doP0) {
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[0][rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) mfma_rb(I1{}, I2{}, rb, acc);   // P0 (W_hh0) on dG0
-        reduce_store(acc, 1, 2);
-      }
-    }
-    // ---- the group's 8 K-slice partials are in this XCD's L2
-    if (doP1Q) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        add_l2(grp, 1);
-        const uint64_t ts = __builtin_amdgcn_s_memrealtime();
-        int ok = 1;
-        while (ld_rlx(grp) < BKB * s) {
-          __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - ts > (uint64_t)a.timeout_ticks || ld_rlx(a.bar + BAR_ERR * L)) {
-            st_rlx(a.bar + BAR_ERR * L, 1);
-            ok = 0;
-            break;
-          }
-        }
-        *status = ok ? 0 : 1;
-      }
-      __syncthreads();
-      if (*status != 0) {
-        fail();
-        return;
-      }
-    }
-    // ---- cell backward of the owned cells: dh = dh_from_above + partial sums in kb order
-    const bool act = l1cell ? act1 : act0;
-    const int t = l1cell ? t1 : t0;
-    if (act) {
-      float dh = dho;
-      if (l1cell ? doP1Q : true) {
-        // the group's partial tiles: a wave-uniform buffer base (a per-lane base would force a
-        // waterfall loop over the 64 lanes' descriptors), the cell's offset in voffset
-        const float* base = a.part + (int64_t)jb * BKB * 3 * BROW * BJ;
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
-                                                                           0x7fffffff, 0x00020000);
-        const uint32_t cell_off = (uint32_t)((cb_ * BJ + kb * 4 + (ce & 3)) * 4);
-        float sq = 0.f, sp = 0.f;
-#pragma unroll
-        for (int k2 = 0; k2 < BKB; ++k2) {
-          const uint32_t o = cell_off + (uint32_t)(k2 * 3 * BROW * BJ * 4);
-          if (l1cell) {
-            sp += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 16));
-          } else {
-            sq += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o + BROW * BJ * 4, 0, 16));
-            if (doP0) sp += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o + 2 * BROW * BJ * 4, 0, 16));
-          }
-        }
-        dh = l1cell ? dh + sp : sq + sp;
-      }
-      const float tc = tanhf(cc);
-      const float dc = dcs + dh * go * (1.f - tc * tc);
-      const float di = dc * gg * gi * (1.f - gi);
-      const float df = dc * cp * gf * (1.f - gf);
-      const float dgg = dc * gi * (1.f - gg * gg);
-      const float dO = dh * tc * go * (1.f - go);
-      dcs = dc * gf;
-      float* d = (l1cell ? a.dG1 : a.dG0) + ((int64_t)cb_ * T + t) * G4 + cu;
-      st_wt(d, di);
-      st_wt(d + H, df);
-      st_wt(d + 2 * H, dgg);
-      st_wt(d + 3 * H, dO);
-      if constexpr (BF) {
-        __bf16* db = (l1cell ? a.dG1b : a.dG0b) + ((int64_t)cb_ * T + t) * G4 + cu;
-        const float v4[4] = {di, df, dgg, dO};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          __hip_atomic_store(reinterpret_cast<unsigned short*>(db + q * H),
-                             __builtin_bit_cast(unsigned short, (__bf16)v4[q]), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (s < T && !grid_sync(pa, xcc_id, xcc_wgs, xcc_n, census, status, s)) {
-      fail();
-      return;
-    }
-  }
-}
-
-int g_bwd_ok = -1;
-constexpr int kBwdLds = (BSLOTS + 8 * 2 * 4 * 4 * 16 * 4) * 4;   // slots + the fp32 W_hh0 slice
-
-template <bool BF>
-bool bwd_fits_one() {
-  int per = 0;
-  const void* k = reinterpret_cast<const void*>(lstm2_bwd_persist_kernel<BF>);
-  return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds) == hipSuccess &&
-         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm2_bwd_persist_kernel<BF>, BNT, kBwdLds) ==
-             hipSuccess &&
-         per >= 1;
-}
-
-bool bwd_fits() {
-  if (g_bwd_ok < 0) {
-    int dev = 0;
-    hipDeviceProp_t p;
-    g_bwd_ok = hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess &&
-               p.multiProcessorCount == 256 && bwd_fits_one<false>() && bwd_fits_one<true>();
-  }
-  return g_bwd_ok == 1;
-}
 
 }  // namespace
 
@@ -2015,25 +1467,6 @@ extern "C" int autovc_lstm_fwd_xcd_bf16(int B, int T, int H, const float* gx, in
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
   AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
   hipLaunchKernelGGL((lstm_xcd_fwd_kernel<512, true>), dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
-  AVC_CHECK_LAUNCH(fn);
-  return avc::kOk;
-}
-
-extern "C" int autovc_lstm_bwd_xcd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
-                                       const float* gates, const float* c_all, const float* W_hh, float* dG,
-                                       void* workspace, hipStream_t stream) {
-  static const char* fn = "autovc_lstm_bwd_xcd_f32";
-  AVC_CHECK_ARG(T > 0 && autovc_lstm_xcd_supported(B, H),
-                "%s: unsupported shape B=%d H=%d on this device (needs B=64, H=512, 8 XCDs x 32 CUs)", fn, B, H);
-  AVC_CHECK_ARG(gates && c_all && W_hh && dG && workspace, "%s: null pointer", fn);
-  AVC_CHECK_ARG(AVC_ALIGNED16(dG) && AVC_ALIGNED16(workspace), "%s: dG / workspace must be 16-byte aligned", fn);
-  XBArgs a;
-  a.B = B; a.T = T; a.dh = dh_out; a.d_ldb = d_ldb; a.d_ldt = d_ldt; a.gates = gates; a.c = c_all; a.W = W_hh;
-  a.dG = dG;
-  a.bar = static_cast<int*>(workspace);
-  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
-  AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
-  hipLaunchKernelGGL(lstm_xcd_bwd_kernel<512>, dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
 }
@@ -2169,66 +1602,4 @@ extern "C" int autovc_fault_status(hipStream_t stream, int clear, int* out) {
   return avc::kOk;
 }
 
-// ---- persistent decoder lstm2 backward (lstm2_bwd_persist_kernel)
-extern "C" int autovc_lstm2_bwd_persist_supported(int B, int H) { return (B == BROW && H == 1024 && bwd_fits()) ? 1 : 0; }
 
-extern "C" int64_t autovc_lstm2_bwd_persist_workspace_bytes(int B, int T, int H) {
-  if (B != BROW || T <= 0 || H != 1024) return -1;
-  return BB_BYTES + (int64_t)32 * BKB * 3 * BROW * BJ * 4;
-}
-
-static int lstm2_bwd_persist_launch(bool bf, int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                    const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                    const void* W_hh1, const void* W_ih1, const void* W_hh0, float* dG1, float* dG0,
-                                    uint16_t* dG1b, uint16_t* dG0b, void* workspace, hipStream_t stream,
-                                    const char* fn) {
-  AVC_CHECK_ARG(T > 0 && autovc_lstm2_bwd_persist_supported(B, H),
-                "%s: unsupported shape B=%d H=%d on this device (needs B=64, H=1024, 8 XCDs x 32 CUs)", fn, B, H);
-  AVC_CHECK_ARG(dh1_out && gates1 && c1 && gates0 && c0 && W_hh1 && W_ih1 && W_hh0 && dG1 && dG0 && workspace &&
-                    (!bf || (dG1b && dG0b)),
-                "%s: null pointer", fn);
-  AVC_CHECK_ARG(AVC_ALIGNED16(dG1) && AVC_ALIGNED16(dG0) && AVC_ALIGNED16(workspace) &&
-                    (!bf || (AVC_ALIGNED16(dG1b) && AVC_ALIGNED16(dG0b))),
-                "%s: dG / workspace must be 16-byte aligned", fn);
-  BArgs a = {};
-  a.B = B; a.T = T; a.dh1 = dh1_out; a.d_ldb = d_ldb; a.d_ldt = d_ldt;
-  a.g1 = gates1; a.c1 = c1; a.g0 = gates0; a.c0 = c0;
-  if (bf) {
-    a.W1b = static_cast<const __bf16*>(W_hh1); a.Wi1b = static_cast<const __bf16*>(W_ih1);
-    a.W0b = static_cast<const __bf16*>(W_hh0);
-  } else {
-    a.W1 = static_cast<const float*>(W_hh1); a.Wi1 = static_cast<const float*>(W_ih1);
-    a.W0 = static_cast<const float*>(W_hh0);
-  }
-  a.dG1 = dG1; a.dG0 = dG0;
-  a.dG1b = reinterpret_cast<__bf16*>(dG1b); a.dG0b = reinterpret_cast<__bf16*>(dG0b);
-  a.bar = static_cast<int*>(workspace);
-  a.part = reinterpret_cast<float*>(static_cast<char*>(workspace) + BB_BYTES);
-  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
-  AVC_HIP(avc::zero_async(workspace, BB_BYTES, stream), fn);
-  if (bf)
-    hipLaunchKernelGGL(lstm2_bwd_persist_kernel<true>, dim3(256), dim3(BNT), kBwdLds, stream, a);
-  else
-    hipLaunchKernelGGL(lstm2_bwd_persist_kernel<false>, dim3(256), dim3(BNT), kBwdLds, stream, a);
-  AVC_CHECK_LAUNCH(fn);
-  return avc::kOk;
-}
-
-extern "C" int autovc_lstm2_bwd_persist_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                            const float* gates1, const float* c1, const float* gates0,
-                                            const float* c0, const float* W_hh1, const float* W_ih1,
-                                            const float* W_hh0, float* dG1, float* dG0, void* workspace,
-                                            hipStream_t stream) {
-  return lstm2_bwd_persist_launch(false, B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, gates0, c0, W_hh1, W_ih1, W_hh0,
-                                  dG1, dG0, nullptr, nullptr, workspace, stream, "autovc_lstm2_bwd_persist_f32");
-}
-
-extern "C" int autovc_lstm2_bwd_persist_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb,
-                                             int64_t d_ldt, const float* gates1, const float* c1,
-                                             const float* gates0, const float* c0, const uint16_t* W_hh1_b,
-                                             const uint16_t* W_ih1_b, const uint16_t* W_hh0_b, float* dG1,
-                                             uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, void* workspace,
-                                             hipStream_t stream) {
-  return lstm2_bwd_persist_launch(true, B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, gates0, c0, W_hh1_b, W_ih1_b,
-                                  W_hh0_b, dG1, dG0, dG1_b, dG0_b, workspace, stream, "autovc_lstm2_bwd_persist_bf16");
-}

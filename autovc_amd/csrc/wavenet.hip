@@ -157,32 +157,11 @@ __device__ inline float mol_noise(int j, int64_t t, int utt, const WnArgs& a) {
   return logf(-logf(u));
 }
 
-// Butterfly reduction of NV per-lane partial sums over the 64 lanes of a wave: NV-1
-// shuffles for the halving rounds instead of 6*NV.  On return lane L with
-// (L & (64/NV - 1)) == 0 holds the full sum of value L / (64/NV).  Every array index is a
-// compile-time constant (template recursion): a runtime index would make the compiler
-// demote the array to LDS, which costs ~15 us per launch.
-template <int N, int M>
-__device__ inline void butterfly(float* cur, int lane) {
-  if constexpr (M >= 1) {
-    if constexpr (N > 1) {
-      const bool up = (lane & M) != 0;
-#pragma unroll
-      for (int j = 0; j < N / 2; ++j) {
-        const float keep = up ? cur[j + N / 2] : cur[j];
-        const float send = up ? cur[j] : cur[j + N / 2];
-        cur[j] = keep + __shfl_xor(send, M);
-      }
-      butterfly<N / 2, M / 2>(cur, lane);
-    } else {
-      cur[0] += __shfl_xor(cur[0], M);
-      butterfly<1, M / 2>(cur, lane);
-    }
-  }
-}
-
-// The same halving reduction on gfx950's cross-lane hardware instead of ds_bpermute (an LDS
-// round trip per shuffle): level 0 pairs lanes l, l ^ 32 with v_permlane32_swap, level 1 l,
+// Butterfly reduction of NV per-lane partial sums over the 64 lanes of a wave (NV-1
+// exchanges for the halving rounds instead of 6*NV; every array index a compile-time
+// constant, so nothing is demoted to LDS) on gfx950's cross-lane hardware instead of
+// ds_bpermute (an LDS round trip per shuffle, 4-5 % slower per WaveNet sample step,
+// profiles/r04/wn_grid_ab.txt): level 0 pairs lanes l, l ^ 32 with v_permlane32_swap, level 1 l,
 // l ^ 16 with v_permlane16_swap (one swap moves two values: the kept half of one lane group
 // and the sent half of the other), level 2 l, l ^ 15 (DPP row_mirror), level 3 l, l ^ 7
 // (row_half_mirror), levels 4 / 5 l ^ 2, l ^ 1 (quad_perm).  The pairings generate every
@@ -240,17 +219,13 @@ __device__ inline float wave_reduce_hw(float (&v)[NV], int lane) {
   return cur[0];
 }
 
-#ifndef AVC_WN_HW_REDUCE
-#define AVC_WN_HW_REDUCE 1                    // 0: the ds_bpermute butterfly (tools/build_variant.sh A/B)
-#endif
 template <int NV>
 __device__ inline float wave_reduce_multi(float (&v)[NV], int lane) {
   static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "power-of-two value count");
   float cur[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) cur[j] = v[j];
-  if constexpr (AVC_WN_HW_REDUCE) butterfly_hw<NV, 0>(cur, lane);
-  else butterfly<NV, 32>(cur, lane);
+  butterfly_hw<NV, 0>(cur, lane);
   return cur[0];
 }
 
@@ -890,39 +865,8 @@ __global__ __launch_bounds__(256) void wn_upsample_kernel(UpArgs u, const float*
   }
 }
 
-// ================================================================ XCD-local generation
-// (B <= 8, the r9y9 shapes R = 512, G = 512, S = 256, 3 taps).  Each utterance is an
-// independent chain, so XCD x can run utterance x on its own: its 32 workgroups ("slots",
-// one per CU) step through the layers, the skip tail and the head with every per-layer
-// hand-off (g_l, x_l(t): 3 KB) written into and read from that XCD's L2, separated by a
-// per-XCD phase counter (L2-local atomics) instead of a kernel boundary.  Per layer a slot
-// owns 8 gate units (16 gate rows over the 1792 inputs [x_l(t-2d) | x_l(t-d) | g_(l-1) |
-// x_(l-1)(t)] of wn_layer_kernel's folded-current-tap form: the ring taps enter the GEMV
-// directly, no past-tap launches), 16 residual rows and 8 skip rows of the previous layer.
-// The weights (136 KB per slot and phase) are the bulk of a phase's bytes, so they are moved
-// off the critical chain: 4 "loader" waves fetch the NEXT phase's rows into registers while
-// the phase runs and write them to LDS once the 4 "compute" waves have read the current ones;
-// the compute waves' chain per phase is wait -> hand-off loads (sc1) -> dot products from
-// LDS -> gate / residual -> stores -> arrive.  Every slot draws the sample itself from the
-// previous step's h1 (same Philox stream, the same value in all 32).  26 phases per sample
-// step: layers 0..L-1, the last layer's skip rows, h1.
-__device__ int g_wn_fault = 0;         // sticky: an XCD-local generation timed out (autovc_wavenet_fault)
-constexpr int kXW = 8;                 // waves per slot workgroup: 4 compute + 4 loader
-constexpr int kXCW = 4;                // compute waves
-constexpr int kXUW = 8 / kXCW;         // gate units per compute wave (2)
-constexpr int kXGR = 2 * kXUW;         // gate rows per compute wave (4)
-constexpr int kXXR = 16 / kXCW;        // residual x rows per compute wave (4)
-constexpr int kXSR = 8 / kXCW;         // skip / head rows per compute wave (2)
-constexpr int kXSlots = 32;            // slots per XCD
-constexpr int kXLn = 32;               // ints per barrier line (128 B)
-constexpr int kXBarLines = 17;         // census (lines 0..7), phase counters (8..15), error (16)
-static_assert(kCtrSlots % kXLn == 0, "barrier block starts on a line");
-constexpr int kXKX = 1792;             // gate width K*R + H
-constexpr int kXC = kXKX / 256;        // 256-float chunks of the gate GEMV (7)
-constexpr int kXG4 = 16 * kXKX / 4;    // float4 of the gate rows of a slot (7168)
-constexpr int kXR4 = 24 * 256 / 4;     // float4 of the residual / skip / head rows (1536)
-constexpr int kXLd = (kXG4 + kXR4) / (64 * (kXW - kXCW));   // float4 per loader lane (34)
-static_assert(kXLd * 64 * (kXW - kXCW) == kXG4 + kXR4, "loader map");
+// ================================================================ persistent generation helpers
+__device__ int g_wn_fault = 0;         // sticky: a persistent generation timed out (autovc_wavenet_fault)
 
 // A wave-uniform base pointer forced into SGPRs: a buffer descriptor built from a value the
 // compiler keeps in VGPRs (e.g. live across divergent code) otherwise becomes a waterfall loop
@@ -947,312 +891,6 @@ __device__ __forceinline__ f32x4 ld4_ro(const float* base, int off) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(base), (short)0, 0x7fffffff,
                                                                      0x00020000);
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)off * 4u, 0, 0));
-}
-
-__global__ __launch_bounds__(64 * kXW, 1) void wn_xcd_kernel(WnArgs a, int t0, int t1, int* bar, int timeout_ticks) {
-  constexpr int R = 512, H = 256, S = 256;
-  __shared__ __attribute__((aligned(16))) float s_w[4 * (kXG4 + kXR4)];   // this phase's weight rows
-  __shared__ float s_mol[kMaxNO];
-  __shared__ float s_in;
-  __shared__ float s_x[16];              // this slot's rows of the residual input x_{l-1}(t)
-  __shared__ float s_skip[8];            // this slot's skip accumulator rows
-  __shared__ int s_info[3];              // xcc, slot, status
-  __shared__ int s_ok;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool compute = w < kXCW;
-  if (tid == 0) {
-    unsigned x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    const int xcc = (int)(x & 15);
-    const int slot = xcc < 8 ? __hip_atomic_fetch_add(bar + xcc * kXLn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 99;
-    s_info[0] = xcc;
-    s_info[1] = slot;
-    s_info[2] = (xcc < 8 && slot < kXSlots) ? 0 : 1;
-    if (s_info[2]) __hip_atomic_store(bar + 16 * kXLn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const int u = __builtin_amdgcn_readfirstlane(s_info[0]), slot = __builtin_amdgcn_readfirstlane(s_info[1]);
-  if (s_info[2] || u >= a.B) return;     // a group short of slots times out below
-  const int L = a.n_layers, T = a.T, RING = a.RING, NPH = L + 2;
-  int* ctr = bar + (8 + u) * kXLn;
-  int* err = bar + 16 * kXLn;
-  int phase = 0;                          // phases every slot of the XCD has arrived at
-  bool ok = true;
-  const float* W2 = head_base(a) + (int64_t)S * S + S;
-  const float* b2 = W2 + (int64_t)a.NO * S;
-  const float* b1 = head_base(a) + (int64_t)S * S;
-
-  // ---- loader waves: the next phase's rows, registers -> LDS.  Loader wave lw owns gate
-  // rows kGRL lw .. (each 7 float4 per lane) and residual rows kRRL lw .. (1 float4 per lane):
-  // every load is a wave-uniform row base plus a lane offset, so the addressing stays scalar.
-  constexpr int kNLW = kXW - kXCW, kGRL = 16 / kNLW, kRRL = 24 / kNLW;
-  static_assert(kGRL * kXC + kRRL == kXLd, "loader rows");
-  const int lw = w - kXCW;
-  f32x4 lreg[kXLd];                      // (loader waves only)
-  auto load_next = [&](int ph) {          // global -> registers
-    if (ph < L) {
-#pragma unroll
-      for (int k = 0; k < kGRL; ++k) {
-        const int row = kGRL * lw + k, unit = 8 * slot + (row >> 1);
-        const float* base = layer_base(a, ph) + (int64_t)(unit + (row & 1) * H) * kXKX;
-#pragma unroll
-        for (int c = 0; c < kXC; ++c) lreg[kXC * k + c] = ld4_ro(base, 256 * c + 4 * lane);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kRRL; ++k) {
-      const int row = kRRL * lw + k;     // residual block row 0..23
-      const float* base = nullptr;
-      if (ph == L + 1) {
-        if (row >= 16) base = head_base(a) + (int64_t)(8 * slot + row - 16) * 256;
-      } else if (ph >= 1 && (ph < L || row >= 16)) {
-        const int prow = row < 16 ? 16 * slot + row : R + 8 * slot + (row - 16);
-        base = layer_base(a, ph - 1) + (int64_t)a.G * kXKX + (int64_t)prow * H;
-      }
-      if (base != nullptr) lreg[kGRL * kXC + k] = ld4_ro(base, 4 * lane);
-    }
-  };
-  auto store_next = [&]() {               // registers -> LDS (rows a phase does not read get stale data)
-#pragma unroll
-    for (int k = 0; k < kGRL; ++k)
-#pragma unroll
-      for (int c = 0; c < kXC; ++c)
-        *reinterpret_cast<f32x4*>(s_w + (kGRL * lw + k) * kXKX + 256 * c + 4 * lane) = lreg[kXC * k + c];
-#pragma unroll
-    for (int k = 0; k < kRRL; ++k)
-      *reinterpret_cast<f32x4*>(s_w + 4 * kXG4 + (kRRL * lw + k) * 256 + 4 * lane) = lreg[kGRL * kXC + k];
-  };
-  if (!compute) {
-    load_next(0);
-    store_next();
-    load_next(1 % NPH);
-  }
-  __syncthreads();
-
-  auto arrive = [&]() {
-    if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the hand-off stores are in L2
-    lds_barrier();
-    if (tid == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    ++phase;
-  };
-  auto wait = [&]() {
-    if (tid == 0) {
-      const uint64_t c0 = __builtin_amdgcn_s_memrealtime();
-      int good = 1;
-      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < kXSlots * phase) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - c0 > (uint64_t)timeout_ticks ||
-            __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          good = 0;
-          break;
-        }
-      }
-      s_ok = good;
-    }
-    lds_barrier();
-    ok = s_ok != 0;
-  };
-  // end of a phase: loaders move the next phase's rows into LDS (the compute waves read the
-  // current ones before the arrive) and fetch the one after
-  int gph = 0;                            // global phase index of this launch (0 = step t0, layer 0)
-  auto finish_phase = [&]() {
-    arrive();
-    ++gph;
-  };
-
-  if (!compute) {
-    // the loader waves' loop: the same barriers as the compute waves' (wait, the two of the
-    // sampling phase, arrive), with the register rows live only here
-    for (int t = t0; t < t1 && ok; ++t)
-      for (int ph = 0; ph < NPH && ok; ++ph) {
-        if (gph > 0) wait();
-        if (!ok) break;
-        if (ph == 0) { lds_barrier(); lds_barrier(); }
-        arrive();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        store_next();
-        load_next((gph + 2) % NPH);
-        ++gph;
-      }
-    return;
-  }
-  for (int t = t0; t < t1 && ok; ++t) {
-    const int ts = t & (RING - 1), prow = t % a.Tch;
-    for (int ph = 0; ph < NPH && ok; ++ph) {
-      if (gph > 0) wait();
-      if (!ok) break;
-      if (ph < L) {
-        const int l = ph, d = 1 << (l % a.lps);
-        // ---- compute waves: wave w owns units 8 slot + kXUW w .. +kXUW (gate rows kXGR w ..
-        // of the LDS block: [unit tanh, unit sigmoid] pairs), residual x rows kXXR w .. and
-        // skip rows 16 + kXSR w .. of the LDS residual block
-        f32x4 in[kXC];
-        float pre[kXGR];
-        if (compute) {
-          const float* x2 = ring_row(a, l, (t - 2 * d) & (RING - 1)) + (int64_t)u * R;
-          const float* x1 = ring_row(a, l, (t - d) & (RING - 1)) + (int64_t)u * R;
-          in[0] = ld4_l2(x2, 4 * lane);
-          in[1] = ld4_l2(x2, 256 + 4 * lane);
-          in[2] = ld4_l2(x1, 4 * lane);
-          in[3] = ld4_l2(x1, 256 + 4 * lane);
-          const float* pr = a.pre + ((int64_t)prow * a.B + u) * ((int64_t)L * a.G) + (int64_t)l * a.G;
-          const int u0 = 8 * slot + kXUW * w;
-#pragma unroll
-          for (int q = 0; q < kXUW; ++q) { pre[2 * q] = pr[u0 + q]; pre[2 * q + 1] = pr[H + u0 + q]; }
-          if (l >= 1) {
-            const float* gp = gbuf_of(a, l - 1) + (int64_t)u * H;
-            const float* xp = ring_row(a, l - 1, ts) + (int64_t)u * R;
-            in[4] = ld4_l2(gp, 4 * lane);
-            in[5] = ld4_l2(xp, 4 * lane);
-            in[6] = ld4_l2(xp, 256 + 4 * lane);
-          }
-        }
-        if (l == 0) {
-          // ---- the sample of step t-1 from its h1 (every slot draws the same value), then x_0(t)
-          const int tp = t - 1;
-          constexpr int MR = 32 / kXCW;        // MoL rows per compute wave (16)
-          if (compute && tp >= 0) {
-            const f32x4 hv = ld4_l2(a.h1 + (int64_t)u * S, 4 * lane);
-            float accm[MR];
-#pragma unroll
-            for (int q = 0; q < MR; ++q) {
-              const int row = min(MR * w + q, a.NO - 1);
-              accm[q] = dot4(ld4(W2 + (int64_t)row * S + 4 * lane), hv, 0.f);
-            }
-            const float v = wave_reduce_multi<MR>(accm, lane);
-            const int r = MR * w + lane / (64 / MR);
-            if ((lane & (64 / MR - 1)) == 0 && r < a.NO) s_mol[r] = v + b2[r];
-          }
-          lds_barrier();
-          if (tid == 0) {
-            float smp = 0.f, in_v = 0.f;
-            if (tp >= 0) smp = mol_sample(s_mol, a.NO / 3, tp, a.utt_base + u, a);
-            if (a.teacher != nullptr && t < a.teacher_len) in_v = a.teacher[(int64_t)u * a.teacher_len + t];
-            else if (tp >= 0) in_v = smp;
-            s_in = in_v;
-            if (slot == 0) {
-              a.yin[(int64_t)u * T + t] = in_v;
-              if (tp >= 0) {
-                a.y_out[(int64_t)u * T + tp] = smp;
-                if (a.mol_out)
-                  for (int j = 0; j < a.NO; ++j) a.mol_out[((int64_t)u * T + tp) * a.NO + j] = s_mol[j];
-              }
-            }
-          }
-          lds_barrier();
-          if (compute) {
-            const float in_v = s_in;
-            in[4] = f32x4{0.f, 0.f, 0.f, 0.f};   // layer 0: no g_(l-1) block (its weights are zero)
-#pragma unroll
-            for (int c = 5; c < 7; ++c) {
-              const int i = 256 * (c - 5) + 4 * lane;
-              const f32x4 fw = ld4(a.packed + i), fb = ld4(a.packed + R + i);
-              in[c] = f32x4{in_v * fw[0] + fb[0], in_v * fw[1] + fb[1], in_v * fw[2] + fb[2], in_v * fw[3] + fb[3]};
-            }
-            if (tid < 16) {                   // x_0(t): this slot's 16 rows
-              const int row = 16 * slot + tid;
-              const float xv = in_v * a.packed[row] + a.packed[R + row];
-              ring_row(a, 0, ts)[(int64_t)u * R + row] = xv;
-              s_x[tid] = xv;
-            }
-          }
-        }
-        if (compute) {
-          // ---- dot products from the LDS rows
-          float accg[kXGR];
-#pragma unroll
-          for (int r = 0; r < kXGR; ++r) accg[r] = 0.f;
-#pragma unroll
-          for (int c = 0; c < kXC; ++c)
-#pragma unroll
-            for (int r = 0; r < kXGR; ++r)
-              accg[r] = dot4(*reinterpret_cast<const f32x4*>(s_w + (kXGR * w + r) * kXKX + 256 * c + 4 * lane), in[c],
-                             accg[r]);
-          // lane (64 / kXGR) r holds gate row r; the sigmoid row of a pair sits 64 / kXGR lanes up
-          constexpr int GS = 64 / kXGR;
-          const float zv = wave_reduce_multi<kXGR>(accg, lane);
-          const float zs = __shfl(zv, (lane + GS) & 63);
-          if (lane % (2 * GS) == 0) {
-            const int q = lane / (2 * GS), un = 8 * slot + kXUW * w + q;
-            float pt = pre[0], ps = pre[1];   // pre[2 q], pre[2 q + 1] without a dynamic register index
-#pragma unroll
-            for (int k = 1; k < kXUW; ++k)
-              if (q == k) { pt = pre[2 * k]; ps = pre[2 * k + 1]; }
-            gbuf_of(a, l)[(int64_t)u * H + un] = tanhf(zv + pt) * avc_sigmoid(zs + ps);
-          }
-          if (l >= 1) {
-            constexpr int RR = kXXR + kXSR <= 8 ? 8 : 16;   // residual values per wave, padded
-            float accr[RR];
-#pragma unroll
-            for (int r = 0; r < RR; ++r) accr[r] = 0.f;
-            const float* rw = s_w + 4 * kXG4;
-#pragma unroll
-            for (int r = 0; r < kXXR; ++r)
-              accr[r] = dot4(*reinterpret_cast<const f32x4*>(rw + (kXXR * w + r) * 256 + 4 * lane), in[4], 0.f);
-#pragma unroll
-            for (int r = 0; r < kXSR; ++r)
-              accr[kXXR + r] = dot4(*reinterpret_cast<const f32x4*>(rw + (16 + kXSR * w + r) * 256 + 4 * lane), in[4], 0.f);
-            const float v = wave_reduce_multi<RR>(accr, lane);   // lane (64 / RR) j: value j
-            const float* pbias = layer_base(a, l - 1) + (int64_t)a.G * kXKX + (int64_t)(R + S) * H;
-            const int j = lane / (64 / RR);
-            if (lane % (64 / RR) == 0 && j < kXXR) {
-              const int xr = 16 * slot + kXXR * w + j;
-              const float xv = (v + pbias[xr] + s_x[kXXR * w + j]) * kSqrtHalf;
-              ring_row(a, l, ts)[(int64_t)u * R + xr] = xv;
-              s_x[kXXR * w + j] = xv;
-            } else if (lane % (64 / RR) == 0 && j < kXXR + kXSR) {
-              const int k = kXSR * w + j - kXXR;
-              const float sv = v + pbias[R + 8 * slot + k];
-              s_skip[k] = l - 1 == 0 ? sv : (a.legacy ? (s_skip[k] + sv) * kSqrtHalf : s_skip[k] + sv);
-            }
-          }
-        }
-      } else if (ph == L) {
-        // ---- tail: the last layer's skip rows (LDS residual rows 16..23) -> the global skip sum
-        if (compute) {
-          const f32x4 g = ld4_l2(gbuf_of(a, L - 1) + (int64_t)u * H, 4 * lane);
-          const float* rw = s_w + 4 * kXG4;
-          float acc[kXSR];
-#pragma unroll
-          for (int r = 0; r < kXSR; ++r)
-            acc[r] = dot4(*reinterpret_cast<const f32x4*>(rw + (16 + kXSR * w + r) * 256 + 4 * lane), g, 0.f);
-          const float v = wave_reduce_multi<kXSR>(acc, lane);
-          if (lane % (64 / kXSR) == 0) {
-            const int k = kXSR * w + lane / (64 / kXSR);
-            const float* pbias = layer_base(a, L - 1) + (int64_t)a.G * kXKX + (int64_t)(R + S) * H;
-            const float sv = v + pbias[R + 8 * slot + k];
-            const float sk = L - 1 == 0 ? sv : (a.legacy ? (s_skip[k] + sv) * kSqrtHalf : s_skip[k] + sv);
-            a.skip[(int64_t)u * S + 8 * slot + k] = sk;
-          }
-        }
-      } else {
-        // ---- head: h1 = relu(W1 relu(skip) + b1), this slot's 8 rows (LDS rows 16..23)
-        if (compute) {
-          f32x4 x = ld4_l2(a.skip + (int64_t)u * S, 4 * lane);
-          x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
-          const float* rw = s_w + 4 * kXG4;
-          float acc[kXSR];
-#pragma unroll
-          for (int r = 0; r < kXSR; ++r)
-            acc[r] = dot4(*reinterpret_cast<const f32x4*>(rw + (16 + kXSR * w + r) * 256 + 4 * lane), x, 0.f);
-          const float v = wave_reduce_multi<kXSR>(acc, lane);
-          if (lane % (64 / kXSR) == 0) {
-            const int hr = 8 * slot + kXSR * w + lane / (64 / kXSR);
-            a.h1[(int64_t)u * S + hr] = fmaxf(v + b1[hr], 0.f);
-          }
-        }
-      }
-      finish_phase();
-    }
-  }
-  if (!ok) {
-    // a phase timed out (the XCD's 32 workgroups were not all resident): poison this
-    // utterance's outputs of the call and raise the device fault word the host checks
-    if (slot == 0)
-      for (int t = t0 + tid; t < t1; t += blockDim.x) a.y_out[(int64_t)u * T + t] = __builtin_nanf("");
-    if (tid == 0) __hip_atomic_fetch_or(&g_wn_fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // ================================================================ all-CU weight-resident generation
@@ -1350,9 +988,6 @@ __device__ __forceinline__ float2 ld2_l2(const float* base, int off) {   // sc1 
 // 3 the chain waves' LDS handshake, 4 past-tap inputs, 5 past-tap consumers, 6 skip sums, 7 h1.
 __device__ int g_wn_grid_diag[5] = {};
 
-#ifndef AVC_WN_SPIN_SLEEP
-#define AVC_WN_SPIN_SLEEP 1                   // a chain wave's retry pause (tools/build_variant.sh A/B)
-#endif
 // bounded spin state of one wave: the deadline, the device-wide error word, what it waits for
 struct Spin {
   uint64_t t0;
@@ -1364,7 +999,7 @@ struct Spin {
   int n = 0;
   __device__ bool tick() {                    // false: give up (timed out, or another wave did)
     if (!slow && (++n & 3) != 0) {            // the error word and the clock every 4th retry
-      if (AVC_WN_SPIN_SLEEP) __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(1);
       return true;
     }
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
@@ -1486,15 +1121,6 @@ __device__ __forceinline__ bool wn_grid_past_tap_chunk(const WnArgs& a, int lp, 
   return true;
 }
 
-#ifdef AVC_WN_GRID_TRACE
-// phase timeline of workgroups 0 and 137 at one steady-state step (tools/wn_grid_trace.py):
-// [wg][phase][start, inputs in, partials summed, past taps in, published], s_memrealtime
-__device__ int g_wn_grid_trace[2][kGMaxL + 2][5];
-#define WN_GT(k)                                                                                      \
-  if (trc && t == t0 + 64) g_wn_grid_trace[os == 0 ? 0 : 1][p][k] = (int)__builtin_amdgcn_s_memrealtime()
-#else
-#define WN_GT(k)
-#endif
 
 // NB: utterance slots of the launch (1, 2, 4 or 8 >= B; slots >= B compute on utterance 0
 // and are dropped), so every per-utterance loop is straight-line code
@@ -1586,9 +1212,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
 
   // =========================== chain waves 0-3: lane o = granule o
   const int o = wave * 64 + lane;
-#ifdef AVC_WN_GRID_TRACE
-  const bool trc = (os == 0 || os == 137) && wave == 0 && lane == 0;
-#endif
   int kx = 0;                                 // chain_sync rounds
   int cur_t = t0, cur_p = 0;                  // (diagnostics of a timed-out wait)
   bool ok = true;
@@ -1655,7 +1278,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
     for (int p = 0; p < L + 2 && ok; ++p, par ^= 1) {
       cur_t = t;
       cur_p = p;
-      WN_GT(0);
       float acc[NV];
 #pragma unroll
       for (int j = 0; j < NV; ++j) acc[j] = 0.f;
@@ -1689,7 +1311,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
             fetch_w2();                       // in flight during the h1 wait; live in this phase only
             f32x4 gh[NB];
             if (!poll_granules<NB>(a.gh1, o, B, tp + 1, gh, errw, ticks, 7, 0)) { ok = false; break; }
-            WN_GT(1);
 #pragma unroll
             for (int b = 0; b < NB; ++b) s_h1[b * 256 + o] = gh[b][0];
             if (!chain_sync(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
@@ -1773,7 +1394,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
             ok = false;
             break;
           }
-          WN_GT(1);
           const float wa0 = wgl[0], wa1 = wgl[1], wa2 = wgl[2], wb0 = wgl[3], wb1 = wgl[4], wb2 = wgl[5];
 #pragma unroll
           for (int b = 0; b < NB; ++b) {
@@ -1795,7 +1415,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
         // producers run
         fetch_res(l);
         if (!reduce_park(acc)) { ok = false; break; }
-        WN_GT(2);
         if (wave == 0 && lane < B) {
           const int b = lane;
           float pta = 0.f, ptb = 0.f;
@@ -1810,7 +1429,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
             pta = pva.x;
             ptb = pvb.x;
           }
-          WN_GT(3);
           const float za = psum(b) + (pre_a + pta), zb = psum(NB + b) + (pre_b + ptb);
           const float gv = tanhf(za) * avc_sigmoid(zb);
           float x0n, x1n;
@@ -1825,7 +1443,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
             skip_acc = l - 1 == 0 ? sv : (a.legacy ? (skip_acc + sv) * kSqrtHalf : skip_acc + sv);
           }
           st4_sc1(a.gring + ((int64_t)l * RING + ts) * RB4, (b * 256 + os) * 4, gv, x0n, x1n, t + 1);
-          WN_GT(4);
         }
         ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
       } else if (p == L) {
@@ -1835,31 +1452,25 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
           ok = false;
           break;
         }
-        WN_GT(1);
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[b] = rw2 * gin[b][0];
         if (!reduce_park(acc)) { ok = false; break; }
-        WN_GT(2);
         if (wave == 0 && lane < B) {
           const float sv = psum(lane) + bsk_last;
           const float sk = L - 1 == 0 ? sv : (a.legacy ? (skip_acc + sv) * kSqrtHalf : skip_acc + sv);
           st4_sc1(a.gsk, (lane * 256 + os) * 4, sk, 0.f, 0.f, t + 1);
-          WN_GT(4);
         }
         noise(t);
       } else {
         // ---- head: h1 row os = relu(W1[os] relu(skip) + b1[os])
         f32x4 gs[NB];
         if (!poll_granules<NB>(a.gsk, o, B, t + 1, gs, errw, ticks, 6, L + 1)) { ok = false; break; }
-        WN_GT(1);
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[b] = w1o * fmaxf(gs[b][0], 0.f);
         if (!reduce_park(acc)) { ok = false; break; }
-        WN_GT(2);
         if (wave == 0 && lane < B) {
           const float h = fmaxf(psum(lane) + b1o, 0.f);
           st4_sc1(a.gh1, (lane * 256 + os) * 4, h, 0.f, 0.f, t + 1);
-          WN_GT(4);
           a.h1[(int64_t)lane * S + os] = h;   // plain copy for the last step's sample (wn_final_sample_kernel)
         }
       }
@@ -1945,25 +1556,24 @@ int get_graph(const WnArgs& a, int steps, int slot0, int prow0, hipGraphExec_t* 
   return avc::kOk;
 }
 
-// XCD-local generation: AVC_WN_XCD=0 / autovc_wavenet_set_xcd(0) select the per-layer launches
-int g_wn_xcd = [] { const char* e = getenv("AVC_WN_XCD"); return e ? atoi(e) : 0; }();
 int g_wn_timeout_ticks = 100000000;   // 1 s of s_memrealtime (100 MHz) per phase wait
-
-bool xcd_eligible(int B, int n_layers, int taps, int R, int G, int S) {
-  if (!g_wn_xcd || B > 8 || n_layers < 1 || taps != 3 || R != 512 || G != 512 || S != 256) return false;
-  static const bool dev_ok = [] {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    return cus == 8 * kXSlots;              // 8 XCDs x 32 CUs (MI355X)
-  }();
-  return dev_ok;
-}
 
 // All-CU weight-resident generation (wn_grid_kernel): 0 never, 1 every eligible batch, 2 (the
 // default) up to two utterances — the measured crossover: B = 1 86.5, B = 2 101.1 us per sample
 // step against 103.8 / 104.6 for the launches, B = 4 and up slower (profiles/r04/wn_grid_ab.txt).
-int g_wn_grid = [] { const char* e = getenv("AVC_WN_GRID"); return e ? atoi(e) : 2; }();
+// AVC_WN_GRID outside 0..2 is rejected by the first generate call (g_wn_grid_bad), as
+// autovc_wavenet_set_grid rejects it, rather than read as "every batch" with its fault unread
+int g_wn_grid_bad = 0;
+int g_wn_grid = [] {
+  const char* e = getenv("AVC_WN_GRID");
+  if (!e) return 2;
+  if ((e[0] == '0' || e[0] == '1' || e[0] == '2') && e[1] == 0) return e[0] - '0';
+  g_wn_grid_bad = 1;
+  return 2;
+}();
+// which path the last autovc_wavenet_generate_f32 call took: 0 the per-layer launches, 1 the
+// all-CU persistent kernel (whose fault word the caller must read)
+int g_wn_last_path = 0;
 
 template <int NB>
 bool grid_attr(int bytes) {
@@ -2006,29 +1616,17 @@ int64_t ring_frames(int n_layers, int lps, int K) {
 extern "C" {
 
 
-int autovc_wavenet_set_xcd(int on) {
-  AVC_CHECK_ARG(on == 0 || on == 1, "autovc_wavenet_set_xcd: 0 or 1");
-  g_wn_xcd = on;
-  return avc::kOk;
-}
-
-int autovc_wavenet_get_xcd(void) { return g_wn_xcd; }
-
 int autovc_wavenet_set_grid(int on) {
   AVC_CHECK_ARG(on == 0 || on == 1 || on == 2, "autovc_wavenet_set_grid: 0 (off), 1 (B <= 8) or 2 (B <= 2)");
   g_wn_grid = on;
+  g_wn_grid_bad = 0;
   return avc::kOk;
 }
 
 int autovc_wavenet_get_grid(void) { return g_wn_grid; }
 
-#ifdef AVC_WN_GRID_TRACE
-extern "C" int autovc_wavenet_grid_trace(int* out) {   // trace builds only: 2 x 26 x 5 ints
-  AVC_HIP(hipDeviceSynchronize(), "hipDeviceSynchronize");
-  AVC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wn_grid_trace), sizeof(int) * 2 * (kGMaxL + 2) * 5), "trace");
-  return avc::kOk;
-}
-#endif
+int autovc_wavenet_last_path(void) { return g_wn_last_path; }
+
 
 int autovc_wavenet_grid_diag(int clear, int* out5) {
   AVC_CHECK_ARG(out5 != nullptr, "autovc_wavenet_grid_diag: null out");
@@ -2078,7 +1676,7 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
                          2 * (int64_t)n_layers * B * G + (int64_t)(S / kHR) * B * kMaxNO + 7 * 64;
   const int64_t grid = 16 * ((int64_t)n_layers * ring_frames(n_layers, layers_per_stack, taps) * B * 256 + 2 * (int64_t)B * 256) +
                        8 * 2 * (int64_t)n_layers * B * 512;   // wn_grid_kernel's tagged granules
-  return floats * 4 + kCtrSlots * 4 + (int64_t)kXBarLines * kXLn * 4 + kGErrInts * 4 + grid + 1024;
+  return floats * 4 + kCtrSlots * 4 + kGErrInts * 4 + grid + 1024;
 }
 
 int autovc_wavenet_upsample_f32(int B, int Tc, int C, int n_stages, const int* scales, const float* c,
@@ -2110,6 +1708,8 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
                                 int teacher_len, float* y_out, float* mol_out, void* workspace, int graph_steps,
                                 hipStream_t stream) {
   static const char* fn = "autovc_wavenet_generate_f32";
+  AVC_CHECK_ARG(!g_wn_grid_bad, "%s: AVC_WN_GRID must be 0 (per-layer launches), 1 (all-CU kernel for B <= 8) or 2 "
+                "(all-CU kernel for B <= 2, the default)", fn);
   AVC_CHECK_ARG(B > 0 && T > 0 && 0 <= t0 && t0 < t1 && t1 <= T, "%s: bad range B=%d T=%d t=[%d,%d)", fn, B, T, t0, t1);
   AVC_CHECK_ARG(Tch > 0 && t1 - t0 <= Tch, "%s: chunk [%d,%d) longer than the conditioning chunk %d", fn, t0, t1, Tch);
   AVC_CHECK_ARG(n_layers >= 1 && n_layers + 2 < kCtrSlots && layers_per_stack >= 1 && layers_per_stack <= 16 &&
@@ -2144,8 +1744,7 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   a.ptap = ws;                 ws += round64(2 * (int64_t)n_layers * B * G);
   a.molp = ws;                 ws += round64((int64_t)(S / kHR) * B * kMaxNO);
   a.ctr = reinterpret_cast<int*>(ws);
-  int* xbar = a.ctr + kCtrSlots;   // the XCD-local generation's census / phase counters
-  int* gerr = xbar + kXBarLines * kXLn;   // the all-CU generation's error word (one line)
+  int* gerr = a.ctr + kCtrSlots;   // the all-CU generation's error word (one line)
   {
     float* g = reinterpret_cast<float*>(gerr + kGErrInts);
     a.gring = g;  g += 4 * (int64_t)n_layers * RING * B * 256;
@@ -2162,26 +1761,16 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
                 "%s: workspace layout overflow", fn);
 
   if (t0 == 0) AVC_HIP(avc::zero_async(workspace, (size_t)used, stream), "zero_async");
+  g_wn_last_path = 0;
   if (grid_eligible(B, n_layers, taps, R, G, S, n_out)) {
     // one persistent launch for the whole call, every gate weight of the chain on chip (wn_grid_kernel)
+    g_wn_last_path = 1;
     AVC_HIP(avc::zero_async(gerr, (size_t)kGErrInts * 4, stream), "zero_async");
     const int lds = 4 * g_lds(n_layers, n_out).total;
     if (B == 1) hipLaunchKernelGGL(wn_grid_kernel<1>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
     else if (B == 2) hipLaunchKernelGGL(wn_grid_kernel<2>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
     else if (B <= 4) hipLaunchKernelGGL(wn_grid_kernel<4>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
     else hipLaunchKernelGGL(wn_grid_kernel<8>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
-    AVC_CHECK_LAUNCH(fn);
-    if (t1 == T) {
-      hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);
-      AVC_CHECK_LAUNCH(fn);
-    }
-    return avc::kOk;
-  }
-  if (xcd_eligible(B, n_layers, taps, R, G, S)) {
-    // one persistent launch for the whole call: utterance x on XCD x (see wn_xcd_kernel)
-    AVC_HIP(avc::zero_async(xbar, (size_t)kXBarLines * kXLn * 4, stream), "zero_async");
-    hipLaunchKernelGGL(wn_xcd_kernel, dim3(8 * kXSlots), dim3(64 * kXW), 0, stream, a, t0, t1, xbar,
-                       g_wn_timeout_ticks);
     AVC_CHECK_LAUNCH(fn);
     if (t1 == T) {
       hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);

@@ -13,7 +13,6 @@
 #include <algorithm>
 
 #include "common.h"
-#include "bn_finalize.h"
 #include "../../include/autovc_hip.h"
 
 namespace {
@@ -405,77 +404,6 @@ __global__ __launch_bounds__(kThreads) void wino_output_stats_kernel(int T, int 
   block_pairs(s1, s2, C, c, part);
 }
 
-// wino_output_stats_kernel with the BatchNorm finalize in the same launch (no separate
-// stats_finalize_raw_kernel): each block writes its partial row through to memory (sc1) and
-// takes a ticket on its (column block, row group rs mod 16) counter; the block that completes
-// a row group sums that group's rows (rs = g, g + 16, ...: sum_partials' order) into a group
-// partial and takes a ticket on the column block's counter; the block that completes the 16
-// groups adds them in group order (sum_partials' order, so mean / var / coef are bit-identical
-// to the two-launch form) and finishes the channels (avc::bn_finalize_channel).  At most 16
-// arrivals per counter (a counter every block hits serialises: measured on the colsum).
-// Workspace (autovc_wino5_bnstats_workspace_bytes): tickets (zeroed once, left zeroed), RS
-// partial rows, 16 group partials.
-using avc::BnFin;
-using avc::kBnTickets;
-
-__global__ __launch_bounds__(kThreads) void wino_output_bnstats_kernel(int T, int C, const float* __restrict__ Yt,
-                                                                  const float* __restrict__ bias, float* __restrict__ y,
-                                                                  int64_t ldy, int64_t ntiles, int* __restrict__ tk,
-                                                                  double* __restrict__ part, double* __restrict__ gpart,
-                                                                  BnFin f) {
-  const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
-  const WaveTiles wt = wave_tiles(T, ntiles);
-  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  if (c < C && wt.live) {
-    f32x4 m[kTPW][8];
-#pragma unroll
-    for (int i = 0; i < kTPW; ++i)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) m[i][k] = ld4(Yt + ((int64_t)k * ntiles + wt.tile0 + i) * C + c);
-    const f32x4 bv = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < kTPW; ++i)
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        f32x4 v = bv;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (kAT[o][k] != 0.f) v += kAT[o][k] * m[i][k];
-        st4(y + (wt.b * T + 4 * (wt.q0 + i) + o) * ldy + c, v);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s1[e] += (double)v[e];
-          s2[e] += (double)v[e] * (double)v[e];
-        }
-      }
-  }
-  // the block's partial row (block_pairs' fixed wave order), written through
-  __shared__ double red[kWaves][64][8];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    red[w][lane][2 * e] = s1[e];
-    red[w][lane][2 * e + 1] = s2[e];
-  }
-  __syncthreads();
-  const int rs = blockIdx.y, RS = gridDim.y, cb = blockIdx.x;
-  if (w == 0 && c < C) {
-    double a8[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      double a = red[0][lane][e];
-#pragma unroll
-      for (int q = 1; q < kWaves; ++q) a += red[q][lane][e];
-      a8[e] = a;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) avc::st_f64x2_sc1(part, ((int64_t)rs * C + c + e) * 2, a8[2 * e], a8[2 * e + 1]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  avc::bn_stats_complete(tk, part, gpart, C, cb * 256, 256, rs, RS, cb, f);
-}
-
 // Input gradient of a conv whose input is the previous layer's BN + activation output:
 // dz = A^T Yd~ (the output transform of the flipped correlation) and, for that layer's
 // BatchNorm backward, part[rs][c] = (sum g, sum g (y - mean)) with g = act'(pre) dz
@@ -678,35 +606,6 @@ extern "C" int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Y
   hipLaunchKernelGGL(wino_output_stats_kernel, dim3((C / 4 + 63) / 64, (unsigned)autovc_wino5_rows(B, T)), dim3(kThreads),
                      0, stream, T, C, Yt, bias, y, ldy, ntiles, part);
   AVC_CHECK_LAUNCH("autovc_wino5_output_stats_f32");
-  return avc::kOk;
-}
-
-extern "C" int64_t autovc_wino5_bnstats_workspace_bytes(int B, int T, int C) {
-  const int64_t RS = autovc_wino5_rows(B, T);
-  if (RS <= 0 || C <= 0) return -1;
-  return (int64_t)kBnTickets * 4 + (RS + 16) * (int64_t)C * 16;
-}
-
-extern "C" int autovc_wino5_output_bnstats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
-                                               int64_t ldy, const float* gamma, const float* beta, float eps,
-                                               float* mean, float* var, float* coef, float* run_mean, float* run_var,
-                                               float momentum, int64_t* nbt, void* workspace, hipStream_t stream) {
-  static const char* fn = "autovc_wino5_output_bnstats_f32";
-  AVC_CHECK_ARG(T % (4 * kTPW) == 0, "%s: T must be a multiple of %d", fn, 4 * kTPW);
-  AVC_CHECK_ARG(B > 0 && T > 0 && C > 0 && C % 4 == 0 && ldy % 4 == 0 && Yt && y && mean && var && coef && workspace,
-                "%s: bad args (T and C multiples of 4)", fn);
-  AVC_CHECK_ARG((C + 255) / 256 <= kBnTickets / 32, "%s: C = %d above %d channels", fn, C, 256 * kBnTickets / 32);
-  AVC_CHECK_ARG(AVC_ALIGNED16(Yt) && AVC_ALIGNED16(y) && (!bias || AVC_ALIGNED16(bias)) && AVC_ALIGNED16(workspace),
-                "%s: alignment", fn);
-  const int64_t ntiles = (int64_t)B * T / 4;
-  const int64_t RS = autovc_wino5_rows(B, T);
-  int* tk = static_cast<int*>(workspace);
-  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kBnTickets * 4);
-  double* gpart = part + RS * (int64_t)C * 2;
-  const BnFin f{gamma, beta, eps, mean, var, coef, run_mean, run_var, momentum, nbt, (int64_t)B * T};
-  hipLaunchKernelGGL(wino_output_bnstats_kernel, dim3((C / 4 + 63) / 64, (unsigned)RS), dim3(kThreads), 0, stream, T, C,
-                     Yt, bias, y, ldy, ntiles, tk, part, gpart, f);
-  AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
 }
 

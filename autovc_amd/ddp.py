@@ -151,8 +151,9 @@ def _run_exchange(items, grad_dtype, world, after=None, gates=None):
     any is waited on; `after(key)` runs as each bucket's mean lands (the Adam slice).
     gates (CUDA only): key -> callable(stream_ptr) that makes the communication stream wait
     until the bucket's gradients are final (functional.GradMarks.wait); the collectives and
-    the bf16 shard sums are then issued on that stream, in gate order, and only the
-    compute stream's finish (mean / copy back, Adam) waits for them."""
+    the bf16 shard sums are then issued on that stream in gate order (bucket i's shard sum
+    before bucket i+1's gate), and only the compute stream's finish (mean / copy back, Adam)
+    waits for them."""
     cls = _exchange(grad_dtype)
     if not gates:
         ex = [(k, cls(chunk, world)) for k, chunk in items]
@@ -181,13 +182,17 @@ def _run_exchange(items, grad_dtype, world, after=None, gates=None):
     # bucket's gate is an event recorded after the bucket's last gradient write of this step,
     # which the compute stream issued after everything earlier that touched the bucket (the
     # previous step's Adam and copy-back, this step's zero_grad)
+    # bucket i's second phase (the bf16 shard sum + all-gather) is issued before bucket i+1's
+    # gate wait, so it runs as soon as its own exchange lands instead of behind every gate
     ex = []
     with torch.cuda.stream(comm):
         for k, chunk in items:
+            if ex:
+                ex[-1][1].reduce()
             gates[k](comm.cuda_stream)
             ex.append((k, cls(chunk, world)))
-        for _, e in ex:
-            e.reduce()
+        if ex:
+            ex[-1][1].reduce()
     for k, e in ex:
         e.finish()
         if after is not None:

@@ -224,9 +224,22 @@ class GradMarks:
             self.events.append(tuple(pair))
         return self.events[k - 1][which]
 
+    # a flat-buffer gradient that autograd accumulates after the op returns (not through
+    # _GradOut's in-place path): final only at the last mark
+    FINAL = 1 << 30
+
     def log(self, buf, k):
         key = (buf.data_ptr(), buf.numel() * buf.element_size())
         self.ready[key] = max(self.ready.get(key, 0), k)
+
+    def snapshot(self):
+        """The mark structure of the backward just recorded (a captured step graph keeps it:
+        graph.StepGraphs restores it before each of that graph's replays)."""
+        return self.n, dict(self.ready), dict(self.side_at)
+
+    def restore(self, snap):
+        self.n, ready, side_at = snap
+        self.ready, self.side_at = dict(ready), dict(side_at)
 
     def mark(self, dev, side, outs):
         self.n += 1
@@ -252,7 +265,7 @@ class GradMarks:
         for (p, n), k in self.ready.items():
             if p < ptr + nbytes and ptr < p + n:
                 r = max(r, k)
-        return r if r else self.n
+        return min(r, self.n) if r else self.n
 
     def wait(self, stream_ptr, k):
         """Make `stream_ptr` wait for mark k's events."""
@@ -342,9 +355,27 @@ class _GradOut:
         self.buf = g if self.acc else torch.empty(shape, device=device, dtype=torch.float32)
         if self.acc and MARKS.active:
             MARKS.log(self.buf, MARKS.n + 1)      # a main-stream write: final at the next mark
+        elif g is not None and MARKS.active:
+            # returned to autograd (padded / mixed destinations), which adds it into the flat
+            # .grad later, in no mark's view: the bucket holding it waits for the last mark
+            MARKS.log(g, GradMarks.FINAL)
 
     def result(self):
         return None if self.acc else self.buf
+
+
+def _bias_outs(p_ih, p_hh, shape, dev):
+    """Destinations of an LSTM layer's two bias gradients (one column-sum launch writes both):
+    both in place when both live in the flat buffer, else two fresh tensors handed to autograd
+    (whose later accumulation the gradient-ready marks then see only at the last mark)."""
+    gi, gh = _GradOut(p_ih, shape, dev), _GradOut(p_hh, shape, dev)
+    if gi.acc == gh.acc:
+        return gi, gh
+    if MARKS.active:
+        for o in (gi, gh):
+            if o.acc:
+                MARKS.log(o.buf, GradMarks.FINAL)
+    return _GradOut(None, shape, dev), _GradOut(None, shape, dev)
 
 
 # ---------------------------------------------------------------- Conv1d + BN + act
@@ -466,9 +497,6 @@ def prepare_weights(convs, lstms, T, training, B=None):
             continue
         mats = [m.weight_hh_l0] if m.num_layers == 1 else [m.weight_hh_l0, m.weight_ih_l1, m.weight_hh_l1]
         kinds = ((6, 8) if training else (6,)) if _bf16_rec(H) else ((7,) if training else ())
-        if m.num_layers == 2 and training and B is not None and lstm2_bwd_persistent(B, H):
-            # the persistent backward reads the (4H, H) weights (or the bf16 copies) as they are
-            kinds = tuple(k for k in kinds if k not in (7, 8))
         for W in mats:
             if _cacheable(W):
                 for kind in kinds:
@@ -700,10 +728,9 @@ def conv_bn_act(x, conv, bn, act, residual=None):
 _CHAIN_ON = os.environ.get("AVC_CONV_CHAIN", "1") != "0"
 
 
-# the stacks' BatchNorm statistics finalized inside the launch that reduces them (fp32:
-# autovc_wino5_output_bnstats_f32, bf16: autovc_bnconv_fwd_bnstats_bf16_f32; bit-identical);
-# AVC_BN_FUSED_STATS=0 keeps the separate finalize launch
-_BN_FUSED_STATS = os.environ.get("AVC_BN_FUSED_STATS", "0") != "0"
+# (The stacks' BatchNorm statistics finalized inside the launch that reduces them measured
+# slower than the separate 5 us finalize launch — fp32 14.58-14.63 vs 14.51-14.52 ms/step, bf16
+# 9.11 vs 8.96-8.98, profiles/r04/ab_bn_fused_stats.txt — and is retired to tools/retired/.)
 
 
 def _chain_ok(x, layers, training):
@@ -776,18 +803,12 @@ class ConvBNChainFn(torch.autograd.Function):
             if training:
                 mean = torch.empty(Co, device=dev, dtype=torch.float32)
                 var = torch.empty(Co, device=dev, dtype=torch.float32)
-                if _BN_FUSED_STATS:   # output transform + statistics + finalize in one launch
-                    ws = _ws(dev, lib.autovc_wino5_bnstats_workspace_bytes(B, T, Co), "chain_fwd_fused")
-                    _lib.call("autovc_wino5_output_bnstats_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co,
-                              _p(g), _p(be), float(epss[l]), mean.data_ptr(), var.data_ptr(), coef.data_ptr(), _p(rm),
-                              _p(rv), float(moms[l]), _p(nbt), ws, _s())
-                else:
-                    part = _ws(dev, RS * Co * 16, "chain_fwd")
-                    _lib.call("autovc_wino5_output_stats_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, part,
-                              _s())
-                    _lib.call("autovc_bn_finalize_f32", RS, M, Co, part, _p(g), _p(be), float(epss[l]),
-                              mean.data_ptr(), var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt),
-                              _s())
+                part = _ws(dev, RS * Co * 16, "chain_fwd")
+                _lib.call("autovc_wino5_output_stats_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, part,
+                          _s())
+                _lib.call("autovc_bn_finalize_f32", RS, M, Co, part, _p(g), _p(be), float(epss[l]),
+                          mean.data_ptr(), var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt),
+                          _s())
             else:
                 _lib.call("autovc_wino5_output_f32", B, T, Co, Yt.data_ptr(), _p(b), y.data_ptr(), Co, _s())
                 mean, var = rm, rv
@@ -970,17 +991,9 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
             else:
                 xin, xcoef, xact, src = ys[-1], coefs[-1], ACT[acts[l - 1]], 0
             coef = torch.empty((4, Co), device=dev, dtype=torch.float32)
-            if training and _BN_FUSED_STATS:   # the statistics finalized inside the reduce launch
-                mean = torch.empty(Co, device=dev, dtype=torch.float32)
-                var = torch.empty(Co, device=dev, dtype=torch.float32)
-                sws = _ws(dev, lib.autovc_bnconv_bnstats_workspace_bytes(M, Co), "chain_fwd_fused")
-                _lib.call("autovc_bnconv_fwd_bnstats_bf16_f32", B, T, Ci, Co, xin.data_ptr(), _p(xcoef), xact,
-                          Wf.data_ptr(), _p(b), y.data_ptr(), _p(g), _p(be), float(epss[l]), mean.data_ptr(),
-                          var.data_ptr(), coef.data_ptr(), _p(rm), _p(rv), float(moms[l]), _p(nbt), sws, src, ws, _s())
-            else:
-                _lib.call("autovc_bnconv_fwd_bf16_f32", B, T, Ci, Co, xin.data_ptr(), _p(xcoef), xact, Wf.data_ptr(),
-                          _p(b), y.data_ptr(), part, src, ws, _s())
-            if training and not _BN_FUSED_STATS:
+            _lib.call("autovc_bnconv_fwd_bf16_f32", B, T, Ci, Co, xin.data_ptr(), _p(xcoef), xact, Wf.data_ptr(),
+                      _p(b), y.data_ptr(), part, src, ws, _s())
+            if training:
                 mean = torch.empty(Co, device=dev, dtype=torch.float32)
                 var = torch.empty(Co, device=dev, dtype=torch.float32)
                 _lib.call("autovc_bn_finalize_f32", RS, M, Co, part, _p(g), _p(be), float(epss[l]), mean.data_ptr(),
@@ -1281,18 +1294,6 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     B, T, I = x.shape
     H = W_hh.shape[1]
     dev = x.device
-    if not _bf16_rec(H) and lstm_xcd(B, H) and _XCD_BWD_ON:
-        # one XCD-local persistent launch (the recurrent product reads W_hh untransposed)
-        dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-        ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmx")
-        mark = _grad_mark(dev)
-        _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
-                  W_hh.data_ptr(), dG.data_ptr(), ws, _s())
-        if _XCD_FLUSH == "before":
-            _flush_grad_queue(after=mark)
-        elif _XCD_FLUSH == "after":
-            _flush_grad_queue()
-        return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs)
     # W_hh^T (fp32, or its bf16 copy under bf16): from the step's weight scope when there is one
     WT = conv_weight(W_hh, 8 if _bf16_rec(H) else 7)
     # split-K of the recurrent product (same box, alternating): fp32 4 ways at H=1024 (256
@@ -1337,9 +1338,7 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
                                                      splits=_splits_for(4 * H, H, M), accumulate=go.acc), dG, h)
         dWhh = go.result()
     if needs[3] or needs[4]:
-        gi, gh = _GradOut(p_bih, (4 * H,), dev), _GradOut(p_bhh, (4 * H,), dev)
-        if gi.acc != gh.acc:
-            gi, gh = _GradOut(None, (4 * H,), dev), _GradOut(None, (4 * H,), dev)
+        gi, gh = _bias_outs(p_bih, p_bhh, (4 * H,), dev)
         _grad_launch(dev, (gi, gh), lambda gi=gi, gh=gh: colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc),
                      dG)
         dbih, dbhh = gi.result(), gh.result()
@@ -1347,6 +1346,59 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
         dx = torch.empty_like(x)
         gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I)
     return dx, dWih, dWhh, dbih, dbhh
+
+
+# Time-chunked LSTM weight gradients: decoder lstm2's four dW GEMMs
+# (3 x 4096 x 1024 + 4096 x 512 over K = B*T) run in AVC_DW_CHUNKS pieces of T / chunks steps
+# each, started on the gradient side stream as the stacked backward finishes each chunk,
+# instead of as four whole-sequence GEMMs released beside lstm1's backward.  Chunk order is
+# fixed (deterministic); the sums differ from the whole-sequence GEMM's only in fp32 order.
+# Measured and NOT adopted (profiles/r05/ab_dw_chunks.txt, alternating, one box): fp32
+# 14.53 ms/step whole vs 15.69-15.72 (4 chunks) and 16.62 (2); bf16 9.02-9.05 vs 9.74-9.78 and
+# 10.12-10.19.  The stacked backward's step launches need three workgroups on every CU at once;
+# beside a weight-gradient GEMM (one 67 KB-LDS workgroup per CU, the reserve keeping room for
+# one step workgroup) each step runs in three rounds, which costs far more than the GEMMs
+# that were spilling past lstm1's backward.  0 / 1 = off (the default).
+_DW_CHUNKS = int(os.environ.get("AVC_DW_CHUNKS", "0"))
+
+
+def _chunked_dw_plan(T, specs, dev):
+    """(chunks, Tc, jobs) for the time-chunked weight gradients of one stacked backward, or
+    None (off, T not divisible, or a destination outside the optimizer's flat buffer — the
+    chunks accumulate into it).  specs: (dG, input, W, param, tap0, needed) per weight."""
+    n = _DW_CHUNKS
+    if n < 2 or not _GRAD_STREAM_ON or T % n or T // n < 4:
+        return None
+    jobs = []
+    for dG, X, W, p, tap0, need in specs:
+        if not need:
+            continue
+        go = _GradOut(p, W.shape, dev)
+        if not go.acc:
+            return None
+        jobs.append((go, dG, X, tap0))
+    return n, T // n, jobs
+
+
+def _queue_dw_chunk(jobs, B, T, t0, Tc, dev):
+    """Queue the weight-gradient GEMMs of steps [t0, t0 + Tc) (autovc_gemm_tchunk_*) for the
+    side stream, accumulating into the flat gradient buffer."""
+    for go, dG, X, tap0 in jobs:
+        M, N = go.buf.shape
+
+        def fn(go=go, dG=dG, X=X, tap0=tap0, M=M, N=N):
+            K = B * Tc
+            lib = _lib.load()
+            if _PRECISION[0] == "bf16":
+                sp = lib.autovc_gemm_bf16_splits(M, N, K, 1)
+                name = "autovc_gemm_tchunk_bf16_f32"
+            else:
+                sp = _splits_for(M, N, K)
+                name = "autovc_gemm_tchunk_f32"
+            ws = _ws(dev, 4 * lib.autovc_gemm_workspace_floats(M, N, sp), "gemm") if sp > 1 else 0
+            _lib.call(name, M, N, B, T, t0, Tc, dG.data_ptr(), dG.shape[2], X.data_ptr(), X.shape[2], tap0,
+                      go.buf.data_ptr(), N, 1, sp, ws, _s())
+        _grad_launch(dev, go, fn, dG, X)
 
 
 # decoder lstm2 forward (fp32) as ONE persistent weight-stationary launch
@@ -1368,9 +1420,7 @@ class DeviceFault(RuntimeError):
 _FAULT_BITS = (
     (1, "lstm_persist_kernel / lstm2_rs_kernel, two layers (decoder lstm2 forward)", "h/c", "AVC_LSTM2_PERSIST=0"),
     (2, "lstm_xcd_fwd_kernel (decoder lstm1 forward)", "h/c", "AVC_LSTM_XCD=0"),
-    (4, "lstm_xcd_bwd_kernel (decoder lstm1 backward)", "gate gradients", "AVC_LSTM_XCD_BWD=0"),
     (8, "lstm_persist_kernel, one layer (decoder lstm1 forward)", "h/c", "AVC_LSTM_PERSIST=0"),
-    (16, "lstm2_bwd_persist_kernel (decoder lstm2 backward)", "gate gradients", "AVC_LSTM2_BWD_PERSIST=0"),
 )
 
 
@@ -1408,13 +1458,10 @@ def lstm_persistent(B, H):
 _XCD_ON = os.environ.get("AVC_LSTM_XCD", "1") != "0"
 
 
-# the backward the same way is opt-in (AVC_LSTM_XCD_BWD=1): alone 4.2 vs 9.3 us per step, but
-# in the training step the split-K launches' idle CUs host ~1 ms of queued weight-gradient
-# GEMMs that the all-CU persistent kernel cannot, so the step measured 15.91 (released beside
-# it) / 16.93 (after it) / 15.99-16.03 (deferred) vs 15.65-15.67 ms with the split-K backward
-# (profiles/r03/ab_lstm_xcd.txt).  AVC_XCD_FLUSH picks where the queued gradients go.
-_XCD_BWD_ON = os.environ.get("AVC_LSTM_XCD_BWD", "0") != "0"
-_XCD_FLUSH = os.environ.get("AVC_XCD_FLUSH", "before")
+# The backward the same way (lstm_xcd_bwd_kernel: 4.2 vs 9.3 us per step alone) lost inside
+# the training step, where the split-K launches' idle CUs host queued weight-gradient GEMMs
+# (15.91-16.93 vs 15.65 ms/step, profiles/r03/ab_lstm_xcd.txt): retired to
+# tools/retired/ (round 5), the fused split-K backward step is the product path.
 
 
 def lstm_xcd(B, H):
@@ -1505,72 +1552,59 @@ class LSTM2StackFn(torch.autograd.Function):
             splits //= 2
         dG1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
         dG0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-        if lstm2_bwd_persistent(B, H):
-            LSTM2StackFn._backward_persistent(ctx, dh1, dG1, dG0)
-            grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
-            grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)
-            return (grads0[0], *grads0[1:], *grads1[1:], None)
         # the (H, 4H) transposes (bf16 copies under bf16), from the step's weight scope if any
         kt = 8 if _bf16_rec(H) else 7
         WT1, WIT1, WT0 = conv_weight(W_hh1, kt), conv_weight(W_ih1, kt), conv_weight(W_hh0, kt)
         ws = _ws(dev, 4 * _lib.load().autovc_lstm2_bwd_workspace_floats(B, H, splits), "lstm")
+        bf = _bf16_rec(H)
+        if bf:
+            dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
+
+        def steps(s0, s1):
+            if bf:
+                _lib.call("autovc_lstm2_bwd_range_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(),
+                          c1.data_ptr(), g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(),
+                          WT0.data_ptr(), dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), splits,
+                          s0, s1, ws, _s())
+            else:
+                _lib.call("autovc_lstm2_bwd_range_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(),
+                          c1.data_ptr(), g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(),
+                          WT0.data_ptr(), dG1.data_ptr(), dG0.data_ptr(), splits, s0, s1, ws, _s())
+
         mark = _grad_mark(dev)   # queued weight gradients run beside the recurrences
-        if _bf16_rec(H):
-            dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
-            _lib.call("autovc_lstm2_bwd_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                      g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(),
-                      dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), splits, ws, _s())
-        else:
-            _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                      g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(), WT0.data_ptr(), dG1.data_ptr(),
-                      dG0.data_ptr(), splits, ws, _s())
-        _flush_grad_queue(after=mark)
-        grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
-        grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)
-        return (grads0[0], *grads0[1:], *grads1[1:], None)
-
-
-    @staticmethod
-    def _backward_persistent(ctx, dh1, dG1, dG0):
-        """Both recurrences' backward as ONE persistent weight-stationary launch
-        (autovc_lstm2_bwd_persist_*: the (4H, H) weights themselves, or their bf16 copies
-        under bf16).  The weight gradients queued before it stay queued and are released at
-        the next recurrence (lstm1's backward): launched beside a kernel that needs every CU
-        they would only delay its start (AVC_LSTM2_BWD_FLUSH=beside releases them here)."""
-        x, W_ih0, W_hh0, h0, c0, g0, W_ih1, W_hh1, h1, c1, g1 = ctx.saved_tensors
-        B, T, _ = x.shape
-        H = W_hh0.shape[1]
-        dev = x.device
-        lib = _lib.load()
-        ws = _ws(dev, lib.autovc_lstm2_bwd_persist_workspace_bytes(B, T, H), "lstm2bp")
-        mark = _grad_mark(dev) if _BWD_FLUSH == "beside" else None
-        if _bf16_rec(H):
-            W1b, Wi1b, W0b = conv_weight(W_hh1, 6), conv_weight(W_ih1, 6), conv_weight(W_hh0, 6)
-            dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
-            _lib.call("autovc_lstm2_bwd_persist_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                      g0.data_ptr(), c0.data_ptr(), W1b.data_ptr(), Wi1b.data_ptr(), W0b.data_ptr(), dG1.data_ptr(),
-                      dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), ws, _s())
-        else:
-            _lib.call("autovc_lstm2_bwd_persist_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                      g0.data_ptr(), c0.data_ptr(), W_hh1.data_ptr(), W_ih1.data_ptr(), W_hh0.data_ptr(),
-                      dG1.data_ptr(), dG0.data_ptr(), ws, _s())
-        if mark is not None:
+        dw = _chunked_dw_plan(T, ((dG1, h0, W_ih1, ctx.params[1][0], 0, need1[1]),
+                                  (dG1, h1, W_hh1, ctx.params[1][1], -1, need1[2]),
+                                  (dG0, x, W_ih0, ctx.params[0][0], 0, need0[1]),
+                                  (dG0, h0, W_hh0, ctx.params[0][1], -1, need0[2])), dev)
+        if dw is None:
+            steps(0, T + 1)
             _flush_grad_queue(after=mark)
+            grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
+            grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)
+            return (grads0[0], *grads0[1:], *grads1[1:], None)
+        # time-chunked weight gradients: after iterations [0, (c + 1) Tc + 1) the last
+        # (c + 1) Tc steps of both layers' dG are final, so chunk c's four dW GEMMs start
+        # on the side stream while the recurrence runs the next chunk
+        nch, Tc, jobs = dw
+        s0 = 0
+        for c in range(nch):
+            s1 = T + 1 if c == nch - 1 else (c + 1) * Tc + 1
+            steps(s0, s1)
+            if c == 0:
+                _flush_grad_queue(after=mark)
+            _queue_dw_chunk(jobs, B, T, T - (c + 1) * Tc, Tc, dev)
+            if c < nch - 1:     # the last chunk waits for the next recurrence, like every other dW
+                _flush_grad_queue(after=_grad_mark(dev))
+            s0 = s1
+        grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False, False, False) + tuple(need1[3:]))
+        grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], (need0[0], False, False) + tuple(need0[3:]))
+        return (grads0[0], None, None, *grads0[3:], None, None, *grads1[3:], None)
 
 
-# decoder lstm2 backward as ONE persistent launch (lstm2_bwd_persist_kernel) — opt-in
-# (AVC_LSTM2_BWD_PERSIST=1, B = 64, H = 1024, 256 CUs): measured slower than the per-step
-# product + pointwise launches (T = 128: fp32 28.9 vs 24.4 us per wavefront step, bf16 21.0
-# vs 14.8; training step 20.0 vs 14.6 ms before the reduction / prefetch fixes,
-# profiles/r04/lstm2_bwd_persist_time.txt): the per-step group reduction of the K-slice
-# partials, the write-through dG hand-off and the grid barrier cost ~11 us per step, against
-# the launch pair's ~5 us (DESIGN.md section 4, round 4)
-_BWD_PERSIST_ON = os.environ.get("AVC_LSTM2_BWD_PERSIST", "0") != "0"
-_BWD_FLUSH = os.environ.get("AVC_LSTM2_BWD_FLUSH", "defer")
-
-
-def lstm2_bwd_persistent(B, H):
-    return _BWD_PERSIST_ON and bool(_lib.load().autovc_lstm2_bwd_persist_supported(B, H))
+# The persistent decoder-lstm2 backward (lstm2_bwd_persist_kernel: 28.9 vs 24.4 us per
+# wavefront step fp32, 21.0 vs 14.8 bf16, profiles/r04/lstm2_bwd_persist_time.txt) is retired to
+# tools/retired/ (round 5): its per-step K-slice reduction, hand-off and grid barrier cost more
+# than the launch boundary it saves.
 
 
 class BLSTMLayerFn(torch.autograd.Function):
@@ -1628,9 +1662,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                      b_conv=(T, H, -1 if d == 0 else 1), splits=_splits_for(G, H, M), accumulate=go.acc)
                 grads[iH] = go.result()
             if ctx.needs_input_grad[iBi] or ctx.needs_input_grad[iBh]:
-                gi, gh = _GradOut(pBi, (G,), dev), _GradOut(pBh, (G,), dev)
-                if gi.acc != gh.acc:
-                    gi, gh = _GradOut(None, (G,), dev), _GradOut(None, (G,), dev)
+                gi, gh = _bias_outs(pBi, pBh, (G,), dev)
                 colsum(dG2[:, d * G:(d + 1) * G], gi.buf, gh.buf, accumulate=gi.acc)
                 grads[iBi], grads[iBh] = gi.result(), gh.result()
         dx = None

@@ -69,7 +69,10 @@ class StepGraphs:
         with torch.no_grad():
             for b, s in zip(self.module.buffers(), saved):
                 b.copy_(s)
-        return graph, static, out
+        # the gradient-ready marks this graph records (data-parallel exchange): each cached
+        # graph has its own mark structure, restored before each of its replays
+        marks = AF.MARKS.snapshot() if AF.MARKS.active else None
+        return graph, static, out, marks
 
     def run(self, key, *inputs):
         full_key = (key,) + tuple((tuple(t.shape), t.dtype, t.device) for t in inputs)
@@ -77,7 +80,9 @@ class StepGraphs:
         if entry is None:
             entry = self._capture(inputs)
             self._graphs[full_key] = entry
-        graph, static, out = entry
+        graph, static, out, marks = entry
+        if marks is not None:
+            AF.MARKS.restore(marks)
         for s, t in zip(static, inputs):
             if s.data_ptr() != t.data_ptr():
                 s.copy_(t)

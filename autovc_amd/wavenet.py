@@ -331,34 +331,21 @@ class WaveNet(nn.Module):
                       pre.data_ptr(), chunk, int(seed) & ((1 << 64) - 1), int(utt_base), float(log_scale_min),
                       _lib.ptr(tch), 0 if tch is None else tch.shape[1], y.data_ptr(), _lib.ptr(mol),
                       ws.data_ptr(), int(graph_steps), stream)
-        # the persistent generations poison their outputs and set a fault word if a hand-off
-        # wait timed out (their workgroups were not all resident): surface it here.  Reading
-        # the word synchronises the device, so only those modes pay for it.
-        fault = ctypes.c_int(0)
-        grid_mode = lib.autovc_wavenet_get_grid()
-        if lib.autovc_wavenet_get_xcd() or (grid_mode == 1 or (grid_mode == 2 and B <= 2)):
+        # the all-CU generation poisons its outputs and sets a fault word if a hand-off wait
+        # timed out (its 256 workgroups were not all resident): read it whenever that kernel
+        # ran (reading synchronises the device, so the per-layer launches do not pay for it)
+        # and raise — never silently regenerate on another path
+        if lib.autovc_wavenet_last_path() == 1:
+            fault = ctypes.c_int(0)
             _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(fault))
-        if fault.value & 2:
-            diag = (ctypes.c_int * 5)()
-            _lib.call("autovc_wavenet_grid_diag", 1, ctypes.addressof(diag))
-            if grid_mode == 2:
-                # the default (B <= 2) choice, not a request: warn, keep to the per-layer launches
-                # in this process, and generate again
-                warnings.warn("wn_grid_kernel (all-CU WaveNet generation) could not keep its 256 workgroups "
-                              f"resident (wait {tuple(diag)} timed out; another process on this GPU?): "
-                              "using the per-layer launches from now on", RuntimeWarning)
-                _lib.call("autovc_wavenet_set_grid", 0)
-                return self.generate(c, T=T, teacher=teacher, seed=seed, utt_base=utt_base,
-                                     return_mol=return_mol, log_scale_min=log_scale_min, chunk=chunk,
-                                     graph_steps=graph_steps)
-            raise RuntimeError("wn_grid_kernel (all-CU WaveNet generation): a hand-off wait timed out "
-                               f"(kind, step, phase, workgroup, tag seen = {tuple(diag)}) — its 256 workgroups were not all "
-                               "resident (another process on this GPU?); outputs are NaN. Set AVC_WN_GRID=0 to use "
-                               "the per-layer launches.")
-        if fault.value:
-            raise RuntimeError("wn_xcd_kernel (XCD-local WaveNet generation): a per-XCD phase wait timed out — "
-                               "its workgroups were not all resident (another process on this GPU?); outputs are NaN. "
-                               "Set AVC_WN_XCD=0 to use the per-layer launches.")
+            if fault.value:
+                diag = (ctypes.c_int * 5)()
+                _lib.call("autovc_wavenet_grid_diag", 1, ctypes.addressof(diag))
+                raise Fh.DeviceFault(
+                    "wn_grid_kernel (all-CU WaveNet generation): a hand-off wait timed out "
+                    f"(kind, step, phase, workgroup, tag seen = {tuple(diag)}) — its 256 workgroups were not all "
+                    "resident (another process on this GPU?); outputs are NaN.  Run one generation process per "
+                    "GPU (INTEGRATION.md, Co-residency) or set AVC_WN_GRID=0 for the per-layer launches.")
         return (y, mol) if return_mol else y
 
     def incremental_forward(self, initial_input=None, c=None, g=None, T=100, test_inputs=None,

@@ -88,6 +88,19 @@ int autovc_preprocess_f64(const void* x, int x_is_f64, const int64_t* wav_off, i
  * summing the partials in split order; by default slabs + a reduce launch, measured faster).
  */
 int64_t autovc_gemm_workspace_floats(int M, int N, int splits);
+/* The weight gradient of one time chunk of an LSTM layer (replaces the chunk's share of
+ * torch's dW = dG^T x / dG^T h_{t-1} over all frames, model_vc_mel.py:104): steps
+ * [t0, t0 + Tc) of each of B sequences of T steps,
+ *   C[M,N] (+)= sum_b sum_t A[(b*T + t)*lda + m] * Bm[(b*T + t + b_tap0)*ldb + n]
+ * (b_tap0 = -1: the previous step's h, zero at t = 0).  K = B*Tc; splits / workspace as
+ * autovc_gemm_f32 (bf16: autovc_gemm_bf16_splits of (M, N, B*Tc)).  The chunks of a
+ * sequence summed in order give the whole-sequence gradient up to fp32 summation order. */
+int autovc_gemm_tchunk_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
+                           const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate,
+                           int splits, float* workspace, hipStream_t stream);
+int autovc_gemm_tchunk_bf16_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
+                                const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate,
+                                int splits, float* workspace, hipStream_t stream);
 int autovc_gemm_f32(int M, int N, int K,
                     const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
                     const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
@@ -211,15 +224,6 @@ int autovc_wino5_input_bn_f32(int B, int T, int C, const float* y, int64_t ldy, 
                               float* out, hipStream_t stream);
 int autovc_wino5_output_stats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
                                   int64_t ldy, double* part, hipStream_t stream);
-/* output_stats + autovc_bn_finalize_f32 in ONE launch (the block completing the statistics
- * finalizes; bit-identical): mean, var, coef, running stats, num_batches_tracked as
- * autovc_bn_finalize_f32 with M = B*T.  workspace: autovc_wino5_bnstats_workspace_bytes bytes,
- * ZEROED before its first use and left zeroed (its first 4 KB are tickets); C <= 8192. */
-int64_t autovc_wino5_bnstats_workspace_bytes(int B, int T, int C);
-int autovc_wino5_output_bnstats_f32(int B, int T, int C, const float* Yt, const float* bias, float* y,
-                                    int64_t ldy, const float* gamma, const float* beta, float eps, float* mean,
-                                    float* var, float* coef, float* run_mean, float* run_var, float momentum,
-                                    int64_t* nbt, void* workspace, hipStream_t stream);
 int autovc_wino5_output_bnbwd_f32(int B, int T, int C, const float* Yt, const float* yprev, int64_t ldy,
                                   const float* coef, int act, float* dz, int64_t lddz, double* part,
                                   hipStream_t stream);
@@ -272,15 +276,6 @@ int64_t autovc_bnconv_workspace_floats(int B, int T, int Ci, int Co);
 int autovc_bnconv_fwd_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef, int x_act,
                                const void* Wf, const float* bias, float* y, double* part, int src, float* workspace,
                                hipStream_t stream);
-/* autovc_bnconv_fwd_bf16_f32 + autovc_bn_finalize_f32 (train statistics), the finalize inside
- * the reduce launch (bit-identical).  stats_ws: autovc_bnconv_bnstats_workspace_bytes(B*T, Co)
- * bytes, ZEROED before its first use and left zeroed (its first 4 KB are tickets). */
-int64_t autovc_bnconv_bnstats_workspace_bytes(int64_t M, int N);
-int autovc_bnconv_fwd_bnstats_bf16_f32(int B, int T, int Ci, int Co, const void* x, const float* x_coef, int x_act,
-                                       const void* Wf, const float* bias, float* y, const float* gamma,
-                                       const float* beta, float eps, float* mean, float* var, float* coef,
-                                       float* run_mean, float* run_var, float momentum, int64_t* nbt, void* stats_ws,
-                                       int src, float* workspace, hipStream_t stream);
 int autovc_bnconv_dx_bf16_f32(int B, int T, int Co, int Ci, const void* dy, const void* Wd, float* dz,
                               const float* y_prev, const float* coef_prev, int act_prev, double* part, int src,
                               float* workspace, hipStream_t stream);
@@ -401,14 +396,6 @@ int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb
 int autovc_lstm_fwd_xcd_bf16(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                              const uint16_t* W_hh_b, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                              float* gates, void* workspace, hipStream_t stream);
-/* Its backward (BPTT of autovc_lstm_bwd_f32 with reverse = 0) the same way: slot s of XCD x
- * reduces dh_rec for units 16s .. 16s+15 of rows 8x .. 8x+7 over K = 4H with W_hh's columns
- * in registers (W_hh as stored, (4H, H): no transpose) and writes those cells' dG; the dG
- * rows of the group are the per-step hand-off (L2, per-XCD step counter).  dh_out may be
- * null.  Same workspace and support rule as autovc_lstm_fwd_xcd_f32. */
-int autovc_lstm_bwd_xcd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
-                            const float* gates, const float* c_all, const float* W_hh, float* dG,
-                            void* workspace, hipStream_t stream);
 /* Co-residency failures reach the caller without a per-call sync: a persistent launch
  * whose grid barrier timed out writes NaN over the h / c it owns (so the loss turns NaN)
  * and sets bit 0 of a sticky per-device fault word.  autovc_fault_status (synchronises
@@ -448,27 +435,20 @@ int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ld
                          const float* gates1, const float* c1, const float* gates0, const float* c0,
                          const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
                          float* dG0, int splits, float* workspace, hipStream_t stream);
-/* autovc_lstm2_bwd_f32 / _bf16 as ONE persistent, weight-stationary launch
- * (csrc/lstm2_persist.hip, lstm2_bwd_persist_kernel; replaces the BPTT of nn.LSTM(512, 1024,
- * 2) at model_vc_mel.py:104,118 as the reference's autograd runs it, solver_encoder.py:296):
- * 256 workgroups (one per CU, 8 XCDs x 32), each holding a (512 gate rows x 32 units) slice
- * of W_hh1, W_ih1 and W_hh0 in registers for the whole sequence; per wavefront step the
- * three products over its K slice, the group's K-slice partials summed inside the XCD, the
- * cell backward of the 4 x 64 cells it owns, and a grid barrier.  Weights are the (4H, H)
- * parameters themselves (fp32) or their RNE bf16 copies (_bf16, which also writes dG*_b).
- * Needs B = 64, H = 1024, 256 CUs (autovc_lstm2_bwd_persist_supported) and every workgroup
- * resident at once (Co-residency; fault bit 16). */
-int autovc_lstm2_bwd_persist_supported(int B, int H);
-int64_t autovc_lstm2_bwd_persist_workspace_bytes(int B, int T, int H);
-int autovc_lstm2_bwd_persist_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                 const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                 const float* W_hh1, const float* W_ih1, const float* W_hh0, float* dG1,
-                                 float* dG0, void* workspace, hipStream_t stream);
-int autovc_lstm2_bwd_persist_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                  const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                  const uint16_t* W_hh1_b, const uint16_t* W_ih1_b, const uint16_t* W_hh0_b,
-                                  float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, void* workspace,
-                                  hipStream_t stream);
+/* autovc_lstm2_bwd_f32 / _bf16 issued in pieces: wavefront iterations s in [s_begin, s_end)
+ * of 0..T (iteration s finishes layer 1's step T-1-s and layer 0's step T-s; after
+ * iterations [0, s_end) both layers' dG are final for every t >= T + 1 - s_end).  Calls
+ * covering 0..T in order, on one stream and one workspace, are one full call: the caller
+ * starts each finished time chunk's weight gradients (autovc_gemm_tchunk_*) in between. */
+int autovc_lstm2_bwd_range_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                               const float* gates1, const float* c1, const float* gates0, const float* c0,
+                               const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
+                               float* dG0, int splits, int s_begin, int s_end, float* workspace, hipStream_t stream);
+int autovc_lstm2_bwd_range_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
+                                float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits, int s_begin,
+                                int s_end, float* workspace, hipStream_t stream);
 int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
                          const float* W_hh_b, float* h, float* c_all, float* gates,
                          hipStream_t stream);
@@ -558,14 +538,6 @@ int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, 
  *   autovc_wavenet_ring_frames: frames of the per-layer input rings (power of two >=
  *            (taps-1) * max dilation + 1).
  */
-/* XCD-local generation (B <= 8, R = G = 512, S = 256, 3 taps, 8 XCDs x 32 CUs): utterance x
- * runs on XCD x as ONE persistent launch per autovc_wavenet_generate_f32 call, every per-layer
- * hand-off inside that XCD's L2.  set_xcd(1/0) selects it (default: AVC_WN_XCD, 0 if unset);
- * a phase wait that times out (set_timeout_ticks: s_memrealtime ticks, 0 = 1 s) writes NaN
- * over the utterance's outputs of the call and sets the fault word autovc_wavenet_fault reads
- * (synchronising; clear != 0 resets it). */
-int autovc_wavenet_set_xcd(int on);
-int autovc_wavenet_get_xcd(void);
 /* All-CU weight-resident generation (B <= 8, R = 512, G = 512, S = 256, 3 taps, 8..24 layers, a
  * 256-CU device): ONE persistent launch per autovc_wavenet_generate_f32 call whose 256
  * workgroups keep every gate weight of the sample chain on chip and hand each phase's outputs
@@ -573,15 +545,21 @@ int autovc_wavenet_get_xcd(void);
  * arguments and outputs; a hand-off wait that times out poisons the call's samples with NaN and
  * sets bit 2 of the autovc_wavenet_fault word.
  * Mode (AVC_WN_GRID or autovc_wavenet_set_grid): 0 never, 1 for every eligible batch, 2 (the
- * default) for B <= 2, where it beats the launches; it takes precedence
- * over the XCD form. */
+ * default) for B <= 2, where it beats the launches; any other AVC_WN_GRID
+ * value makes autovc_wavenet_generate_f32 fail.  autovc_wavenet_last_path: 1 if the last
+ * generate call ran the all-CU kernel (its caller must read autovc_wavenet_fault), 0 if the
+ * per-layer launches. */
 int autovc_wavenet_set_grid(int on);
 int autovc_wavenet_get_grid(void);
+int autovc_wavenet_last_path(void);
 /* The first wait of the all-CU generation that timed out since the last clear: out5 = {kind
  * (0 none, 1 layer inputs, 2 past-tap sums, 3 LDS handshake, 4 past-tap inputs, 5 past-tap
  * consumers, 6 skip sums, 7 h1), step, phase (or job), workgroup, last tag seen (-1 if not
  * recorded)}; synchronises the device. */
 int autovc_wavenet_grid_diag(int clear, int* out5);
+/* The all-CU generation's spin budget per wait in s_memrealtime ticks (0 = 1 s; a tiny value
+ * forces the timeout path in tests) and its sticky fault word (bit 2: a wait timed out and the
+ * call's samples are NaN); autovc_wavenet_fault synchronises, clear != 0 resets it. */
 int autovc_wavenet_set_timeout_ticks(int ticks);
 int autovc_wavenet_fault(int clear, int* out);
 int64_t autovc_wavenet_ring_frames(int n_layers, int layers_per_stack, int taps);

@@ -163,72 +163,3 @@ def test_bf16_chain_eval_mode(cuda, mode):
         o1, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", mode, training=False)
         o0, _, _ = _run_prec(copy.deepcopy(layers), x, None, x, "bf16", 0, training=False)
     assert _rel(o1, ref) < 1.5 * _rel(o0, ref) + 1e-4
-
-
-@pytest.mark.parametrize("name,chans,acts,res,B,T", [
-    ("postnet", [80, 512, 512, 512, 512, 80], ["tanh"] * 4 + ["none"], True, 8, 128),
-    ("encoder", [336, 512, 512, 512], ["relu"] * 3, False, 64, 128),
-    ("decoder", [320, 512, 512, 512], ["relu"] * 3, False, 3, 16),
-])
-def test_fused_bn_statistics_bit_identical(cuda, name, chans, acts, res, B, T):
-    """The fp32 stacks' BatchNorm statistics finalized inside the output transform's launch
-    (autovc_wino5_output_bnstats_f32: ticketed row-group and column-block completion, the
-    two-launch form's summation order) against output_stats + autovc_bn_finalize_f32: outputs,
-    every gradient and the running statistics bit for bit, over two calls (the tickets are
-    left zeroed), at ragged channel counts (80) and row-block counts below 16 (B=3, T=16)."""
-    import copy
-    from autovc_amd import functional as AF
-    g = torch.Generator().manual_seed(5)
-    x = torch.clamp(torch.randn(B, T, chans[0], generator=g) * 0.18 + 0.43, 0, 1).to(cuda)
-    dz = (torch.randn(B, T, chans[-1], generator=g) * 1e-3).to(cuda)
-    residual = torch.randn(B, T, chans[-1], generator=g).to(cuda) if res else None
-    layers = _stack(chans, acts, seed=6)
-    prev = AF._BN_FUSED_STATS
-    outs = {}
-    try:
-        for fused in (True, False):
-            AF._BN_FUSED_STATS = fused
-            mods = copy.deepcopy(layers)
-            _run(mods, x, dz, residual, chain=True)                 # first call: running stats step 1
-            outs[fused] = _run(mods, x, dz, residual, chain=True)   # second call reuses the tickets
-    finally:
-        AF._BN_FUSED_STATS = prev
-    (o1, g1, s1), (o0, g0, s0) = outs[True], outs[False]
-    assert torch.equal(o1, o0)
-    for k in g0:
-        assert torch.equal(g1[k], g0[k]), k
-    for (m1, v1, n1), (m0, v0, n0) in zip(s1, s0):
-        assert n1 == n0 == 2 and torch.equal(m1, m0) and torch.equal(v1, v0)
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("B,T", [(64, 128), (1, 8)])
-def test_bf16_fused_bn_statistics_bit_identical(cuda, mode, B, T):
-    """The bf16 stacks' BatchNorm statistics finalized inside the split-K reduce launch
-    (autovc_bnconv_fwd_bnstats_bf16_f32) against the reduce + autovc_bn_finalize_f32: outputs,
-    gradients and running statistics bit for bit over two calls, at M = 8 (fewer row blocks
-    than 16 groups) and at config 2's M = 8192."""
-    import copy
-    from autovc_amd import functional as AF
-    chans, acts = [80, 512, 512, 512, 512, 80], ["tanh"] * 4 + ["none"]
-    g = torch.Generator().manual_seed(7)
-    x = torch.clamp(torch.randn(B, T, chans[0], generator=g) * 0.18 + 0.43, 0, 1).to(cuda)
-    dz = (torch.randn(B, T, chans[-1], generator=g) * 1e-3).to(cuda)
-    residual = torch.randn(B, T, chans[-1], generator=g).to(cuda)
-    layers = _stack(chans, acts, seed=8)
-    prev = AF._BN_FUSED_STATS
-    outs = {}
-    try:
-        for fused in (True, False):
-            AF._BN_FUSED_STATS = fused
-            mods = copy.deepcopy(layers)
-            _run_prec(mods, x, dz, residual, "bf16", mode)
-            outs[fused] = _run_prec(mods, x, dz, residual, "bf16", mode)
-    finally:
-        AF._BN_FUSED_STATS = prev
-    (o1, g1, s1), (o0, g0, s0) = outs[True], outs[False]
-    assert torch.equal(o1, o0)
-    for k in g0:
-        assert torch.equal(g1[k], g0[k]), k
-    for (m1, v1, n1), (m0, v0, n0) in zip(s1, s0):
-        assert n1 == n0 == 2 and torch.equal(m1, m0) and torch.equal(v1, v0)

@@ -303,39 +303,6 @@ def test_xcd_local_lstm_timeout_surfaces(cuda):
     assert "AVC_LSTM2_PERSIST" not in str(ei.value)
 
 
-@pytest.mark.parametrize("T", [1, 2, 128])
-def test_xcd_local_lstm_backward_matches_split_k_launches(cuda, T):
-    """The lstm1 backward as one XCD-local persistent launch (autovc_lstm_bwd_xcd_f32) against
-    the per-step split-K launches (autovc_lstm_bwd_f32 on W_hh^T): dG within fp32
-    summation-order noise (relative to its max), repeat calls bit-identical."""
-    from autovc_amd import _lib, functional as AF
-    if not _xcd_supported():
-        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
-    B, H = 64, 512
-    AF.check_device_faults(cuda)
-    gx, W, _, _ = _inputs(B, T, H, cuda, seed=11)
-    _, c, g = _run1("autovc_lstm_fwd_f32", B, T, H, gx, W[0], cuda)
-    dh = (torch.randn(B, T, H, generator=torch.Generator().manual_seed(3)) * 0.1).to(cuda)
-    WT = W[0].t().contiguous()
-    ref = torch.empty(B, T, 4 * H, device=cuda)
-    ws = torch.empty(4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, 8), dtype=torch.uint8, device=cuda)
-    _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(), WT.data_ptr(),
-              ref.data_ptr(), 0, 8, ws.data_ptr(), _lib.stream_ptr(cuda))
-    wx = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
-    outs = []
-    for _ in range(2):
-        got = torch.full((B, T, 4 * H), float("nan"), device=cuda)
-        _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(),
-                  W[0].data_ptr(), got.data_ptr(), wx.data_ptr(), _lib.stream_ptr(cuda))
-        torch.cuda.synchronize()
-        outs.append(got)
-    AF.check_device_faults(cuda)
-    assert bool(torch.isfinite(outs[0]).all())
-    err = (outs[0].double() - ref.double()).abs().max().item() / ref.abs().max().item()
-    assert err < 2e-5, err
-    assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("T", [3, 128])
 def test_xcd_local_lstm_bf16_matches_bf16_per_step_launches(cuda, T):
     """autovc_lstm_fwd_xcd_bf16 against the per-step bf16 launches (autovc_lstm_fwd_bf16): the
@@ -366,105 +333,3 @@ def test_xcd_local_lstm_bf16_matches_bf16_per_step_launches(cuda, T):
         d = (a.double() - r.double()).abs()
         assert d.max().item() < 2e-2 * max(r.abs().max().item(), 1e-30), (name, d.max().item())
         assert d.mean().item() < 1e-4 * max(r.abs().max().item(), 1e-30), (name, d.mean().item())
-
-
-def _bwd_supported():
-    from autovc_amd import _lib
-    return bool(_lib.load().autovc_lstm2_bwd_persist_supported(64, 1024))
-
-
-def _bwd_inputs(B, T, H, dev, seed=21):
-    """A forward of the per-step stacked launches (real gate / cell values) plus random
-    upstream gradients."""
-    gx, W, b1, b2 = _inputs(B, T, H, dev, seed)
-    h0, c0, g0, h1, c1, g1 = _run("autovc_lstm2_fwd_f32", B, T, H, gx, W, b1, b2, dev)
-    g = torch.Generator().manual_seed(seed + 1)
-    dh1 = (torch.randn(B, T, H, generator=g) * 0.1).to(dev)
-    return W, (h0, c0, g0, h1, c1, g1), dh1
-
-
-def _bwd_ref(B, T, H, W, fw, dh1, dev, bf16):
-    from autovc_amd import _lib
-    h0, c0, g0, h1, c1, g1 = fw
-    WT = [w.t().contiguous() for w in (W[2], W[1], W[0])]          # W_hh1^T, W_ih1^T, W_hh0^T
-    splits = 4 if not bf16 else 2
-    ws = torch.empty(_lib.load().autovc_lstm2_bwd_workspace_floats(B, H, splits), device=dev)
-    dG1, dG0 = (torch.full((B, T, 4 * H), float("nan"), device=dev) for _ in range(2))
-    if bf16:
-        WTb = [w.to(torch.bfloat16) for w in WT]
-        dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
-        _lib.call("autovc_lstm2_bwd_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                  g0.data_ptr(), c0.data_ptr(), WTb[0].data_ptr(), WTb[1].data_ptr(), WTb[2].data_ptr(),
-                  dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), splits, ws.data_ptr(),
-                  _lib.stream_ptr(dev))
-    else:
-        _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                  g0.data_ptr(), c0.data_ptr(), WT[0].data_ptr(), WT[1].data_ptr(), WT[2].data_ptr(),
-                  dG1.data_ptr(), dG0.data_ptr(), splits, ws.data_ptr(), _lib.stream_ptr(dev))
-    torch.cuda.synchronize()
-    return dG1, dG0
-
-
-def _bwd_persist(B, T, H, W, fw, dh1, dev, bf16, ws=None):
-    from autovc_amd import _lib
-    h0, c0, g0, h1, c1, g1 = fw
-    if ws is None:
-        ws = torch.empty(_lib.load().autovc_lstm2_bwd_persist_workspace_bytes(B, T, H), dtype=torch.uint8, device=dev)
-    dG1, dG0 = (torch.full((B, T, 4 * H), float("nan"), device=dev) for _ in range(2))
-    W1, Wi1, W0 = W[2], W[1], W[0]
-    if bf16:
-        Wb = [w.to(torch.bfloat16) for w in (W1, Wi1, W0)]
-        dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
-        _lib.call("autovc_lstm2_bwd_persist_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                  g0.data_ptr(), c0.data_ptr(), Wb[0].data_ptr(), Wb[1].data_ptr(), Wb[2].data_ptr(),
-                  dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), ws.data_ptr(), _lib.stream_ptr(dev))
-    else:
-        _lib.call("autovc_lstm2_bwd_persist_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(), c1.data_ptr(),
-                  g0.data_ptr(), c0.data_ptr(), W1.data_ptr(), Wi1.data_ptr(), W0.data_ptr(), dG1.data_ptr(),
-                  dG0.data_ptr(), ws.data_ptr(), _lib.stream_ptr(dev))
-    torch.cuda.synchronize()
-    return dG1, dG0
-
-
-@pytest.mark.parametrize("bf16", [False, True], ids=["fp32", "bf16"])
-@pytest.mark.parametrize("T", [1, 2, 128])
-def test_persistent_lstm2_backward_matches_per_step_launches(cuda, T, bf16):
-    """Decoder lstm2's backward as one persistent weight-stationary launch
-    (autovc_lstm2_bwd_persist_*) against the per-step product + pointwise launches
-    (autovc_lstm2_bwd_*, which the Generator tests pin to the reference): dG of both layers
-    within fp32 summation-order noise relative to their max (bf16: the products' bf16
-    operands round differently once the partial sums differ, 2e-2); a second call
-    bit-identical; no fault recorded."""
-    from autovc_amd import functional as AF
-    if not _bwd_supported():
-        pytest.skip("persistent lstm2 backward needs 8 XCDs x 32 CUs")
-    B, H = 64, 1024
-    AF.check_device_faults(cuda)
-    W, fw, dh1 = _bwd_inputs(B, T, H, cuda)
-    ref = _bwd_ref(B, T, H, W, fw, dh1, cuda, bf16)
-    got = _bwd_persist(B, T, H, W, fw, dh1, cuda, bf16)
-    AF.check_device_faults(cuda)
-    for name, a, r in zip(["dG1", "dG0"], got, ref):
-        assert bool(torch.isfinite(a).all()), name
-        err = (a.double() - r.double()).abs().max().item() / max(r.abs().max().item(), 1e-30)
-        assert err < (2e-2 if bf16 else 2e-5), (name, err)
-    again = _bwd_persist(B, T, H, W, fw, dh1, cuda, bf16)
-    for a, b in zip(got, again):
-        assert torch.equal(a, b)
-
-
-def test_persistent_lstm2_backward_timeout_surfaces(cuda):
-    from autovc_amd import _lib, functional as AF
-    if not _bwd_supported():
-        pytest.skip("persistent lstm2 backward needs 8 XCDs x 32 CUs")
-    B, H, T = 64, 1024, 8
-    AF.check_device_faults(cuda)
-    W, fw, dh1 = _bwd_inputs(B, T, H, cuda)
-    _lib.call("autovc_lstm_persist_set_timeout_ticks", 1)
-    try:
-        dG1, dG0 = _bwd_persist(B, T, H, W, fw, dh1, cuda, False)
-    finally:
-        _lib.call("autovc_lstm_persist_set_timeout_ticks", 0)
-    assert bool(torch.isnan(dG0).any())
-    with pytest.raises(AF.DeviceFault, match="lstm2_bwd_persist_kernel.*AVC_LSTM2_BWD_PERSIST=0"):
-        AF.check_device_faults(cuda)

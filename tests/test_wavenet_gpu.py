@@ -36,19 +36,17 @@ def _cond(B, Tc, seed=4321):
     return torch.from_numpy(np.clip(rs.normal(0.43, 0.18, (B, 80, Tc)), 0, 1).astype(np.float32))
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["launches", "xcd", "grid"])
-def xcd(request):
-    """Run a test with the per-layer launches, with the XCD-local persistent generation
-    (wn_xcd_kernel: B <= 8 on 8 XCDs x 32 CUs) and with the all-CU weight-resident generation
-    (wn_grid_kernel: B <= 8, 8..24 layers, 256 CUs); other shapes use the launches either way."""
+@pytest.fixture(params=[0, 1], ids=["launches", "grid"])
+def wn_mode(request):
+    """Run a test with the per-layer launches and with the all-CU weight-resident generation
+    (wn_grid_kernel: B <= 8, 8..24 layers, 256 CUs); other shapes use the launches either way.
+    (The XCD-local form this fixture also ran until round 4 is retired: tools/retired/.)"""
     from autovc_amd import _lib
     lib = _lib.load()
-    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
-    _lib.call("autovc_wavenet_set_xcd", int(request.param == 1))
-    _lib.call("autovc_wavenet_set_grid", int(request.param == 2))
+    prev = lib.autovc_wavenet_get_grid()
+    _lib.call("autovc_wavenet_set_grid", int(request.param == 1))
     yield request.param
-    _lib.call("autovc_wavenet_set_xcd", prev[0])
-    _lib.call("autovc_wavenet_set_grid", prev[1])
+    _lib.call("autovc_wavenet_set_grid", prev)
 
 
 def rel(a, b):
@@ -68,7 +66,7 @@ def test_upsample_matches_oracle(cuda):
 
 
 @pytest.mark.parametrize("B,layers,stacks", [(3, 24, 4), (9, 6, 2)])
-def test_teacher_forced_mol_and_samples(cuda, B, layers, stacks, xcd):
+def test_teacher_forced_mol_and_samples(cuda, B, layers, stacks, wn_mode):
     hp = ow.small_hparams(layers=layers, stacks=stacks)
     m, W = _model(hp, cuda)
     c = _cond(B, 2)
@@ -84,7 +82,7 @@ def test_teacher_forced_mol_and_samples(cuda, B, layers, stacks, xcd):
     assert (y.double().cpu() - y_ref).abs().max().item() < 1e-4
 
 
-def test_free_running_matches_oracle(cuda, xcd):
+def test_free_running_matches_oracle(cuda, wn_mode):
     hp = ow.HPARAMS
     m, W = _model(hp, cuda)
     c = _cond(2, 2, seed=7)
@@ -107,7 +105,7 @@ def test_graph_replay_is_bit_exact(cuda):
     assert torch.equal(a, b) and torch.equal(a, d)
 
 
-def test_batch_shard_and_chunk_invariance(cuda, xcd):
+def test_batch_shard_and_chunk_invariance(cuda, wn_mode):
     hp = ow.small_hparams()
     m, _ = _model(hp, cuda)
     c = _cond(3, 2).to(cuda)
@@ -118,7 +116,7 @@ def test_batch_shard_and_chunk_invariance(cuda, xcd):
     assert (full - chunked).abs().max().item() < 1e-5
 
 
-def test_wavegen_api(cuda, xcd):
+def test_wavegen_api(cuda, wn_mode):
     from autovc_amd import synthesis
     torch.manual_seed(0)
     model = synthesis.build_model().to(cuda)      # r9y9 init, weight norm still attached
@@ -148,7 +146,7 @@ def test_error_behaviour(cuda):
         m.generate(c.cpu())
 
 
-def test_full_size_config4_shard_invariance(cuda, xcd):
+def test_full_size_config4_shard_invariance(cuda, wn_mode):
     """BASELINE config 4 at full size (8 utterances x 32,768 samples, 24 layers): sharding the
     batch by rank (utt_base) reproduces the single-batch run over 256 ring wraps and 256
     conditioning chunks; every sample finite and in [-1, 1]."""
@@ -179,63 +177,8 @@ def test_two_tiles_direct_launches_equal_graphs(cuda):
     assert torch.equal(a, b) and torch.equal(a, d)
 
 
-def test_xcd_generation_matches_launches(cuda):
-    """The XCD-local persistent generation (one utterance per XCD, per-layer hand-offs in the
-    XCD's L2) against the per-layer launches: 8 utterances, 24 layers, 2,048 free-running
-    samples (16 ring wraps, 16 conditioning chunks) within fp32 summation-order noise, and
-    the MoL parameters of a teacher-forced run within 1e-5; no fault recorded."""
-    import ctypes
+def _set_modes(grid):
     from autovc_amd import _lib
-    if _lib.load().autovc_lstm_xcd_supported(64, 512) == 0:
-        pytest.skip("needs 8 XCDs x 32 CUs")
-    hp = ow.HPARAMS
-    m, _ = _model(hp, cuda)
-    c = _cond(8, 8, seed=29).to(cuda)
-    rs = np.random.RandomState(5)
-    teacher = torch.from_numpy(rs.uniform(-0.9, 0.9, (8, 2048)).astype(np.float32)).to(cuda)
-    prev = _lib.load().autovc_wavenet_get_xcd()
-    out = {}
-    try:
-        for mode in (0, 1):
-            _lib.call("autovc_wavenet_set_xcd", mode)
-            y = m.generate(c, seed=13, log_scale_min=LSM)
-            _, mol = m.generate(c, seed=13, log_scale_min=LSM, teacher=teacher, return_mol=True)
-            out[mode] = (y, mol)
-    finally:
-        _lib.call("autovc_wavenet_set_xcd", prev)
-    (y0, m0), (y1, m1) = out[0], out[1]
-    assert torch.isfinite(y1).all() and torch.isfinite(m1).all()
-    assert rel(m1, m0) < 1e-5
-    assert (y1 - y0).abs().max().item() < 1e-4
-    f = ctypes.c_int(0)
-    _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(f))
-    assert f.value == 0
-
-
-def test_xcd_generation_timeout_surfaces(cuda):
-    """A phase wait that gives up (forced: a 1-tick timeout) poisons the outputs and raises."""
-    from autovc_amd import _lib
-    if _lib.load().autovc_lstm_xcd_supported(64, 512) == 0:
-        pytest.skip("needs 8 XCDs x 32 CUs")
-    hp = ow.small_hparams()
-    m, _ = _model(hp, cuda)
-    c = _cond(2, 1).to(cuda)
-    prev = _lib.load().autovc_wavenet_get_xcd()
-    try:
-        _lib.call("autovc_wavenet_set_xcd", 1)
-        _lib.call("autovc_wavenet_set_timeout_ticks", 1)
-        with pytest.raises(RuntimeError, match="wn_xcd_kernel"):
-            m.generate(c, seed=1, log_scale_min=LSM)
-    finally:
-        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        _lib.call("autovc_wavenet_set_xcd", prev)
-    y = m.generate(c, seed=1, log_scale_min=LSM)          # the next call runs clean
-    assert torch.isfinite(y).all()
-
-
-def _set_modes(xcd, grid):
-    from autovc_amd import _lib
-    _lib.call("autovc_wavenet_set_xcd", xcd)
     _lib.call("autovc_wavenet_set_grid", grid)
 
 
@@ -257,16 +200,16 @@ def test_grid_generation_matches_launches(cuda, B):
     c = _cond(B, 8, seed=31).to(cuda)
     rs = np.random.RandomState(6)
     teacher = torch.from_numpy(rs.uniform(-0.9, 0.9, (B, 2048)).astype(np.float32)).to(cuda)
-    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
+    prev = lib.autovc_wavenet_get_grid()
     out = {}
     try:
         for mode in (0, 1):
-            _set_modes(0, mode)
+            _set_modes(mode)
             y = m.generate(c, seed=17, log_scale_min=LSM)
             _, mol = m.generate(c, seed=17, log_scale_min=LSM, teacher=teacher, return_mol=True)
             out[mode] = (y, mol)
     finally:
-        _set_modes(*prev)
+        _set_modes(prev)
     (y0, m0), (y1, m1) = out[0], out[1]
     assert torch.isfinite(y1).all() and torch.isfinite(m1).all()
     assert rel(m1, m0) < 1e-5
@@ -278,53 +221,56 @@ def test_grid_generation_matches_launches(cuda, B):
 
 def test_grid_generation_timeout_surfaces(cuda):
     """A hand-off wait that gives up (forced: a 1-tick timeout) with the all-CU form requested
-    (mode 1) poisons the outputs and raises; the next call runs clean."""
-    from autovc_amd import _lib
+    (mode 1) poisons the outputs and raises DeviceFault; the next call runs clean."""
+    from autovc_amd import _lib, functional as AF
     lib = _lib.load()
     if lib.autovc_lstm_xcd_supported(64, 512) == 0:
         pytest.skip("needs 8 XCDs x 32 CUs")
     hp = ow.small_hparams(layers=8, stacks=2)
     m, _ = _model(hp, cuda)
     c = _cond(2, 1).to(cuda)
-    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
+    prev = lib.autovc_wavenet_get_grid()
     try:
-        _set_modes(0, 1)
+        _set_modes(1)
         _lib.call("autovc_wavenet_set_timeout_ticks", 1)
-        with pytest.raises(RuntimeError, match="wn_grid_kernel"):
+        with pytest.raises(AF.DeviceFault, match="wn_grid_kernel.*AVC_WN_GRID=0"):
             m.generate(c, seed=1, log_scale_min=LSM)
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
         y = m.generate(c, seed=1, log_scale_min=LSM)      # the next call runs clean
         assert torch.isfinite(y).all()
     finally:
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        _set_modes(*prev)
+        _set_modes(prev)
 
 
 def test_grid_default_mode_small_batches(cuda):
     """Mode 2 (the default) runs the all-CU form for up to two utterances: B = 1 and B = 2
-    equal mode 1 bit for bit, B = 3 equals the launches bit for bit.  If its wait gives up (forced: a 1-tick
-    timeout) it warns, keeps to the launches in this process and returns the launches' samples."""
-    from autovc_amd import _lib
+    equal mode 1 bit for bit, B = 3 equals the launches bit for bit.  If its wait gives up
+    (forced: a 1-tick timeout) the call raises DeviceFault naming AVC_WN_GRID=0 — it does not
+    regenerate on the launches — and the mode is unchanged."""
+    from autovc_amd import _lib, functional as AF
     lib = _lib.load()
     if lib.autovc_lstm_xcd_supported(64, 512) == 0:
         pytest.skip("needs 8 XCDs x 32 CUs")
     hp = ow.small_hparams(layers=8, stacks=2)
     m, _ = _model(hp, cuda)
     c1, c2, c3 = _cond(1, 2, seed=3).to(cuda), _cond(2, 2, seed=4).to(cuda), _cond(3, 2, seed=5).to(cuda)
-    prev = (lib.autovc_wavenet_get_xcd(), lib.autovc_wavenet_get_grid())
+    prev = lib.autovc_wavenet_get_grid()
     try:
         out = {}
         for mode in (0, 1, 2):
-            _set_modes(0, mode)
+            _set_modes(mode)
             out[mode] = tuple(m.generate(c, seed=5, log_scale_min=LSM) for c in (c1, c2, c3))
+            assert lib.autovc_wavenet_last_path() == (1 if mode == 1 else 0)   # the last call was B = 3
         assert torch.equal(out[2][0], out[1][0]) and torch.equal(out[2][1], out[1][1])
         assert torch.equal(out[2][2], out[0][2])
-        _set_modes(0, 2)
+        _set_modes(2)
         _lib.call("autovc_wavenet_set_timeout_ticks", 1)
-        with pytest.warns(RuntimeWarning, match="wn_grid_kernel"):
-            y = m.generate(c1, seed=5, log_scale_min=LSM)
-        assert lib.autovc_wavenet_get_grid() == 0
-        assert torch.equal(y, out[0][0])
+        with pytest.raises(AF.DeviceFault, match="wn_grid_kernel.*AVC_WN_GRID=0"):
+            m.generate(c1, seed=5, log_scale_min=LSM)
+        assert lib.autovc_wavenet_get_grid() == 2
+        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
+        assert torch.equal(m.generate(c1, seed=5, log_scale_min=LSM), out[2][0])   # the next call runs clean
     finally:
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        _set_modes(*prev)
+        _set_modes(prev)

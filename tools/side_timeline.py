@@ -43,10 +43,12 @@ def install():
     orig_mark = AF._grad_mark
     orig_join = AF.join_grad_stream
     nrec = [0]
+    nfl = [0]
 
     def fb(self, x, e):
         _state["n"] = 0
         nrec[0] = 0
+        nfl[0] = 0
         stamp("step_start", torch.cuda.current_stream())
         out = orig_fb(self, x, e)
         stamp("step_end", torch.cuda.current_stream())
@@ -65,8 +67,9 @@ def install():
     def flush(beside_recurrence=True, after=None):
         # functional._flush_grad_queue with stamps: main when the recurrence is done, side
         # when its batch starts and ends
+        nfl[0] += 1
         if beside_recurrence:
-            stamp(f"rec{nrec[0]}_end", torch.cuda.current_stream())
+            stamp(f"rec{nrec[0]}_end.{nfl[0]}", torch.cuda.current_stream())
         if not AF._GRAD_QUEUE:
             return
         items = list(AF._GRAD_QUEUE)
@@ -78,7 +81,7 @@ def install():
             side.wait_event(after)
         else:
             side.wait_stream(main)
-        tag = f"side{nrec[0]}" if beside_recurrence else "side_final"
+        tag = f"side{nrec[0]}.{nfl[0]}" if beside_recurrence else "side_final"
         stamp(f"{tag}_begin(n={len(items)})", side)
         AF._GRAD_STREAM_ACTIVE[0] = True
         AF._GRAD_PENDING.add(side.device.index)
@@ -150,7 +153,8 @@ def main():
             print(f"  {lab:30s} {mean[lab]:9.1f} .. {end:9.1f}  ({end - mean[lab]:8.1f} us)")
         if lab.startswith("rec") and "_begin" in lab:
             tag = lab.split("_begin")[0]
-            end = mean.get(f"{tag}_end")
+            ends = [v for k, v in mean.items() if k.startswith(f"{tag}_end")]
+            end = max(ends) if ends else None
             if end is not None:
                 print(f"  {lab:30s} {mean[lab]:9.1f} .. {end:9.1f}  ({end - mean[lab]:8.1f} us)")
 
