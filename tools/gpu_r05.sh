@@ -22,6 +22,10 @@ for STEP in ${1//,/ }; do
     lbt) timeout -k 10 300 python -u tools/lstm_bwd_time.py fp32 > gpurun_out/lstm_bwd_time${TAG}.txt 2> gpurun_out/lbt.err && \
          timeout -k 10 300 python -u tools/lstm_bwd_time.py bf16 >> gpurun_out/lstm_bwd_time${TAG}.txt 2>> gpurun_out/lbt.err ;;
     lbtprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/lbtprof${TAG} -o run --output-format csv -- python tools/lstm_bwd_time.py ${LBT_PREC:-fp32} > gpurun_out/lbtprof${TAG}.log 2>&1 ;;
+    gemmpmc) for W in ours blas; do
+               timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -d gpurun_out/gpmc_$W -o run --output-format csv -- python tools/gemm_pmc.py $W ${GEMM_SHAPE:-4096 1024 8192} 10 > gpurun_out/gpmc_$W.log 2>&1 || exit 1
+               timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d gpurun_out/gpmc2_$W -o run --output-format csv -- python tools/gemm_pmc.py $W ${GEMM_SHAPE:-4096 1024 8192} 10 > gpurun_out/gpmc2_$W.log 2>&1 || exit 1
+             done ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
   rc=$?

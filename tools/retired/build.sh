@@ -1,0 +1,21 @@
+#!/bin/bash
+# Compile the retired variants' sources (as of commit 226dc43, round 4) for gfx950 on the CPU:
+# object files only, never linked into the product library.   bash tools/retired/build.sh
+set -e
+cd "$(dirname "$0")/../.."
+REV=${RETIRED_REV:-226dc43}
+OUT=tools/retired/build
+rm -rf "$OUT" && mkdir -p "$OUT/src/autovc_amd/csrc" "$OUT/src/include"
+for f in common.h bn_finalize.h twiddle1024.h lstm2_persist.hip wavenet.hip winograd.hip gemm.hip; do
+  git show "$REV:autovc_amd/csrc/$f" > "$OUT/src/autovc_amd/csrc/$f"
+done
+git show "$REV:include/autovc_hip.h" > "$OUT/src/include/autovc_hip.h"
+for f in lstm2_persist wavenet winograd gemm; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I"$OUT/src/include" \
+    -x hip -c "$OUT/src/autovc_amd/csrc/$f.hip" -o "$OUT/$f.o" &
+done
+wait
+# the trace build of the all-CU WaveNet kernel
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -DAVC_WN_GRID_TRACE \
+  -I"$OUT/src/include" -x hip -c "$OUT/src/autovc_amd/csrc/wavenet.hip" -o "$OUT/wavenet_trace.o"
+ls -la "$OUT"/*.o
