@@ -29,6 +29,17 @@ from . import functional as AF
 # a side-stream branch; the cause was the memset nodes those single-stream graphs held
 # (DESIGN.md section 9, round 4), not the queue depth, so the bound is off by default.
 MAX_AHEAD = int(os.environ.get("AVC_GRAPH_MAX_AHEAD", "0"))
+# AVC_CAPTURE_DEBUG=1: raise if device memory was returned to the HIP runtime (a hipFree:
+# "segment.all.freed" of the caching allocator) while a step graph was being captured — the
+# kind of free that aborted a capture in round 4 (an unreachable earlier Solver's graphs and
+# private pool finalised by the cyclic collector inside the capture).
+# Refcount-driven frees of ordinary tensors only return blocks to the caching allocator (no
+# HIP call) and are allowed.
+CAPTURE_DEBUG = os.environ.get("AVC_CAPTURE_DEBUG") == "1"
+
+
+class CaptureFreeError(RuntimeError):
+    """Device memory was released to the runtime during a step-graph capture (debug check)."""
 
 
 class StepGraphs:
@@ -59,11 +70,16 @@ class StepGraphs:
         # the next test's bf16 capture).  Collect first, then keep the collector off.
         gc.collect()
         gc.disable()
+        freed0 = torch.cuda.memory_stats(dev).get("segment.all.freed", 0) if CAPTURE_DEBUG else 0
         try:
             with torch.cuda.graph(graph):
                 out = self.fn(*static)
         finally:
             gc.enable()
+        if CAPTURE_DEBUG:
+            freed = torch.cuda.memory_stats(dev).get("segment.all.freed", 0) - freed0
+            if freed:
+                raise CaptureFreeError(f"{freed} device memory segment(s) were freed during a step-graph capture")
         if self.debug_dot:
             graph.debug_dump(self.debug_dot)
         with torch.no_grad():
