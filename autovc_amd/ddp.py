@@ -40,6 +40,7 @@ import torch.distributed as dist
 
 DEFAULT_BUCKET_BYTES = 16 << 20
 last_schedule: list = []      # (bucket key, gradient-ready mark) of the last overlapped step, in issue order
+comm_joins = 0                # explicit compute-stream waits on the communication stream (one per step)
 
 
 def init_from_env(backend=None):
@@ -197,6 +198,14 @@ def _run_exchange(items, grad_dtype, world, after=None, gates=None):
         e.finish()
         if after is not None:
             after(k)
+    # An explicit join, not an accident of ordering: the compute stream waits for everything
+    # issued on the communication stream (its RCCL kernels and bf16 shard sums) before the next
+    # step's graph replay, whose persistent kernels need every CU of the device to themselves
+    # (Co-residency) — an RCCL kernel still holding CUs would make their grid
+    # barriers time out.
+    torch.cuda.current_stream(dev).wait_stream(comm)
+    global comm_joins
+    comm_joins += 1
 
 
 def allreduce_gradients(optimizer, bucket_bytes=DEFAULT_BUCKET_BYTES, grad_dtype=None):

@@ -579,8 +579,7 @@ def main():
     # each hold part of the chip, so ranks sharing a device use the per-step launches.
     share = os.environ.get("AVC_BENCH_SHARE_DEVICE") == "1"
     if share:
-        for k in ("AVC_LSTM2_PERSIST", "AVC_LSTM_XCD", "AVC_LSTM_XCD_BWD", "AVC_LSTM_PERSIST", "AVC_WN_GRID",
-                  "AVC_WN_XCD"):
+        for k in ("AVC_LSTM2_PERSIST", "AVC_LSTM_XCD", "AVC_LSTM_PERSIST", "AVC_WN_GRID"):
             os.environ[k] = "0"
     from autovc_amd import ddp
     rank, world = ddp.init_from_env(backend="gloo" if share else None)
@@ -617,10 +616,14 @@ def main():
     dt = time.perf_counter() - t0
     from autovc_amd import functional as AF
     AF.check_device_faults(dev)      # a co-residency failure of a persistent launch raises here
+    rank_ms = [round(dt / args.steps * 1000, 3)]
     if world > 1:
+        # every rank's own time (the line reports them) and the max over ranks (the value)
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+        ts = [torch.zeros_like(t) for _ in range(world)]
+        torch.distributed.all_gather(ts, t)
+        rank_ms = [round(float(x.item()) / args.steps * 1000, 3) for x in ts]
+        dt = max(float(x.item()) for x in ts)
     last_loss = float(losses[0].item())
 
     def timed_steps(n):
@@ -680,6 +683,9 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1000, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16", "data": "synthetic (clamped N(0.43,0.18) mels, unit-norm*0.8 emb)",
+            "dist_backend": torch.distributed.get_backend() if world > 1 else None,
+            "world_size": torch.distributed.get_world_size() if world > 1 else 1,
+            "rank_ms_per_step": rank_ms,
             "config": {"workload": "AutoVC Generator training step (solver_encoder.py), fwd+bwd+Adam",
                        "global_batch": B * world, "seq_len": T, "n_mels": 80, "parallelism": f"dp{world}",
                        "hip_graph": not args.no_graph,

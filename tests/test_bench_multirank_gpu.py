@@ -25,6 +25,10 @@ def test_bench_two_ranks_one_json_line():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 128
     assert d["value"] > 0 and d["steps"] == 2 and d["scaling"] == "weak"
+    # self-validating multi-rank line: the process group's own backend and size, every rank's
+    # time, and the value computed from the slowest rank
+    assert d["dist_backend"] == "gloo" and d["world_size"] == 2 and len(d["rank_ms_per_step"]) == 2
+    assert abs(d["ms_per_step"] - max(d["rank_ms_per_step"])) < 1e-2
 
 
 def test_plain_bench_gpus2_spawns_two_ranks():

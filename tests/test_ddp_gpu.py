@@ -51,6 +51,7 @@ def _worker(rank, world, port, out_dir, grad_dtype, overlap):
     torch.cuda.synchronize()
     torch.save([f.cpu() for f in solver.g_optimizer.flat_params()], os.path.join(out_dir, f"rank{rank}.pt"))
     torch.save([r for _, r in ddp.last_schedule], os.path.join(out_dir, f"sched{rank}.pt"))
+    torch.save(torch.tensor([ddp.comm_joins]), os.path.join(out_dir, f"joins{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,6 +67,7 @@ def _run_ranks(tmp_path, grad_dtype, overlap):
         p.join(timeout=300)
         assert p.exitcode == 0, p.exitcode
     _run_ranks.schedule = torch.load(os.path.join(tmp_path, "sched0.pt"), weights_only=True)
+    _run_ranks.joins = [int(torch.load(os.path.join(tmp_path, f"joins{r}.pt"), weights_only=True)) for r in range(2)]
     return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
 
 
@@ -98,6 +100,9 @@ def test_two_rank_graph_step_equals_mean_gradient_step(cuda, tmp_path, overlap):
     if overlap:
         sched = _run_ranks.schedule
         assert sched == sorted(sched) and len(set(sched)) >= 2 and sched[0] < sched[-1], sched
+        # every overlapped step ends with the explicit compute-stream wait on the communication
+        # stream (the next replay's persistent kernels never share the device with a collective)
+        assert _run_ranks.joins == [STEPS, STEPS], _run_ranks.joins
     ref = _reference(cuda)
     for a, b in zip(ranks[0], ranks[1]):
         assert torch.equal(a, b)                     # the ranks stay in lockstep
