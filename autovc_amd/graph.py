@@ -38,6 +38,10 @@ MAX_AHEAD = int(os.environ.get("AVC_GRAPH_MAX_AHEAD", "0"))
 CAPTURE_DEBUG = os.environ.get("AVC_CAPTURE_DEBUG") == "1"
 
 
+def _segments_freed(dev):
+    return torch.cuda.memory_stats(dev).get("segment.all.freed", 0)
+
+
 class CaptureFreeError(RuntimeError):
     """Device memory was released to the runtime during a step-graph capture (debug check)."""
 
@@ -70,14 +74,17 @@ class StepGraphs:
         # the next test's bf16 capture).  Collect first, then keep the collector off.
         gc.collect()
         gc.disable()
-        freed0 = torch.cuda.memory_stats(dev).get("segment.all.freed", 0) if CAPTURE_DEBUG else 0
+        # The counter is read inside the capture: torch.cuda.graph's entry empties the cache
+        # (legitimate hipFree calls before capture begins), which must not count.
+        freed = 0
         try:
             with torch.cuda.graph(graph):
+                freed0 = _segments_freed(dev) if CAPTURE_DEBUG else 0
                 out = self.fn(*static)
+                freed = _segments_freed(dev) - freed0 if CAPTURE_DEBUG else 0
         finally:
             gc.enable()
         if CAPTURE_DEBUG:
-            freed = torch.cuda.memory_stats(dev).get("segment.all.freed", 0) - freed0
             if freed:
                 raise CaptureFreeError(f"{freed} device memory segment(s) were freed during a step-graph capture")
         if self.debug_dot:
