@@ -1205,7 +1205,7 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
   float* const mir = a.gmir + (int64_t)xcc * kMirSlots * B * 256 * 4;    // this XCD's slots
   const int64_t MS4 = (int64_t)B * 256 * 4;                               // floats of one slot
   int mrank = 32;
-  if (MIR && wave == 0) {
+  if (MIR && wave == 1) {
     if (lane == 0) mrank = __hip_atomic_fetch_add(errw + kMirCensus + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mrank = __builtin_amdgcn_readfirstlane(mrank);   // >= 32: a surplus workgroup of this XCD fetches nothing
   }
@@ -1314,7 +1314,7 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
   // MIR: wave 0 copies this workgroup's share of phase (t, p)'s inputs (source src, tag stag)
   // into the XCD's mirror slot; false: the wait gave up
   auto mir_fetch = [&](const float* src, int stag, int t, int p) -> bool {
-    if (!MIR || wave != 0 || mrank >= 32) return true;
+    if (!MIR || wave != 1 || mrank >= 32) return true;
     const int col = 8 * mrank + (lane & 7), b = lane >> 3;
     const bool act = b < NB;
     const int bs = b < B ? b : 0;
