@@ -175,8 +175,6 @@ sig("autovc_wavenet_packed_floats", c_int, c_int, c_int, c_int, c_int, c_int)
 sig("autovc_wavenet_set_grid", c_int)
 sig("autovc_wavenet_get_grid")
 sig("autovc_wavenet_last_path")
-sig("autovc_wavenet_set_mirror", c_int, c_int)
-sig("autovc_wavenet_get_mirror")
 sig("autovc_wavenet_grid_diag", c_int, c_ptr)
 sig("autovc_wavenet_set_timeout_ticks", c_int)
 sig("autovc_wavenet_fault", c_int, c_ptr)

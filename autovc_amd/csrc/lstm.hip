@@ -318,7 +318,20 @@ struct BwdArgs {
   float* dc_state;                             // (B,H)
   float* P; int S;                             // (S,B,H) partials or null
   __bf16* dGb;                                 // bf16 copy of dG (bf16 recurrences) or null
+  int prio;                                    // fused steps: raise the waves' issue priority
 };
+
+// The fused backward steps run at wave priority 3 (s_setprio): beside the gradient side
+// stream's GEMM waves — older, and so ahead in the SIMD's issue arbitration at equal priority —
+// the latency-bound step's waves issue first.  fp32 step 14.30-14.35 vs 14.37-14.41 ms, bf16
+// 9.01-9.03 alike (profiles/r05/ab_lstm_prio.txt); AVC_LSTM_PRIO=0 turns it off.
+int lstm_prio() {
+  static const int on = [] { const char* e = getenv("AVC_LSTM_PRIO"); return e && e[0] == '0' ? 0 : 1; }();
+  return on;
+}
+__device__ __forceinline__ void step_priority(int prio) {
+  if (__builtin_amdgcn_readfirstlane(prio)) __builtin_amdgcn_s_setprio(3);
+}
 
 // Pointwise pass of one backward step: thread per (b, j).  Every operand is loaded
 // unconditionally before first use (optional operands are template switches, the previous
@@ -600,6 +613,7 @@ __global__ __launch_bounds__(64 * NW_) void lstm_bwd_fused_kernel(BwdArgs a, con
                                                                  const float* WT, FusedTile f) {
   using C = Tile<KCH_, NW_, D_>;
   __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
+  step_priority(a.prio);
   const int B = a.B, T = a.T, H = a.H;
   const int j0 = blockIdx.x * TN, b0 = blockIdx.y * TB, s = blockIdx.z;
   const int K4 = BF ? 2 * H : 4 * H, ks = K4 / S, kb = s * ks;
@@ -623,6 +637,7 @@ __global__ __launch_bounds__(64 * NW_) void lstm2_bwd_fused_kernel(BwdArgs a1, B
                                                                   const float* WT0, FusedTile f) {
   using C = Tile<KCH_, NW_, D_>;
   __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
+  step_priority(a1.prio);
   const int B = a1.B, T = a1.T, H = a1.H;
   const int nt = H / TN, prod = blockIdx.x / nt, ct = blockIdx.x % nt, j0 = ct * TN;
   const int b0 = blockIdx.y * TB, s = blockIdx.z;
@@ -1097,6 +1112,7 @@ extern "C" int autovc_lstm_bwd_f32(int B, int T, int H, const float* dh_out, int
   float* P = workspace;
   float* dcs = workspace + (int64_t)splits * B * H;
   BwdArgs a{B, T, H, dh_out, d_ldb, d_ldt, gates, c_all, dG, dcs, P, splits};
+  a.prio = lstm_prio();
   return lstm_bwd_steps<false>(a, reverse, dG, W_hh_T, workspace, stream, "autovc_lstm_bwd_f32");
 }
 
@@ -1185,6 +1201,7 @@ extern "C" int autovc_lstm2_bwd_range_f32(int B, int T, int H, const float* dh1_
   float* dcs0 = dcs1 + BH;
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits};
+  a1.prio = a0.prio = lstm_prio();
   // splits 8: the wide-tile products (64 x 64 per workgroup, never fused); 2 / 4: 32 x 32 tiles
   return lstm2_bwd_steps<false>(a1, a0, splits, dG1, dG0, W_hh1_T, W_ih1_T, W_hh0_T, workspace, stream,
                                 "autovc_lstm2_bwd_f32", s_begin, s_end);
@@ -1326,6 +1343,7 @@ extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, in
   float* P = workspace;
   float* dcs = workspace + (int64_t)splits * B * H;
   BwdArgs a{B, T, H, dh_out, d_ldb, d_ldt, gates, c_all, dG, dcs, P, splits, reinterpret_cast<__bf16*>(dG_b)};
+  a.prio = lstm_prio();
   return lstm_bwd_steps<true>(a, reverse, reinterpret_cast<const float*>(dG_b), reinterpret_cast<const float*>(W_hh_T_b),
                               workspace, stream, "autovc_lstm_bwd_bf16");
 }
@@ -1355,6 +1373,7 @@ extern "C" int autovc_lstm2_bwd_range_bf16(int B, int T, int H, const float* dh1
   float* dcs0 = dcs1 + BH;
   BwdArgs a1{B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, dG1, dcs1, P1, splits, reinterpret_cast<__bf16*>(dG1_b)};
   BwdArgs a0{B, T, H, nullptr, 0, 0, gates0, c0, dG0, dcs0, PQ0, 2 * splits, reinterpret_cast<__bf16*>(dG0_b)};
+  a1.prio = a0.prio = lstm_prio();
   return lstm2_bwd_steps<true>(a1, a0, splits, reinterpret_cast<const float*>(dG1_b),
                                reinterpret_cast<const float*>(dG0_b), reinterpret_cast<const float*>(W_hh1_T_b),
                                reinterpret_cast<const float*>(W_ih1_T_b), reinterpret_cast<const float*>(W_hh0_T_b),

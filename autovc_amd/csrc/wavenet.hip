@@ -68,8 +68,6 @@ struct WnArgs {
   float* gsk;        // (B, 256) x {skip sum, -, -, step + 1}
   float* gh1;        // (B, 256) x {h1, -, -, step + 1}
   float* gpt;        // (2 parities, n_layers, B, 512) x {past-tap sum, step + 1} (8 bytes)
-  float* gmir;       // mirrored form: (8 XCDs, kMirSlots, B, 256) x {v0, v1, v2, mirror tag}
-  int* gepoch;       // mirrored form: the call counter that tags a call's mirror granules
   int* ctr;
   const float* teacher;
   int teacher_len;
@@ -929,27 +927,6 @@ constexpr int kGMaxL = 24;
 constexpr int kGMaxB = 8;
 constexpr int kGFault = 2;
 constexpr int kGErrInts = 32;                 // the error word's line (ints)
-// Mirrored all-gather (MIR): each phase's input granules are read from the fabric once per
-// XCD instead of once per workgroup.  Chain wave 0 of every workgroup, on reaching a phase,
-// first fetches its share of the phase's inputs — columns 8 r .. 8 r + 7 of every utterance,
-// r = the workgroup's rank among the 32 of its XCD, one granule per lane — with sc1 loads and
-// re-publishes them with plain 16-byte stores into its XCD's mirror slot, where they stay in
-// that XCD's L2; then every chain lane polls the mirror (sc1 loads: L1 bypassed, L2-served)
-// instead of the 256 producers.  A mirror granule's tag is
-// (call epoch << 24) | (phase index of the call), so a granule of another phase or call never
-// matches; kMirSlots = 4 rotating slots are enough: a fetcher can publish phase q only after
-// 8 producers consumed phase q - 1, which needed every workgroup's phase q - 2 output, so every
-// reader of its XCD is past phase q - 3.  Ranks come from per-XCD census counters in the
-// error word's line (zeroed every launch): any placement works, and an XCD that does not get
-// exactly 32 workgroups leaves mirror columns unfilled — its readers time out into the fault
-// path, never read wrong data.
-constexpr int kMirSlots = 4;
-constexpr int kMirCensus = 16;                // errw ints 16..23: workgroups seen per XCD
-__device__ __forceinline__ int mir_tag(int epoch, int t, int t0, int L, int p) {
-  return (int)(((uint32_t)epoch & 0xffu) << 24 | ((uint32_t)((t - t0) * (L + 2) + p) & 0xffffffu));
-}
-__device__ __forceinline__ int mir_slot(int t, int t0, int L, int p) { return ((t - t0) * (L + 2) + p) & (kMirSlots - 1); }
-__host__ __device__ inline int64_t g_mirror_f4(int B) { return (int64_t)8 * kMirSlots * B * 256; }
 
 struct GLds {                                 // float offsets into the dynamic LDS block
   int gw, h1, molp, mol, gum, in, part, xres, cnt, total;
@@ -1145,12 +1122,9 @@ __device__ __forceinline__ bool wn_grid_past_tap_chunk(const WnArgs& a, int lp, 
 }
 
 
-__global__ void wn_epoch_kernel(int* e) { *e = *e + 1; }
-
 // NB: utterance slots of the launch (1, 2, 4 or 8 >= B; slots >= B compute on utterance 0
-// and are dropped), so every per-utterance loop is straight-line code.  MIR: the mirrored
-// all-gather (a ninth, fetcher wave; see kMirSlots).
-template <int NB, bool MIR>
+// and are dropped), so every per-utterance loop is straight-line code
+template <int NB>
 __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0, int t1, int* errw, int ticks) {
   // no mul-add contraction: the NB instantiations (1, 2, 4, 8 utterance slots) must round every
   // utterance's arithmetic the same way (batch invariance: an utterance's samples do not depend
@@ -1195,21 +1169,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
   // access left in this XCD's L2 (system-scope acquire = buffer_inv sc0 sc1) before the first.
   if (tid < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
-  int xcc = 0, epoch = 0;
-  if constexpr (MIR) {
-    unsigned xr;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
-    xcc = (int)(xr & 7);
-    epoch = __builtin_amdgcn_readfirstlane(__hip_atomic_load(a.gepoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  }
-  float* const mir = a.gmir + (int64_t)xcc * kMirSlots * B * 256 * 4;    // this XCD's slots
-  const int64_t MS4 = (int64_t)B * 256 * 4;                               // floats of one slot
-  int mrank = 32;
-  if (MIR && wave == 1) {
-    if (lane == 0) mrank = __hip_atomic_fetch_add(errw + kMirCensus + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mrank = __builtin_amdgcn_readfirstlane(mrank);   // >= 32: a surplus workgroup of this XCD fetches nothing
-  }
-
 
   if (wave >= 4) {
     // =========================== past-tap waves: blocks of layer lp = os % L
@@ -1311,31 +1270,6 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
     const float* sp = s_part + par * 256;
     return ((sp[j] + sp[64 + j]) + sp[128 + j]) + sp[192 + j];
   };
-  // MIR: wave 0 copies this workgroup's share of phase (t, p)'s inputs (source src, tag stag)
-  // into the XCD's mirror slot; false: the wait gave up
-  auto mir_fetch = [&](const float* src, int stag, int t, int p) -> bool {
-    if (!MIR || wave != 1 || mrank >= 32) return true;
-    const int col = 8 * mrank + (lane & 7), b = lane >> 3;
-    const bool act = b < NB;
-    const int bs = b < B ? b : 0;
-    Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 8, t, p};
-    f32x4 g;
-    while (true) {
-      asm volatile("" ::: "memory");
-      g = ld4_l2(src, (bs * 256 + col) * 4);
-      if (__builtin_amdgcn_ballot_w64(act && tag_of(g) != stag) == 0) break;
-      sp.seen = __builtin_amdgcn_readfirstlane(tag_of(g));
-      if (!sp.tick()) return false;
-    }
-    if (act && b < B) {   // plain store through a wave-uniform descriptor: the line stays in this XCD's L2
-      g[3] = __int_as_float(mir_tag(epoch, t, t0, L, p));
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-          wave_uniform(mir + mir_slot(t, t0, L, p) * MS4), (short)0, 0x7fffffff, 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, g), r,
-                                             (uint32_t)(b * 256 + col) * 16u, 0, 0);
-    }
-    return true;
-  };
 
   noise(t0 - 1);
   float skip_acc = 0.f;                       // epilogue lane b: the skip sum of utterance b
@@ -1374,13 +1308,9 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
           // ---- the MoL parameters of step t-1 from its h1, then the draw (every workgroup)
           const int tp = t - 1;
           if (tp >= 0) {
-            if (!mir_fetch(a.gh1, t, t, 0)) { ok = false; break; }
             fetch_w2();                       // in flight during the h1 wait; live in this phase only
             f32x4 gh[NB];
-            const bool got = MIR ? poll_granules<NB>(mir + mir_slot(t, t0, L, 0) * MS4, o, B,
-                                                     mir_tag(epoch, t, t0, L, 0), gh, errw, ticks, 7, 0)
-                                 : poll_granules<NB>(a.gh1, o, B, tp + 1, gh, errw, ticks, 7, 0);
-            if (!got) { ok = false; break; }
+            if (!poll_granules<NB>(a.gh1, o, B, tp + 1, gh, errw, ticks, 7, 0)) { ok = false; break; }
 #pragma unroll
             for (int b = 0; b < NB; ++b) s_h1[b * 256 + o] = gh[b][0];
             if (!chain_sync(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
@@ -1460,15 +1390,7 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
         } else {
           // ---- this step's granules of layer l-1: [g_(l-1)[o] | x_(l-1)[2o], [2o + 1]]
           f32x4 gin[NB];
-          if (!mir_fetch(a.gring + ((int64_t)(l - 1) * RING + ts) * RB4, t + 1, t, l)) {
-            ok = false;
-            break;
-          }
-          const bool got = MIR ? poll_granules<NB>(mir + mir_slot(t, t0, L, l) * MS4, o, B,
-                                                   mir_tag(epoch, t, t0, L, l), gin, errw, ticks, 1, l)
-                               : poll_granules<NB>(a.gring + ((int64_t)(l - 1) * RING + ts) * RB4, o, B, t + 1,
-                                                   gin, errw, ticks, 1, l);
-          if (!got) {
+          if (!poll_granules<NB>(a.gring + ((int64_t)(l - 1) * RING + ts) * RB4, o, B, t + 1, gin, errw, ticks, 1, l)) {
             ok = false;
             break;
           }
@@ -1526,15 +1448,7 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
       } else if (p == L) {
         // ---- tail: the last layer's skip row os; wave 3 then draws the next sample's noise
         f32x4 gin[NB];
-        if (!mir_fetch(a.gring + ((int64_t)(L - 1) * RING + ts) * RB4, t + 1, t, L)) {
-          ok = false;
-          break;
-        }
-        const bool got = MIR ? poll_granules<NB>(mir + mir_slot(t, t0, L, L) * MS4, o, B,
-                                                 mir_tag(epoch, t, t0, L, L), gin, errw, ticks, 1, L)
-                             : poll_granules<NB>(a.gring + ((int64_t)(L - 1) * RING + ts) * RB4, o, B, t + 1, gin,
-                                                 errw, ticks, 1, L);
-        if (!got) {
+        if (!poll_granules<NB>(a.gring + ((int64_t)(L - 1) * RING + ts) * RB4, o, B, t + 1, gin, errw, ticks, 1, L)) {
           ok = false;
           break;
         }
@@ -1550,11 +1464,7 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
       } else {
         // ---- head: h1 row os = relu(W1[os] relu(skip) + b1[os])
         f32x4 gs[NB];
-        if (!mir_fetch(a.gsk, t + 1, t, L + 1)) { ok = false; break; }
-        const bool got = MIR ? poll_granules<NB>(mir + mir_slot(t, t0, L, L + 1) * MS4, o, B,
-                                                 mir_tag(epoch, t, t0, L, L + 1), gs, errw, ticks, 6, L + 1)
-                             : poll_granules<NB>(a.gsk, o, B, t + 1, gs, errw, ticks, 6, L + 1);
-        if (!got) { ok = false; break; }
+        if (!poll_granules<NB>(a.gsk, o, B, t + 1, gs, errw, ticks, 6, L + 1)) { ok = false; break; }
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[b] = w1o * fmaxf(gs[b][0], 0.f);
         if (!reduce_park(acc)) { ok = false; break; }
@@ -1664,25 +1574,15 @@ int g_wn_grid = [] {
 // which path the last autovc_wavenet_generate_f32 call took: 0 the per-layer launches, 1 the
 // all-CU persistent kernel (whose fault word the caller must read)
 int g_wn_last_path = 0;
-// the all-CU kernel's all-gather: 0 every workgroup polls the producers, 1 the per-XCD mirror
-// (kMirSlots), for batches of at least g_wn_mirror_min utterances (AVC_WN_MIRROR=0 / 1,
-// autovc_wavenet_set_mirror)
-int g_wn_mirror = [] {
-  const char* e = getenv("AVC_WN_MIRROR");
-  return e && e[0] == '1' ? 1 : 0;
-}();
-int g_wn_mirror_min = 1;
 
-template <int NB, bool MIR>
-bool grid_attr1(int bytes) {
+template <int NB>
+bool grid_attr(int bytes) {
   int per = 0;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(wn_grid_kernel<NB, MIR>),
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(wn_grid_kernel<NB>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess &&
-         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wn_grid_kernel<NB, MIR>, 64 * kGrW, bytes) == hipSuccess &&
+         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wn_grid_kernel<NB>, 64 * kGrW, bytes) == hipSuccess &&
          per >= 1;
 }
-template <int NB>
-bool grid_attr(int bytes) { return grid_attr1<NB, false>(bytes) && grid_attr1<NB, true>(bytes); }
 
 bool grid_eligible(int B, int n_layers, int taps, int R, int G, int S, int NO) {
   if (!g_wn_grid || (g_wn_grid == 2 && B > 2) || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
@@ -1724,15 +1624,6 @@ int autovc_wavenet_set_grid(int on) {
 }
 
 int autovc_wavenet_get_grid(void) { return g_wn_grid; }
-
-int autovc_wavenet_set_mirror(int on, int min_batch) {
-  AVC_CHECK_ARG((on == 0 || on == 1) && min_batch >= 1, "autovc_wavenet_set_mirror: on 0 / 1, min_batch >= 1");
-  g_wn_mirror = on;
-  g_wn_mirror_min = min_batch;
-  return avc::kOk;
-}
-
-int autovc_wavenet_get_mirror(void) { return g_wn_mirror ? g_wn_mirror_min : 0; }
 
 int autovc_wavenet_last_path(void) { return g_wn_last_path; }
 
@@ -1785,8 +1676,7 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
                          2 * (int64_t)n_layers * B * G + (int64_t)(S / kHR) * B * kMaxNO + 7 * 64;
   const int64_t grid = 16 * ((int64_t)n_layers * ring_frames(n_layers, layers_per_stack, taps) * B * 256 + 2 * (int64_t)B * 256) +
                        8 * 2 * (int64_t)n_layers * B * 512;   // wn_grid_kernel's tagged granules
-  const int64_t mirror = 128 + 16 * g_mirror_f4(B);          // its epoch line and per-XCD mirror slots
-  return floats * 4 + kCtrSlots * 4 + kGErrInts * 4 + grid + mirror + 1024;
+  return floats * 4 + kCtrSlots * 4 + kGErrInts * 4 + grid + 1024;
 }
 
 int autovc_wavenet_upsample_f32(int B, int Tc, int C, int n_stages, const int* scales, const float* c,
@@ -1867,15 +1757,7 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
   a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32);
   a.utt_base = utt_base; a.log_scale_min = log_scale_min;
   const int64_t used = reinterpret_cast<char*>(a.gpt + 2 * 2 * (int64_t)n_layers * B * 512) - static_cast<char*>(workspace);
-  // the mirror's epoch and slots follow the zeroed range: the epoch counts every call of this
-  // workspace, and a slot's granules only match their own call's tags
-  {
-    char* m = static_cast<char*>(workspace) + (used + 127) / 128 * 128;
-    a.gepoch = reinterpret_cast<int*>(m);
-    a.gmir = reinterpret_cast<float*>(m + 128);
-  }
-  const int64_t end = reinterpret_cast<char*>(a.gmir + 4 * g_mirror_f4(B)) - static_cast<char*>(workspace);
-  AVC_CHECK_ARG(end <= autovc_wavenet_workspace_bytes(B, T, n_layers, layers_per_stack, taps, R, G, S),
+  AVC_CHECK_ARG(used <= autovc_wavenet_workspace_bytes(B, T, n_layers, layers_per_stack, taps, R, G, S),
                 "%s: workspace layout overflow", fn);
 
   if (t0 == 0) AVC_HIP(avc::zero_async(workspace, (size_t)used, stream), "zero_async");
@@ -1885,25 +1767,10 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
     g_wn_last_path = 1;
     AVC_HIP(avc::zero_async(gerr, (size_t)kGErrInts * 4, stream), "zero_async");
     const int lds = 4 * g_lds(n_layers, n_out).total;
-    const bool mir = g_wn_mirror && B >= g_wn_mirror_min;
-    if (mir) {
-      hipLaunchKernelGGL(wn_epoch_kernel, dim3(1), dim3(1), 0, stream, a.gepoch);
-      AVC_CHECK_LAUNCH(fn);
-    }
-#define AVC_WNG(NB, M) hipLaunchKernelGGL((wn_grid_kernel<NB, M>), dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, \
-                                          gerr, g_wn_timeout_ticks)
-    if (mir) {
-      if (B == 1) AVC_WNG(1, true);
-      else if (B == 2) AVC_WNG(2, true);
-      else if (B <= 4) AVC_WNG(4, true);
-      else AVC_WNG(8, true);
-    } else {
-      if (B == 1) AVC_WNG(1, false);
-      else if (B == 2) AVC_WNG(2, false);
-      else if (B <= 4) AVC_WNG(4, false);
-      else AVC_WNG(8, false);
-    }
-#undef AVC_WNG
+    if (B == 1) hipLaunchKernelGGL(wn_grid_kernel<1>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else if (B == 2) hipLaunchKernelGGL(wn_grid_kernel<2>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else if (B <= 4) hipLaunchKernelGGL(wn_grid_kernel<4>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else hipLaunchKernelGGL(wn_grid_kernel<8>, dim3(256), dim3(64 * kGrW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
     AVC_CHECK_LAUNCH(fn);
     if (t1 == T) {
       hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);

@@ -552,16 +552,10 @@ int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, 
 int autovc_wavenet_set_grid(int on);
 int autovc_wavenet_get_grid(void);
 int autovc_wavenet_last_path(void);
-/* The all-CU kernel's all-gather for batches of >= min_batch utterances (on = 1; AVC_WN_MIRROR):
- * a fetcher wave per workgroup reads its share of each phase's granules once per XCD and
- * re-publishes them into that XCD's mirror (read through its L2) instead of every workgroup
- * reading all of them from the fabric; same results bit for bit.  get: min_batch, 0 = off. */
-int autovc_wavenet_set_mirror(int on, int min_batch);
-int autovc_wavenet_get_mirror(void);
 /* The first wait of the all-CU generation that timed out since the last clear: out5 = {kind
  * (0 none, 1 layer inputs, 2 past-tap sums, 3 LDS handshake, 4 past-tap inputs, 5 past-tap
- * consumers, 6 skip sums, 7 h1, 8 the mirror's fetcher), step, phase (or job), workgroup,
- * last tag seen (-1 if not recorded)}; synchronises the device. */
+ * consumers, 6 skip sums, 7 h1), step, phase (or job), workgroup, last tag seen (-1 if not
+ * recorded)}; synchronises the device. */
 int autovc_wavenet_grid_diag(int clear, int* out5);
 /* The all-CU generation's spin budget per wait in s_memrealtime ticks (0 = 1 s; a tiny value
  * forces the timeout path in tests) and its sticky fault word (bit 2: a wait timed out and the

@@ -36,20 +36,17 @@ def _cond(B, Tc, seed=4321):
     return torch.from_numpy(np.clip(rs.normal(0.43, 0.18, (B, 80, Tc)), 0, 1).astype(np.float32))
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["launches", "grid", "mirror"])
+@pytest.fixture(params=[0, 1], ids=["launches", "grid"])
 def wn_mode(request):
-    """Run a test with the per-layer launches, with the all-CU weight-resident generation
-    (wn_grid_kernel: B <= 8, 8..24 layers, 256 CUs; other shapes use the launches either way)
-    and with that kernel's per-XCD mirrored all-gather (autovc_wavenet_set_mirror).  (The
-    XCD-local form this fixture also ran until round 4 is retired: tools/retired/.)"""
+    """Run a test with the per-layer launches and with the all-CU weight-resident generation
+    (wn_grid_kernel: B <= 8, 8..24 layers, 256 CUs); other shapes use the launches either way.
+    (The XCD-local form this fixture also ran until round 4 is retired: tools/retired/.)"""
     from autovc_amd import _lib
     lib = _lib.load()
-    prev, prev_m = lib.autovc_wavenet_get_grid(), lib.autovc_wavenet_get_mirror()
-    _lib.call("autovc_wavenet_set_grid", int(request.param >= 1))
-    _lib.call("autovc_wavenet_set_mirror", int(request.param == 2), 1)
+    prev = lib.autovc_wavenet_get_grid()
+    _lib.call("autovc_wavenet_set_grid", int(request.param == 1))
     yield request.param
     _lib.call("autovc_wavenet_set_grid", prev)
-    _lib.call("autovc_wavenet_set_mirror", int(prev_m > 0), max(prev_m, 1))
 
 
 def rel(a, b):
@@ -276,50 +273,4 @@ def test_grid_default_mode_small_batches(cuda):
         assert torch.equal(m.generate(c1, seed=5, log_scale_min=LSM), out[2][0])   # the next call runs clean
     finally:
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        _set_modes(prev)
-
-
-@pytest.mark.parametrize("B", [8, 3, 1])
-def test_mirror_all_gather_bit_identical(cuda, B):
-    """The per-XCD mirrored all-gather (one fabric read per granule per XCD, re-published into
-    the XCD's L2) changes only how each phase's inputs travel: 24 layers, 1,024 free-running
-    samples over 8 conditioning chunks (8 persistent launches: the mirror's call epoch
-    advances every launch, its 4 slots rotate 26 times per sample) and a teacher-forced run's
-    MoL parameters equal the direct all-CU form bit for bit; no fault recorded; a forced
-    1-tick timeout raises DeviceFault and the next call runs clean."""
-    import ctypes
-    from autovc_amd import _lib, functional as AF
-    lib = _lib.load()
-    if lib.autovc_lstm_xcd_supported(64, 512) == 0:
-        pytest.skip("needs 8 XCDs x 32 CUs")
-    hp = ow.HPARAMS
-    m, _ = _model(hp, cuda)
-    c = _cond(B, 4, seed=37).to(cuda)
-    teacher = torch.from_numpy(np.random.RandomState(8).uniform(-0.9, 0.9, (B, 1024)).astype(np.float32)).to(cuda)
-    prev, prev_m = lib.autovc_wavenet_get_grid(), lib.autovc_wavenet_get_mirror()
-    out = {}
-    try:
-        _set_modes(1)
-        for mir in (0, 1, 0, 1):
-            _lib.call("autovc_wavenet_set_mirror", mir, 1)
-            y = m.generate(c, seed=23, log_scale_min=LSM, chunk=128)
-            _, mol = m.generate(c, seed=23, log_scale_min=LSM, teacher=teacher, return_mol=True, chunk=128)
-            assert lib.autovc_wavenet_last_path() == 1
-            if mir in out:
-                assert torch.equal(out[mir][0], y) and torch.equal(out[mir][1], mol)   # repeatable
-            out[mir] = (y, mol)
-        assert torch.isfinite(out[1][0]).all()
-        assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
-        f = ctypes.c_int(0)
-        _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(f))
-        assert f.value == 0
-        _lib.call("autovc_wavenet_set_mirror", 1, 1)
-        _lib.call("autovc_wavenet_set_timeout_ticks", 1)
-        with pytest.raises(AF.DeviceFault, match="wn_grid_kernel.*AVC_WN_GRID=0"):
-            m.generate(c, seed=23, log_scale_min=LSM, chunk=128)
-        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        assert torch.equal(m.generate(c, seed=23, log_scale_min=LSM, chunk=128), out[1][0])
-    finally:
-        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        _lib.call("autovc_wavenet_set_mirror", int(prev_m > 0), max(prev_m, 1))
         _set_modes(prev)

@@ -26,6 +26,10 @@ for STEP in ${1//,/ }; do
                timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -d gpurun_out/gpmc_$W -o run --output-format csv -- python tools/gemm_pmc.py $W ${GEMM_SHAPE:-4096 1024 8192} 10 > gpurun_out/gpmc_$W.log 2>&1 || exit 1
                timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d gpurun_out/gpmc2_$W -o run --output-format csv -- python tools/gemm_pmc.py $W ${GEMM_SHAPE:-4096 1024 8192} 10 > gpurun_out/gpmc2_$W.log 2>&1 || exit 1
              done ;;
+    bwdpmc) for P in fp32 bf16; do
+               timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/bpmc_f_$P -o run --output-format csv -- python tools/lstm_bwd_time.py $P > gpurun_out/bpmc_f_$P.log 2>&1 || exit 1
+               timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d gpurun_out/bpmc_h_$P -o run --output-format csv -- python tools/lstm_bwd_time.py $P > gpurun_out/bpmc_h_$P.log 2>&1 || exit 1
+             done ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
   rc=$?

@@ -18,4 +18,13 @@ wait
 # the trace build of the all-CU WaveNet kernel
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -DAVC_WN_GRID_TRACE \
   -I"$OUT/src/include" -x hip -c "$OUT/src/autovc_amd/csrc/wavenet.hip" -o "$OUT/wavenet_trace.o"
+# the mirrored all-gather (round 5, commit d196949)
+MREV=${MIRROR_REV:-d196949}
+mkdir -p "$OUT/mirror/autovc_amd/csrc" "$OUT/mirror/include"
+for f in common.h twiddle1024.h wavenet.hip; do
+  git show "$MREV:autovc_amd/csrc/$f" > "$OUT/mirror/autovc_amd/csrc/$f"
+done
+git show "$MREV:include/autovc_hip.h" > "$OUT/mirror/include/autovc_hip.h"
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I"$OUT/mirror/include" \
+  -x hip -c "$OUT/mirror/autovc_amd/csrc/wavenet.hip" -o "$OUT/wavenet_mirror.o"
 ls -la "$OUT"/*.o

@@ -4,7 +4,11 @@ faster version of that class could save.  python tools/step_whatif.py [fp32|bf16
   default      the product step
   no_lstm_dw   LSTM weight-gradient GEMMs (W_ih, W_hh) skipped
   no_conv_dw   conv weight-gradient GEMMs (Conv-BN stacks) skipped
-  no_side      every queued weight-gradient launch skipped"""
+  no_side      every queued weight-gradient launch skipped
+  blas_lstm_dw the LSTM weight-gradient GEMMs on torch.mm (hipBLASLt; the h_{t-1} shift and
+               its first-frame mask ignored: the price of a library-speed GEMM there)
+  blas_plain   additionally every unmasked GEMM (no conv view) on torch.mm
+Variants: python tools/step_whatif.py fp32 default blas_lstm_dw ..."""
 import contextlib
 import os
 import sys
@@ -27,10 +31,29 @@ def run(prec, variant, steps=20, warm=5):
             return
         return orig_launch(dev, outs, fn, *inputs)
 
+    def blas(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, accumulate=False, a_off=0, b_off=0, c_off=0, bias1=None,
+             bias2=None, **_):
+        Am = A.reshape(-1)[a_off:].as_strided((K, M) if ta else (M, K), (lda, 1))
+        Am = Am.t() if ta else Am
+        Bm = B.reshape(-1)[b_off:].as_strided((K, N) if tb else (N, K), (ldb, 1))
+        Bm = Bm if tb else Bm.t()
+        Cm = C.reshape(-1)[c_off:].as_strided((M, N), (ldc, 1))
+        if accumulate:
+            Cm.addmm_(Am, Bm)
+        else:
+            Cm.copy_(Am @ Bm)
+        for b in (bias1, bias2):
+            if b is not None:
+                Cm.add_(b[:N])
+
     def gemm(M, N, K, *a, **k):
         # the LSTM dW GEMMs: M = 4H rows, K = B*T, both operands transposed
-        if variant == "no_lstm_dw" and M in (4096, 2048) and K == 8192 and a[2] == 1 and a[5] == 1:
+        lstm_dw = M in (4096, 2048) and K == 8192 and a[2] == 1 and a[5] == 1
+        if variant == "no_lstm_dw" and lstm_dw:
             return
+        plain = not k.get("a_conv") and not k.get("b_conv")
+        if (variant == "blas_lstm_dw" and lstm_dw) or (variant == "blas_plain" and (lstm_dw or plain)):
+            return blas(M, N, K, *a, **{n: v for n, v in k.items() if n not in ("a_conv", "b_conv", "splits")})
         return orig_gemm(M, N, K, *a, **k)
     AF._grad_launch = launch
     AF.gemm = gemm
@@ -61,7 +84,8 @@ def run(prec, variant, steps=20, warm=5):
 
 def main():
     prec = sys.argv[1] if len(sys.argv) > 1 else "fp32"
-    for v in ("default", "no_lstm_dw", "no_side", "default"):
+    torch.backends.cuda.matmul.allow_tf32 = False
+    for v in sys.argv[2:] or ("default", "no_lstm_dw", "no_side", "default"):
         print(f"{prec} {v:12s} {run(prec, v):7.3f} ms/step", flush=True)
 
 
