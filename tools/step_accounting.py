@@ -11,10 +11,10 @@ import sys
 CATS = [
     ("lstm2 fwd (persistent)", r"lstm_persist_kernel<1024|lstm2_rs_kernel"),
     ("lstm2 fwd (per step)", r"lstm2_fwd_step"),
-    ("lstm2 bwd products", r"lstm2_bwd_rec"),
+    ("lstm2 bwd (fused step / products)", r"lstm2_bwd_rec|lstm2_bwd_fused"),
     ("lstm2 bwd pointwise", r"lstm2_bwd_pointwise"),
     ("lstm1 fwd", r"lstm_fwd_step|lstm_persist_kernel<512|lstm_xcd_fwd"),
-    ("lstm1 bwd", r"lstm_bwd_(rec|pointwise)|lstm_xcd_bwd"),
+    ("lstm1 bwd", r"lstm_bwd_(rec|pointwise|fused)|lstm_xcd_bwd"),
     ("encoder BLSTM", r"blstm_"),
     ("GEMM fp32", r"gemm_kernel<"),
     ("GEMM bf16", r"gemm_bf16_kernel<"),
