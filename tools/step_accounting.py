@@ -33,7 +33,10 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
-    seg = rows[adam[-2] + 1:adam[-1] + 1]
+    # --adam N: the step ending at the N-th Adam launch (0-based; default the last one) — a bench
+    # trace holds the fp32 steps first, then the bf16 ones
+    n = int(sys.argv[sys.argv.index("--adam") + 1]) if "--adam" in sys.argv else len(adam) - 1
+    seg = rows[adam[n - 1] + 1:adam[n] + 1]
     t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
     cat = collections.Counter()
     calls = collections.Counter()
