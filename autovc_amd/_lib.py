@@ -45,7 +45,6 @@ sig("autovc_preprocess_f64", c_ptr, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_
     c_ptr, c_ptr)
 sig("autovc_gemm_workspace_floats", c_int, c_int, c_int)
 sig("autovc_gemm_set_lds_reserve", c_int)
-sig("autovc_gemm_set_cc", c_int)
 sig("autovc_stream_create_cu_mask", c_int, c_ptr, c_ptr)
 sig("autovc_stream_destroy", c_ptr)
 sig("autovc_event_create", c_ptr)
@@ -53,7 +52,6 @@ sig("autovc_event_destroy", c_ptr)
 sig("autovc_event_record_any", c_ptr, c_ptr)
 sig("autovc_stream_wait_event", c_ptr, c_ptr)
 sig("autovc_stamp", c_ptr, c_ptr)
-sig("autovc_xcc_probe", c_ptr, c_ptr)
 sig("autovc_gemm_bf16_splits", c_int, c_int, c_int, c_int)
 sig("autovc_gemm_batched_f32", c_int, c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_int, c_ptr, c_i64, c_i64, c_int,
     c_ptr, c_i64, c_i64, c_int, c_ptr)

@@ -93,19 +93,7 @@ __global__ void stamp_kernel(unsigned long long* dst) {
   const unsigned long long t = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) dst[0] = t;
 }
-__global__ void xcc_kernel(int* dst) {
-  unsigned x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  if (threadIdx.x == 0) dst[0] = (int)(x & 15);
-}
 }  // namespace
-
-extern "C" int autovc_xcc_probe(int* dst, hipStream_t stream) {
-  AVC_CHECK_ARG(dst != nullptr, "autovc_xcc_probe: null destination");
-  hipLaunchKernelGGL(xcc_kernel, dim3(1), dim3(64), 0, stream, dst);
-  AVC_CHECK_LAUNCH("autovc_xcc_probe");
-  return avc::kOk;
-}
 
 extern "C" int autovc_stamp(uint64_t* dst, hipStream_t stream) {
   AVC_CHECK_ARG(dst != nullptr, "autovc_stamp: null destination");

@@ -829,162 +829,6 @@ __global__ __launch_bounds__(256) void splitk_stats_kernel(int64_t M, int64_t N,
   }
 }
 
-// ---------------------------------------------------------------- K-strided x K-strided fp32
-// The weight gradients C (+)= A^T B with A (K x M) and B (K x N) both K-strided (dW = dG^T x,
-// dW_hh = dG^T h_{t-1}: B may carry the conv mask of Opnd, e.g. the one-frame shift), on
-// 128 x 128 tiles by ONE 4-wave workgroup per CU (each wave 64 x 64 = 2 x 2 blocks of
-// v_mfma_f32_32x32x2_f32).  The operands never pass through VGPRs: every k-stage (32 k-rows
-// of A's and B's 128 columns, 32 KB) is copied global -> LDS by the LDS-DMA
-// (buffer_load_dwordx4 ... lds, 16 bytes per lane; a masked element reads as zero through the
-// descriptor's range check), CC_NS = 3 stages deep: iteration kt waits with a counted vmcnt
-// for stage kt only (stage kt + 1 stays in flight across the raw barrier), issues stage
-// kt + 2 into the buffer read in iteration kt - 1, and multiplies stage kt out of LDS.  The
-// LDS image is row-linear per DMA instruction (two k-rows of 512 bytes); odd k-rows hold
-// their columns rotated by 32 floats (the rotation is applied to the SOURCE address), so the
-// two lane halves of an A or B fragment read (k-rows 2k and 2k + 1) hit disjoint banks.
-// Same numbers as gemm_kernel for the same k order?  No: the k order inside a stage differs,
-// so results agree to fp32 summation-order noise, not bit for bit; the selection is global
-// (AVC_GEMM_CC), so a run uses one kernel throughout (graph replay == eager).
-constexpr int CC_BM = 128, CC_BN = 128, CC_NT = 256;
-
-// one LDS-DMA instruction: 16 bytes per lane from rsrc + off into lds_dst + 16 lane (a plain
-// device function: the LDS address-space cast inside a template kernel's body made this
-// clang drop the template's host launch stubs)
-__device__ __forceinline__ void cc_dma16(__amdgpu_buffer_rsrc_t r, float* lds_dst, uint32_t off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, off, 0, 0, 0);
-}
-
-template <int CC_NS, int CC_BK>
-__global__ __launch_bounds__(CC_NT, 1) void gemm_cc_kernel(int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C,
-                                                          int64_t ldc, int accumulate, int k_per_split,
-                                                          float* __restrict__ slab) {
-  constexpr int CC_IMG = CC_BK * 128;                    // floats of one operand's stage image
-  constexpr int CC_STAGE = 2 * CC_IMG;                   // A image, then B image
-  constexpr int PW = CC_BK / 4;                          // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) float lds[CC_NS * CC_STAGE];
-  // wave-uniform in SGPRs: the DMA's descriptor and LDS base (M0) must be scalar, or the
-  // compiler wraps every DMA in a lane-by-lane loop
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  // XCD-aware tile order (speed only), as gemm_kernel
-  const int nx = gridDim.x, nwg = gridDim.x * gridDim.y;
-  const int Lb = blockIdx.x + nx * blockIdx.y;
-  const int xcd = Lb % 8, slot = Lb / 8, qq = nwg / 8, rr = nwg % 8;
-  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
-  const int m0 = (logical / nx) * CC_BM, n0 = (logical % nx) * CC_BN;
-  const int kbeg = blockIdx.z * k_per_split;
-  const int kend = min(K, kbeg + k_per_split);
-  const int nk = (kend - kbeg + CC_BK - 1) / CC_BK;
-
-  // DMA map: wave w issues instructions j = 0..7 of a stage; instruction g = 8 w + j copies
-  // k-rows 2 (g & 15), 2 (g & 15) + 1 of A (g < 16) or B; lane i: row 2 (g & 15) + (i >> 5),
-  // LDS columns 4 (i & 31) .. + 3 = source columns c .. c + 3, c = (4 (i & 31) - 32 (row & 1)) & 127
-  const int hrow = lane >> 5;
-  const int dcol = (4 * (lane & 31) - 32 * hrow) & 127;
-  const bool isB = wave >= 2;                              // waves 0, 1: A; waves 2, 3: B
-  const Opnd& O = isB ? B : A;
-  const int c0 = (isB ? n0 : m0) + dcol;                   // this lane's first source column
-  const int R = isB ? N : M;
-  const bool col_ok = c0 < R;                              // R % 4 == 0: a float4 is all in or all out
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(O.p), (short)0,
-                                                                        (int)kOOB, 0x00020000);
-  const bool conv = O.conv_T > 0;
-  const int tapc = conv ? c0 / O.conv_C : 0;               // conv view: the column's tap
-  const int shift = conv ? O.tap0 : 0;
-  // per DMA row j (k = kbeg + kt BK + 2 ((wave & 1) 8 + j) + hrow): the byte offset of the next
-  // stage's copy and (conv view) the row's frame position in its sequence, both advanced by
-  // one stage (BK rows) per issue — issue() runs for kt = 0, 1, 2, ... in order
-  uint32_t off[PW];
-  int tp[PW];
-  const uint32_t step_off = (uint32_t)(CC_BK * O.ld * 4);
-  const int step_t = conv ? CC_BK % O.conv_T : 0;
-#pragma unroll
-  for (int j = 0; j < PW; ++j) {
-    const int k = kbeg + 2 * ((wave & 1) * PW + j) + hrow;
-    off[j] = (uint32_t)(((int64_t)(k + shift) * O.ld + c0) * 4);
-    tp[j] = conv ? k % O.conv_T : 0;
-  }
-  auto issue = [&](int kt) {
-    const int buf = kt % CC_NS;
-    float* img = lds + buf * CC_STAGE + (isB ? CC_IMG : 0);
-#pragma unroll
-    for (int j = 0; j < PW; ++j) {
-      const int pr = (wave & 1) * PW + j;                   // row pair of this operand
-      const int k = kbeg + kt * CC_BK + 2 * pr + hrow;
-      bool ok = col_ok && k < kend;
-      if (conv) ok = ok && (unsigned)(tp[j] + tapc + shift) < (unsigned)O.conv_T;
-      cc_dma16(rsrc, img + 2 * pr * 128, ok ? off[j] : kOOB);
-      off[j] += step_off;
-      if (conv) {
-        tp[j] += step_t;
-        if (tp[j] >= O.conv_T) tp[j] -= O.conv_T;
-      }
-    }
-  };
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-#pragma unroll
-  for (int s0 = 0; s0 < CC_NS - 1; ++s0)
-    if (s0 < nk) issue(s0);
-  const int li = lane & 31, h = lane >> 5;
-  for (int kt = 0; kt < nk; ++kt) {
-    // stage kt landed; the stages issued after it (up to NS - 2) stay in flight
-    const int ahead = min(CC_NS - 2, nk - 1 - kt);        // stages to leave in flight
-    if (ahead * PW == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead * PW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + CC_NS - 1 < nk) issue(kt + CC_NS - 1);
-    const float* As = lds + (kt % CC_NS) * CC_STAGE;
-    const float* Bs = As + CC_IMG;
-#pragma unroll
-    for (int kk = 0; kk < CC_BK; kk += 2) {
-      const int rowo = (kk + h) * 128;
-      float af[2], bf[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = As[rowo + ((wr * 64 + i * 32 + li + 32 * h) & 127)];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = Bs[rowo + ((wc * 64 + j * 32 + li + 32 * h) & 127)];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
-  }
-
-  // epilogue (gemm_kernel's C/D map of 32x32: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
-  float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
-  const int64_t ld = slab ? N : ldc;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wc * 64 + j * 32 + li;
-    if (n >= N) continue;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < M) {
-          float v = acc[i][j][r];
-          float* dst = out + (int64_t)m * ld + n;
-          if (!slab && accumulate) v += *dst;
-          *dst = v;
-        }
-      }
-    }
-  }
-}
-
 bool aligned_ld(int64_t ld) { return (ld & 3) == 0; }
 
 // Tile configurations (id -> BM, BN, BK; waves of 64x64 unless noted)
@@ -1018,10 +862,6 @@ Batch g_batch = {0, 0, 0, nullptr};   // set by gemm_impl for every launch
 // (fp32 15.91-15.92 vs 15.61-15.65 ms/step, bf16 11.24-11.30 vs 9.99-10.00;
 // profiles/r03/ab_gemm_fixup.txt; identical losses)
 const bool g_fixup = [] { const char* e = getenv("AVC_GEMM_FIXUP"); return e && e[0] == '1'; }();
-// AVC_GEMM_CC=<v> / autovc_gemm_set_cc: the fp32 K-strided x K-strided GEMMs (weight
-// gradients) on gemm_cc_kernel: 1 = 3 stages of 32 k (96 KB LDS), 2 = 2 x 32 (64 KB),
-// 3 = 4 x 16 (64 KB), 4 = 3 x 16 (48 KB); 0 = the register-staged tiles
-int g_gemm_cc = [] { const char* e = getenv("AVC_GEMM_CC"); return e && e[0] >= '1' && e[0] <= '4' ? e[0] - '0' : 0; }();
 constexpr int kTickets = 16384;          // tile counters at the head of a split-K workspace (64 KiB)
 constexpr unsigned kLdsPerCU = 160 * 1024;
 
@@ -1209,21 +1049,6 @@ void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t s
   }
 }
 
-template <int NS, int BK>
-void launch_cc(dim3 g, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob, float* C, int64_t ldc, int acc, int kps,
-               float* sl) {
-  hipLaunchKernelGGL((gemm_cc_kernel<NS, BK>), g, dim3(CC_NT), dyn_lds_for(4u * NS * 2 * BK * 128), st, M, N, K, oa, ob,
-                     C, ldc, acc, kps, sl);
-}
-
-void launch_gemm_cc(int v, dim3 g, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob, float* C, int64_t ldc,
-                    int acc, int kps, float* sl) {
-  if (v == 1) launch_cc<3, 32>(g, st, M, N, K, oa, ob, C, ldc, acc, kps, sl);
-  else if (v == 2) launch_cc<2, 32>(g, st, M, N, K, oa, ob, C, ldc, acc, kps, sl);
-  else if (v == 3) launch_cc<4, 16>(g, st, M, N, K, oa, ob, C, ldc, acc, kps, sl);
-  else launch_cc<3, 16>(g, st, M, N, K, oa, ob, C, ldc, acc, kps, sl);
-}
-
 }  // namespace
 
 // split-K workspace: kTickets tile counters (zero before the first call, left zero by every
@@ -1285,9 +1110,7 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
     }();
     cfg = g_force_cfg >= 0 ? kCfg[g_force_cfg] : t128 >= 512 ? kCfg[wino_cfg] : kCfg[8];
   }
-  const bool cc = g_gemm_cc && !bf16 && batch == 1 && a_trans && b_trans && !a_conv_T && seg_len == 0 &&
-                  (int64_t)K * std::max(lda, ldb) < (int64_t)kOOB / 8;
-  const int BKc = cc ? (g_gemm_cc <= 2 ? 32 : 16) : cfg.bk;
+  const int BKc = cfg.bk;
   int64_t kps = ((int64_t)K + splits - 1) / splits;
   kps = ((kps + BKc - 1) / BKc) * BKc;
   splits = (int)((K + kps - 1) / kps);
@@ -1295,21 +1118,6 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   AVC_CHECK_ARG(splits == 1 || workspace, "autovc_gemm_f32: split-K needs a workspace");
   Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0, nullptr, 0, seg_len, seg_T, seg_t0};
   Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0, nullptr, 0, seg_len, seg_T, seg_t0};
-  if (cc) {
-    AVC_CHECK_ARG(!bias1 && !bias2, "autovc_gemm_f32: the K-strided weight-gradient kernel takes no bias");
-    const dim3 g((N + CC_BN - 1) / CC_BN, (M + CC_BM - 1) / CC_BM, splits);
-    float* sl = splits > 1 ? workspace + kTickets : nullptr;
-    launch_gemm_cc(g_gemm_cc, g, stream, M, N, K, oa, ob, C, ldc, accumulate, (int)kps, sl);
-    AVC_CHECK_LAUNCH("autovc_gemm/cc");
-    if (splits > 1) {
-      const int gx = (N + 255) / 256;
-      const int gy = (int)std::max<int64_t>(1, std::min<int64_t>(M, 4096 / gx + 1));
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, gy), dim3(256), 0, stream, (int64_t)M, (int64_t)N, splits, sl, C,
-                         ldc, bias1, bias2, accumulate);
-      AVC_CHECK_LAUNCH("autovc_gemm/splitk_reduce");
-    }
-    return avc::kOk;
-  }
   const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, batch > 1 ? batch : splits);
   const bool fixup = splits > 1 && g_fixup && (int64_t)grid.x * grid.y <= kTickets;
   float* slab = splits > 1 ? workspace + kTickets : nullptr;
@@ -1518,12 +1326,6 @@ extern "C" int autovc_bnconv_dw_bf16_f32(int B, int T, int Co, int Ci, const voi
   const Opnd ob{(const float*)x, Ci, T, Ci, -2, x_coef, x_act};
   return bn_gemm(x_coef ? 2 : 0, src, 1, 1, Co, 5 * Ci, M, oa, ob, dWf, nullptr, 0, nullptr, nullptr, 0, nullptr,
                  workspace, stream);
-}
-
-extern "C" int autovc_gemm_set_cc(int on) {
-  AVC_CHECK_ARG(on >= 0 && on <= 4, "autovc_gemm_set_cc: 0 .. 4");
-  g_gemm_cc = on;
-  return avc::kOk;
 }
 
 extern "C" int autovc_gemm_set_lds_reserve(int bytes) {

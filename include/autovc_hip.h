@@ -106,11 +106,6 @@ int autovc_gemm_f32(int M, int N, int K,
                     const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                     float* C, int64_t ldc, const float* bias1, const float* bias2,
                     int accumulate, int splits, float* workspace, hipStream_t stream);
-/* Kernel choice for the fp32 GEMMs whose operands are both K-strided (a_trans = b_trans = 1,
- * no A conv view: the weight gradients): 1 = the LDS-DMA kernel (128 x 128 tiles, one
- * workgroup per CU, operands copied global -> LDS three k-stages ahead), 0 = the register-staged
- * tiles.  The two sum each k-stage in a different order (fp32 noise apart).  AVC_GEMM_CC. */
-int autovc_gemm_set_cc(int on);
 /* LDS bytes per CU that GEMM launches (fp32 and bf16) leave free from now on (0 = none):
  * their workgroups are padded so that no more of them share a CU than fit beside that
  * reserve — a latency-bound kernel on another stream keeps a slot on every CU. */
@@ -137,9 +132,6 @@ int autovc_stream_wait_event(hipStream_t stream, hipEvent_t ev);
  * captured graph, so a replay's streams can be time-stamped without a tracer (which
  * serialises them). */
 int autovc_stamp(uint64_t* dst, hipStream_t stream);
-/* Measurement only: a one-workgroup kernel that stores the XCD it ran on (HW_REG_XCC_ID) into
- * *dst — with a one-CU masked stream (autovc_stream_create_cu_mask) it maps mask bits to XCDs. */
-int autovc_xcc_probe(int* dst, hipStream_t stream);
 /* Same contract, bf16 compute (BASELINE config 3, "bf16 with fp32 master"): the fp32
  * operands are rounded to bf16 (RNE) as they are staged, v_mfma_f32_32x32x16_bf16
  * accumulates in fp32, C / bias / accumulate stay fp32 — the numerics of a torch.autocast

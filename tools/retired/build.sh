@@ -27,4 +27,13 @@ done
 git show "$MREV:include/autovc_hip.h" > "$OUT/mirror/include/autovc_hip.h"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I"$OUT/mirror/include" \
   -x hip -c "$OUT/mirror/autovc_amd/csrc/wavenet.hip" -o "$OUT/wavenet_mirror.o"
+# the LDS-DMA weight-gradient GEMM (round 5, commit 9d01bc2)
+CREV=${CC_REV:-9d01bc2}
+mkdir -p "$OUT/cc/autovc_amd/csrc" "$OUT/cc/include"
+for f in common.h gemm.hip; do
+  git show "$CREV:autovc_amd/csrc/$f" > "$OUT/cc/autovc_amd/csrc/$f"
+done
+git show "$CREV:include/autovc_hip.h" > "$OUT/cc/include/autovc_hip.h"
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I"$OUT/cc/include" \
+  -x hip -c "$OUT/cc/autovc_amd/csrc/gemm.hip" -o "$OUT/gemm_cc.o"
 ls -la "$OUT"/*.o
