@@ -1090,6 +1090,13 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
       AVC_CHECK_ARG(pl.splits <= splits || workspace,
                     "autovc_gemm_bf16_f32: split-K plan needs the workspace of autovc_gemm_bf16_splits");
       splits = pl.splits;
+      // the weight gradients (both operands K-strided) at most 2 splits: they run on the gradient
+      // side stream beside the recurrences, where half the chip for twice as long costs the
+      // step less than 4-way slabs and their reduce (training step 8.53-8.55 vs 8.99-9.05 ms;
+      // 3 splits 8.67-8.68, 1 split 8.75-8.79; profiles/r05/ab_bf16_dw_splits.txt).
+      // AVC_BF16_DW_SPLITS=<n> sets the cap (0 = the plan's choice)
+      static const int dw_cap = [] { const char* e = getenv("AVC_BF16_DW_SPLITS"); return e ? atoi(e) : 2; }();
+      if (dw_cap > 0 && a_trans && b_trans) splits = std::min(splits, dw_cap);
     }
   }
   GemmShape cfg = bf16 ? pick_config_bf16(M, N, batch > 1 ? batch : splits) : pick_config(M, N, K, splits);
@@ -1210,9 +1217,12 @@ int small_splits(int M, int N, int K) {
   return std::max(1, s);
 }
 
-BnPlan plan_bn(int M, int N, int K) {
+BnPlan plan_bn(int M, int N, int K, bool dw) {
   const PlanBf16 pl = plan_bf16(M, N, K, small_splits(M, N, K));
   int splits = pl.splits;
+  // (the stacks' weight gradients keep the plan's split: capping it at 2 or 1 measured
+  // slower, 8.70-8.73 / 9.27-9.29 vs 8.53-8.55 ms/step, profiles/r05/ab_bf16_dw_splits.txt)
+  (void)dw;
   const GemmShape cfg = pl.cfg >= 0 ? kCfgBf16[pl.cfg] : pick_config_bf16(M, N, splits);
   int64_t kps = ((int64_t)K + splits - 1) / splits;
   kps = (kps + cfg.bk - 1) / cfg.bk * cfg.bk;
@@ -1226,7 +1236,7 @@ constexpr int kStatsRows = 256;
 int bn_gemm(int bnop, int src, int a_trans, int b_trans, int M, int N, int K, Opnd oa, Opnd ob, float* C,
             const float* bias, int mode, const float* yp, const float* coefp, int actp, double* part, float* ws,
             hipStream_t st) {
-  const BnPlan pl = plan_bn(M, N, K);
+  const BnPlan pl = plan_bn(M, N, K, a_trans && b_trans);
   const dim3 grid((N + pl.cfg.bn - 1) / pl.cfg.bn, (M + pl.cfg.bm - 1) / pl.cfg.bm, pl.splits);
   g_batch = Batch{0, 0, 0, nullptr};
   const int id = pl.cfg.id;
@@ -1275,7 +1285,7 @@ extern "C" int autovc_bnconv_stats_rows(int64_t M) { return (int)std::max<int64_
 extern "C" int64_t autovc_bnconv_workspace_floats(int B, int T, int Ci, int Co) {
   if (B <= 0 || T <= 0 || Ci <= 0 || Co <= 0) return 0;
   const int M = B * T;
-  const BnPlan f = plan_bn(M, Co, 5 * Ci), x = plan_bn(M, Ci, 5 * Co), w = plan_bn(Co, 5 * Ci, M);
+  const BnPlan f = plan_bn(M, Co, 5 * Ci, false), x = plan_bn(M, Ci, 5 * Co, false), w = plan_bn(Co, 5 * Ci, M, true);
   return std::max({(int64_t)f.splits * M * Co, (int64_t)x.splits * M * Ci, (int64_t)w.splits * Co * 5 * Ci});
 }
 

@@ -90,7 +90,8 @@ _GRAD_STREAMS: dict = {}
 # LDS left free per CU for the recurrence's step workgroup (37 KB) while side GEMMs run;
 # measured per precision (bench.py, same box, alternating): fp32 21.1 ms/step with room
 # kept vs 21.9 without; bf16 13.1 without vs 13.3 with (its 128x128 tiles run better 2/CU)
-GRAD_LDS_RESERVE = {"fp32": int(os.environ.get("AVC_GRAD_LDS_RESERVE", "38912")), "bf16": 0}
+GRAD_LDS_RESERVE = {"fp32": int(os.environ.get("AVC_GRAD_LDS_RESERVE", "38912")),
+                    "bf16": int(os.environ.get("AVC_GRAD_LDS_RESERVE_BF16", "0"))}
 
 
 def _grad_stream(dev):
@@ -322,7 +323,9 @@ _DW_MIN_BLOCKS = int(os.environ.get("AVC_DW_MIN_BLOCKS", "1024"))
 
 
 def _splits_for(M, N, K):
-    """Split-K factor for the long-K weight-gradient GEMMs: >= 1024 blocks of 64x64 output
+    """Split-K factor for the long-K weight-gradient GEMMs (fp32; capping it at 2 or 1 measured
+    slower, 14.48-14.50 / 14.70-14.79 vs 14.39-14.42 ms/step, profiles/r05/ab_bf16_dw_splits.txt;
+    the bf16 plan caps its own at 2): >= 1024 blocks of 64x64 output
     tiles (4 per CU) while each split keeps >= 1024 k (tools/gemm_bench.hip sweep: conv dW
     512x2560x8192 42.7 TF unsplit -> 81.6 TF at 4 splits).  Tiny outputs (the BLSTM weight
     gradients, 128 x 32..512 over K = B*T = 8192: 2-16 tiles) split deep instead — up to 64
@@ -1306,6 +1309,9 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
         splits //= 2
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+    # (keeping the batch past this recurrence, to run beside the encoder BLSTMs instead,
+    # measured slower: bf16 9.06-9.07 vs 9.03, fp32 15.62-15.64 vs 14.41-14.46 ms,
+    # profiles/r05/ab_grad_defer.txt)
     mark = _grad_mark(dev)   # queued weight gradients run beside this latency-bound recurrence
     if _bf16_rec(H):
         dGb = torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16)
