@@ -1301,8 +1301,10 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     WT = conv_weight(W_hh, 8 if _bf16_rec(H) else 7)
     # split-K of the recurrent product (same box, alternating): fp32 4 ways at H=1024 (256
     # workgroups; 8 ways: +0.1 ms/step), 8 ways at H=512 (fills the chip: -0.15 ms); bf16
-    # 8 ways everywhere (half the bytes per workgroup: -0.15 ms).  AVC_LSTM_SPLITS overrides.
-    splits = int(os.environ.get("AVC_LSTM_SPLITS", "0")) or (8 if (H <= 512 or _bf16_rec(H)) else 4)
+    # 4 ways with the fused steps (decoder lstm1: 8.46-8.52 vs 8.55-8.57 ms/step for 8 ways,
+    # profiles/r05/ab_lstm1_splits.txt; 8 ways measured best with the launch pair, round 2).
+    # AVC_LSTM_SPLITS overrides.
+    splits = int(os.environ.get("AVC_LSTM_SPLITS", "0")) or (4 if _bf16_rec(H) else (8 if H <= 512 else 4))
     # the recurrent K (4H fp32 floats, 2H bf16 pairs) must cut into multiples of 64 per split
     kdim = 2 * H if _bf16_rec(H) else 4 * H
     while splits > 1 and kdim % (64 * splits):
