@@ -94,6 +94,9 @@ sig("autovc_gemm_bf16_f32", c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,
     c_ptr, c_i64, c_int, c_int, c_int, c_int,
     c_ptr, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_ptr)
+sig("autovc_gemm_bf16src_f32", c_int, c_int, c_int, c_ptr, c_i64, c_int,
+    c_ptr, c_i64, c_int, c_int, c_int, c_int,
+    c_ptr, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_int, c_ptr)
 sig("autovc_bn_workspace_bytes", c_int)
 sig("autovc_bn_stats_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_f32, c_ptr,
     c_ptr, c_ptr)

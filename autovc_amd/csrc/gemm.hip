@@ -545,17 +545,22 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
       if (bias1) bsum += bias1[n];
       if (bias2) bsum += bias2[n];
     }
+    if (!slab && accumulate) {   // every prior value in flight before the first store
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = m0 + wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (m < M) acc[i][j][r] = (acc[i][j][r] + bsum) + out[m * ld + n];
+        }
+      bsum = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t m = m0 + wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < M) {
-          float v = acc[i][j][r] + bsum;
-          float* dst = out + m * ld + n;
-          if (!slab && accumulate) v += *dst;
-          *dst = v;
-        }
+        if (m < M) out[m * ld + n] = acc[i][j][r] + bsum;
       }
     }
   }
@@ -730,17 +735,22 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
       if (bias1) bsum += bias1[n];
       if (bias2) bsum += bias2[n];
     }
+    if (!slab && accumulate) {   // every prior value in flight before the first store
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = m0 + wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (m < M) acc[i][j][r] = (acc[i][j][r] + bsum) + out[m * ld + n];
+        }
+      bsum = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t m = m0 + wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < M) {
-          float v = acc[i][j][r] + bsum;
-          float* dst = out + m * ld + n;
-          if (!slab && accumulate) v += *dst;
-          *dst = v;
-        }
+        if (m < M) out[m * ld + n] = acc[i][j][r] + bsum;
       }
     }
   }
@@ -984,7 +994,11 @@ PlanBf16 plan_bf16(int M, int N, int K, int requested) {
   if (t2 >= 16) {
     int s = (int)std::max<int64_t>(1, std::min<int64_t>(4, (256 + t2 / 2) / t2));
     while (s > 1 && K / s < 512) --s;
-    return {2, s};
+    // shallow K (<= 1024) cannot split its way to a full chip: one 256-row tile per CU on
+    // 32-128 CUs left the encoder BLSTM projections (8192 x 128 x 512) at 25 us; the caller's
+    // split on 128 / 64 tiles fills the chip (AVC_BF16_SHALLOW=0: the old plan)
+    static const bool shallow = [] { const char* e = getenv("AVC_BF16_SHALLOW"); return !e || e[0] != '0'; }();
+    if (!(shallow && K <= 1024 && t2 * s < 256)) return {2, s};
   }
   return {-1, requested};
 }
@@ -1019,14 +1033,14 @@ void launch_gemm_bn_bf16(int id, dim3 grid, hipStream_t st, int M, int N, int K,
   }
 }
 
-template <int BM, int BN, int BK, int WM, int WN>
+template <int BM, int BN, int BK, int WM, int WN, int SRC = 0>
 void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
                          float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   // two stages in flight only on the 256-row tiles, and not for 256x256 with both operands
   // K-strided (spills): tools/gemm_bf16_bench.hip, profiles/r02/gemm_bf16_deep.txt
 #define AVC_DEEP(AR, BR) (BM == 256 && !(BN == 256 && !(AR) && !(BR)))
-#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, AVC_DEEP(AR, BR)>), grid, dim3(NT), \
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, AVC_DEEP(AR, BR), 0, SRC>), grid, dim3(NT), \
                                          dyn_lds_for(bf16_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, \
                                          K, oa, ob, C, ldc, b1, b2, acc, kps, slab, g_batch)
   if (!a_trans && !b_trans) AVC_L(true, true);
@@ -1037,16 +1051,25 @@ void launch_layouts_bf16(int a_trans, int b_trans, dim3 grid, hipStream_t st, in
 #undef AVC_DEEP
 }
 
+template <int SRC>
+void launch_gemm_bf16_src(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa,
+                          Opnd ob, float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps,
+                          float* slab) {
+  switch (id) {
+    case 0: launch_layouts_bf16<128, 128, 64, 64, 64, SRC>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 2: launch_layouts_bf16<256, 128, 64, 64, 64, SRC>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 3: launch_layouts_bf16<256, 256, 64, 128, 64, SRC>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 4: launch_layouts_bf16<256, 256, 32, 128, 64, SRC>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    default: launch_layouts_bf16<64, 64, 64, 32, 32, SRC>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+  }
+}
+
+// src: 0 = fp32 operands, 1 = A held as bf16 (autovc_gemm_bf16src_f32)
 void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa,
                       Opnd ob, float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps,
-                      float* slab) {
-  switch (id) {
-    case 0: launch_layouts_bf16<128, 128, 64, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
-    case 2: launch_layouts_bf16<256, 128, 64, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
-    case 3: launch_layouts_bf16<256, 256, 64, 128, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
-    case 4: launch_layouts_bf16<256, 256, 32, 128, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
-    default: launch_layouts_bf16<64, 64, 64, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
-  }
+                      float* slab, int src = 0) {
+  if (src == 1) launch_gemm_bf16_src<1>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab);
+  else launch_gemm_bf16_src<0>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab);
 }
 
 }  // namespace
@@ -1063,12 +1086,15 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
                                const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                float* C, int64_t ldc, const float* bias1, const float* bias2,
                                int accumulate, int splits, float* workspace, hipStream_t stream,
-                               int seg_len = 0, int seg_T = 0, int seg_t0 = 0) {
+                               int seg_len = 0, int seg_T = 0, int seg_t0 = 0, int src = 0) {
   AVC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "autovc_gemm: negative dims");
   if (M == 0 || N == 0) return avc::kOk;
   AVC_CHECK_ARG(A && B && C, "autovc_gemm: null operand");
   AVC_CHECK_ARG(AVC_ALIGNED16(A) && AVC_ALIGNED16(B), "autovc_gemm: A/B must be 16-byte aligned");
   AVC_CHECK_ARG(aligned_ld(lda) && aligned_ld(ldb), "autovc_gemm: lda/ldb must be multiples of 4");
+  AVC_CHECK_ARG(src == 0 || (src == 1 && bf16 && batch == 1 && !a_conv_T && !seg_len && lda % 8 == 0 &&
+                             (a_trans ? M % 8 == 0 : K % 8 == 0)),
+                "autovc_gemm_bf16src_f32: src 1 needs a plain bf16 A with lda and its contiguous dim multiples of 8");
   // the contiguous extent of each operand must be a multiple of 4 (float4 staging)
   AVC_CHECK_ARG(a_trans ? (M % 4 == 0) : (K % 4 == 0), "autovc_gemm: A contiguous dim %% 4 != 0");
   AVC_CHECK_ARG(b_trans ? (N % 4 == 0) : (K % 4 == 0), "autovc_gemm: B contiguous dim %% 4 != 0");
@@ -1132,7 +1158,7 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
                       : Batch{0, 0, 0, fixup ? reinterpret_cast<int*>(workspace) : nullptr};
   if (bf16)
     launch_gemm_bf16(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate,
-                     (int)kps, slab);
+                     (int)kps, slab, src);
   else
     launch_gemm(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
                 slab);
@@ -1191,6 +1217,20 @@ extern "C" int autovc_gemm_tchunk_bf16_f32(int M, int N, int B, int T, int t0, i
                                            const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc,
                                            int accumulate, int splits, float* workspace, hipStream_t stream) {
   return gemm_tchunk(true, M, N, B, T, t0, Tc, A, lda, Bm, ldb, b_tap0, C, ldc, accumulate, splits, workspace, stream);
+}
+
+// autovc_gemm_bf16_f32 with A read from a bf16 copy the producer already wrote (src = 1;
+// lda in bf16 elements): half of A's operand bytes.  The recurrences' backward writes the
+// gate gradients twice (dG fp32, dGb = RNE(dG)), so the weight and input gradients that
+// read dGb equal autovc_gemm_bf16_f32 on dG bit for bit.
+extern "C" int autovc_gemm_bf16src_f32(int M, int N, int K,
+                                       const void* A, int64_t lda, int a_trans,
+                                       const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
+                                       float* C, int64_t ldc, const float* bias1, const float* bias2,
+                                       int accumulate, int splits, float* workspace, int src, hipStream_t stream) {
+  return gemm_impl(true, 1, 0, 0, 0, M, N, K, reinterpret_cast<const float*>(A), lda, a_trans, 0, 0, 0, B, ldb,
+                   b_trans, b_conv_T, b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream,
+                   0, 0, 0, src);
 }
 
 extern "C" int autovc_gemm_bf16_splits(int M, int N, int K, int requested) {

@@ -302,9 +302,11 @@ def current_precision():
 
 
 def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_conv=None,
-         bias1=None, bias2=None, accumulate=False, splits=1, a_off=0, b_off=0, c_off=0):
+         bias1=None, bias2=None, accumulate=False, splits=1, a_off=0, b_off=0, c_off=0, a_bf16=None):
     """C[M,N] (+)= A(m,k) B(k,n) (+bias); offsets are in floats from the tensors' data.
-    bf16 MFMA under precision("bf16"), exact fp32 MFMA otherwise."""
+    bf16 MFMA under precision("bf16"), exact fp32 MFMA otherwise.  a_bf16: a bf16 tensor laid
+    out like A holding RNE(A) (a producer's own copy); under bf16 the GEMM reads it instead
+    of A (autovc_gemm_bf16src_f32, half of A's bytes, the same result)."""
     ac = a_conv or (0, 0, 0)
     bc = b_conv or (0, 0, 0)
     ws = 0
@@ -312,6 +314,11 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
         splits = _lib.load().autovc_gemm_bf16_splits(M, N, K, splits)
     if splits > 1:
         ws = _ws(C.device, 4 * _lib.load().autovc_gemm_workspace_floats(M, N, splits), "gemm")
+    if a_bf16 is not None and _PRECISION[0] == "bf16" and a_conv is None and _BF16_SRC:
+        _lib.call("autovc_gemm_bf16src_f32", M, N, K, a_bf16.data_ptr() + 2 * a_off, lda, a_trans,
+                  B.data_ptr() + 4 * b_off, ldb, b_trans, bc[0], bc[1], bc[2],
+                  C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, 1, _s())
+        return
     fn = "autovc_gemm_bf16_f32" if _PRECISION[0] == "bf16" else "autovc_gemm_f32"
     _lib.call(fn, M, N, K,
               A.data_ptr() + 4 * a_off, lda, a_trans, ac[0], ac[1], ac[2],
@@ -319,6 +326,8 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
               C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, _s())
 
 
+# the LSTM weight / input gradients read the backward's bf16 dG copy (AVC_BF16_SRC=0: dG)
+_BF16_SRC = os.environ.get("AVC_BF16_SRC", "1") != "0"
 _DW_MIN_BLOCKS = int(os.environ.get("AVC_DW_MIN_BLOCKS", "1024"))
 
 
@@ -1323,13 +1332,16 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
         _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
                   WT.data_ptr(), dG.data_ptr(), 0, splits, ws, _s())
     _flush_grad_queue(after=mark)
-    return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs)
+    return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=dGb if _bf16_rec(H) else None)
 
 
-def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
+def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=None):
     """Parameter gradients (queued beside the next recurrence, into the flat gradient
-    buffer) and dx of one large-H layer from its gate gradients dG (B, T, 4H)."""
+    buffer) and dx of one large-H layer from its gate gradients dG (B, T, 4H).  dGb: the
+    recurrence's bf16 copy of dG (bf16 recurrences), which the GEMMs read instead of dG."""
     p_ih, p_hh, p_bih, p_bhh = params
+    kb = {"a_bf16": dGb} if dGb is not None else {}
+    keep = (dGb,) if dGb is not None else ()
     B, T, I = x.shape
     H = h.shape[2]
     dev = x.device
@@ -1338,12 +1350,14 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
     if needs[1]:
         go = _GradOut(p_ih, W_ih.shape, dev)
         _grad_launch(dev, go, lambda go=go: gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I,
-                                                     splits=_splits_for(4 * H, I, M), accumulate=go.acc), dG, x)
+                                                     splits=_splits_for(4 * H, I, M), accumulate=go.acc, **kb),
+                     dG, x, *keep)
         dWih = go.result()
     if needs[2]:
         go = _GradOut(p_hh, (4 * H, H), dev)
         _grad_launch(dev, go, lambda go=go: gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
-                                                     splits=_splits_for(4 * H, H, M), accumulate=go.acc), dG, h)
+                                                     splits=_splits_for(4 * H, H, M), accumulate=go.acc, **kb),
+                     dG, h, *keep)
         dWhh = go.result()
     if needs[3] or needs[4]:
         gi, gh = _bias_outs(p_bih, p_bhh, (4 * H,), dev)
@@ -1352,7 +1366,7 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs):
         dbih, dbhh = gi.result(), gh.result()
     if needs[0]:
         dx = torch.empty_like(x)
-        gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I)
+        gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I, **kb)
     return dx, dWih, dWhh, dbih, dbhh
 
 
@@ -1587,8 +1601,9 @@ class LSTM2StackFn(torch.autograd.Function):
         if dw is None:
             steps(0, T + 1)
             _flush_grad_queue(after=mark)
-            grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]))
-            grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0)
+            grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]),
+                                         dGb=dG1b if bf else None)
+            grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0, dGb=dG0b if bf else None)
             return (grads0[0], *grads0[1:], *grads1[1:], None)
         # time-chunked weight gradients: after iterations [0, (c + 1) Tc + 1) the last
         # (c + 1) Tc steps of both layers' dG are final, so chunk c's four dW GEMMs start
@@ -1615,6 +1630,12 @@ class LSTM2StackFn(torch.autograd.Function):
 # than the launch boundary it saves.
 
 
+# AVC_BLSTM_CAT=0: the encoder BLSTM's per-direction projection GEMMs (two 128-column outputs
+# forward, and a dx pair whose second GEMM accumulates)
+_BLSTM_CAT = os.environ.get("AVC_BLSTM_CAT", "1") != "0"
+_BLSTM_SIDE = os.environ.get("AVC_BLSTM_SIDE", "1") != "0"
+
+
 class BLSTMLayerFn(torch.autograd.Function):
     """One bidirectional nn.LSTM layer with H=32 (encoder, model_vc_mel.py:61)."""
 
@@ -1627,20 +1648,28 @@ class BLSTMLayerFn(torch.autograd.Function):
         G = 4 * H
         dev = x.device
         gx = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32)
-        gemm(B * T, G, I, x, I, 0, Wih_f, I, 0, gx, 2 * G, bias1=bih_f, bias2=bhh_f)
-        gemm(B * T, G, I, x, I, 0, Wih_b, I, 0, gx, 2 * G, bias1=bih_b, bias2=bhh_b, c_off=G)
+        if _BLSTM_CAT:
+            # both directions' projections as one GEMM over [W_ih_f; W_ih_b] (same sums; one
+            # 8192 x 256 output instead of two 128-column ones), reused by the backward's dx
+            Wcat = torch.cat((Wih_f, Wih_b), 0)
+            gemm(B * T, 2 * G, I, x, I, 0, Wcat, I, 0, gx, 2 * G, bias1=torch.cat((bih_f, bih_b)),
+                 bias2=torch.cat((bhh_f, bhh_b)))
+        else:
+            Wcat = None
+            gemm(B * T, G, I, x, I, 0, Wih_f, I, 0, gx, 2 * G, bias1=bih_f, bias2=bhh_f)
+            gemm(B * T, G, I, x, I, 0, Wih_b, I, 0, gx, 2 * G, bias1=bih_b, bias2=bhh_b, c_off=G)
         h = torch.empty((B, T, 2 * H), device=dev, dtype=torch.float32)
         c = torch.empty((B, T, 2 * H), device=dev, dtype=torch.float32)
         gates = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32) if save else None
         _lib.call("autovc_blstm_fwd_f32", B, T, H, 2, gx.data_ptr(), Whh_f.data_ptr(), Whh_b.data_ptr(),
                   h.data_ptr(), c.data_ptr(), _p(gates), _s())
-        ctx.save_for_backward(x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates)
+        ctx.save_for_backward(x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates, Wcat)
         ctx.params = ((Wih_f, Whh_f, bih_f, bhh_f), (Wih_b, Whh_b, bih_b, bhh_b))
         return h
 
     @staticmethod
     def backward(ctx, dh):
-        x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates = ctx.saved_tensors
+        x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates, Wcat = ctx.saved_tensors
         if gates is None:
             raise RuntimeError("BLSTM backward needs the forward run with gradients enabled")
         dh = dh.contiguous()
@@ -1656,28 +1685,36 @@ class BLSTMLayerFn(torch.autograd.Function):
         _flush_grad_queue(after=mark)
         grads = [None] * 10
         dG2 = dG.view(M, 2 * G)
+        # the weight / bias gradients go to the side stream like the large LSTMs' (_grad_launch;
+        # AVC_BLSTM_SIDE=0 keeps them on the main stream): released beside the next recurrence
+        launch = _grad_launch if _BLSTM_SIDE else (lambda _dev, _outs, fn, *_in: fn())
         for d, (iW, iH, iBi, iBh) in enumerate(((1, 2, 3, 4), (5, 6, 7, 8))):
             pW, pH, pBi, pBh = ctx.params[d]
             if ctx.needs_input_grad[iW]:
                 go = _GradOut(pW, pW.shape, dev)
-                gemm(G, I, M, dG, 2 * G, 1, x, I, 1, go.buf, I, a_off=d * G, splits=_splits_for(G, I, M),
-                     accumulate=go.acc)
+                launch(dev, go, lambda go=go, d=d: gemm(G, I, M, dG, 2 * G, 1, x, I, 1, go.buf, I, a_off=d * G,
+                                                        splits=_splits_for(G, I, M), accumulate=go.acc), dG, x)
                 grads[iW] = go.result()
             if ctx.needs_input_grad[iH]:
                 go = _GradOut(pH, pH.shape, dev)
                 # previous step in processing order: t-1 forward, t+1 backward direction
-                gemm(G, H, M, dG, 2 * G, 1, h, 2 * H, 1, go.buf, H, a_off=d * G, b_off=d * H,
-                     b_conv=(T, H, -1 if d == 0 else 1), splits=_splits_for(G, H, M), accumulate=go.acc)
+                launch(dev, go, lambda go=go, d=d: gemm(G, H, M, dG, 2 * G, 1, h, 2 * H, 1, go.buf, H, a_off=d * G,
+                                                        b_off=d * H, b_conv=(T, H, -1 if d == 0 else 1),
+                                                        splits=_splits_for(G, H, M), accumulate=go.acc), dG, h)
                 grads[iH] = go.result()
             if ctx.needs_input_grad[iBi] or ctx.needs_input_grad[iBh]:
                 gi, gh = _bias_outs(pBi, pBh, (G,), dev)
-                colsum(dG2[:, d * G:(d + 1) * G], gi.buf, gh.buf, accumulate=gi.acc)
+                launch(dev, (gi, gh), lambda gi=gi, gh=gh, d=d: colsum(dG2[:, d * G:(d + 1) * G], gi.buf, gh.buf,
+                                                                        accumulate=gi.acc), dG)
                 grads[iBi], grads[iBh] = gi.result(), gh.result()
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            gemm(M, I, G, dG, 2 * G, 0, Wih_f, I, 1, dx, I)
-            gemm(M, I, G, dG, 2 * G, 0, Wih_b, I, 1, dx, I, a_off=G, accumulate=True)
+            if Wcat is not None:   # dx = [dG_f dG_b] [W_ih_f; W_ih_b]: one K = 2G GEMM, no accumulate pass
+                gemm(M, I, 2 * G, dG, 2 * G, 0, Wcat, I, 1, dx, I)
+            else:
+                gemm(M, I, G, dG, 2 * G, 0, Wih_f, I, 1, dx, I)
+                gemm(M, I, G, dG, 2 * G, 0, Wih_b, I, 1, dx, I, a_off=G, accumulate=True)
         grads[0] = dx
         return tuple(grads)
 

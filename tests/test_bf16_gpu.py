@@ -169,3 +169,39 @@ def test_lstm2_bf16_stacked_backward_wide_tiles(cuda, monkeypatch, B, H):
         grads[splits] = [xd.grad] + [p.grad for p in pd]
     for a, b in zip(grads["8"], grads["4"]):
         assert rel(a, b) < 5e-3   # a partial sum order flips a few bf16 roundings of dG
+
+
+@pytest.mark.parametrize("M,N,K,at,bt,bconv,acc", [
+    (4096, 1024, 8192, 1, 1, None, 1),          # LSTM dW_ih (planned 256x256, 2 splits), accumulate
+    (2048, 512, 64 * 128, 1, 1, (128, 512, -1), 0),   # dW_hh: B = h one step back (conv form)
+    (8192, 1024, 4096, 0, 1, None, 0),          # dx = dG W_ih (256x256, split)
+    (8192, 320, 2048, 0, 1, None, 0),           # decoder lstm1 dx (320 inputs)
+    (1000, 520, 520, 0, 0, None, 1),            # ragged, 64-tile fallback, accumulate
+])
+def test_gemm_bf16src_equals_fp32_source(cuda, M, N, K, at, bt, bconv, acc):
+    """autovc_gemm_bf16src_f32 reading a bf16 copy RNE(A) gives autovc_gemm_bf16_f32's result
+    on the fp32 A bit for bit (the staging rounds A the same way)."""
+    from autovc_amd import functional as AF
+    g = torch.Generator().manual_seed(M + N + K)
+    A = (torch.randn(K, M, generator=g) if at else torch.randn(M, K, generator=g)).to(cuda)
+    Bm = (torch.randn(K, N, generator=g) if bt else torch.randn(N, K, generator=g)).to(cuda)
+    C0 = torch.randn(M, N, generator=g).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    kw = dict(b_conv=bconv, accumulate=bool(acc), bias1=None if at else bias)
+    with AF.precision("bf16"):
+        C1 = C0.clone()
+        AF.gemm(M, N, K, A, A.shape[1], at, Bm, Bm.shape[1], bt, C1, N, **kw)
+        C2 = C0.clone()
+        AF.gemm(M, N, K, A, A.shape[1], at, Bm, Bm.shape[1], bt, C2, N, a_bf16=A.bfloat16(), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2)
+
+
+def test_gemm_bf16src_rejects_unaligned_lead(cuda):
+    from autovc_amd import _lib
+    A = torch.zeros(64, 68, device=cuda, dtype=torch.bfloat16)
+    B = torch.zeros(68, 64, device=cuda)
+    C = torch.zeros(64, 64, device=cuda)
+    with pytest.raises(ValueError, match="multiples of 8"):
+        _lib.call("autovc_gemm_bf16src_f32", 64, 64, 68, A.data_ptr(), 68, 0, B.data_ptr(), 64, 1, 0, 0, 0,
+                  C.data_ptr(), 64, 0, 0, 0, 1, 0, 1, 0)
