@@ -1064,12 +1064,16 @@ void launch_gemm_bf16_src(int id, int a_trans, int b_trans, dim3 grid, hipStream
   }
 }
 
-// src: 0 = fp32 operands, 1 = A held as bf16 (autovc_gemm_bf16src_f32)
+// src: bit 0 = A, bit 1 = B held as bf16 (autovc_gemm_bf16src_f32); 0 = fp32 operands
 void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa,
                       Opnd ob, float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps,
                       float* slab, int src = 0) {
-  if (src == 1) launch_gemm_bf16_src<1>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab);
-  else launch_gemm_bf16_src<0>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab);
+  switch (src) {
+    case 1: launch_gemm_bf16_src<1>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 2: launch_gemm_bf16_src<2>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 3: launch_gemm_bf16_src<3>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    default: launch_gemm_bf16_src<0>(id, a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+  }
 }
 
 }  // namespace
@@ -1092,9 +1096,12 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   AVC_CHECK_ARG(A && B && C, "autovc_gemm: null operand");
   AVC_CHECK_ARG(AVC_ALIGNED16(A) && AVC_ALIGNED16(B), "autovc_gemm: A/B must be 16-byte aligned");
   AVC_CHECK_ARG(aligned_ld(lda) && aligned_ld(ldb), "autovc_gemm: lda/ldb must be multiples of 4");
-  AVC_CHECK_ARG(src == 0 || (src == 1 && bf16 && batch == 1 && !a_conv_T && !seg_len && lda % 8 == 0 &&
-                             (a_trans ? M % 8 == 0 : K % 8 == 0)),
-                "autovc_gemm_bf16src_f32: src 1 needs a plain bf16 A with lda and its contiguous dim multiples of 8");
+  AVC_CHECK_ARG(src >= 0 && src <= 3 && (src == 0 || (bf16 && batch == 1 && !seg_len)),
+                "autovc_gemm_bf16src_f32: bad src %d", src);
+  AVC_CHECK_ARG(!(src & 1) || (!a_conv_T && lda % 8 == 0 && (a_trans ? M % 8 == 0 : K % 8 == 0)),
+                "autovc_gemm_bf16src_f32: a bf16 A must be plain with lda and its contiguous dim multiples of 8");
+  AVC_CHECK_ARG(!(src & 2) || (!b_conv_T && ldb % 8 == 0 && (b_trans ? N % 8 == 0 : K % 8 == 0)),
+                "autovc_gemm_bf16src_f32: a bf16 B must be plain with ldb and its contiguous dim multiples of 8");
   // the contiguous extent of each operand must be a multiple of 4 (float4 staging)
   AVC_CHECK_ARG(a_trans ? (M % 4 == 0) : (K % 4 == 0), "autovc_gemm: A contiguous dim %% 4 != 0");
   AVC_CHECK_ARG(b_trans ? (N % 4 == 0) : (K % 4 == 0), "autovc_gemm: B contiguous dim %% 4 != 0");
@@ -1219,17 +1226,17 @@ extern "C" int autovc_gemm_tchunk_bf16_f32(int M, int N, int B, int T, int t0, i
   return gemm_tchunk(true, M, N, B, T, t0, Tc, A, lda, Bm, ldb, b_tap0, C, ldc, accumulate, splits, workspace, stream);
 }
 
-// autovc_gemm_bf16_f32 with A read from a bf16 copy the producer already wrote (src = 1;
-// lda in bf16 elements): half of A's operand bytes.  The recurrences' backward writes the
+// autovc_gemm_bf16_f32 with A (src bit 0) and / or B (bit 1) read from bf16 copies the
+// producers already wrote (ld in bf16 elements): half of those operands' bytes.  The recurrences' backward writes the
 // gate gradients twice (dG fp32, dGb = RNE(dG)), so the weight and input gradients that
 // read dGb equal autovc_gemm_bf16_f32 on dG bit for bit.
 extern "C" int autovc_gemm_bf16src_f32(int M, int N, int K,
                                        const void* A, int64_t lda, int a_trans,
-                                       const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
+                                       const void* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                        float* C, int64_t ldc, const float* bias1, const float* bias2,
                                        int accumulate, int splits, float* workspace, int src, hipStream_t stream) {
-  return gemm_impl(true, 1, 0, 0, 0, M, N, K, reinterpret_cast<const float*>(A), lda, a_trans, 0, 0, 0, B, ldb,
-                   b_trans, b_conv_T, b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream,
+  return gemm_impl(true, 1, 0, 0, 0, M, N, K, reinterpret_cast<const float*>(A), lda, a_trans, 0, 0, 0,
+                   reinterpret_cast<const float*>(B), ldb, b_trans, b_conv_T, b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream,
                    0, 0, 0, src);
 }
 

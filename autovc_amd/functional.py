@@ -302,11 +302,13 @@ def current_precision():
 
 
 def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_conv=None,
-         bias1=None, bias2=None, accumulate=False, splits=1, a_off=0, b_off=0, c_off=0, a_bf16=None):
+         bias1=None, bias2=None, accumulate=False, splits=1, a_off=0, b_off=0, c_off=0, a_bf16=None,
+         b_bf16=None):
     """C[M,N] (+)= A(m,k) B(k,n) (+bias); offsets are in floats from the tensors' data.
-    bf16 MFMA under precision("bf16"), exact fp32 MFMA otherwise.  a_bf16: a bf16 tensor laid
-    out like A holding RNE(A) (a producer's own copy); under bf16 the GEMM reads it instead
-    of A (autovc_gemm_bf16src_f32, half of A's bytes, the same result)."""
+    bf16 MFMA under precision("bf16"), exact fp32 MFMA otherwise.  a_bf16 / b_bf16: bf16
+    tensors laid out like A / B holding RNE(A) / RNE(B) (a producer's own copy, a per-step
+    weight copy); under bf16 the GEMM reads them instead (autovc_gemm_bf16src_f32, half of
+    those operands' bytes, the same result)."""
     ac = a_conv or (0, 0, 0)
     bc = b_conv or (0, 0, 0)
     ws = 0
@@ -314,10 +316,14 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
         splits = _lib.load().autovc_gemm_bf16_splits(M, N, K, splits)
     if splits > 1:
         ws = _ws(C.device, 4 * _lib.load().autovc_gemm_workspace_floats(M, N, splits), "gemm")
-    if a_bf16 is not None and _PRECISION[0] == "bf16" and a_conv is None and _BF16_SRC:
-        _lib.call("autovc_gemm_bf16src_f32", M, N, K, a_bf16.data_ptr() + 2 * a_off, lda, a_trans,
-                  B.data_ptr() + 4 * b_off, ldb, b_trans, bc[0], bc[1], bc[2],
-                  C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, 1, _s())
+    src = 0
+    if _PRECISION[0] == "bf16" and _BF16_SRC:
+        src = (1 if a_bf16 is not None and a_conv is None else 0) | (2 if b_bf16 is not None and b_conv is None else 0)
+    if src:
+        pa = a_bf16.data_ptr() + 2 * a_off if src & 1 else A.data_ptr() + 4 * a_off
+        pb = b_bf16.data_ptr() + 2 * b_off if src & 2 else B.data_ptr() + 4 * b_off
+        _lib.call("autovc_gemm_bf16src_f32", M, N, K, pa, lda, a_trans, pb, ldb, b_trans, bc[0], bc[1], bc[2],
+                  C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, src, _s())
         return
     fn = "autovc_gemm_bf16_f32" if _PRECISION[0] == "bf16" else "autovc_gemm_f32"
     _lib.call(fn, M, N, K,
@@ -326,8 +332,18 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
               C.data_ptr() + 4 * c_off, ldc, _p(bias1), _p(bias2), int(accumulate), splits, ws, _s())
 
 
-# the LSTM weight / input gradients read the backward's bf16 dG copy (AVC_BF16_SRC=0: dG)
+# the LSTM weight / input gradients read the backward's bf16 dG copy, and the LSTM input
+# projections / input gradients the step's bf16 W_ih copy (AVC_BF16_SRC=0: the fp32 tensors)
 _BF16_SRC = os.environ.get("AVC_BF16_SRC", "1") != "0"
+_BF16_WSRC = os.environ.get("AVC_BF16_WSRC", "1") != "0"     # the W_ih copies alone
+
+
+def _wbf16(W):
+    """The step's cached bf16 copy of a 2-D LSTM weight under bf16 (None otherwise)."""
+    if (_PRECISION[0] != "bf16" or not (_BF16_SRC and _BF16_WSRC) or not _cacheable(W) or W.dim() != 2
+            or W.shape[1] % 8):
+        return None
+    return conv_weight(W, 6)
 _DW_MIN_BLOCKS = int(os.environ.get("AVC_DW_MIN_BLOCKS", "1024"))
 
 
@@ -513,6 +529,9 @@ def prepare_weights(convs, lstms, T, training, B=None):
             if _cacheable(W):
                 for kind in kinds:
                     add(kind, W)
+        W = m.weight_ih_l0   # the input projection's (and input gradient's) bf16 operand (_wbf16)
+        if _bf16_rec(H) and _BF16_SRC and _BF16_WSRC and _cacheable(W) and W.shape[1] % 8 == 0:
+            add(6, W)
     for conv in convs:
         W = conv.weight
         if not _cacheable(W) or W.shape[2] != KS:
@@ -1255,7 +1274,8 @@ class LSTMLayerFn(torch.autograd.Function):
         H = W_hh.shape[1]
         dev = x.device
         gx = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-        gemm(B * T, 4 * H, I, x, I, 0, W_ih, I, 0, gx, 4 * H, bias1=b_ih, bias2=b_hh)
+        gemm(B * T, 4 * H, I, x, I, 0, W_ih, I, 0, gx, 4 * H, bias1=b_ih, bias2=b_hh,
+             b_bf16=_wbf16(W_ih) if _bf16_rec(H) else None)
         h = torch.empty((B, T, H), device=dev, dtype=torch.float32)
         c = torch.empty((B, T, H), device=dev, dtype=torch.float32)
         gates = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
@@ -1366,7 +1386,7 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=None):
         dbih, dbhh = gi.result(), gh.result()
     if needs[0]:
         dx = torch.empty_like(x)
-        gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I, **kb)
+        gemm(M, I, 4 * H, dG, 4 * H, 0, W_ih, I, 1, dx, I, b_bf16=_wbf16(W_ih) if dGb is not None else None, **kb)
     return dx, dWih, dWhh, dbih, dbhh
 
 
@@ -1505,7 +1525,8 @@ class LSTM2StackFn(torch.autograd.Function):
         H = W_hh0.shape[1]
         dev = x.device
         gx0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-        gemm(B * T, 4 * H, I, x, I, 0, W_ih0, I, 0, gx0, 4 * H, bias1=b_ih0, bias2=b_hh0)
+        gemm(B * T, 4 * H, I, x, I, 0, W_ih0, I, 0, gx0, 4 * H, bias1=b_ih0, bias2=b_hh0,
+             b_bf16=_wbf16(W_ih0) if _bf16_rec(H) else None)
         h0, c0, h1, c1 = (torch.empty((B, T, H), device=dev, dtype=torch.float32) for _ in range(4))
         g0 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
         g1 = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32) if save else None
@@ -1633,7 +1654,16 @@ class LSTM2StackFn(torch.autograd.Function):
 # AVC_BLSTM_CAT=0: the encoder BLSTM's per-direction projection GEMMs (two 128-column outputs
 # forward, and a dx pair whose second GEMM accumulates)
 _BLSTM_CAT = os.environ.get("AVC_BLSTM_CAT", "1") != "0"
-_BLSTM_SIDE = os.environ.get("AVC_BLSTM_SIDE", "1") != "0"
+# the BLSTM weight/bias gradients on the side stream: under bf16 only (bench, alternating:
+# bf16 8.03-8.04 vs 8.29-8.30 ms/step; fp32 14.46 vs 14.37-14.39, where the side stream is
+# already full; profiles/r05/ab_blstm_side.txt).  AVC_BLSTM_SIDE=1 / 0 forces it either way
+_BLSTM_SIDE_ENV = os.environ.get("AVC_BLSTM_SIDE")
+
+
+def _blstm_side():
+    if _BLSTM_SIDE_ENV is not None:
+        return _BLSTM_SIDE_ENV != "0"
+    return _PRECISION[0] == "bf16"
 
 
 class BLSTMLayerFn(torch.autograd.Function):
@@ -1685,9 +1715,9 @@ class BLSTMLayerFn(torch.autograd.Function):
         _flush_grad_queue(after=mark)
         grads = [None] * 10
         dG2 = dG.view(M, 2 * G)
-        # the weight / bias gradients go to the side stream like the large LSTMs' (_grad_launch;
-        # AVC_BLSTM_SIDE=0 keeps them on the main stream): released beside the next recurrence
-        launch = _grad_launch if _BLSTM_SIDE else (lambda _dev, _outs, fn, *_in: fn())
+        # under bf16 the weight / bias gradients go to the side stream like the large LSTMs'
+        # (_grad_launch, released beside the next recurrence; _blstm_side)
+        launch = _grad_launch if _blstm_side() else (lambda _dev, _outs, fn, *_in: fn())
         for d, (iW, iH, iBi, iBh) in enumerate(((1, 2, 3, 4), (5, 6, 7, 8))):
             pW, pH, pBi, pBh = ctx.params[d]
             if ctx.needs_input_grad[iW]:

@@ -141,14 +141,15 @@ int autovc_gemm_bf16_f32(int M, int N, int K,
                          const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                          float* C, int64_t ldc, const float* bias1, const float* bias2,
                          int accumulate, int splits, float* workspace, hipStream_t stream);
-/* autovc_gemm_bf16_f32 with A held as bf16 (src = 1; A plain, lda in bf16 elements, lda and
- * A's contiguous dimension multiples of 8): a producer's own bf16 copy of the operand (the
- * LSTM backward's dGb = RNE(dG)) read as is — half of A's bytes, the same result as
- * autovc_gemm_bf16_f32 on the fp32 operand.  B, C and the rest as autovc_gemm_bf16_f32
+/* autovc_gemm_bf16_f32 with A (src bit 0) and / or B (bit 1) held as bf16 (such an operand
+ * plain, its ld in bf16 elements, ld and contiguous dimension multiples of 8): a producer's
+ * own bf16 copy (the LSTM backward's dGb = RNE(dG), a per-step bf16 weight copy) read as is —
+ * half of that operand's bytes, the same result as autovc_gemm_bf16_f32 on the fp32
+ * operand.  The rest as autovc_gemm_bf16_f32
  * (the reference computes these as torch.autocast bf16 matmuls inside nn.LSTM's backward,
  * model_vc_mel.py:115-116,122 under BASELINE config 3). */
 int autovc_gemm_bf16src_f32(int M, int N, int K, const void* A, int64_t lda, int a_trans,
-                            const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
+                            const void* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                             float* C, int64_t ldc, const float* bias1, const float* bias2,
                             int accumulate, int splits, float* workspace, int src, hipStream_t stream);
 /* The split-K count autovc_gemm_bf16_f32 uses for this shape when the caller asks for

@@ -191,10 +191,17 @@ def test_gemm_bf16src_equals_fp32_source(cuda, M, N, K, at, bt, bconv, acc):
     with AF.precision("bf16"):
         C1 = C0.clone()
         AF.gemm(M, N, K, A, A.shape[1], at, Bm, Bm.shape[1], bt, C1, N, **kw)
-        C2 = C0.clone()
-        AF.gemm(M, N, K, A, A.shape[1], at, Bm, Bm.shape[1], bt, C2, N, a_bf16=A.bfloat16(), **kw)
+        srcs = [{"a_bf16": A.bfloat16()}]
+        if bconv is None:   # a bf16 B (the per-step weight copies) alone and with a bf16 A
+            srcs += [{"b_bf16": Bm.bfloat16()}, {"a_bf16": A.bfloat16(), "b_bf16": Bm.bfloat16()}]
+        outs = []
+        for src in srcs:
+            C2 = C0.clone()
+            AF.gemm(M, N, K, A, A.shape[1], at, Bm, Bm.shape[1], bt, C2, N, **src, **kw)
+            outs.append(C2)
     torch.cuda.synchronize()
-    assert torch.equal(C1, C2)
+    for C2 in outs:
+        assert torch.equal(C1, C2)
 
 
 def test_gemm_bf16src_rejects_unaligned_lead(cuda):
@@ -202,6 +209,6 @@ def test_gemm_bf16src_rejects_unaligned_lead(cuda):
     A = torch.zeros(64, 68, device=cuda, dtype=torch.bfloat16)
     B = torch.zeros(68, 64, device=cuda)
     C = torch.zeros(64, 64, device=cuda)
-    with pytest.raises(ValueError, match="multiples of 8"):
+    with pytest.raises(ValueError, match="multiples of 8"):   # lda 68
         _lib.call("autovc_gemm_bf16src_f32", 64, 64, 68, A.data_ptr(), 68, 0, B.data_ptr(), 64, 1, 0, 0, 0,
                   C.data_ptr(), 64, 0, 0, 0, 1, 0, 1, 0)
