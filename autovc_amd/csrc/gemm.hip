@@ -917,6 +917,8 @@ GemmShape pick_config(int M, int N, int K, int splits) {
     return e ? atoi(e) : 9;
   }();
   if (bigk >= 0 && bigk < NCFG && t128 >= 256 && K >= 4096) return kCfg[bigk];
+  // (cfg 13 — BK 32, two k-stages in flight — for these measured slower in the step, with the
+  // BLSTM weight gradients split 32 / 16 / 8 ways: profiles/r05/ab_blstm_side2.txt)
   if (splits > 1) return kCfg[3];
   return kCfg[small >= 0 && small < NCFG ? small : 8];
 }

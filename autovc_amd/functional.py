@@ -500,6 +500,18 @@ def conv_weight(W, kind):
     return out
 
 
+def _cat_scoped(a, b):
+    """torch.cat((a, b)) of two parameters, once per weight scope (the encoder runs twice)."""
+    cache = _WSCOPE[0] if (_cacheable(a) and _cacheable(b)) else None
+    key = ("cat", a.data_ptr(), b.data_ptr(), tuple(a.shape), tuple(b.shape))
+    if cache is not None and key in cache:
+        return cache[key]
+    out = torch.cat((a.detach(), b.detach()), 0)
+    if cache is not None:
+        cache[key] = out
+    return out
+
+
 def prepare_weights(convs, lstms, T, training, B=None):
     """Inside a weight_scope: compute, in one launch, every transform the ConvNorm layers
     `convs` (nn.Conv1d, k=5) will use for sequences of T frames — the Winograd pair for
@@ -1654,16 +1666,34 @@ class LSTM2StackFn(torch.autograd.Function):
 # AVC_BLSTM_CAT=0: the encoder BLSTM's per-direction projection GEMMs (two 128-column outputs
 # forward, and a dx pair whose second GEMM accumulates)
 _BLSTM_CAT = os.environ.get("AVC_BLSTM_CAT", "1") != "0"
-# the BLSTM weight/bias gradients on the side stream: under bf16 only (bench, alternating:
-# bf16 8.03-8.04 vs 8.29-8.30 ms/step; fp32 14.46 vs 14.37-14.39, where the side stream is
-# already full; profiles/r05/ab_blstm_side.txt).  AVC_BLSTM_SIDE=1 / 0 forces it either way
+# the BLSTM weight/bias gradients on the side stream (bench, alternating, one box): bf16 all of
+# them (mode 1: 8.03-8.04 vs 8.29-8.30 ms/step on the main stream; 7.98-8.00 vs 8.01-8.03 for
+# mode 2); fp32 all but the last-differentiated pass's (mode 2: 14.00-14.02 vs 14.22-14.32 on
+# the main stream; mode 1 14.46, where the side stream's tail then runs past the backward).
+# profiles/r05/ab_blstm_side.txt, ab_blstm_side2.txt.  AVC_BLSTM_SIDE=0 / 1 / 2 forces a mode
 _BLSTM_SIDE_ENV = os.environ.get("AVC_BLSTM_SIDE")
 
 
-def _blstm_side():
-    if _BLSTM_SIDE_ENV is not None:
-        return _BLSTM_SIDE_ENV != "0"
-    return _PRECISION[0] == "bf16"
+_BLSTM_LAST_PASS = [False]   # set around the encoder pass whose backward ends the step
+
+
+@contextlib.contextmanager
+def blstm_last_pass(flag=True):
+    """Mark the BLSTM layers run inside the block as the ones whose backward comes last (the
+    Generator's full pass: its encoder is differentiated after the code-only second pass's).
+    Their weight gradients then stay on the main stream when AVC_BLSTM_SIDE=2: queued there
+    they would only lengthen the side stream's tail past the end of the backward."""
+    prev = _BLSTM_LAST_PASS[0]
+    _BLSTM_LAST_PASS[0] = flag
+    try:
+        yield
+    finally:
+        _BLSTM_LAST_PASS[0] = prev
+
+
+def _blstm_side(last_pass):
+    mode = _BLSTM_SIDE_ENV if _BLSTM_SIDE_ENV is not None else ("1" if _PRECISION[0] == "bf16" else "2")
+    return mode == "1" or (mode == "2" and not last_pass)
 
 
 class BLSTMLayerFn(torch.autograd.Function):
@@ -1681,9 +1711,9 @@ class BLSTMLayerFn(torch.autograd.Function):
         if _BLSTM_CAT:
             # both directions' projections as one GEMM over [W_ih_f; W_ih_b] (same sums; one
             # 8192 x 256 output instead of two 128-column ones), reused by the backward's dx
-            Wcat = torch.cat((Wih_f, Wih_b), 0)
-            gemm(B * T, 2 * G, I, x, I, 0, Wcat, I, 0, gx, 2 * G, bias1=torch.cat((bih_f, bih_b)),
-                 bias2=torch.cat((bhh_f, bhh_b)))
+            Wcat = _cat_scoped(Wih_f, Wih_b)
+            gemm(B * T, 2 * G, I, x, I, 0, Wcat, I, 0, gx, 2 * G, bias1=_cat_scoped(bih_f, bih_b),
+                 bias2=_cat_scoped(bhh_f, bhh_b))
         else:
             Wcat = None
             gemm(B * T, G, I, x, I, 0, Wih_f, I, 0, gx, 2 * G, bias1=bih_f, bias2=bhh_f)
@@ -1695,6 +1725,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                   h.data_ptr(), c.data_ptr(), _p(gates), _s())
         ctx.save_for_backward(x, Wih_f, Whh_f, Wih_b, Whh_b, h, c, gates, Wcat)
         ctx.params = ((Wih_f, Whh_f, bih_f, bhh_f), (Wih_b, Whh_b, bih_b, bhh_b))
+        ctx.last_pass = _BLSTM_LAST_PASS[0]
         return h
 
     @staticmethod
@@ -1717,7 +1748,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         dG2 = dG.view(M, 2 * G)
         # under bf16 the weight / bias gradients go to the side stream like the large LSTMs'
         # (_grad_launch, released beside the next recurrence; _blstm_side)
-        launch = _grad_launch if _blstm_side() else (lambda _dev, _outs, fn, *_in: fn())
+        launch = _grad_launch if _blstm_side(ctx.last_pass) else (lambda _dev, _outs, fn, *_in: fn())
         for d, (iW, iH, iBi, iBh) in enumerate(((1, 2, 3, 4), (5, 6, 7, 8))):
             pW, pH, pBi, pBh = ctx.params[d]
             if ctx.needs_input_grad[iW]:

@@ -212,7 +212,8 @@ class Generator(nn.Module):
             AF.prepare_weights(self.conv_layers() if full else [c[0].conv for c in self.encoder.convolutions],
                                [self.decoder.lstm1, self.decoder.lstm2] if full else [], x.shape[-2], self.training,
                                B=x.shape[0])
-        code_real = self.encoder.encode(x, c_org)                       # :182
+        with AF.blstm_last_pass(c_trg is not None):   # the full pass's encoder is differentiated last
+            code_real = self.encoder.encode(x, c_org)                   # :182
         if c_trg is None:
             return code_real                                            # :183-184
         T = x.shape[-2]
