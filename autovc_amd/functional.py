@@ -872,6 +872,7 @@ class ConvBNChainFn(torch.autograd.Function):
                   _p(g), _p(be), float(epss[-1]), ACT[acts[-1]], _p(res), C, z.data_ptr(), C, _s())
         if training:
             ctx.spec = spec
+            ctx.last_pass = _BLSTM_LAST_PASS[0]
             ctx.ys, ctx.coefs, ctx.means, ctx.varis, ctx.xts = ys, coefs, means, varis, xts
             ctx.x = x
             ctx.z = z if acts[-1] != "none" else None
@@ -948,7 +949,12 @@ class ConvBNChainFn(torch.autograd.Function):
                     _lib.call("autovc_gemm_batched_f32", 8, Co, Ci, nt, Dt.data_ptr(), Co, nt * Co, 1, Xt.data_ptr(),
                               Ci, nt * Ci, 1, Mt.data_ptr(), Ci, Co * Ci, 0, _s())
                     _lib.call("autovc_wino5_wgrad_f32", Co, Ci, Mt.data_ptr(), go.buf.data_ptr(), int(go.acc), _s())
-                _grad_launch(dev, go, dw, Dt, Xt)
+                # (AVC_LAST_CONV_MAIN=1: the last-differentiated encoder pass's conv weight
+                # gradients on the main stream instead of the final side batch)
+                if ctx.last_pass and _last_conv_main():
+                    dw()
+                else:
+                    _grad_launch(dev, go, dw, Dt, Xt)
                 grads[7 * l] = go.result()
             xts[l] = None
             if need_dx:
@@ -1062,6 +1068,7 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                   _p(g), _p(be), float(epss[-1]), ACT[acts[-1]], _p(res), C, z.data_ptr(), C, _s())
         if training:
             ctx.spec, ctx.mode = spec, mode
+            ctx.last_pass = _BLSTM_LAST_PASS[0]
             ctx.ys, ctx.coefs, ctx.means, ctx.varis, ctx.zbs = ys, coefs, means, varis, zbs
             ctx.x = x
             ctx.z = z if acts[-1] != "none" else None
@@ -1140,7 +1147,10 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                               xact, dWf.data_ptr(), wsrc, ws, _s())
                     _lib.call("autovc_conv_unpack_grad_f32", Co, Ci, KS, dWf.data_ptr(), go.buf.data_ptr(),
                               int(go.acc), _s())
-                _grad_launch(dev, go, dw, dy, xin, xcoef)
+                if ctx.last_pass and _last_conv_main():   # (as ConvBNChainFn)
+                    dw()
+                else:
+                    _grad_launch(dev, go, dw, dy, xin, xcoef)
                 grads[7 * l] = go.result()
             if l > 0 or needs[1]:
                 Wd = conv_weight(W, 5 if h else 3)
@@ -1675,6 +1685,17 @@ _BLSTM_SIDE_ENV = os.environ.get("AVC_BLSTM_SIDE")
 
 
 _BLSTM_LAST_PASS = [False]   # set around the encoder pass whose backward ends the step
+# the last-differentiated encoder pass's conv weight gradients on the main stream, as they are
+# produced, instead of as the final side batch that runs alone after the join: bf16 7.90-7.93
+# vs 7.96-7.97 ms/step, fp32 neutral (14.13 vs 14.11-14.16; profiles/r05/ab_last_conv_main.txt).
+# AVC_LAST_CONV_MAIN=1 / 0 forces it; the default follows the precision
+_LAST_CONV_MAIN_ENV = os.environ.get("AVC_LAST_CONV_MAIN")
+
+
+def _last_conv_main():
+    if _LAST_CONV_MAIN_ENV is not None:
+        return _LAST_CONV_MAIN_ENV == "1"
+    return _PRECISION[0] == "bf16"
 
 
 @contextlib.contextmanager
