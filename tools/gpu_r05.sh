@@ -11,6 +11,8 @@ for STEP in ${1//,/ }; do
     tests) timeout -k 10 ${T_TESTS:-1500} python -u -m pytest ${PYTEST_FILES:-tests} -m gpu ${PYTEST_X--x} -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/tests.log 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) timeout -k 10 900 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err ;;
+    benchprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/benchprof -o run --output-format csv -- python bench.py ${BENCH_ARGS} > gpurun_out/benchprof.json 2> gpurun_out/benchprof.err && \
+               rm -f gpurun_out/benchprof/run_kernel_trace.csv ;;   # the full bench's trace exceeds what gpurun copies back
     qbench) timeout -k 10 300 python bench.py --no-cpu-baseline --no-wavenet --no-e2e --no-roofline ${BENCH_ARGS} > gpurun_out/qbench${TAG}.json 2> gpurun_out/qbench${TAG}.err ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof${PROF_TAG} -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-wavenet --no-e2e --no-roofline ${PROF_ARGS} > gpurun_out/prof${PROF_TAG}.log 2>&1 ;;
     timeline) timeout -k 10 300 python -u tools/side_timeline.py fp32 ${TL_REPS:-10} > gpurun_out/side_timeline_fp32${TAG}.txt 2> gpurun_out/side_timeline.err && \
