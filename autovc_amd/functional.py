@@ -89,9 +89,11 @@ _GRAD_PRIORITY = int(os.environ.get("AVC_GRAD_PRIORITY", "0"))
 _GRAD_STREAMS: dict = {}
 # LDS left free per CU for the recurrence's step workgroup (37 KB) while side GEMMs run;
 # measured per precision (bench.py, same box, alternating): fp32 21.1 ms/step with room
-# kept vs 21.9 without; bf16 13.1 without vs 13.3 with (its 128x128 tiles run better 2/CU)
+# kept vs 21.9 without (round 5 again: 14.06-14.08 vs 14.16-14.20); bf16 13.1 without vs 13.3
+# with in round 2, but with round 5's 256-row side GEMMs and the BLSTM weight gradients beside
+# the recurrences the room pays there too: 7.85-7.88 vs 7.91-7.93 (profiles/r05/ab_lds_reserve_r5.txt)
 GRAD_LDS_RESERVE = {"fp32": int(os.environ.get("AVC_GRAD_LDS_RESERVE", "38912")),
-                    "bf16": int(os.environ.get("AVC_GRAD_LDS_RESERVE_BF16", "0"))}
+                    "bf16": int(os.environ.get("AVC_GRAD_LDS_RESERVE_BF16", "38912"))}
 
 
 def _grad_stream(dev):
