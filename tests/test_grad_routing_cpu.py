@@ -1,0 +1,80 @@
+"""Host logic of the weight-gradient routing (no GPU): which BLSTM / conv weight gradients go to
+the gradient side stream, by precision and by encoder pass (functional.blstm_last_pass; the
+Generator's full pass is differentiated last)."""
+from autovc_amd import functional as AF
+
+
+def test_blstm_last_pass_flag_nests_and_restores():
+    assert AF._BLSTM_LAST_PASS[0] is False
+    with AF.blstm_last_pass(True):
+        assert AF._BLSTM_LAST_PASS[0] is True
+        with AF.blstm_last_pass(False):
+            assert AF._BLSTM_LAST_PASS[0] is False
+        assert AF._BLSTM_LAST_PASS[0] is True
+    assert AF._BLSTM_LAST_PASS[0] is False
+
+
+def test_blstm_side_defaults_by_precision(monkeypatch):
+    monkeypatch.setattr(AF, "_BLSTM_SIDE_ENV", None)
+    with AF.precision("fp32"):      # mode 2: every pass but the last-differentiated one
+        assert AF._blstm_side(last_pass=False) is True
+        assert AF._blstm_side(last_pass=True) is False
+    with AF.precision("bf16"):      # mode 1: all of them
+        assert AF._blstm_side(last_pass=False) is True
+        assert AF._blstm_side(last_pass=True) is True
+
+
+def test_blstm_side_overrides(monkeypatch):
+    for mode, expect in (("0", (False, False)), ("1", (True, True)), ("2", (True, False))):
+        monkeypatch.setattr(AF, "_BLSTM_SIDE_ENV", mode)
+        for prec in ("fp32", "bf16"):
+            with AF.precision(prec):
+                assert (AF._blstm_side(False), AF._blstm_side(True)) == expect
+
+
+def test_last_conv_main_defaults_and_override(monkeypatch):
+    monkeypatch.setattr(AF, "_LAST_CONV_MAIN_ENV", None)
+    with AF.precision("fp32"):
+        assert AF._last_conv_main() is False
+    with AF.precision("bf16"):
+        assert AF._last_conv_main() is True
+    monkeypatch.setattr(AF, "_LAST_CONV_MAIN_ENV", "0")
+    with AF.precision("bf16"):
+        assert AF._last_conv_main() is False
+
+
+def test_generator_marks_only_the_full_pass(monkeypatch):
+    """Generator.forward wraps the encoder of the full pass (c_trg given) in
+    blstm_last_pass(True) and the code-only pass in blstm_last_pass(False)."""
+    import torch
+    from autovc_amd import model_vc_mel as MV
+
+    seen = []
+
+    class Probe(torch.nn.Module):
+        dim_neck = 1
+
+        def encode(self, x, c_org):
+            seen.append(AF._BLSTM_LAST_PASS[0])
+            return torch.zeros(x.shape[0], 2)
+
+    g = MV.Generator.__new__(MV.Generator)
+    torch.nn.Module.__init__(g)
+    g.encoder = Probe()
+    x = torch.zeros(1, 4, 80)
+    g.forward(x, torch.zeros(1, 256), None)
+    assert seen == [False]
+
+    class Stop(Exception):
+        pass
+
+    def stop(*a):   # the full pass stops right after its encoder
+        raise Stop()
+
+    monkeypatch.setattr(AF.FrameConcatFn, "apply", staticmethod(stop))
+    try:
+        g.forward(x, torch.zeros(1, 256), torch.zeros(1, 256))
+    except Stop:
+        pass
+    assert seen == [False, True]
+    assert AF._BLSTM_LAST_PASS[0] is False
