@@ -119,14 +119,6 @@ sig("autovc_lstm_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_pt
 sig("autovc_lstm2_bwd_workspace_floats", c_int, c_int, c_int)
 sig("autovc_lstm2_bwd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr)
-sig("autovc_lstm2_bwd_range_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-    c_ptr, c_ptr, c_ptr, c_int, c_int, c_int, c_ptr, c_ptr)
-sig("autovc_lstm2_bwd_range_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-    c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int, c_int, c_ptr, c_ptr)
-sig("autovc_gemm_tchunk_f32", c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_int, c_ptr, c_i64,
-    c_int, c_int, c_ptr, c_ptr)
-sig("autovc_gemm_tchunk_bf16_f32", c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_i64, c_ptr, c_i64, c_int, c_ptr,
-    c_i64, c_int, c_int, c_ptr, c_ptr)
 sig("autovc_lstm2_persist_workspace_bytes", c_int, c_int, c_int)
 sig("autovc_lstm2_persist_supported", c_int, c_int)
 sig("autovc_lstm2_fwd_persist_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,

@@ -42,12 +42,6 @@ struct Opnd {
   // element = act(coef[c] x + coef[C + c]) for a frame inside its sequence, else 0
   const float* coef;
   int act;
-  // time-chunked K (CK operands only, seg_len > 0): the K rows are (sequence b, step t) pairs of
-  // an NTC activation with seg_T steps per sequence, restricted to steps [seg_t0, seg_t0 +
-  // seg_len) of every sequence — logical row k is memory row (k / seg_len) * seg_T +
-  // seg_t0 + k % seg_len; a conv mask then sees step seg_t0 + k % seg_len.  The weight
-  // gradient of one time chunk of an LSTM layer.
-  int seg_len = 0, seg_T = 0, seg_t0 = 0;
 };
 
 // the fused Conv-BN stacks' transform of a stored pre-BN value (bn.hip apply_kernel's fmaf).
@@ -68,70 +62,7 @@ constexpr int kBnMaxC = 1024;
 // start z * (a, b, c) floats further (no split-K then).
 struct Batch {
   int64_t a, b, c;
-  int* tk;          // split-K tile tickets (in-kernel fixup), null: slabs + splitk_reduce_kernel
 };
-
-// Split-K without a second launch: every split of a tile writes its partial accumulators
-// to its slab in the lanes' own layout (16 floats per lane per 32x32 block, 16-B sc1 stores:
-// written through, so another XCD's sc1 loads see them), waits for the stores, and one
-// lane takes a ticket on the tile's counter (agent-scope atomic).  The split that takes
-// the last ticket reads the others' partials (sc1 loads) and sums all splits in split order
-// — the order of splitk_reduce_kernel, so the result is bit-identical to the two-launch
-// form — then writes C through the normal epilogue and returns the counter to zero (the
-// counters start zeroed and every call leaves them zero).
-template <int TI, int TJ>
-__device__ __forceinline__ bool splitk_fixup(f32x16 (&acc)[TI][TJ], float* slab, int* tk, int tile, int ntiles) {
-  constexpr int TF = TI * TJ * 1024;                         // floats of one wave's blocks
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int z = blockIdx.z, S = gridDim.z;
-  const int64_t tile_f = (int64_t)nw * TF;
-  auto blk = [&](int s, int i, int j) {
-    return ((int64_t)s * ntiles + tile) * tile_f + (int64_t)wave * TF + (i * TJ + j) * 1024 + lane * 16;
-  };
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)0x80000000u, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
-                                               (uint32_t)((blk(z, i, j) + 4 * q) * 4), 0, 16);
-      }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __shared__ int s_last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(tk + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == S - 1;
-    if (s_last) __hip_atomic_store(tk + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!s_last) return false;
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      f32x16 tot;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) tot[e] = 0.f;
-      for (int sp = 0; sp < S; ++sp) {
-        if (sp == z) {
-          tot += acc[i][j];
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                           r, (uint32_t)((blk(sp, i, j) + 4 * q) * 4), 0, 16));
-            tot[4 * q] += v[0]; tot[4 * q + 1] += v[1]; tot[4 * q + 2] += v[2]; tot[4 * q + 3] += v[3];
-          }
-        }
-      }
-      acc[i][j] = tot;
-    }
-  return true;
-}
 
 // One operand tile (ROWS x BK) of a stage: staging map, LDS image and fragment reads.
 //   RK: LDS [ROWS][BK+4], staged as float4 along k, fragments read with ds_read_b128.
@@ -167,7 +98,6 @@ struct OpTile {
   bool rok[PER];            // RK: row inside the operand
   int tpos[PER];            // conv: frame position in its sequence (RK: fixed; CK: advancing)
   int kpos[PER];            // CK: frame index of the slot
-  int tseg[PER];            // CK, time-chunked K: the slot's step inside its chunk
   int kk;                   // RK: k of the thread's slots
   int tap, kmod;            // conv: RK: k / C, k % C (advancing); CK: q / C (fixed)
   int step_q, step_r;       // conv: RK: BK / C, BK % C; CK: -, BK % T (uniform)
@@ -202,14 +132,8 @@ struct OpTile {
         }
       } else {
         kpos[i] = (int)k;
-        int64_t row = k;
-        if (o.seg_len > 0) {
-          const int64_t sb = k / o.seg_len;
-          tseg[i] = (int)(k - sb * o.seg_len);
-          row = sb * o.seg_T + o.seg_t0 + tseg[i];
-        }
-        off[i] = (uint32_t)((((row + shift) * o.ld) + r) * EB);
-        if (o.conv_T > 0) tpos[i] = o.seg_len > 0 ? o.seg_t0 + tseg[i] : (int)(k % o.conv_T);
+        off[i] = (uint32_t)((((k + shift) * o.ld) + r) * EB);
+        if (o.conv_T > 0) tpos[i] = (int)(k % o.conv_T);
         if (i == 0) {
           rowok = r < R;
           if (o.conv_T > 0) tap = (int)(r / o.conv_C);
@@ -269,14 +193,7 @@ struct OpTile {
         dst[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? off[i] : kOOB, 0, 0));
         off[i] += (uint32_t)(BK * o.ld * EB);
         kpos[i] += BK;
-        if (o.seg_len > 0) {  // time-chunked K: skip the steps outside the chunk
-          tseg[i] += BK;
-          while (tseg[i] >= o.seg_len) {
-            tseg[i] -= o.seg_len;
-            off[i] += (uint32_t)((int64_t)(o.seg_T - o.seg_len) * o.ld * EB);
-          }
-          if (o.conv_T > 0) tpos[i] = o.seg_t0 + tseg[i];
-        } else if (o.conv_T > 0) {   // (frame + BK) % T with the uniform BK % T
+        if (o.conv_T > 0) {   // (frame + BK) % T with the uniform BK % T
           tpos[i] += step_r;
           if (tpos[i] >= o.conv_T) tpos[i] -= o.conv_T;
         }
@@ -530,10 +447,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
   }
 
   // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  if (slab && bat.tk) {
-    if (!splitk_fixup<TI, TJ>(acc, slab, bat.tk, logical, nwg)) return;
-    slab = nullptr;                    // the last split writes C with the full sum
-  }
   float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
   const int64_t ld = slab ? N : ldc;
 #pragma unroll
@@ -720,10 +633,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     }
   }
 
-  if (slab && bat.tk) {
-    if (!splitk_fixup<TI, TJ>(acc, slab, bat.tk, logical, nwg)) return;
-    slab = nullptr;                    // the last split writes C with the full sum
-  }
   float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
   const int64_t ld = slab ? N : ldc;
 #pragma unroll
@@ -866,13 +775,7 @@ int g_force_cfg = -1;  // tools/gemm_bench.hip overrides this
 // stream (autovc_gemm_set_lds_reserve): each workgroup is padded with unused dynamic LDS
 // so that the largest count that still fits in 160 KiB - reserve is also the most that fit.
 unsigned g_lds_reserve = 0;
-Batch g_batch = {0, 0, 0, nullptr};   // set by gemm_impl for every launch
-// split-K in one launch (splitk_fixup) only with AVC_GEMM_FIXUP=1: the partials' write-through
-// stores and the serial last-split tail measured slower than slabs + splitk_reduce_kernel
-// (fp32 15.91-15.92 vs 15.61-15.65 ms/step, bf16 11.24-11.30 vs 9.99-10.00;
-// profiles/r03/ab_gemm_fixup.txt; identical losses)
-const bool g_fixup = [] { const char* e = getenv("AVC_GEMM_FIXUP"); return e && e[0] == '1'; }();
-constexpr int kTickets = 16384;          // tile counters at the head of a split-K workspace (64 KiB)
+Batch g_batch = {0, 0, 0};   // set by gemm_impl for every launch
 constexpr unsigned kLdsPerCU = 160 * 1024;
 
 unsigned dyn_lds_for(unsigned static_bytes) {
@@ -1020,7 +923,7 @@ void launch_bn_bf16(dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opn
   constexpr bool DEEP = BM == 256 && !(BN == 256 && !AR && !BR);
   hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, DEEP, BNOP, SRC>), grid, dim3(NT),
                      dyn_lds_for(bf16_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, K, oa, ob, (float*)nullptr,
-                     (int64_t)N, (const float*)nullptr, (const float*)nullptr, 0, kps, slab, Batch{0, 0, 0, nullptr});
+                     (int64_t)N, (const float*)nullptr, (const float*)nullptr, 0, kps, slab, Batch{0, 0, 0});
 }
 
 template <bool AR, bool BR, int BNOP, int SRC>
@@ -1080,25 +983,23 @@ void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t s
 
 }  // namespace
 
-// split-K workspace: kTickets tile counters (zero before the first call, left zero by every
-// call) followed by the partial slabs (tiles rounded up to 256 x 256)
+// split-K workspace: the partial slabs (tiles rounded up to 256 x 256), summed in split order
+// by splitk_reduce_kernel
 extern "C" int64_t autovc_gemm_workspace_floats(int M, int N, int splits) {
-  return splits > 1 ? kTickets + (int64_t)splits * ((M + 255) / 256 * 256) * ((N + 255) / 256 * 256) : 0;
+  return splits > 1 ? (int64_t)splits * ((M + 255) / 256 * 256) * ((N + 255) / 256 * 256) : 0;
 }
 
-// seg (seg_len > 0): time-chunked K for both operands (CK, Opnd::seg_len)
 static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c_bs, int M, int N, int K,
                                const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
                                const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                                float* C, int64_t ldc, const float* bias1, const float* bias2,
-                               int accumulate, int splits, float* workspace, hipStream_t stream,
-                               int seg_len = 0, int seg_T = 0, int seg_t0 = 0, int src = 0) {
+                               int accumulate, int splits, float* workspace, hipStream_t stream, int src = 0) {
   AVC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "autovc_gemm: negative dims");
   if (M == 0 || N == 0) return avc::kOk;
   AVC_CHECK_ARG(A && B && C, "autovc_gemm: null operand");
   AVC_CHECK_ARG(AVC_ALIGNED16(A) && AVC_ALIGNED16(B), "autovc_gemm: A/B must be 16-byte aligned");
   AVC_CHECK_ARG(aligned_ld(lda) && aligned_ld(ldb), "autovc_gemm: lda/ldb must be multiples of 4");
-  AVC_CHECK_ARG(src >= 0 && src <= 3 && (src == 0 || (bf16 && batch == 1 && !seg_len)),
+  AVC_CHECK_ARG(src >= 0 && src <= 3 && (src == 0 || (bf16 && batch == 1)),
                 "autovc_gemm_bf16src_f32: bad src %d", src);
   AVC_CHECK_ARG(!(src & 1) || (!a_conv_T && lda % 8 == 0 && (a_trans ? M % 8 == 0 : K % 8 == 0)),
                 "autovc_gemm_bf16src_f32: a bf16 A must be plain with lda and its contiguous dim multiples of 8");
@@ -1158,13 +1059,11 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   splits = (int)((K + kps - 1) / kps);
   if (splits < 1) splits = 1;
   AVC_CHECK_ARG(splits == 1 || workspace, "autovc_gemm_f32: split-K needs a workspace");
-  Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0, nullptr, 0, seg_len, seg_T, seg_t0};
-  Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0, nullptr, 0, seg_len, seg_T, seg_t0};
+  Opnd oa{A, lda, a_conv_T, a_conv_C, a_tap0, nullptr, 0};
+  Opnd ob{B, ldb, b_conv_T, b_conv_C, b_tap0, nullptr, 0};
   const dim3 grid((N + cfg.bn - 1) / cfg.bn, (M + cfg.bm - 1) / cfg.bm, batch > 1 ? batch : splits);
-  const bool fixup = splits > 1 && g_fixup && (int64_t)grid.x * grid.y <= kTickets;
-  float* slab = splits > 1 ? workspace + kTickets : nullptr;
-  g_batch = batch > 1 ? Batch{a_bs, b_bs, c_bs, nullptr}
-                      : Batch{0, 0, 0, fixup ? reinterpret_cast<int*>(workspace) : nullptr};
+  float* slab = splits > 1 ? workspace : nullptr;
+  g_batch = batch > 1 ? Batch{a_bs, b_bs, c_bs} : Batch{0, 0, 0};
   if (bf16)
     launch_gemm_bf16(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate,
                      (int)kps, slab, src);
@@ -1172,7 +1071,7 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
     launch_gemm(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
                 slab);
   AVC_CHECK_LAUNCH("autovc_gemm");
-  if (splits > 1 && !fixup) {
+  if (splits > 1) {
     const int gx = (N + 255) / 256;
     const int gy = (int)std::max<int64_t>(1, std::min<int64_t>(M, 4096 / gx + 1));
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, gy), dim3(256), 0, stream, (int64_t)M, (int64_t)N,
@@ -1200,33 +1099,6 @@ extern "C" int autovc_gemm_bf16_f32(int M, int N, int K,
                    b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream);
 }
 
-// Weight gradient of one time chunk (steps [t0, t0 + Tc) of each of B sequences of T steps):
-//   C[M,N] (+)= sum_b sum_t A[(b T + t) lda + m] * Bm[(b T + t + b_tap0) ldb + n]
-// (the Bm term is zero where t + b_tap0 < 0; b_tap0 = -1: the previous step's h).  Both
-// operands K-strided (CK), K = B * Tc; splits / workspace as autovc_gemm_f32.
-static int gemm_tchunk(bool bf16, int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
-                       const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate, int splits,
-                       float* workspace, hipStream_t stream) {
-  AVC_CHECK_ARG(B > 0 && T > 0 && Tc > 0 && t0 >= 0 && t0 + Tc <= T && (b_tap0 == 0 || b_tap0 == -1),
-                "autovc_gemm_tchunk: bad chunk B=%d T=%d t0=%d Tc=%d tap0=%d", B, T, t0, Tc, b_tap0);
-  AVC_CHECK_ARG(A && Bm, "autovc_gemm_tchunk: null operand");
-  AVC_CHECK_ARG(4 * ((int64_t)B * T + 2) * std::max(lda, ldb) < (int64_t)kOOB, "autovc_gemm_tchunk: operands >= 2 GiB");
-  return gemm_impl(bf16, 1, 0, 0, 0, M, N, B * Tc, A, lda, 1, 0, 0, 0, Bm, ldb,
-                   1, b_tap0 ? T : 0, b_tap0 ? N : 0, b_tap0, C, ldc, nullptr, nullptr, accumulate, splits, workspace,
-                   stream, Tc, T, t0);
-}
-
-extern "C" int autovc_gemm_tchunk_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
-                                      const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate,
-                                      int splits, float* workspace, hipStream_t stream) {
-  return gemm_tchunk(false, M, N, B, T, t0, Tc, A, lda, Bm, ldb, b_tap0, C, ldc, accumulate, splits, workspace, stream);
-}
-
-extern "C" int autovc_gemm_tchunk_bf16_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
-                                           const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc,
-                                           int accumulate, int splits, float* workspace, hipStream_t stream) {
-  return gemm_tchunk(true, M, N, B, T, t0, Tc, A, lda, Bm, ldb, b_tap0, C, ldc, accumulate, splits, workspace, stream);
-}
 
 // autovc_gemm_bf16_f32 with A (src bit 0) and / or B (bit 1) read from bf16 copies the
 // producers already wrote (ld in bf16 elements): half of those operands' bytes.  The recurrences' backward writes the
@@ -1239,7 +1111,7 @@ extern "C" int autovc_gemm_bf16src_f32(int M, int N, int K,
                                        int accumulate, int splits, float* workspace, int src, hipStream_t stream) {
   return gemm_impl(true, 1, 0, 0, 0, M, N, K, reinterpret_cast<const float*>(A), lda, a_trans, 0, 0, 0,
                    reinterpret_cast<const float*>(B), ldb, b_trans, b_conv_T, b_conv_C, b_tap0, C, ldc, bias1, bias2, accumulate, splits, workspace, stream,
-                   0, 0, 0, src);
+                   src);
 }
 
 extern "C" int autovc_gemm_bf16_splits(int M, int N, int K, int requested) {
@@ -1287,7 +1159,7 @@ int bn_gemm(int bnop, int src, int a_trans, int b_trans, int M, int N, int K, Op
             hipStream_t st) {
   const BnPlan pl = plan_bn(M, N, K, a_trans && b_trans);
   const dim3 grid((N + pl.cfg.bn - 1) / pl.cfg.bn, (M + pl.cfg.bm - 1) / pl.cfg.bm, pl.splits);
-  g_batch = Batch{0, 0, 0, nullptr};
+  g_batch = Batch{0, 0, 0};
   const int id = pl.cfg.id;
   // (layout, BNOP, SRC) combinations of the stacks; anything else is the plain fp32-source GEMM
   if (!a_trans && !b_trans && bnop == 1 && src == 0) launch_gemm_bn_bf16<true, true, 1, 0>(id, grid, st, M, N, K, oa, ob, pl.kps, ws);

@@ -1124,24 +1124,17 @@ extern "C" int64_t autovc_lstm2_bwd_workspace_floats(int B, int H, int splits) {
 namespace {
 // the stacked backward wavefront: launch pair s = 0..T of autovc_lstm2_bwd_f32, or (fused)
 // the first pointwise pass and T fused launches
-// s_begin / s_end: the wavefront iterations s (0..T) to issue — a call split into ranges runs
-// the same launches as one call (autovc_lstm2_bwd_range_*: the weight gradients of each
-// finished time chunk can start between them)
 template <bool BF>
 int lstm2_bwd_steps(const BwdArgs& a1, const BwdArgs& a0, int splits, const float* d1, const float* d0,
                     const float* w1, const float* wi, const float* w0, float* workspace, hipStream_t stream,
-                    const char* fn, int s_begin = 0, int s_end = -1) {
+                    const char* fn) {
   const int B = a1.B, T = a1.T, H = a1.H;
-  if (s_end < 0) s_end = T + 1;
-  AVC_CHECK_ARG(0 <= s_begin && s_begin <= s_end && s_end <= T + 1, "%s: bad step range [%d, %d) for T=%d", fn,
-                s_begin, s_end, T);
   const int64_t BH = (int64_t)B * H;
   const bool wide = splits == 8;
   const bool fused = bwd_fused() && !wide;
   float* dcs0 = workspace + (int64_t)(3 * splits + 1) * BH;
   FusedTile f{reinterpret_cast<int*>(workspace + (int64_t)(3 * splits + 2) * BH)};
-  if (s_begin > 0) {
-  } else if (fused) {
+  if (fused) {
     // layer 0's carried cell gradient and the tile counters (contiguous); product 2 of the
     // first launch writes zero slabs itself
     AVC_HIP(avc::zero_async(dcs0, 4 * (BH + ceil4(2 * bwd_tiles(B, H))), stream), fn);
@@ -1152,7 +1145,7 @@ int lstm2_bwd_steps(const BwdArgs& a1, const BwdArgs& a0, int splits, const floa
   }
   const dim3 pgrid((H / 4 + 63) / 64, B, 2);
   const dim3 rgrid = wide ? dim3(3 * H / TNW, (B + TBW - 1) / TBW, splits) : dim3(3 * H / TN, (B + TB - 1) / TB, splits);
-  for (int s = s_begin; s < s_end; ++s) {
+  for (int s = 0; s <= T; ++s) {
     const int t1 = T - 1 - s, t0 = T - s;
     if (!fused || s == 0) {
       if (splits == 8) hipLaunchKernelGGL((lstm2_bwd_pointwise_kernel<8>), pgrid, dim3(64), 0, stream, a1, a0, t1, t0);
@@ -1180,11 +1173,10 @@ int lstm2_bwd_steps(const BwdArgs& a1, const BwdArgs& a0, int splits, const floa
 // product of the recurrent launch instead of a GEMM over all frames after layer 1 ends,
 // and layer 0 starts one step behind layer 1 instead of T steps.  Same per-element sums
 // as the unstacked path except that layer 0's dh_t adds its 2S partials in one order.
-extern "C" int autovc_lstm2_bwd_range_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                          const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                          const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T,
-                                          float* dG1, float* dG0, int splits, int s_begin, int s_end,
-                                          float* workspace, hipStream_t stream) {
+extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                    const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                    const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
+                                    float* dG0, int splits, float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(T > 0 && lstm_shape_ok(B, H), "autovc_lstm2_bwd_f32: bad dims");
   AVC_CHECK_ARG((splits == 2 || splits == 4 || splits == 8) && (4 * H) % (KCH * splits) == 0 &&
                     (splits < 8 || H % TNW == 0),
@@ -1204,15 +1196,7 @@ extern "C" int autovc_lstm2_bwd_range_f32(int B, int T, int H, const float* dh1_
   a1.prio = a0.prio = lstm_prio();
   // splits 8: the wide-tile products (64 x 64 per workgroup, never fused); 2 / 4: 32 x 32 tiles
   return lstm2_bwd_steps<false>(a1, a0, splits, dG1, dG0, W_hh1_T, W_ih1_T, W_hh0_T, workspace, stream,
-                                "autovc_lstm2_bwd_f32", s_begin, s_end);
-}
-
-extern "C" int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                    const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                    const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
-                                    float* dG0, int splits, float* workspace, hipStream_t stream) {
-  return autovc_lstm2_bwd_range_f32(B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, gates0, c0, W_hh1_T, W_ih1_T, W_hh0_T,
-                                    dG1, dG0, splits, 0, T + 1, workspace, stream);
+                                "autovc_lstm2_bwd_f32");
 }
 
 extern "C" int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
@@ -1351,12 +1335,11 @@ extern "C" int autovc_lstm_bwd_bf16(int B, int T, int H, const float* dh_out, in
 // autovc_lstm2_bwd_f32 with the recurrent products on bf16 copies (precision "bf16"): the
 // pointwise passes also write dG1_b / dG0_b, which the next launch's products read; W*T_b are
 // RNE bf16 copies of the (H, 4H) transposes.  Cell backward, dG, partials fp32.
-extern "C" int autovc_lstm2_bwd_range_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                           const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                           const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b,
-                                           const uint16_t* W_hh0_T_b, float* dG1, uint16_t* dG1_b, float* dG0,
-                                           uint16_t* dG0_b, int splits, int s_begin, int s_end, float* workspace,
-                                           hipStream_t stream) {
+extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
+                                     const float* gates1, const float* c1, const float* gates0, const float* c0,
+                                     const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
+                                     float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits,
+                                     float* workspace, hipStream_t stream) {
   AVC_CHECK_ARG(T > 0 && bf16_shape_ok(B, H), "autovc_lstm2_bwd_bf16: bad dims");
   AVC_CHECK_ARG((splits == 2 || splits == 4 || splits == 8) && (2 * H) % (KCH * splits) == 0 &&
                     (splits < 8 || H % TNW == 0),
@@ -1377,16 +1360,7 @@ extern "C" int autovc_lstm2_bwd_range_bf16(int B, int T, int H, const float* dh1
   return lstm2_bwd_steps<true>(a1, a0, splits, reinterpret_cast<const float*>(dG1_b),
                                reinterpret_cast<const float*>(dG0_b), reinterpret_cast<const float*>(W_hh1_T_b),
                                reinterpret_cast<const float*>(W_ih1_T_b), reinterpret_cast<const float*>(W_hh0_T_b),
-                               workspace, stream, "autovc_lstm2_bwd_bf16", s_begin, s_end);
-}
-
-extern "C" int autovc_lstm2_bwd_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                     const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                     const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
-                                     float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits,
-                                     float* workspace, hipStream_t stream) {
-  return autovc_lstm2_bwd_range_bf16(B, T, H, dh1_out, d_ldb, d_ldt, gates1, c1, gates0, c0, W_hh1_T_b, W_ih1_T_b,
-                                     W_hh0_T_b, dG1, dG1_b, dG0, dG0_b, splits, 0, T + 1, workspace, stream);
+                               workspace, stream, "autovc_lstm2_bwd_bf16");
 }
 
 // The product's decoder-lstm2 launch (autovc_lstm2_fwd_f32's two-layer wavefront) with every

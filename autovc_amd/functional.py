@@ -56,8 +56,7 @@ class _Workspace:
             if buf is not None:
                 cls._retired.append(buf)
                 size = max(size, 2 * buf.numel())
-            # zeroed: a split-K GEMM workspace starts with tile counters that must be zero
-            # (every call leaves them zero again, csrc/gemm.hip splitk_fixup)
+            # zeroed: workspaces holding tile counters (the fused LSTM backward's) start at zero
             buf = torch.zeros(size, dtype=torch.uint8, device=device)
             cls._bufs[key] = buf
         return buf
@@ -118,10 +117,45 @@ def _grad_launch(dev, outs, fn, *inputs):
     22.2 -> 22.9 ms/step)."""
     outs = outs if isinstance(outs, tuple) else (outs,)
     if not (all(o.acc for o in outs) and _GRAD_STREAM_ON):
-        fn()
+        _main_grad(dev, outs, fn, *inputs)
         return
     # run later under the same precision; the destinations are final once the batch is done
     _GRAD_QUEUE.append((dev, fn, inputs, _PRECISION[0], outs))
+
+
+# flat-buffer byte ranges [lo, hi) that a released side-stream batch accumulates into, each
+# with the event recorded on the side stream right after that batch (cleared at the join)
+_SIDE_WRITES: list = []
+
+
+def _ranges(outs):
+    return [(o.buf.data_ptr(), o.buf.data_ptr() + o.buf.numel() * o.buf.element_size()) for o in outs if o.acc]
+
+
+def _main_grad(dev, outs, fn, *inputs):
+    """Run the gradient launches `fn` on the main stream NOW, ordered after every side-stream
+    write to the same flat-buffer ranges.  A parameter used twice in a step (the encoder runs
+    twice per Generator step) has both passes' gradients accumulated into one .grad slice;
+    when one pass's launches went to the side stream and the other's run on the main stream
+    (blstm_last_pass / _last_conv_main routing), the two read-modify-writes must not overlap:
+    if a launch into the range is still queued, this one joins the queue behind it (same
+    stream, same order); if a released batch wrote it, the main stream waits for that batch's
+    event first (in a step-graph capture: an edge from the side branch)."""
+    outs = outs if isinstance(outs, tuple) else (outs,)
+    mine = _ranges(outs)
+    if mine and _GRAD_STREAM_ON:
+        def hit(rs):
+            return any(lo < h and l < hi for lo, hi in mine for l, h in rs)
+        if any(hit(_ranges(item[4])) for item in _GRAD_QUEUE):
+            _GRAD_QUEUE.append((dev, fn, inputs, _PRECISION[0], outs))
+            return
+        main = torch.cuda.current_stream(dev)
+        waited = set()
+        for lo, hi, ev in _SIDE_WRITES:
+            if id(ev) not in waited and hit([(lo, hi)]):
+                main.wait_event(ev)
+                waited.add(id(ev))
+    fn()
 
 
 def _grad_mark(dev):
@@ -171,6 +205,11 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
         _PRECISION[0] = prev_prec
         _lib.call("autovc_gemm_set_lds_reserve", 0)
         _GRAD_STREAM_ACTIVE[0] = False
+    written = [r for item in items for r in _ranges(item[4])]
+    if written:
+        ev = torch.cuda.Event()
+        ev.record(side)
+        _SIDE_WRITES.extend((lo, hi, ev) for lo, hi in written)
     if MARKS.active:
         MARKS.mark(dev, side, [o for item in items for o in item[4]])
 
@@ -179,6 +218,7 @@ def join_grad_stream(dev=None):
     """Release queued gradient work and make the current stream wait for the gradient
     stream (before anything reads the gradients)."""
     _flush_grad_queue(beside_recurrence=False)
+    _SIDE_WRITES.clear()
     if not _GRAD_PENDING:
         return
     dev = dev or torch.device("cuda", torch.cuda.current_device())
@@ -954,7 +994,7 @@ class ConvBNChainFn(torch.autograd.Function):
                 # (AVC_LAST_CONV_MAIN=1: the last-differentiated encoder pass's conv weight
                 # gradients on the main stream instead of the final side batch)
                 if ctx.last_pass and _last_conv_main():
-                    dw()
+                    _main_grad(dev, go, dw, Dt, Xt)
                 else:
                     _grad_launch(dev, go, dw, Dt, Xt)
                 grads[7 * l] = go.result()
@@ -1150,7 +1190,7 @@ class ConvBNChainBf16Fn(torch.autograd.Function):
                     _lib.call("autovc_conv_unpack_grad_f32", Co, Ci, KS, dWf.data_ptr(), go.buf.data_ptr(),
                               int(go.acc), _s())
                 if ctx.last_pass and _last_conv_main():   # (as ConvBNChainFn)
-                    dw()
+                    _main_grad(dev, go, dw, dy, xin, xcoef)
                 else:
                     _grad_launch(dev, go, dw, dy, xin, xcoef)
                 grads[7 * l] = go.result()
@@ -1414,57 +1454,10 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=None):
     return dx, dWih, dWhh, dbih, dbhh
 
 
-# Time-chunked LSTM weight gradients: decoder lstm2's four dW GEMMs
-# (3 x 4096 x 1024 + 4096 x 512 over K = B*T) run in AVC_DW_CHUNKS pieces of T / chunks steps
-# each, started on the gradient side stream as the stacked backward finishes each chunk,
-# instead of as four whole-sequence GEMMs released beside lstm1's backward.  Chunk order is
-# fixed (deterministic); the sums differ from the whole-sequence GEMM's only in fp32 order.
-# Measured and NOT adopted (profiles/r05/ab_dw_chunks.txt, alternating, one box): fp32
-# 14.53 ms/step whole vs 15.69-15.72 (4 chunks) and 16.62 (2); bf16 9.02-9.05 vs 9.74-9.78 and
-# 10.12-10.19.  The stacked backward's step launches need three workgroups on every CU at once;
-# beside a weight-gradient GEMM (one 67 KB-LDS workgroup per CU, the reserve keeping room for
-# one step workgroup) each step runs in three rounds, which costs far more than the GEMMs
-# that were spilling past lstm1's backward.  0 / 1 = off (the default).
-_DW_CHUNKS = int(os.environ.get("AVC_DW_CHUNKS", "0"))
-
-
-def _chunked_dw_plan(T, specs, dev):
-    """(chunks, Tc, jobs) for the time-chunked weight gradients of one stacked backward, or
-    None (off, T not divisible, or a destination outside the optimizer's flat buffer — the
-    chunks accumulate into it).  specs: (dG, input, W, param, tap0, needed) per weight."""
-    n = _DW_CHUNKS
-    if n < 2 or not _GRAD_STREAM_ON or T % n or T // n < 4:
-        return None
-    jobs = []
-    for dG, X, W, p, tap0, need in specs:
-        if not need:
-            continue
-        go = _GradOut(p, W.shape, dev)
-        if not go.acc:
-            return None
-        jobs.append((go, dG, X, tap0))
-    return n, T // n, jobs
-
-
-def _queue_dw_chunk(jobs, B, T, t0, Tc, dev):
-    """Queue the weight-gradient GEMMs of steps [t0, t0 + Tc) (autovc_gemm_tchunk_*) for the
-    side stream, accumulating into the flat gradient buffer."""
-    for go, dG, X, tap0 in jobs:
-        M, N = go.buf.shape
-
-        def fn(go=go, dG=dG, X=X, tap0=tap0, M=M, N=N):
-            K = B * Tc
-            lib = _lib.load()
-            if _PRECISION[0] == "bf16":
-                sp = lib.autovc_gemm_bf16_splits(M, N, K, 1)
-                name = "autovc_gemm_tchunk_bf16_f32"
-            else:
-                sp = _splits_for(M, N, K)
-                name = "autovc_gemm_tchunk_f32"
-            ws = _ws(dev, 4 * lib.autovc_gemm_workspace_floats(M, N, sp), "gemm") if sp > 1 else 0
-            _lib.call(name, M, N, B, T, t0, Tc, dG.data_ptr(), dG.shape[2], X.data_ptr(), X.shape[2], tap0,
-                      go.buf.data_ptr(), N, 1, sp, ws, _s())
-        _grad_launch(dev, go, fn, dG, X)
+# Time-chunked LSTM weight gradients (round 5, AVC_DW_CHUNKS: lstm2's dW GEMMs started per
+# finished time chunk) measured slower (fp32 14.53 vs 15.69-16.62 ms/step, bf16 9.02 vs
+# 9.74-10.19; profiles/r05/ab_dw_chunks.txt) and are retired to tools/retired/ (buildable from
+# 35d60fe): the whole-sequence GEMMs released beside lstm1's backward stay.
 
 
 # decoder lstm2 forward (fp32) as ONE persistent weight-stationary launch
@@ -1627,46 +1620,21 @@ class LSTM2StackFn(torch.autograd.Function):
         if bf:
             dG1b, dG0b = (torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16) for _ in range(2))
 
-        def steps(s0, s1):
-            if bf:
-                _lib.call("autovc_lstm2_bwd_range_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(),
-                          c1.data_ptr(), g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(),
-                          WT0.data_ptr(), dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), splits,
-                          s0, s1, ws, _s())
-            else:
-                _lib.call("autovc_lstm2_bwd_range_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(),
-                          c1.data_ptr(), g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(),
-                          WT0.data_ptr(), dG1.data_ptr(), dG0.data_ptr(), splits, s0, s1, ws, _s())
-
         mark = _grad_mark(dev)   # queued weight gradients run beside the recurrences
-        dw = _chunked_dw_plan(T, ((dG1, h0, W_ih1, ctx.params[1][0], 0, need1[1]),
-                                  (dG1, h1, W_hh1, ctx.params[1][1], -1, need1[2]),
-                                  (dG0, x, W_ih0, ctx.params[0][0], 0, need0[1]),
-                                  (dG0, h0, W_hh0, ctx.params[0][1], -1, need0[2])), dev)
-        if dw is None:
-            steps(0, T + 1)
-            _flush_grad_queue(after=mark)
-            grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]),
-                                         dGb=dG1b if bf else None)
-            grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0, dGb=dG0b if bf else None)
-            return (grads0[0], *grads0[1:], *grads1[1:], None)
-        # time-chunked weight gradients: after iterations [0, (c + 1) Tc + 1) the last
-        # (c + 1) Tc steps of both layers' dG are final, so chunk c's four dW GEMMs start
-        # on the side stream while the recurrence runs the next chunk
-        nch, Tc, jobs = dw
-        s0 = 0
-        for c in range(nch):
-            s1 = T + 1 if c == nch - 1 else (c + 1) * Tc + 1
-            steps(s0, s1)
-            if c == 0:
-                _flush_grad_queue(after=mark)
-            _queue_dw_chunk(jobs, B, T, T - (c + 1) * Tc, Tc, dev)
-            if c < nch - 1:     # the last chunk waits for the next recurrence, like every other dW
-                _flush_grad_queue(after=_grad_mark(dev))
-            s0 = s1
-        grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False, False, False) + tuple(need1[3:]))
-        grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], (need0[0], False, False) + tuple(need0[3:]))
-        return (grads0[0], None, None, *grads0[3:], None, None, *grads1[3:], None)
+        if bf:
+            _lib.call("autovc_lstm2_bwd_bf16", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(),
+                      c1.data_ptr(), g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(),
+                      WT0.data_ptr(), dG1.data_ptr(), dG1b.data_ptr(), dG0.data_ptr(), dG0b.data_ptr(), splits,
+                      ws, _s())
+        else:
+            _lib.call("autovc_lstm2_bwd_f32", B, T, H, dh1.data_ptr(), T * H, H, g1.data_ptr(),
+                      c1.data_ptr(), g0.data_ptr(), c0.data_ptr(), WT1.data_ptr(), WIT1.data_ptr(),
+                      WT0.data_ptr(), dG1.data_ptr(), dG0.data_ptr(), splits, ws, _s())
+        _flush_grad_queue(after=mark)
+        grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]),
+                                     dGb=dG1b if bf else None)
+        grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0, dGb=dG0b if bf else None)
+        return (grads0[0], *grads0[1:], *grads1[1:], None)
 
 
 # The persistent decoder-lstm2 backward (lstm2_bwd_persist_kernel: 28.9 vs 24.4 us per
@@ -1771,7 +1739,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         dG2 = dG.view(M, 2 * G)
         # under bf16 the weight / bias gradients go to the side stream like the large LSTMs'
         # (_grad_launch, released beside the next recurrence; _blstm_side)
-        launch = _grad_launch if _blstm_side(ctx.last_pass) else (lambda _dev, _outs, fn, *_in: fn())
+        launch = _grad_launch if _blstm_side(ctx.last_pass) else _main_grad
         for d, (iW, iH, iBi, iBh) in enumerate(((1, 2, 3, 4), (5, 6, 7, 8))):
             pW, pH, pBi, pBh = ctx.params[d]
             if ctx.needs_input_grad[iW]:

@@ -83,24 +83,9 @@ int autovc_preprocess_f64(const void* x, int x_is_f64, const int64_t* wav_off, i
  * *_conv_T > 0 turns the operand into the im2col view of an NTC activation with T frames
  * per sequence, C channels and first tap offset tap0 (-2 for k=5/pad=2; -1 = "previous
  * frame").  splits > 1 = split-K with a workspace of autovc_gemm_workspace_floats floats
- * whose first 64 KiB (tile counters) must be zero before its first use; every call leaves
- * them zero (AVC_GEMM_FIXUP=1: the splits of a tile finish in one launch, the last to arrive
- * summing the partials in split order; by default slabs + a reduce launch, measured faster).
+ * (partial slabs, summed in split order by a reduce launch: deterministic).
  */
 int64_t autovc_gemm_workspace_floats(int M, int N, int splits);
-/* The weight gradient of one time chunk of an LSTM layer (replaces the chunk's share of
- * torch's dW = dG^T x / dG^T h_{t-1} over all frames, model_vc_mel.py:104): steps
- * [t0, t0 + Tc) of each of B sequences of T steps,
- *   C[M,N] (+)= sum_b sum_t A[(b*T + t)*lda + m] * Bm[(b*T + t + b_tap0)*ldb + n]
- * (b_tap0 = -1: the previous step's h, zero at t = 0).  K = B*Tc; splits / workspace as
- * autovc_gemm_f32 (bf16: autovc_gemm_bf16_splits of (M, N, B*Tc)).  The chunks of a
- * sequence summed in order give the whole-sequence gradient up to fp32 summation order. */
-int autovc_gemm_tchunk_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
-                           const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate,
-                           int splits, float* workspace, hipStream_t stream);
-int autovc_gemm_tchunk_bf16_f32(int M, int N, int B, int T, int t0, int Tc, const float* A, int64_t lda,
-                                const float* Bm, int64_t ldb, int b_tap0, float* C, int64_t ldc, int accumulate,
-                                int splits, float* workspace, hipStream_t stream);
 int autovc_gemm_f32(int M, int N, int K,
                     const float* A, int64_t lda, int a_trans, int a_conv_T, int a_conv_C, int a_tap0,
                     const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
@@ -446,20 +431,6 @@ int autovc_lstm2_bwd_f32(int B, int T, int H, const float* dh1_out, int64_t d_ld
                          const float* gates1, const float* c1, const float* gates0, const float* c0,
                          const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
                          float* dG0, int splits, float* workspace, hipStream_t stream);
-/* autovc_lstm2_bwd_f32 / _bf16 issued in pieces: wavefront iterations s in [s_begin, s_end)
- * of 0..T (iteration s finishes layer 1's step T-1-s and layer 0's step T-s; after
- * iterations [0, s_end) both layers' dG are final for every t >= T + 1 - s_end).  Calls
- * covering 0..T in order, on one stream and one workspace, are one full call: the caller
- * starts each finished time chunk's weight gradients (autovc_gemm_tchunk_*) in between. */
-int autovc_lstm2_bwd_range_f32(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                               const float* gates1, const float* c1, const float* gates0, const float* c0,
-                               const float* W_hh1_T, const float* W_ih1_T, const float* W_hh0_T, float* dG1,
-                               float* dG0, int splits, int s_begin, int s_end, float* workspace, hipStream_t stream);
-int autovc_lstm2_bwd_range_bf16(int B, int T, int H, const float* dh1_out, int64_t d_ldb, int64_t d_ldt,
-                                const float* gates1, const float* c1, const float* gates0, const float* c0,
-                                const uint16_t* W_hh1_T_b, const uint16_t* W_ih1_T_b, const uint16_t* W_hh0_T_b,
-                                float* dG1, uint16_t* dG1_b, float* dG0, uint16_t* dG0_b, int splits, int s_begin,
-                                int s_end, float* workspace, hipStream_t stream);
 int autovc_blstm_fwd_f32(int B, int T, int H, int ndir, const float* gx, const float* W_hh_f,
                          const float* W_hh_b, float* h, float* c_all, float* gates,
                          hipStream_t stream);

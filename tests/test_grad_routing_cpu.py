@@ -78,3 +78,59 @@ def test_generator_marks_only_the_full_pass(monkeypatch):
         pass
     assert seen == [False, True]
     assert AF._BLSTM_LAST_PASS[0] is False
+
+
+class _FakeStream:
+    def __init__(self, log):
+        self.log = log
+
+    def wait_event(self, ev):
+        self.log.append(("wait", ev))
+
+
+def _out(flat, lo, hi, acc=True):
+    import types
+    return types.SimpleNamespace(acc=acc, buf=flat[lo:hi])
+
+
+def test_main_stream_gradient_orders_after_side_writes_of_the_same_range(monkeypatch):
+    """a parameter whose gradient one encoder pass accumulates on the side
+    stream and the other on the main stream.  _main_grad joins the side queue behind a queued
+    launch into an overlapping flat range, waits for the event of a released side batch that
+    wrote one, and runs at once (no wait) for a disjoint range."""
+    import torch
+    flat = torch.zeros(64)
+    log = []
+    monkeypatch.setattr(AF, "_GRAD_STREAM_ON", True)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda dev=None: _FakeStream(log))
+    monkeypatch.setattr(AF, "_GRAD_QUEUE", [])
+    monkeypatch.setattr(AF, "_SIDE_WRITES", [])
+    dev = torch.device("cpu")
+
+    # (1) a launch into [8, 24) is still queued for the side stream: an overlapping main-stream
+    # launch is queued behind it, not run
+    AF._GRAD_QUEUE.append((dev, lambda: log.append("side"), (), "fp32", (_out(flat, 8, 24),)))
+    AF._main_grad(dev, _out(flat, 16, 20), lambda: log.append("main1"))
+    assert log == [] and len(AF._GRAD_QUEUE) == 2
+    AF._GRAD_QUEUE.clear()
+
+    # (2) a released side batch wrote [8, 24): the main stream waits for its event, then runs
+    ev = object()
+    AF._SIDE_WRITES.append((flat[8:24].data_ptr(), flat[24:].data_ptr(), ev))
+    AF._main_grad(dev, (_out(flat, 0, 4), _out(flat, 20, 28)), lambda: log.append("main2"))
+    assert log == [("wait", ev), "main2"]
+
+    # (3) a disjoint range runs at once, with no wait
+    log.clear()
+    AF._main_grad(dev, _out(flat, 32, 40), lambda: log.append("main3"))
+    assert log == ["main3"]
+
+    # (4) destinations outside the flat buffer (acc False) never wait
+    log.clear()
+    AF._main_grad(dev, _out(flat, 8, 24, acc=False), lambda: log.append("main4"))
+    assert log == ["main4"]
+
+    # (5) the join orders the main stream after everything: the record is dropped
+    monkeypatch.setattr(AF, "_GRAD_PENDING", set())
+    AF.join_grad_stream(dev)
+    assert AF._SIDE_WRITES == []

@@ -345,3 +345,50 @@ def test_capture_survives_cyclic_garbage_owning_graphs(cuda, monkeypatch):
         gc.set_threshold(*th)
     eager = _graph_vs_eager_run(cuda, "bf16", True, 8, False, 3)
     _assert_same(eager, replay)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_routed_gradients_in_replays_equal_single_stream(cuda, precision):
+    """the default gradient routing (weight gradients on the side stream, the
+    last-differentiated encoder pass's BLSTM / conv weight gradients on the main stream, both
+    passes accumulating into one flat slice; functional._main_grad orders the main-stream
+    accumulate after the side batch that wrote the same range) captured into the B=64 step graph
+    and replayed twice gives the flat gradients and parameters of the single-stream eager step
+    (AVC_GRAD_STREAM=0) bit for bit.  With the gradient-ready marks active (data parallel), each
+    cached graph's mark structure is restored before its replay."""
+    import bench
+    from autovc_amd import functional as AF
+
+    def run(grad_stream, graph, marks):
+        prev, prev_marks = AF._GRAD_STREAM_ON, AF.MARKS.active
+        try:
+            AF._GRAD_STREAM_ON = grad_stream
+            AF.MARKS.active = marks
+            torch.manual_seed(0)
+            solver = bench.make_solver(cuda, 64)
+            solver.G.train()
+            solver.precision = precision
+            solver.hip_graph = graph
+            x, e = bench.synthetic_batch(64, 128, cuda, 99)
+            snaps = []
+            for _ in range(3):        # capture + two replays
+                solver.train_step(x, e)
+                if marks:
+                    snaps.append(AF.MARKS.snapshot())
+            torch.cuda.synchronize()
+            AF.check_device_faults(cuda)
+            out = ([g.clone() for g in solver.g_optimizer.flat_grads()],
+                   [p.clone() for p in solver.g_optimizer.flat_params()], snaps)
+            del solver
+            return out
+        finally:
+            AF._GRAD_STREAM_ON, AF.MARKS.active = prev, prev_marks
+
+    single = run(False, False, False)
+    routed = run(True, True, True)
+    for a, b in zip(single[0], routed[0]):
+        assert torch.equal(a, b)
+    for a, b in zip(single[1], routed[1]):
+        assert torch.equal(a, b)
+    snaps = routed[2]
+    assert snaps[0][0] > 1 and snaps[0] == snaps[1] == snaps[2]
