@@ -68,6 +68,8 @@ struct WnArgs {
   float* gsk;        // (B, 256) x {skip sum, -, -, step + 1}
   float* gh1;        // (B, 256) x {h1, -, -, step + 1}
   float* gpt;        // (2 parities, n_layers, B, 512) x {past-tap sum, step + 1} (8 bytes)
+  // layer-pipelined generation (wn_pipe_kernel): each layer's skip rows, handed to the tail
+  float* gsl;        // (n_layers, B, 256) x {skip row of layer l, step + 1} (8 bytes)
   int* ctr;
   const float* teacher;
   int teacher_len;
@@ -1484,6 +1486,543 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
   }
 }
 
+// ================================================================ layer-pipelined generation
+// (B <= 8, the r9y9 shapes R = 512, G = 512, S = 256, 3 taps, 24 layers).  ONE persistent launch
+// per autovc_wavenet_generate_f32 call, its 256 workgroups (one per CU, 8 waves) split by LAYER
+// instead of by gate pair: XCD slot x (blocks b with b % 8 == x; placement is a speed matter only,
+// every hand-off is a tagged write-through granule) holds layers 3x, 3x + 1, 3x + 2, ten
+// workgroups each (ranks 0-9, 10-19, 20-29 of the slot); slot 7's ranks 30-31 run the tail (the
+// last layer's skip rows and the skip sum), slot 0's ranks 30-31 the head (h1).  A layer's ten
+// workgroups keep its current-tap gate rows [sqrt(.5) W_2 W_out(l-1) | sqrt(.5) W_2] and layer l-1's
+// residual rows (W_out, W_skip) in VGPRs for the whole call (26 gate pairs x 2304 floats per
+// workgroup, <= 4 gate pairs x 36 floats per lane), so a phase moves only its 768 inputs: the
+// previous layer's 256 granules {g_(l-1)[o], x_(l-1)[2o], x_(l-1)[2o+1], step + 1}, published by
+// 10 producers (not 256 as in wn_grid_kernel's all-gather), mostly inside one XCD.
+//   phase (l, t, u): the 8 waves poll 32 granules each into LDS, an LDS-counter sync, each wave
+//   multiplies its <= 4 gate pairs (2 gate rows over 768 inputs, 3 residual rows over 256; lane L
+//   owns granules 4L..4L+3), one butterfly, and lane q publishes gate pair q's granule for layer l
+//   and layer l-1's skip row {s_(l-1)[o], tag} for the tail.  Utterances are independent chains:
+//   each role serves (t, u) in order, so at B > 1 the utterances travel through the layers one
+//   behind the other instead of sharing every hand-off.
+//   past taps: after the last utterance of step t a layer's workgroups compute P_l(t+1) = W_0
+//   x_l(t+1-2d) + W_1 x_l(t+1-d) for their own rows (weights streamed from memory once per group
+//   of <= 4 utterances) into LDS, where phase (l, t+1, u) adds them: no hand-off at all.
+//   layer 0: every workgroup of layer 0 polls h1 of the previous step, runs the MoL GEMV and the
+//   draw itself (same Philox stream, same value everywhere); its current tap is x_0 = in fw + fb,
+//   so z = in (W_2 fw) + W_2 fb with both products formed once in the prologue.
+//   tail: the skip rows of layers 0..22 accumulated as they arrive, then layer 23's skip rows.
+// A wait that gives up (the 256 workgroups were not all resident) sets the error word every other
+// wait checks, the call's samples are poisoned with NaN and bit 2 of autovc_wavenet_fault is set.
+constexpr int kPW = 8;                        // waves per workgroup
+constexpr int kPQ = 4;                        // gate pairs per wave (at most)
+constexpr int kPLayers = 24;
+
+struct PLds {                                 // float offsets into the dynamic LDS block
+  int wr, x, red, pt, mol, gum, in, cnt, total;
+};
+__host__ __device__ inline PLds p_lds(int NB) {
+  PLds o;
+  int p = 0;
+  // layer l-1's residual rows of this workgroup's gate pairs [wave][q][W_out 2o, 2o + 1, W_skip
+  // o][lane][4] (96 KB; read back every phase while the inputs are polled: in VGPRs for the whole
+  // call they pushed the past-tap pass into spills); layer 0: W2 [wave][m][lane][4]
+  o.wr = p;   p += kPW * kPQ * 3 * 256;
+  o.x = p;    p += 2 * 256 * 4;               // staged input granules [parity][256][4]
+  o.red = p;  p += kPW * 32;                  // per-wave reduced values [wave][32]
+  o.pt = p;   p += NB * kPW * kPQ * 2;        // past taps of the coming step [u][wave][q][2]
+  o.mol = p;  p += 32;                        // MoL parameters (layer 0)
+  o.gum = p;  p += 16;                        // sampling noise (layer 0)
+  o.in = p;   p += 4;                         // the step's input sample (layer 0)
+  o.cnt = p;  p += 4;                         // the waves' LDS sync counter
+  o.total = p;
+  return o;
+}
+
+// LDS-counter sync of the NW waves of a workgroup, bounded like chain_sync (a wave that gave up
+// elsewhere never arrives; the device error word then ends the wait)
+template <int NW>
+__device__ __forceinline__ bool wg_sync(int* cnt, int& k, int lane, int* err, int ticks, int step, int ph) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int want = NW * ++k;
+  Spin sp{__builtin_amdgcn_s_memrealtime(), err, ticks, 3, step, ph};
+  int n = 0;
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+    if ((++n & 255) == 0 && !sp.tick()) return false;
+  asm volatile("" ::: "memory");
+  return true;
+}
+
+// N 16-byte granules per lane at base + off[i] floats (wave-uniform base) until every tag == tag
+template <int N>
+__device__ __forceinline__ bool p_poll(const float* base, const int (&off)[N], int tag, f32x4 (&g)[N], Spin& sp) {
+  while (true) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < N; ++i) g[i] = ld4_l2(base, off[i]);
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) bad |= tag_of(g[i]) ^ tag;
+    if (__builtin_amdgcn_ballot_w64(bad != 0) == 0) return true;
+    sp.seen = __builtin_amdgcn_readfirstlane(tag_of(g[0]));
+    if (!sp.tick()) return false;
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, int t1, int* errw, int ticks) {
+  // fmaf where a sum is formed; no other contraction (every utterance is computed by the same
+  // instruction sequence whatever the batch: batch invariance)
+#pragma clang fp contract(off)
+  constexpr int R = 512, H = 256, S = 256, KX = 3 * 512 + 256, KT = 2 * 512, G = 512;
+  constexpr int UG = NB < 4 ? NB : 4;         // utterances per past-tap pass
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int L = a.n_layers, B = a.B, T = a.T, RING = a.RING, NO = a.NO;
+  const PLds lo = p_lds(NB);
+  f32x4* s_x = reinterpret_cast<f32x4*>(lds + lo.x);
+  f32x4* s_wr = reinterpret_cast<f32x4*>(lds + lo.wr);
+  float* s_red = lds + lo.red;
+  float* s_pt = lds + lo.pt;
+  float* s_mol = lds + lo.mol;
+  float* s_gum = lds + lo.gum;
+  float* s_in = lds + lo.in;
+  int* s_cnt = reinterpret_cast<int*>(lds + lo.cnt);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = blockIdx.x, xs = bid & 7, rk = bid >> 3;
+  // role: 1 = layer `layer` (member j of 10), 2 = tail (j of 2), 3 = head (j of 2), 0 = idle
+  int kind = 0, layer = 0, j = 0;
+  if (rk < 30) { kind = 1; layer = xs * 3 + rk / 10; j = rk % 10; }
+  else if (xs == 7) { kind = 2; j = rk - 30; }
+  else if (xs == 0) { kind = 3; j = rk - 30; }
+  if (kind == 0) return;
+  if (tid == 0) *s_cnt = 0;
+  for (int i = tid; i < NB * kPW * kPQ * 2; i += 64 * kPW) s_pt[i] = 0.f;   // P(0) = 0
+  // the polls are sc1 loads: drop any stale line of the hand-off regions (as wn_grid_kernel)
+  if (tid < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();
+  const int64_t RB4 = (int64_t)B * 256 * 4;   // floats of one ring slot (all utterances)
+  int kx = 0;                                 // wg_sync rounds
+  int par = 0;                                // LDS staging parity
+  bool ok = true;
+  int cur_t = t0;
+  const float* W1 = head_base(a);
+  const float* b1 = W1 + (int64_t)S * S;
+  const float* W2 = b1 + S;
+  const float* b2 = W2 + (int64_t)NO * S;
+
+  if (kind == 1) {
+    // =========================== a layer's workgroup: gate pairs o0 .. o0 + no - 1
+    const int o0 = j < 6 ? 26 * j : 156 + 25 * (j - 6), no = j < 6 ? 26 : 25;
+    const bool l0 = layer == 0;
+    const float* lb = layer_base(a, layer);
+    // this wave's gate pairs: local index w + 8 q; lane q < kPQ runs pair q's epilogue
+    int oq[kPQ];
+    bool vq[kPQ];
+#pragma unroll
+    for (int q = 0; q < kPQ; ++q) {
+      vq[q] = w + 8 * q < no;
+      oq[q] = o0 + (vq[q] ? w + 8 * q : 0);
+    }
+    const bool my_valid = lane < kPQ && w + 8 * lane < no;
+    const int my_o = o0 + (my_valid ? w + 8 * lane : 0);
+    // resident gate weights, lane L's inputs: g[4L + i], x[8L + m] (granules 4L .. 4L + 3); the
+    // residual rows wait in LDS (s_wr)
+    float wa[kPQ][12], wb[kPQ][12];
+    float bo0 = 0.f, bo1 = 0.f, bsk = 0.f;    // lane q: layer l-1's residual biases of pair q
+    float ua = 0.f, va = 0.f, ub = 0.f, vb = 0.f;   // layer 0, lane q: W_2 fw, W_2 fb of rows o, o + H
+    float fw0 = 0.f, fw1 = 0.f, fb0 = 0.f, fb1 = 0.f; // layer 0, lane q: first_conv of channels 2o, 2o + 1
+#pragma unroll
+    for (int q = 0; q < kPQ; ++q) {
+      const float* ra = lb + (int64_t)oq[q] * KX + KT;
+      const float* rb = lb + (int64_t)(oq[q] + H) * KX + KT;
+      const f32x4 ga = ld4(ra + 4 * lane), gb = ld4(rb + 4 * lane);
+      const f32x4 xa0 = ld4(ra + H + 8 * lane), xa1 = ld4(ra + H + 8 * lane + 4);
+      const f32x4 xb0 = ld4(rb + H + 8 * lane), xb1 = ld4(rb + H + 8 * lane + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        wa[q][i] = vq[q] ? ga[i] : 0.f;
+        wb[q][i] = vq[q] ? gb[i] : 0.f;
+        wa[q][4 + i] = vq[q] ? xa0[i] : 0.f;
+        wa[q][8 + i] = vq[q] ? xa1[i] : 0.f;
+        wb[q][4 + i] = vq[q] ? xb0[i] : 0.f;
+        wb[q][8 + i] = vq[q] ? xb1[i] : 0.f;
+      }
+      if (!l0) {
+        const float* pb = layer_base(a, layer - 1) + (int64_t)G * KX;
+        const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 r0 = ld4(pb + (int64_t)(2 * oq[q]) * H + 4 * lane);
+        const f32x4 r1 = ld4(pb + (int64_t)(2 * oq[q] + 1) * H + 4 * lane);
+        const f32x4 sk = ld4(pb + (int64_t)(R + oq[q]) * H + 4 * lane);
+        s_wr[((w * kPQ + q) * 3 + 0) * 64 + lane] = vq[q] ? r0 : z4;
+        s_wr[((w * kPQ + q) * 3 + 1) * 64 + lane] = vq[q] ? r1 : z4;
+        s_wr[((w * kPQ + q) * 3 + 2) * 64 + lane] = vq[q] ? sk : z4;
+      }
+    }
+    if (!l0) {
+      const float* pbias = layer_base(a, layer - 1) + (int64_t)G * KX + (int64_t)(R + S) * H;
+      if (my_valid) { bo0 = pbias[2 * my_o]; bo1 = pbias[2 * my_o + 1]; bsk = pbias[R + my_o]; }
+    } else {
+      // W_2 fw and W_2 fb of this wave's gate rows (lane L: channels 8L .. 8L + 7), one butterfly
+      const f32x4 f0 = ld4(a.packed + 8 * lane), f1 = ld4(a.packed + 8 * lane + 4);
+      const f32x4 c0 = ld4(a.packed + R + 8 * lane), c1 = ld4(a.packed + R + 8 * lane + 4);
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < kPQ; ++q) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s0 = fmaf(wa[q][4 + i], f0[i], s0); s0 = fmaf(wa[q][8 + i], f1[i], s0);
+          s1 = fmaf(wa[q][4 + i], c0[i], s1); s1 = fmaf(wa[q][8 + i], c1[i], s1);
+          s2 = fmaf(wb[q][4 + i], f0[i], s2); s2 = fmaf(wb[q][8 + i], f1[i], s2);
+          s3 = fmaf(wb[q][4 + i], c0[i], s3); s3 = fmaf(wb[q][8 + i], c1[i], s3);
+        }
+        v[4 * q] = s0; v[4 * q + 1] = s1; v[4 * q + 2] = s2; v[4 * q + 3] = s3;
+      }
+      const float r = wave_reduce_hw<16>(v, lane);
+      if ((lane & 3) == 0) s_red[w * 32 + (lane >> 2)] = r;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane < kPQ) {
+        ua = s_red[w * 32 + 4 * lane]; va = s_red[w * 32 + 4 * lane + 1];
+        ub = s_red[w * 32 + 4 * lane + 2]; vb = s_red[w * 32 + 4 * lane + 3];
+        fw0 = a.packed[2 * my_o]; fw1 = a.packed[2 * my_o + 1];
+        fb0 = a.packed[R + 2 * my_o]; fb1 = a.packed[R + 2 * my_o + 1];
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int jo = w + 8 * m;
+        s_wr[m * 64 + lane + w * 4 * 64] = ld4(W2 + (int64_t)(jo < NO ? jo : 0) * S + 4 * lane);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // s_wr: wave-private slices
+    const int d = 1 << (layer % a.lps);
+
+    // P_l(tn) for every utterance into s_pt: x_l(tn - 2d) (W_0), x_l(tn - d) (W_1); per pass (tap,
+    // half) lane L owns channels 256 half + 4L .. + 3 (granules 128 half + 2L, + 1, components 1, 2)
+    auto past = [&](int tn) -> bool {
+      for (int ug = 0; ug < B; ug += UG) {
+        float acc[kPQ * 2 * UG];
+#pragma unroll
+        for (int i = 0; i < kPQ * 2 * UG; ++i) acc[i] = 0.f;
+        for (int tap = 0; tap < 2; ++tap) {
+          const int s = tn - (2 - tap) * d;
+          if (s < 0) continue;
+          const float* xr = a.gring + ((int64_t)layer * RING + (s & (RING - 1))) * RB4;
+          for (int hf = 0; hf < 2; ++hf) {
+            float xin[UG][4];
+#pragma unroll
+            for (int uu = 0; uu < UG; ++uu) {
+              const int u = ug + uu < B ? ug + uu : 0;
+              const int off[2] = {(u * 256 + 128 * hf + 2 * lane) * 4, (u * 256 + 128 * hf + 2 * lane + 1) * 4};
+              f32x4 gx[2];
+              Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 4, tn, layer};
+              if (!p_poll<2>(xr, off, s + 1, gx, sp)) return false;
+              xin[uu][0] = gx[0][1]; xin[uu][1] = gx[0][2]; xin[uu][2] = gx[1][1]; xin[uu][3] = gx[1][2];
+            }
+#pragma unroll
+            for (int q = 0; q < kPQ; ++q) {
+#pragma unroll
+              for (int ab = 0; ab < 2; ++ab) {
+                const f32x4 wv = ld4(lb + (int64_t)(oq[q] + ab * H) * KX + tap * R + 256 * hf + 4 * lane);
+#pragma unroll
+                for (int uu = 0; uu < UG; ++uu) {
+                  float sacc = acc[(q * 2 + ab) * UG + uu];
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) sacc = fmaf(wv[i], xin[uu][i], sacc);
+                  acc[(q * 2 + ab) * UG + uu] = sacc;
+                }
+              }
+            }
+          }
+        }
+        constexpr int NV = kPQ * 2 * UG;      // 8, 16 or 32
+        const float r = wave_reduce_hw<NV>(acc, lane);
+        if ((lane & (64 / NV - 1)) == 0) {
+          const int vi = lane / (64 / NV);
+          const int q = vi / (2 * UG), ab = (vi / UG) & 1, uu = vi % UG;
+          if (ug + uu < B) s_pt[(((ug + uu) * kPW + w) * kPQ + q) * 2 + ab] = r;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      return true;
+    };
+    if (t0 > 0) ok = past(t0);
+
+    for (int t = t0; t < t1 && ok; ++t) {
+      cur_t = t;
+      const int ts = t & (RING - 1), prow = t % a.Tch;
+      for (int u = 0; u < B && ok; ++u) {
+        // epilogue operands of lane q: the conditioning and the past taps of gate pair q
+        float pre_a = 0.f, pre_b = 0.f, pta = 0.f, ptb = 0.f;
+        if (my_valid) {
+          const float* pr = a.pre + ((int64_t)prow * B + u) * ((int64_t)L * G) + (int64_t)layer * G;
+          pre_a = pr[my_o];
+          pre_b = pr[my_o + H];
+          pta = s_pt[((u * kPW + w) * kPQ + lane) * 2];
+          ptb = s_pt[((u * kPW + w) * kPQ + lane) * 2 + 1];
+        }
+        float za = 0.f, zb = 0.f, x0n = 0.f, x1n = 0.f, sv = 0.f;
+        if (l0) {
+          // ---- the previous step's h1 -> MoL parameters -> the draw; then layer 0's gate
+          const int tp = t - 1;
+          f32x4 w2v[4];                       // W2 rows w + 8 m (read while h1 is polled)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) w2v[m] = s_wr[m * 64 + lane + w * 4 * 64];
+          if (tp >= 0) {
+            if (w == 1 && lane < 16) {       // the noise of sample tp (off the critical path)
+              const int jn = lane;
+              if (jn < NO / 3 || jn == 10) s_gum[jn] = mol_noise(jn, tp, a.utt_base + u, a);
+            }
+            const float* hb = a.gh1 + (int64_t)u * 256 * 4;
+            const int off[1] = {(32 * w + (lane & 31)) * 4};
+            f32x4 g[1];
+            Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 7, t, 0};
+            if (!p_poll<1>(hb, off, t, g, sp)) { ok = false; break; }
+            if (lane < 32) s_x[par * 256 + 32 * w + lane] = g[0];
+          }
+          if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+          if (tp >= 0) {
+            float v[4];
+            f32x4 hh = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) hh[i] = s_x[par * 256 + 4 * lane + i][0];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+              float sacc = 0.f;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) sacc = fmaf(w2v[m][i], hh[i], sacc);
+              v[m] = sacc;
+            }
+            const float r = wave_reduce_hw<4>(v, lane);
+            if ((lane & 15) == 0) {
+              const int jo = w + 8 * (lane >> 4);
+              if (jo < NO) s_mol[jo] = r + b2[jo];
+            }
+          }
+          if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+          if (w == 0) {
+            // the mixture pick on 16 lanes (mol_finish's order and tie rule), lane 0 finishes
+            const int jj = lane & 15, nr = NO / 3;
+            float v = -INFINITY;
+            if (tp >= 0 && lane < 16 && jj < nr) {
+              v = s_mol[jj] - s_gum[jj];
+              if (!(v == v)) v = -INFINITY;
+            }
+            int bi = jj;
+#pragma unroll
+            for (int mm = 8; mm >= 1; mm >>= 1) {
+              const float ov = __shfl_xor(v, mm);
+              const int oi = __shfl_xor(bi, mm);
+              if (ov > v || (ov == v && oi < bi)) { v = ov; bi = oi; }
+            }
+            if (lane == 0) {
+              float in_v = 0.f, smp = 0.f;
+              if (tp >= 0) {
+                const float mean = s_mol[nr + bi];
+                const float ls = fmaxf(s_mol[2 * nr + bi], a.log_scale_min);
+                const float x = mean + expf(ls) * s_gum[10];
+                smp = fminf(fmaxf(x, -1.0f), 1.0f);
+              }
+              if (a.teacher != nullptr && t < a.teacher_len) in_v = a.teacher[(int64_t)u * a.teacher_len + t];
+              else if (tp >= 0) in_v = smp;
+              s_in[0] = in_v;
+              if (j == 0) {
+                a.yin[(int64_t)u * T + t] = in_v;
+                if (tp >= 0) {
+                  a.y_out[(int64_t)u * T + tp] = smp;
+                  if (a.mol_out)
+                    for (int qq = 0; qq < NO; ++qq) a.mol_out[((int64_t)u * T + tp) * NO + qq] = s_mol[qq];
+                }
+              }
+            }
+          }
+          if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+          if (my_valid) {
+            const float in_v = s_in[0];
+            za = fmaf(in_v, ua, va) + (pre_a + pta);
+            zb = fmaf(in_v, ub, vb) + (pre_b + ptb);
+            x0n = in_v * fw0 + fb0;
+            x1n = in_v * fw1 + fb1;
+          }
+        } else {
+          // ---- layer l-1's 256 granules of this step (utterance u), staged in LDS; the residual
+          // rows are read back from LDS while they are polled
+          f32x4 wrv[kPQ][3];
+#pragma unroll
+          for (int q = 0; q < kPQ; ++q)
+#pragma unroll
+            for (int r = 0; r < 3; ++r) wrv[q][r] = s_wr[((w * kPQ + q) * 3 + r) * 64 + lane];
+          {
+            const float* src = a.gring + ((int64_t)(layer - 1) * RING + ts) * RB4 + (int64_t)u * 256 * 4;
+            const int off[1] = {(32 * w + (lane & 31)) * 4};
+            f32x4 g[1];
+            Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 1, t, layer};
+            if (!p_poll<1>(src, off, t + 1, g, sp)) { ok = false; break; }
+            if (lane < 32) s_x[par * 256 + 32 * w + lane] = g[0];
+          }
+          if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, layer)) { ok = false; break; }
+          f32x4 in[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) in[i] = s_x[par * 256 + 4 * lane + i];
+          float v[32];
+#pragma unroll
+          for (int q = 0; q < kPQ; ++q) {
+            float sa = 0.f, sb = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              sa = fmaf(wa[q][i], in[i][0], sa);
+              sb = fmaf(wb[q][i], in[i][0], sb);
+              s0 = fmaf(wrv[q][0][i], in[i][0], s0);
+              s1 = fmaf(wrv[q][1][i], in[i][0], s1);
+              s2 = fmaf(wrv[q][2][i], in[i][0], s2);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              sa = fmaf(wa[q][4 + 2 * i], in[i][1], sa);
+              sa = fmaf(wa[q][5 + 2 * i], in[i][2], sa);
+              sb = fmaf(wb[q][4 + 2 * i], in[i][1], sb);
+              sb = fmaf(wb[q][5 + 2 * i], in[i][2], sb);
+            }
+            v[8 * q] = sa; v[8 * q + 1] = sb; v[8 * q + 2] = s0; v[8 * q + 3] = s1; v[8 * q + 4] = s2;
+            v[8 * q + 5] = v[8 * q + 6] = v[8 * q + 7] = 0.f;
+          }
+          const float r = wave_reduce_hw<32>(v, lane);
+          if ((lane & 1) == 0) s_red[w * 32 + (lane >> 1)] = r;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (my_valid) {
+            const float* sr = s_red + w * 32 + 8 * lane;
+            za = sr[0] + (pre_a + pta);
+            zb = sr[1] + (pre_b + ptb);
+            const f32x4 xin = s_x[par * 256 + my_o];
+            x0n = (sr[2] + bo0 + xin[1]) * kSqrtHalf;
+            x1n = (sr[3] + bo1 + xin[2]) * kSqrtHalf;
+            sv = sr[4] + bsk;
+          }
+        }
+        if (my_valid) {
+          const float gv = tanhf(za) * avc_sigmoid(zb);
+          st4_sc1(a.gring + ((int64_t)layer * RING + ts) * RB4, (u * 256 + my_o) * 4, gv, x0n, x1n, t + 1);
+          if (!l0) st2t_sc1(a.gsl + (int64_t)(layer - 1) * B * 256 * 2, (u * 256 + my_o) * 2, sv, t + 1);
+        }
+        par ^= 1;
+      }
+      if (ok && t + 1 < t1 && t + 1 < T) ok = past(t + 1);
+    }
+  } else if (kind == 2) {
+    // =========================== tail: skip rows r = 128 j + 16 w + i of every layer, the skip sum
+    const int r0 = 128 * j + 16 * w;
+    const float* pb = layer_base(a, L - 1) + (int64_t)G * KX;
+    float ws[16][4];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const f32x4 v = ld4(pb + (int64_t)(R + r0 + i) * H + 4 * lane);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ws[i][k] = v[k];
+    }
+    const float bskl = pb[(int64_t)(R + S) * H + R + r0 + (lane & 15)];
+    for (int t = t0; t < t1 && ok; ++t) {
+      cur_t = t;
+      const int ts = t & (RING - 1);
+      for (int u = 0; u < B && ok; ++u) {
+        float acc = 0.f;                      // lane i < 16: the running skip sum of row r0 + i
+        for (int l = 0; l < L - 2; ++l) {
+          const float* sl = a.gsl + ((int64_t)l * B + u) * 256 * 2;
+          Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, l};
+          float2 v;
+          while (true) {
+            asm volatile("" ::: "memory");
+            v = ld2_l2(sl, (r0 + (lane & 15)) * 2);
+            if (__builtin_amdgcn_ballot_w64(__float_as_int(v.y) != t + 1) == 0) break;
+            if (!sp.tick()) { ok = false; break; }
+          }
+          if (!ok) break;
+          acc = l == 0 ? v.x : (a.legacy ? (acc + v.x) * kSqrtHalf : acc + v.x);
+        }
+        if (!ok) break;
+        // layer L-2's skip rows and layer L-1's gate outputs arrive from the same phase
+        const float* sl = a.gsl + ((int64_t)(L - 2) * B + u) * 256 * 2;
+        const float* src = a.gring + ((int64_t)(L - 1) * RING + ts) * RB4 + (int64_t)u * 256 * 4;
+        const int off[4] = {(4 * lane) * 4, (4 * lane + 1) * 4, (4 * lane + 2) * 4, (4 * lane + 3) * 4};
+        f32x4 g[4];
+        float2 v;
+        Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 1, t, L};
+        while (true) {
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < 4; ++i) g[i] = ld4_l2(src, off[i]);
+          v = ld2_l2(sl, (r0 + (lane & 15)) * 2);
+          int bad = __float_as_int(v.y) ^ (t + 1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bad |= tag_of(g[i]) ^ (t + 1);
+          if (__builtin_amdgcn_ballot_w64(bad != 0) == 0) break;
+          if (!sp.tick()) { ok = false; break; }
+        }
+        if (!ok) break;
+        acc = L - 2 == 0 ? v.x : (a.legacy ? (acc + v.x) * kSqrtHalf : acc + v.x);
+        float vals[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float sacc = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) sacc = fmaf(ws[i][k], g[k][0], sacc);
+          vals[i] = sacc;
+        }
+        const float r = wave_reduce_hw<16>(vals, lane);
+        if ((lane & 3) == 0) s_red[w * 32 + (lane >> 2)] = r;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane < 16) {
+          const float svl = s_red[w * 32 + lane] + bskl;
+          const float tot = a.legacy ? (acc + svl) * kSqrtHalf : acc + svl;
+          st4_sc1(a.gsk, (u * 256 + r0 + lane) * 4, tot, 0.f, 0.f, t + 1);
+        }
+      }
+    }
+  } else {
+    // =========================== head: h1 rows r = 128 j + 16 w + i
+    const int r0 = 128 * j + 16 * w;
+    float wh[16][4];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const f32x4 v = ld4(W1 + (int64_t)(r0 + i) * S + 4 * lane);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wh[i][k] = v[k];
+    }
+    const float b1r = b1[r0 + (lane & 15)];
+    for (int t = t0; t < t1 && ok; ++t) {
+      cur_t = t;
+      for (int u = 0; u < B && ok; ++u) {
+        const float* src = a.gsk + (int64_t)u * 256 * 4;
+        const int off[4] = {(4 * lane) * 4, (4 * lane + 1) * 4, (4 * lane + 2) * 4, (4 * lane + 3) * 4};
+        f32x4 g[4];
+        Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, L + 1};
+        if (!p_poll<4>(src, off, t + 1, g, sp)) { ok = false; break; }
+        float vals[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float sacc = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) sacc = fmaf(wh[i][k], fmaxf(g[k][0], 0.f), sacc);
+          vals[i] = sacc;
+        }
+        const float r = wave_reduce_hw<16>(vals, lane);
+        if ((lane & 3) == 0) s_red[w * 32 + (lane >> 2)] = r;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane < 16) {
+          const float h = fmaxf(s_red[w * 32 + lane] + b1r, 0.f);
+          st4_sc1(a.gh1, (u * 256 + r0 + lane) * 4, h, 0.f, 0.f, t + 1);
+          a.h1[(int64_t)u * S + r0 + lane] = h;   // plain copy for the last step's sample (wn_final_sample_kernel)
+        }
+      }
+    }
+  }
+  if (!ok) {
+    if (bid == 0 && w == 0)
+      for (int i = lane; i < B * (t1 - t0); i += 64)
+        a.y_out[(int64_t)(i / (t1 - t0)) * T + t0 + i % (t1 - t0)] = __builtin_nanf("");
+    if (tid == 0) __hip_atomic_fetch_or(&g_wn_fault, kGFault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  (void)cur_t;
+}
+
 // ---- graph cache: a captured S-step graph depends only on WnArgs and S.
 struct GraphKey {
   WnArgs a;
@@ -1561,19 +2100,46 @@ int g_wn_timeout_ticks = 100000000;   // 1 s of s_memrealtime (100 MHz) per phas
 // All-CU weight-resident generation (wn_grid_kernel): 0 never, 1 every eligible batch, 2 (the
 // default) up to two utterances — the measured crossover: B = 1 86.5, B = 2 101.1 us per sample
 // step against 103.8 / 104.6 for the launches, B = 4 and up slower (profiles/r04/wn_grid_ab.txt).
-// AVC_WN_GRID outside 0..2 is rejected by the first generate call (g_wn_grid_bad), as
+// 3: the layer-pipelined kernel (wn_pipe_kernel) for every eligible batch (B <= 8, 24 layers).
+// AVC_WN_GRID outside 0..3 is rejected by the first generate call (g_wn_grid_bad), as
 // autovc_wavenet_set_grid rejects it, rather than read as "every batch" with its fault unread
 int g_wn_grid_bad = 0;
 int g_wn_grid = [] {
   const char* e = getenv("AVC_WN_GRID");
   if (!e) return 2;
-  if ((e[0] == '0' || e[0] == '1' || e[0] == '2') && e[1] == 0) return e[0] - '0';
+  if (e[0] >= '0' && e[0] <= '3' && e[1] == 0) return e[0] - '0';
   g_wn_grid_bad = 1;
   return 2;
 }();
 // which path the last autovc_wavenet_generate_f32 call took: 0 the per-layer launches, 1 the
-// all-CU persistent kernel (whose fault word the caller must read)
+// all-CU persistent kernel, 2 the layer-pipelined persistent kernel (1, 2: the caller must read
+// the fault word)
 int g_wn_last_path = 0;
+
+template <int NB>
+bool pipe_attr(int bytes) {
+  int per = 0;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(wn_pipe_kernel<NB>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess &&
+         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wn_pipe_kernel<NB>, 64 * kPW, bytes) == hipSuccess &&
+         per >= 1;
+}
+
+bool pipe_eligible(int B, int n_layers, int taps, int R, int G, int S, int NO) {
+  if (g_wn_grid != 3 || B > 8 || n_layers != kPLayers || taps != 3 || R != 512 || G != 512 || S != 256 || NO > kMaxNO)
+    return false;
+  static int ok = -1;
+  if (ok < 0) {
+    ok = 0;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus == 256 &&
+        pipe_attr<1>(4 * p_lds(1).total) && pipe_attr<2>(4 * p_lds(2).total) && pipe_attr<4>(4 * p_lds(4).total) &&
+        pipe_attr<8>(4 * p_lds(8).total))
+      ok = 1;
+  }
+  return ok == 1;
+}
 
 template <int NB>
 bool grid_attr(int bytes) {
@@ -1585,7 +2151,7 @@ bool grid_attr(int bytes) {
 }
 
 bool grid_eligible(int B, int n_layers, int taps, int R, int G, int S, int NO) {
-  if (!g_wn_grid || (g_wn_grid == 2 && B > 2) || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
+  if (!g_wn_grid || g_wn_grid == 3 || (g_wn_grid == 2 && B > 2) || B > kGMaxB || n_layers < 8 || n_layers > kGMaxL || taps != 3 || R != 512 || G != 512 ||
       S != 256 || NO > kMaxNO)
     return false;
   static int ok = -1;
@@ -1617,7 +2183,7 @@ extern "C" {
 
 
 int autovc_wavenet_set_grid(int on) {
-  AVC_CHECK_ARG(on == 0 || on == 1 || on == 2, "autovc_wavenet_set_grid: 0 (off), 1 (B <= 8) or 2 (B <= 2)");
+  AVC_CHECK_ARG(on >= 0 && on <= 3, "autovc_wavenet_set_grid: 0 (off), 1 (B <= 8), 2 (B <= 2) or 3 (layer-pipelined, B <= 8)");
   g_wn_grid = on;
   g_wn_grid_bad = 0;
   return avc::kOk;
@@ -1675,7 +2241,8 @@ int64_t autovc_wavenet_workspace_bytes(int B, int T, int n_layers, int layers_pe
   const int64_t floats = ring + (int64_t)B * T + 2 * (int64_t)B * S + 2 * (int64_t)B * (G / 2) +
                          2 * (int64_t)n_layers * B * G + (int64_t)(S / kHR) * B * kMaxNO + 7 * 64;
   const int64_t grid = 16 * ((int64_t)n_layers * ring_frames(n_layers, layers_per_stack, taps) * B * 256 + 2 * (int64_t)B * 256) +
-                       8 * 2 * (int64_t)n_layers * B * 512;   // wn_grid_kernel's tagged granules
+                       8 * 2 * (int64_t)n_layers * B * 512 +  // wn_grid_kernel's tagged granules
+                       8 * (int64_t)n_layers * B * 256;       // wn_pipe_kernel's skip-row granules
   return floats * 4 + kCtrSlots * 4 + kGErrInts * 4 + grid + 1024;
 }
 
@@ -1708,8 +2275,8 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
                                 int teacher_len, float* y_out, float* mol_out, void* workspace, int graph_steps,
                                 hipStream_t stream) {
   static const char* fn = "autovc_wavenet_generate_f32";
-  AVC_CHECK_ARG(!g_wn_grid_bad, "%s: AVC_WN_GRID must be 0 (per-layer launches), 1 (all-CU kernel for B <= 8) or 2 "
-                "(all-CU kernel for B <= 2, the default)", fn);
+  AVC_CHECK_ARG(!g_wn_grid_bad, "%s: AVC_WN_GRID must be 0 (per-layer launches), 1 (all-CU kernel for B <= 8), 2 "
+                "(all-CU kernel for B <= 2, the default) or 3 (layer-pipelined kernel for B <= 8)", fn);
   AVC_CHECK_ARG(B > 0 && T > 0 && 0 <= t0 && t0 < t1 && t1 <= T, "%s: bad range B=%d T=%d t=[%d,%d)", fn, B, T, t0, t1);
   AVC_CHECK_ARG(Tch > 0 && t1 - t0 <= Tch, "%s: chunk [%d,%d) longer than the conditioning chunk %d", fn, t0, t1, Tch);
   AVC_CHECK_ARG(n_layers >= 1 && n_layers + 2 < kCtrSlots && layers_per_stack >= 1 && layers_per_stack <= 16 &&
@@ -1751,17 +2318,35 @@ int autovc_wavenet_generate_f32(int B, int T, int t0, int t1, int n_layers, int 
     a.gsk = g;    g += 4 * (int64_t)B * 256;
     a.gh1 = g;    g += 4 * (int64_t)B * 256;
     a.gpt = g;    g += 2 * 2 * (int64_t)n_layers * B * 512;
+    a.gsl = g;    g += 2 * (int64_t)n_layers * B * 256;
   }
   a.teacher = teacher; a.teacher_len = teacher ? teacher_len : 0;
   a.y_out = y_out; a.mol_out = mol_out;
   a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32);
   a.utt_base = utt_base; a.log_scale_min = log_scale_min;
-  const int64_t used = reinterpret_cast<char*>(a.gpt + 2 * 2 * (int64_t)n_layers * B * 512) - static_cast<char*>(workspace);
+  const int64_t used = reinterpret_cast<char*>(a.gsl + 2 * (int64_t)n_layers * B * 256) - static_cast<char*>(workspace);
   AVC_CHECK_ARG(used <= autovc_wavenet_workspace_bytes(B, T, n_layers, layers_per_stack, taps, R, G, S),
                 "%s: workspace layout overflow", fn);
 
   if (t0 == 0) AVC_HIP(avc::zero_async(workspace, (size_t)used, stream), "zero_async");
   g_wn_last_path = 0;
+  if (pipe_eligible(B, n_layers, taps, R, G, S, n_out)) {
+    // one persistent launch for the whole call, each layer's current-tap and residual rows on
+    // ten CUs of their own, utterances flowing through the layers (wn_pipe_kernel)
+    g_wn_last_path = 2;
+    AVC_HIP(avc::zero_async(gerr, (size_t)kGErrInts * 4, stream), "zero_async");
+    const int lds = 4 * p_lds(B == 1 ? 1 : B == 2 ? 2 : B <= 4 ? 4 : 8).total;
+    if (B == 1) hipLaunchKernelGGL(wn_pipe_kernel<1>, dim3(256), dim3(64 * kPW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else if (B == 2) hipLaunchKernelGGL(wn_pipe_kernel<2>, dim3(256), dim3(64 * kPW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else if (B <= 4) hipLaunchKernelGGL(wn_pipe_kernel<4>, dim3(256), dim3(64 * kPW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    else hipLaunchKernelGGL(wn_pipe_kernel<8>, dim3(256), dim3(64 * kPW), lds, stream, a, t0, t1, gerr, g_wn_timeout_ticks);
+    AVC_CHECK_LAUNCH(fn);
+    if (t1 == T) {
+      hipLaunchKernelGGL(wn_final_sample_kernel, dim3(1, (B + kBT - 1) / kBT), dim3(256), 0, stream, a, T);
+      AVC_CHECK_LAUNCH(fn);
+    }
+    return avc::kOk;
+  }
   if (grid_eligible(B, n_layers, taps, R, G, S, n_out)) {
     // one persistent launch for the whole call, every gate weight of the chain on chip (wn_grid_kernel)
     g_wn_last_path = 1;

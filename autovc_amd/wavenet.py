@@ -335,14 +335,17 @@ class WaveNet(nn.Module):
         # timed out (its 256 workgroups were not all resident): read it whenever that kernel
         # ran (reading synchronises the device, so the per-layer launches do not pay for it)
         # and raise — never silently regenerate on another path
-        if lib.autovc_wavenet_last_path() == 1:
+        path = lib.autovc_wavenet_last_path()
+        if path in (1, 2):
             fault = ctypes.c_int(0)
             _lib.call("autovc_wavenet_fault", 1, ctypes.addressof(fault))
             if fault.value:
                 diag = (ctypes.c_int * 5)()
                 _lib.call("autovc_wavenet_grid_diag", 1, ctypes.addressof(diag))
+                name = ("wn_grid_kernel (all-CU WaveNet generation)" if path == 1 else
+                        "wn_pipe_kernel (layer-pipelined WaveNet generation)")
                 raise Fh.DeviceFault(
-                    "wn_grid_kernel (all-CU WaveNet generation): a hand-off wait timed out "
+                    f"{name}: a hand-off wait timed out "
                     f"(kind, step, phase, workgroup, tag seen = {tuple(diag)}) — its 256 workgroups were not all "
                     "resident (another process on this GPU?); outputs are NaN.  Run one generation process per "
                     "GPU (INTEGRATION.md, Co-residency) or set AVC_WN_GRID=0 for the per-layer launches.")
