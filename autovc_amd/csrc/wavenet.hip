@@ -999,8 +999,9 @@ struct Spin {
   int seen = -1;                              // the tag last observed (diagnostics)
   bool slow = false;                          // off the critical path: long sleeps, every check
   int n = 0;
+  int chk = 3;                                // the error word and the clock every (chk + 1)th retry
   __device__ bool tick() {                    // false: give up (timed out, or another wave did)
-    if (!slow && (++n & 3) != 0) {            // the error word and the clock every 4th retry
+    if (!slow && (++n & chk) != 0) {
       __builtin_amdgcn_s_sleep(1);
       return true;
     }
@@ -1489,15 +1490,18 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
 // ================================================================ layer-pipelined generation
 // (B <= 8, the r9y9 shapes R = 512, G = 512, S = 256, 3 taps, 24 layers).  ONE persistent launch
 // per autovc_wavenet_generate_f32 call, its 256 workgroups (one per CU, 8 waves) split by LAYER
-// instead of by gate pair: XCD slot x (blocks b with b % 8 == x; placement is a speed matter only,
-// every hand-off is a tagged write-through granule) holds layers 3x, 3x + 1, 3x + 2, ten
-// workgroups each (ranks 0-9, 10-19, 20-29 of the slot); slot 7's ranks 30-31 run the tail (the
-// last layer's skip rows and the skip sum), slot 0's ranks 30-31 the head (h1).  A layer's ten
-// workgroups keep its current-tap gate rows [sqrt(.5) W_2 W_out(l-1) | sqrt(.5) W_2] and layer l-1's
-// residual rows (W_out, W_skip) in VGPRs for the whole call (26 gate pairs x 2304 floats per
-// workgroup, <= 4 gate pairs x 36 floats per lane), so a phase moves only its 768 inputs: the
-// previous layer's 256 granules {g_(l-1)[o], x_(l-1)[2o], x_(l-1)[2o+1], step + 1}, published by
-// 10 producers (not 256 as in wn_grid_kernel's all-gather), mostly inside one XCD.
+// instead of by gate pair: layer l runs on ten workgroups of XCD slot l % 8 (blocks b with
+// b % 8 == l % 8, ranks b / 8 in [10 (l / 8), 10 (l / 8) + 10)), so every layer-to-layer hand-off
+// crosses XCDs — measured (tools/wn_pipe_trace.py, profiles/r06/wn_pipe_trace_*.txt) a same-XCD
+// hop of 16-byte write-through granules took 1.6-2.6 us from the last producer's store to the
+// consumer's poll, a cross-XCD hop 0.6-0.9 us.  Slot 0's ranks 30-31 run the tail (the last
+// layer's skip rows and the skip sum), slot 1's the head (h1 and the MoL head's partial sums);
+// placement is a speed matter only: every hand-off is a tagged write-through granule.
+// A layer's ten workgroups keep its current-tap gate rows [sqrt(.5) W_2 W_out(l-1) | sqrt(.5) W_2]
+// in VGPRs and layer l-1's residual rows (W_out, W_skip) in LDS for the whole call (26 gate pairs
+// x 2304 floats per workgroup), so a phase moves only its 768 inputs: the previous layer's 256
+// granules {g_(l-1)[o], x_(l-1)[2o], x_(l-1)[2o+1], step + 1}, published by 10 producers (not the
+// 256 of wn_grid_kernel's all-gather).
 //   phase (l, t, u): the 8 waves poll 32 granules each into LDS, an LDS-counter sync, each wave
 //   multiplies its <= 4 gate pairs (2 gate rows over 768 inputs, 3 residual rows over 256; lane L
 //   owns granules 4L..4L+3), one butterfly, and lane q publishes gate pair q's granule for layer l
@@ -1507,10 +1511,13 @@ __global__ __launch_bounds__(64 * kGrW, 1) void wn_grid_kernel(WnArgs a, int t0,
 //   past taps: after the last utterance of step t a layer's workgroups compute P_l(t+1) = W_0
 //   x_l(t+1-2d) + W_1 x_l(t+1-d) for their own rows (weights streamed from memory once per group
 //   of <= 4 utterances) into LDS, where phase (l, t+1, u) adds them: no hand-off at all.
-//   layer 0: every workgroup of layer 0 polls h1 of the previous step, runs the MoL GEMV and the
-//   draw itself (same Philox stream, same value everywhere); its current tap is x_0 = in fw + fb,
-//   so z = in (W_2 fw) + W_2 fb with both products formed once in the prologue.
-//   tail: the skip rows of layers 0..22 accumulated as they arrive, then layer 23's skip rows.
+//   head: h1 rows, then the MoL head's partial sums over the workgroup's 128 h1 rows (2 x 30
+//   8-byte granules per utterance).  layer 0: every wave polls those 60 partials, adds them and
+//   runs the mixture pick and the draw itself (the same Philox stream, the same value in every
+//   wave: no LDS, no sync); its current tap is x_0 = in fw + fb, so z = in (W_2 fw) + W_2 fb with
+//   both products formed once in the prologue.
+//   tail: the skip rows of layers 0..21 accumulated as they arrive, then layer 22's (published
+//   with layer 23's gate outputs) and layer 23's skip rows.
 // A wait that gives up (the 256 workgroups were not all resident) sets the error word every other
 // wait checks, the call's samples are poisoned with NaN and bit 2 of autovc_wavenet_fault is set.
 constexpr int kPW = 8;                        // waves per workgroup
@@ -1518,24 +1525,32 @@ constexpr int kPQ = 4;                        // gate pairs per wave (at most)
 constexpr int kPLayers = 24;
 
 struct PLds {                                 // float offsets into the dynamic LDS block
-  int wr, x, red, pt, mol, gum, in, cnt, total;
+  int wr, x, red, pt, h1, cnt, total;
 };
 __host__ __device__ inline PLds p_lds(int NB) {
   PLds o;
   int p = 0;
   // layer l-1's residual rows of this workgroup's gate pairs [wave][q][W_out 2o, 2o + 1, W_skip
   // o][lane][4] (96 KB; read back every phase while the inputs are polled: in VGPRs for the whole
-  // call they pushed the past-tap pass into spills); layer 0: W2 [wave][m][lane][4]
+  // call they pushed the past-tap pass into spills)
   o.wr = p;   p += kPW * kPQ * 3 * 256;
   o.x = p;    p += 2 * 256 * 4;               // staged input granules [parity][256][4]
   o.red = p;  p += kPW * 32;                  // per-wave reduced values [wave][32]
   o.pt = p;   p += NB * kPW * kPQ * 2;        // past taps of the coming step [u][wave][q][2]
-  o.mol = p;  p += 32;                        // MoL parameters (layer 0)
-  o.gum = p;  p += 16;                        // sampling noise (layer 0)
-  o.in = p;   p += 4;                         // the step's input sample (layer 0)
+  o.h1 = p;   p += 128;                       // head: the workgroup's h1 rows
   o.cnt = p;  p += 4;                         // the waves' LDS sync counter
   o.total = p;
   return o;
+}
+
+// role of workgroup bid: 1 = layer `layer` (member j of 10), 2 = tail (j of 2), 3 = head (j of 2),
+// 0 = idle (slots 2-7, ranks 30-31)
+__host__ __device__ inline void pipe_role(int bid, int& kind, int& layer, int& j) {
+  const int xs = bid & 7, rk = bid >> 3;
+  kind = 0; layer = 0; j = 0;
+  if (rk < 30) { kind = 1; layer = (rk / 10) * 8 + xs; j = rk % 10; }
+  else if (xs == 0) { kind = 2; j = rk - 30; }
+  else if (xs == 1) { kind = 3; j = rk - 30; }
 }
 
 // LDS-counter sync of the NW waves of a workgroup, bounded like chain_sync (a wave that gave up
@@ -1553,9 +1568,11 @@ __device__ __forceinline__ bool wg_sync(int* cnt, int& k, int lane, int* err, in
   return true;
 }
 
-// N 16-byte granules per lane at base + off[i] floats (wave-uniform base) until every tag == tag
+// N 16-byte granules per lane at base + off[i] floats (wave-uniform base) until every tag == tag;
+// the error word and the clock every 32nd retry (each check is a round trip the data may arrive in)
 template <int N>
 __device__ __forceinline__ bool p_poll(const float* base, const int (&off)[N], int tag, f32x4 (&g)[N], Spin& sp) {
+  sp.chk = 31;
   while (true) {
     asm volatile("" ::: "memory");
 #pragma unroll
@@ -1568,6 +1585,31 @@ __device__ __forceinline__ bool p_poll(const float* base, const int (&off)[N], i
     if (!sp.tick()) return false;
   }
 }
+// one 8-byte {value, tag} granule per lane
+__device__ __forceinline__ bool p_poll2(const float* base, int off, int tag, float2& v, Spin& sp) {
+  sp.chk = 31;
+  while (true) {
+    asm volatile("" ::: "memory");
+    v = ld2_l2(base, off);
+    if (__builtin_amdgcn_ballot_w64(__float_as_int(v.y) != tag) == 0) return true;
+    sp.seen = __builtin_amdgcn_readfirstlane(__float_as_int(v.y));
+    if (!sp.tick()) return false;
+  }
+}
+
+#ifdef AVC_WN_PIPE_TRACE
+// diagnostic build (tools/wn_pipe_trace.py): s_memrealtime stamps of wave 0 of every workgroup
+// for utterance 0 of steps kTrT0 .. kTrT0 + kTrN - 1: [step][workgroup][event]
+constexpr int kTrT0 = 64, kTrN = 4, kTrE = 8;
+__device__ uint64_t g_pipe_trace[kTrN * 256 * kTrE];
+#define PIPE_STAMP(T, U, E)                                                                          \
+  do {                                                                                              \
+    if ((U) == 0 && (T) >= kTrT0 && (T) < kTrT0 + kTrN && w == 0 && lane == 0)                   \
+      g_pipe_trace[(((T) - kTrT0) * 256 + bid) * kTrE + (E)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define PIPE_STAMP(T, U, E) do {} while (0)
+#endif
 
 template <int NB>
 __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, int t1, int* errw, int ticks) {
@@ -1583,17 +1625,12 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
   f32x4* s_wr = reinterpret_cast<f32x4*>(lds + lo.wr);
   float* s_red = lds + lo.red;
   float* s_pt = lds + lo.pt;
-  float* s_mol = lds + lo.mol;
-  float* s_gum = lds + lo.gum;
-  float* s_in = lds + lo.in;
+  float* s_h1 = lds + lo.h1;
   int* s_cnt = reinterpret_cast<int*>(lds + lo.cnt);
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bid = blockIdx.x, xs = bid & 7, rk = bid >> 3;
-  // role: 1 = layer `layer` (member j of 10), 2 = tail (j of 2), 3 = head (j of 2), 0 = idle
-  int kind = 0, layer = 0, j = 0;
-  if (rk < 30) { kind = 1; layer = xs * 3 + rk / 10; j = rk % 10; }
-  else if (xs == 7) { kind = 2; j = rk - 30; }
-  else if (xs == 0) { kind = 3; j = rk - 30; }
+  const int bid = blockIdx.x;
+  int kind, layer, j;
+  pipe_role(bid, kind, layer, j);
   if (kind == 0) return;
   if (tid == 0) *s_cnt = 0;
   for (int i = tid; i < NB * kPW * kPQ * 2; i += 64 * kPW) s_pt[i] = 0.f;   // P(0) = 0
@@ -1601,10 +1638,10 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
   if (tid < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
   const int64_t RB4 = (int64_t)B * 256 * 4;   // floats of one ring slot (all utterances)
+  float* gmolp = a.gsl + (int64_t)(L - 1) * B * 256 * 2;   // the MoL partials: [u][head wg][32] granules
   int kx = 0;                                 // wg_sync rounds
   int par = 0;                                // LDS staging parity
   bool ok = true;
-  int cur_t = t0;
   const float* W1 = head_base(a);
   const float* b1 = W1 + (int64_t)S * S;
   const float* W2 = b1 + S;
@@ -1631,6 +1668,7 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
     float bo0 = 0.f, bo1 = 0.f, bsk = 0.f;    // lane q: layer l-1's residual biases of pair q
     float ua = 0.f, va = 0.f, ub = 0.f, vb = 0.f;   // layer 0, lane q: W_2 fw, W_2 fb of rows o, o + H
     float fw0 = 0.f, fw1 = 0.f, fb0 = 0.f, fb1 = 0.f; // layer 0, lane q: first_conv of channels 2o, 2o + 1
+    float b2l = 0.f;                          // layer 0, lane j < 32: the MoL head bias of output j
 #pragma unroll
     for (int q = 0; q < kPQ; ++q) {
       const float* ra = lb + (int64_t)oq[q] * KX + KT;
@@ -1687,11 +1725,7 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
         fw0 = a.packed[2 * my_o]; fw1 = a.packed[2 * my_o + 1];
         fb0 = a.packed[R + 2 * my_o]; fb1 = a.packed[R + 2 * my_o + 1];
       }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int jo = w + 8 * m;
-        s_wr[m * 64 + lane + w * 4 * 64] = ld4(W2 + (int64_t)(jo < NO ? jo : 0) * S + 4 * lane);
-      }
+      b2l = b2[(lane & 31) < NO ? (lane & 31) : 0];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // s_wr: wave-private slices
     const int d = 1 << (layer % a.lps);
@@ -1748,7 +1782,6 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
     if (t0 > 0) ok = past(t0);
 
     for (int t = t0; t < t1 && ok; ++t) {
-      cur_t = t;
       const int ts = t & (RING - 1), prow = t % a.Tch;
       for (int u = 0; u < B && ok; ++u) {
         // epilogue operands of lane q: the conditioning and the past taps of gate pair q
@@ -1761,83 +1794,57 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
           ptb = s_pt[((u * kPW + w) * kPQ + lane) * 2 + 1];
         }
         float za = 0.f, zb = 0.f, x0n = 0.f, x1n = 0.f, sv = 0.f;
+        PIPE_STAMP(t, u, 0);
         if (l0) {
-          // ---- the previous step's h1 -> MoL parameters -> the draw; then layer 0's gate
+          // ---- the draw of sample t-1 in every wave: the head's MoL partials (lane j < 32 from
+          // head workgroup 0, lane 32 + j from head workgroup 1), the mixture pick on lanes 0..15
           const int tp = t - 1;
-          f32x4 w2v[4];                       // W2 rows w + 8 m (read while h1 is polled)
-#pragma unroll
-          for (int m = 0; m < 4; ++m) w2v[m] = s_wr[m * 64 + lane + w * 4 * 64];
+          float in_v = 0.f, smp = 0.f, mol = 0.f;
           if (tp >= 0) {
-            if (w == 1 && lane < 16) {       // the noise of sample tp (off the critical path)
-              const int jn = lane;
-              if (jn < NO / 3 || jn == 10) s_gum[jn] = mol_noise(jn, tp, a.utt_base + u, a);
-            }
-            const float* hb = a.gh1 + (int64_t)u * 256 * 4;
-            const int off[1] = {(32 * w + (lane & 31)) * 4};
-            f32x4 g[1];
+            const int jn = lane & 15;
+            float gum = 0.f;                  // the noise of sample tp, before the poll
+            if (lane < 16 && (jn < NO / 3 || jn == 10)) gum = mol_noise(jn, tp, a.utt_base + u, a);
+            const int jo = lane & 31;
+            float2 pv;
             Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 7, t, 0};
-            if (!p_poll<1>(hb, off, t, g, sp)) { ok = false; break; }
-            if (lane < 32) s_x[par * 256 + 32 * w + lane] = g[0];
-          }
-          if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
-          if (tp >= 0) {
-            float v[4];
-            f32x4 hh = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) hh[i] = s_x[par * 256 + 4 * lane + i][0];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-              float sacc = 0.f;
-#pragma unroll
-              for (int i = 0; i < 4; ++i) sacc = fmaf(w2v[m][i], hh[i], sacc);
-              v[m] = sacc;
+            if (!p_poll2(gmolp + (int64_t)u * 256 * 2, ((lane >> 5) * 32 + (jo < NO ? jo : 0)) * 2, t, pv, sp)) {
+              ok = false;
+              break;
             }
-            const float r = wave_reduce_hw<4>(v, lane);
-            if ((lane & 15) == 0) {
-              const int jo = w + 8 * (lane >> 4);
-              if (jo < NO) s_mol[jo] = r + b2[jo];
-            }
-          }
-          if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
-          if (w == 0) {
-            // the mixture pick on 16 lanes (mol_finish's order and tie rule), lane 0 finishes
-            const int jj = lane & 15, nr = NO / 3;
+            PIPE_STAMP(t, u, 1);
+            const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(pv.x), __float_as_uint(pv.x), false, false);
+            mol = (__uint_as_float(rr[0]) + __uint_as_float(rr[1])) + b2l;
+            const int nr = NO / 3;
             float v = -INFINITY;
-            if (tp >= 0 && lane < 16 && jj < nr) {
-              v = s_mol[jj] - s_gum[jj];
+            if (lane < nr) {
+              v = mol - gum;
               if (!(v == v)) v = -INFINITY;
             }
-            int bi = jj;
+            int bi = jn;
 #pragma unroll
-            for (int mm = 8; mm >= 1; mm >>= 1) {
+            for (int mm = 8; mm >= 1; mm >>= 1) {   // ties to the lowest index (mol_finish's rule)
               const float ov = __shfl_xor(v, mm);
               const int oi = __shfl_xor(bi, mm);
               if (ov > v || (ov == v && oi < bi)) { v = ov; bi = oi; }
             }
-            if (lane == 0) {
-              float in_v = 0.f, smp = 0.f;
-              if (tp >= 0) {
-                const float mean = s_mol[nr + bi];
-                const float ls = fmaxf(s_mol[2 * nr + bi], a.log_scale_min);
-                const float x = mean + expf(ls) * s_gum[10];
-                smp = fminf(fmaxf(x, -1.0f), 1.0f);
-              }
-              if (a.teacher != nullptr && t < a.teacher_len) in_v = a.teacher[(int64_t)u * a.teacher_len + t];
-              else if (tp >= 0) in_v = smp;
-              s_in[0] = in_v;
-              if (j == 0) {
-                a.yin[(int64_t)u * T + t] = in_v;
-                if (tp >= 0) {
-                  a.y_out[(int64_t)u * T + tp] = smp;
-                  if (a.mol_out)
-                    for (int qq = 0; qq < NO; ++qq) a.mol_out[((int64_t)u * T + tp) * NO + qq] = s_mol[qq];
-                }
-              }
+            bi = __builtin_amdgcn_readlane(bi, 0);
+            const float mn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mol), nr + bi));
+            const float ls = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mol), 2 * nr + bi)),
+                                   a.log_scale_min);
+            const float g10 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gum), 10));
+            smp = fminf(fmaxf(mn + expf(ls) * g10, -1.0f), 1.0f);
+            in_v = smp;
+          }
+          if (a.teacher != nullptr && t < a.teacher_len) in_v = a.teacher[(int64_t)u * a.teacher_len + t];
+          if (j == 0 && w == 0) {
+            if (lane == 0) a.yin[(int64_t)u * T + t] = in_v;
+            if (tp >= 0) {
+              if (lane == 0) a.y_out[(int64_t)u * T + tp] = smp;
+              if (a.mol_out && lane < NO) a.mol_out[((int64_t)u * T + tp) * NO + lane] = mol;
             }
           }
-          if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, 0)) { ok = false; break; }
+          PIPE_STAMP(t, u, 3);
           if (my_valid) {
-            const float in_v = s_in[0];
             za = fmaf(in_v, ua, va) + (pre_a + pta);
             zb = fmaf(in_v, ub, vb) + (pre_b + ptb);
             x0n = in_v * fw0 + fb0;
@@ -1859,7 +1866,9 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
             if (!p_poll<1>(src, off, t + 1, g, sp)) { ok = false; break; }
             if (lane < 32) s_x[par * 256 + 32 * w + lane] = g[0];
           }
+          PIPE_STAMP(t, u, 1);
           if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, layer)) { ok = false; break; }
+          PIPE_STAMP(t, u, 2);
           f32x4 in[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) in[i] = s_x[par * 256 + 4 * lane + i];
@@ -1886,6 +1895,7 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
             v[8 * q + 5] = v[8 * q + 6] = v[8 * q + 7] = 0.f;
           }
           const float r = wave_reduce_hw<32>(v, lane);
+          PIPE_STAMP(t, u, 3);
           if ((lane & 1) == 0) s_red[w * 32 + (lane >> 1)] = r;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           if (my_valid) {
@@ -1899,13 +1909,16 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
           }
         }
         if (my_valid) {
-          const float gv = tanhf(za) * avc_sigmoid(zb);
+          const float gv = avc_tanh_fast(za) * avc_sigmoid_fast(zb);
           st4_sc1(a.gring + ((int64_t)layer * RING + ts) * RB4, (u * 256 + my_o) * 4, gv, x0n, x1n, t + 1);
           if (!l0) st2t_sc1(a.gsl + (int64_t)(layer - 1) * B * 256 * 2, (u * 256 + my_o) * 2, sv, t + 1);
         }
+        PIPE_STAMP(t, u, 4);
         par ^= 1;
       }
+      PIPE_STAMP(t, 0, 5);
       if (ok && t + 1 < t1 && t + 1 < T) ok = past(t + 1);
+      PIPE_STAMP(t, 0, 6);
     }
   } else if (kind == 2) {
     // =========================== tail: skip rows r = 128 j + 16 w + i of every layer, the skip sum
@@ -1920,50 +1933,54 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
     }
     const float bskl = pb[(int64_t)(R + S) * H + R + r0 + (lane & 15)];
     for (int t = t0; t < t1 && ok; ++t) {
-      cur_t = t;
       const int ts = t & (RING - 1);
       for (int u = 0; u < B && ok; ++u) {
         float acc = 0.f;                      // lane i < 16: the running skip sum of row r0 + i
+        PIPE_STAMP(t, u, 0);
         for (int l = 0; l < L - 2; ++l) {
-          const float* sl = a.gsl + ((int64_t)l * B + u) * 256 * 2;
-          Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, l};
           float2 v;
-          while (true) {
-            asm volatile("" ::: "memory");
-            v = ld2_l2(sl, (r0 + (lane & 15)) * 2);
-            if (__builtin_amdgcn_ballot_w64(__float_as_int(v.y) != t + 1) == 0) break;
-            if (!sp.tick()) { ok = false; break; }
+          Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, l};
+          if (!p_poll2(a.gsl + ((int64_t)l * B + u) * 256 * 2, (r0 + (lane & 15)) * 2, t + 1, v, sp)) {
+            ok = false;
+            break;
           }
-          if (!ok) break;
           acc = l == 0 ? v.x : (a.legacy ? (acc + v.x) * kSqrtHalf : acc + v.x);
         }
         if (!ok) break;
-        // layer L-2's skip rows and layer L-1's gate outputs arrive from the same phase
-        const float* sl = a.gsl + ((int64_t)(L - 2) * B + u) * 256 * 2;
-        const float* src = a.gring + ((int64_t)(L - 1) * RING + ts) * RB4 + (int64_t)u * 256 * 4;
-        const int off[4] = {(4 * lane) * 4, (4 * lane + 1) * 4, (4 * lane + 2) * 4, (4 * lane + 3) * 4};
-        f32x4 g[4];
-        float2 v;
-        Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 1, t, L};
-        while (true) {
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int i = 0; i < 4; ++i) g[i] = ld4_l2(src, off[i]);
-          v = ld2_l2(sl, (r0 + (lane & 15)) * 2);
-          int bad = __float_as_int(v.y) ^ (t + 1);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) bad |= tag_of(g[i]) ^ (t + 1);
-          if (__builtin_amdgcn_ballot_w64(bad != 0) == 0) break;
-          if (!sp.tick()) { ok = false; break; }
+        // layer L-2's skip rows and layer L-1's gate outputs arrive from the same phase: both
+        // polled at once, the gate outputs staged in LDS (32 granules per wave)
+        {
+          const float* sl = a.gsl + ((int64_t)(L - 2) * B + u) * 256 * 2;
+          const float* src = a.gring + ((int64_t)(L - 1) * RING + ts) * RB4 + (int64_t)u * 256 * 4;
+          const int gi = 32 * w + (lane & 31);
+          f32x4 g;
+          float2 v;
+          Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 1, t, L};
+          sp.chk = 31;
+          while (true) {
+            asm volatile("" ::: "memory");
+            g = ld4_l2(src, gi * 4);
+            v = ld2_l2(sl, (r0 + (lane & 15)) * 2);
+            const int bad = (__float_as_int(v.y) ^ (t + 1)) | (tag_of(g) ^ (t + 1));
+            if (__builtin_amdgcn_ballot_w64(bad != 0) == 0) break;
+            if (!sp.tick()) { ok = false; break; }
+          }
+          if (!ok) break;
+          if (lane < 32) s_x[par * 256 + gi] = g;
+          acc = L - 2 == 0 ? v.x : (a.legacy ? (acc + v.x) * kSqrtHalf : acc + v.x);
         }
-        if (!ok) break;
-        acc = L - 2 == 0 ? v.x : (a.legacy ? (acc + v.x) * kSqrtHalf : acc + v.x);
+        PIPE_STAMP(t, u, 1);
+        if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, L)) { ok = false; break; }
+        PIPE_STAMP(t, u, 2);
+        float gin[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gin[i] = s_x[par * 256 + 4 * lane + i][0];
         float vals[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float sacc = 0.f;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) sacc = fmaf(ws[i][k], g[k][0], sacc);
+          for (int k = 0; k < 4; ++k) sacc = fmaf(ws[i][k], gin[k], sacc);
           vals[i] = sacc;
         }
         const float r = wave_reduce_hw<16>(vals, lane);
@@ -1974,10 +1991,13 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
           const float tot = a.legacy ? (acc + svl) * kSqrtHalf : acc + svl;
           st4_sc1(a.gsk, (u * 256 + r0 + lane) * 4, tot, 0.f, 0.f, t + 1);
         }
+        PIPE_STAMP(t, u, 4);
+        par ^= 1;
       }
     }
   } else {
-    // =========================== head: h1 rows r = 128 j + 16 w + i
+    // =========================== head: h1 rows r = 128 j + 16 w + i, then the MoL partial sums
+    // of this workgroup's 128 rows (wave w: outputs w + 8 m; lane L: rows 2L, 2L + 1)
     const int r0 = 128 * j + 16 * w;
     float wh[16][4];
 #pragma unroll
@@ -1987,20 +2007,36 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
       for (int k = 0; k < 4; ++k) wh[i][k] = v[k];
     }
     const float b1r = b1[r0 + (lane & 15)];
+    float w2c[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int jo = w + 8 * m < NO ? w + 8 * m : 0;
+      w2c[m][0] = W2[(int64_t)jo * S + 128 * j + 2 * lane];
+      w2c[m][1] = W2[(int64_t)jo * S + 128 * j + 2 * lane + 1];
+    }
     for (int t = t0; t < t1 && ok; ++t) {
-      cur_t = t;
       for (int u = 0; u < B && ok; ++u) {
-        const float* src = a.gsk + (int64_t)u * 256 * 4;
-        const int off[4] = {(4 * lane) * 4, (4 * lane + 1) * 4, (4 * lane + 2) * 4, (4 * lane + 3) * 4};
-        f32x4 g[4];
-        Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, L + 1};
-        if (!p_poll<4>(src, off, t + 1, g, sp)) { ok = false; break; }
+        PIPE_STAMP(t, u, 0);
+        {
+          const float* src = a.gsk + (int64_t)u * 256 * 4;
+          const int off[1] = {(32 * w + (lane & 31)) * 4};
+          f32x4 g[1];
+          Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, L + 1};
+          if (!p_poll<1>(src, off, t + 1, g, sp)) { ok = false; break; }
+          if (lane < 32) s_x[par * 256 + 32 * w + lane] = g[0];
+        }
+        PIPE_STAMP(t, u, 1);
+        if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, L + 1)) { ok = false; break; }
+        PIPE_STAMP(t, u, 2);
+        float sk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sk[i] = fmaxf(s_x[par * 256 + 4 * lane + i][0], 0.f);
         float vals[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float sacc = 0.f;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) sacc = fmaf(wh[i][k], fmaxf(g[k][0], 0.f), sacc);
+          for (int k = 0; k < 4; ++k) sacc = fmaf(wh[i][k], sk[k], sacc);
           vals[i] = sacc;
         }
         const float r = wave_reduce_hw<16>(vals, lane);
@@ -2008,9 +2044,21 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane < 16) {
           const float h = fmaxf(s_red[w * 32 + lane] + b1r, 0.f);
-          st4_sc1(a.gh1, (u * 256 + r0 + lane) * 4, h, 0.f, 0.f, t + 1);
+          s_h1[16 * w + lane] = h;
           a.h1[(int64_t)u * S + r0 + lane] = h;   // plain copy for the last step's sample (wn_final_sample_kernel)
         }
+        if (!wg_sync<kPW>(s_cnt, kx, lane, errw, ticks, t, L + 1)) { ok = false; break; }
+        const float h0 = s_h1[2 * lane], h1v = s_h1[2 * lane + 1];
+        float mv[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) mv[m] = fmaf(w2c[m][1], h1v, w2c[m][0] * h0);
+        const float p = wave_reduce_hw<4>(mv, lane);
+        if ((lane & 15) == 0) {
+          const int jo = w + 8 * (lane >> 4);
+          if (jo < NO) st2t_sc1(gmolp + (int64_t)u * 256 * 2, (j * 32 + jo) * 2, p, t + 1);
+        }
+        PIPE_STAMP(t, u, 4);
+        par ^= 1;
       }
     }
   }
@@ -2020,7 +2068,6 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
         a.y_out[(int64_t)(i / (t1 - t0)) * T + t0 + i % (t1 - t0)] = __builtin_nanf("");
     if (tid == 0) __hip_atomic_fetch_or(&g_wn_fault, kGFault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  (void)cur_t;
 }
 
 // ---- graph cache: a captured S-step graph depends only on WnArgs and S.
@@ -2204,6 +2251,14 @@ int autovc_wavenet_grid_diag(int clear, int* out5) {
   }
   return avc::kOk;
 }
+
+#ifdef AVC_WN_PIPE_TRACE
+int autovc_wavenet_pipe_trace(uint64_t* out) {   // trace build only (tools/wn_pipe_trace.py)
+  AVC_HIP(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  AVC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_trace), sizeof(g_pipe_trace)), "hipMemcpyFromSymbol");
+  return avc::kOk;
+}
+#endif
 
 int autovc_wavenet_set_timeout_ticks(int ticks) {
   AVC_CHECK_ARG(ticks >= 0, "autovc_wavenet_set_timeout_ticks: ticks >= 0");
