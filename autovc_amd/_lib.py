@@ -169,6 +169,8 @@ sig("autovc_colsum_f32", c_i64, c_int, c_ptr, c_i64, c_ptr, c_ptr, c_int, c_ptr,
 sig("autovc_wavenet_packed_floats", c_int, c_int, c_int, c_int, c_int, c_int)
 sig("autovc_wavenet_set_grid", c_int)
 sig("autovc_wavenet_get_grid")
+sig("autovc_wavenet_grid_explicit")
+sig("autovc_wavenet_reset_grid")
 sig("autovc_wavenet_last_path")
 sig("autovc_wavenet_grid_diag", c_int, c_ptr)
 sig("autovc_wavenet_set_timeout_ticks", c_int)

@@ -1617,7 +1617,12 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
   // instruction sequence whatever the batch: batch invariance)
 #pragma clang fp contract(off)
   constexpr int R = 512, H = 256, S = 256, KX = 3 * 512 + 256, KT = 2 * 512, G = 512;
-  constexpr int UG = NB < 4 ? NB : 4;         // utterances per past-tap pass
+#ifndef AVC_WN_PIPE_UG
+#define AVC_WN_PIPE_UG 4
+#endif
+  // utterances per past-tap pass: 4 (B = 8 54.2 vs 57.9 us per sample step with 2, which keeps the
+  // pass in registers; 4 spills 11 VGPRs of the pass, off the chain: profiles/r06/wn_pipe_v3_ab.txt)
+  constexpr int UG = NB < AVC_WN_PIPE_UG ? NB : AVC_WN_PIPE_UG;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int L = a.n_layers, B = a.B, T = a.T, RING = a.RING, NO = a.NO;
   const PLds lo = p_lds(NB);
@@ -1660,8 +1665,11 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
       vq[q] = w + 8 * q < no;
       oq[q] = o0 + (vq[q] ? w + 8 * q : 0);
     }
-    const bool my_valid = lane < kPQ && w + 8 * lane < no;
-    const int my_o = o0 + (my_valid ? w + 8 * lane : 0);
+    // lane 16 q runs gate pair q's epilogue: after the butterfly its 5 sums sit on lanes 16 q +
+    // 0, 2, 4, 6, 8 of the same DPP row
+    const int my_q = lane >> 4;
+    const bool my_valid = (lane & 15) == 0 && w + 8 * my_q < no;
+    const int my_o = o0 + (my_valid ? w + 8 * my_q : 0);
     // resident gate weights, lane L's inputs: g[4L + i], x[8L + m] (granules 4L .. 4L + 3); the
     // residual rows wait in LDS (s_wr)
     float wa[kPQ][12], wb[kPQ][12];
@@ -1719,9 +1727,9 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
       const float r = wave_reduce_hw<16>(v, lane);
       if ((lane & 3) == 0) s_red[w * 32 + (lane >> 2)] = r;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane < kPQ) {
-        ua = s_red[w * 32 + 4 * lane]; va = s_red[w * 32 + 4 * lane + 1];
-        ub = s_red[w * 32 + 4 * lane + 2]; vb = s_red[w * 32 + 4 * lane + 3];
+      if ((lane & 15) == 0) {
+        ua = s_red[w * 32 + 4 * my_q]; va = s_red[w * 32 + 4 * my_q + 1];
+        ub = s_red[w * 32 + 4 * my_q + 2]; vb = s_red[w * 32 + 4 * my_q + 3];
         fw0 = a.packed[2 * my_o]; fw1 = a.packed[2 * my_o + 1];
         fb0 = a.packed[R + 2 * my_o]; fb1 = a.packed[R + 2 * my_o + 1];
       }
@@ -1731,7 +1739,7 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
     const int d = 1 << (layer % a.lps);
 
     // P_l(tn) for every utterance into s_pt: x_l(tn - 2d) (W_0), x_l(tn - d) (W_1); per pass (tap,
-    // half) lane L owns channels 256 half + 4L .. + 3 (granules 128 half + 2L, + 1, components 1, 2)
+    // quarter) lane L owns channels 128 quarter + 2L, + 1 (granule 64 quarter + L, components 1, 2)
     auto past = [&](int tn) -> bool {
       for (int ug = 0; ug < B; ug += UG) {
         float acc[kPQ * 2 * UG];
@@ -1741,31 +1749,33 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
           const int s = tn - (2 - tap) * d;
           if (s < 0) continue;
           const float* xr = a.gring + ((int64_t)layer * RING + (s & (RING - 1))) * RB4;
-          for (int hf = 0; hf < 2; ++hf) {
-            float xin[UG][4];
+          for (int qt = 0; qt < 4; ++qt) {
+            // the pass's weights are in flight while its inputs (every utterance of the group at
+            // once: one round trip, not one per utterance) are polled
+            float2 wv[kPQ][2];
 #pragma unroll
-            for (int uu = 0; uu < UG; ++uu) {
-              const int u = ug + uu < B ? ug + uu : 0;
-              const int off[2] = {(u * 256 + 128 * hf + 2 * lane) * 4, (u * 256 + 128 * hf + 2 * lane + 1) * 4};
-              f32x4 gx[2];
-              Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 4, tn, layer};
-              if (!p_poll<2>(xr, off, s + 1, gx, sp)) return false;
-              xin[uu][0] = gx[0][1]; xin[uu][1] = gx[0][2]; xin[uu][2] = gx[1][1]; xin[uu][3] = gx[1][2];
-            }
+            for (int q = 0; q < kPQ; ++q)
 #pragma unroll
-            for (int q = 0; q < kPQ; ++q) {
+              for (int ab = 0; ab < 2; ++ab)
+                wv[q][ab] = *reinterpret_cast<const float2*>(lb + (int64_t)(oq[q] + ab * H) * KX + tap * R + 128 * qt +
+                                                             2 * lane);
+            int off[UG];
 #pragma unroll
-              for (int ab = 0; ab < 2; ++ab) {
-                const f32x4 wv = ld4(lb + (int64_t)(oq[q] + ab * H) * KX + tap * R + 256 * hf + 4 * lane);
+            for (int uu = 0; uu < UG; ++uu) off[uu] = ((ug + uu < B ? ug + uu : 0) * 256 + 64 * qt + lane) * 4;
+            f32x4 gx[UG];
+            Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 4, tn, layer};
+            if (!p_poll<UG>(xr, off, s + 1, gx, sp)) return false;
+#pragma unroll
+            for (int q = 0; q < kPQ; ++q)
+#pragma unroll
+              for (int ab = 0; ab < 2; ++ab)
 #pragma unroll
                 for (int uu = 0; uu < UG; ++uu) {
                   float sacc = acc[(q * 2 + ab) * UG + uu];
-#pragma unroll
-                  for (int i = 0; i < 4; ++i) sacc = fmaf(wv[i], xin[uu][i], sacc);
+                  sacc = fmaf(wv[q][ab].x, gx[uu][1], sacc);
+                  sacc = fmaf(wv[q][ab].y, gx[uu][2], sacc);
                   acc[(q * 2 + ab) * UG + uu] = sacc;
                 }
-              }
-            }
           }
         }
         constexpr int NV = kPQ * 2 * UG;      // 8, 16 or 32
@@ -1790,8 +1800,8 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
           const float* pr = a.pre + ((int64_t)prow * B + u) * ((int64_t)L * G) + (int64_t)layer * G;
           pre_a = pr[my_o];
           pre_b = pr[my_o + H];
-          pta = s_pt[((u * kPW + w) * kPQ + lane) * 2];
-          ptb = s_pt[((u * kPW + w) * kPQ + lane) * 2 + 1];
+          pta = s_pt[((u * kPW + w) * kPQ + my_q) * 2];
+          ptb = s_pt[((u * kPW + w) * kPQ + my_q) * 2 + 1];
         }
         float za = 0.f, zb = 0.f, x0n = 0.f, x1n = 0.f, sv = 0.f;
         PIPE_STAMP(t, u, 0);
@@ -1860,6 +1870,8 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
             for (int r = 0; r < 3; ++r) wrv[q][r] = s_wr[((w * kPQ + q) * 3 + r) * 64 + lane];
           {
             const float* src = a.gring + ((int64_t)(layer - 1) * RING + ts) * RB4 + (int64_t)u * 256 * 4;
+            // (two polls in flight, staggered, measured 0.6 us per sample step slower than one:
+            // profiles/r06/wn_pipe_v4_ab_dbpoll.txt)
             const int off[1] = {(32 * w + (lane & 31)) * 4};
             f32x4 g[1];
             Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 1, t, layer};
@@ -1872,6 +1884,7 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
           f32x4 in[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) in[i] = s_x[par * 256 + 4 * lane + i];
+          const f32x4 xin = s_x[par * 256 + my_o];   // x_(l-1)[2o], [2o + 1]: the residual inputs
           float v[32];
 #pragma unroll
           for (int q = 0; q < kPQ; ++q) {
@@ -1896,16 +1909,17 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
           }
           const float r = wave_reduce_hw<32>(v, lane);
           PIPE_STAMP(t, u, 3);
-          if ((lane & 1) == 0) s_red[w * 32 + (lane >> 1)] = r;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          // lane 16 q gathers its pair's sums from lanes + 2, 4, 6, 8 (DPP row_shl: VALU, no LDS)
+          const float r_zb = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r), 0x102, 0xf, 0xf, false));
+          const float r_x0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r), 0x104, 0xf, 0xf, false));
+          const float r_x1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r), 0x106, 0xf, 0xf, false));
+          const float r_sk = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r), 0x108, 0xf, 0xf, false));
           if (my_valid) {
-            const float* sr = s_red + w * 32 + 8 * lane;
-            za = sr[0] + (pre_a + pta);
-            zb = sr[1] + (pre_b + ptb);
-            const f32x4 xin = s_x[par * 256 + my_o];
-            x0n = (sr[2] + bo0 + xin[1]) * kSqrtHalf;
-            x1n = (sr[3] + bo1 + xin[2]) * kSqrtHalf;
-            sv = sr[4] + bsk;
+            za = r + (pre_a + pta);
+            zb = r_zb + (pre_b + ptb);
+            x0n = (r_x0 + bo0 + xin[1]) * kSqrtHalf;
+            x1n = (r_x1 + bo1 + xin[2]) * kSqrtHalf;
+            sv = r_sk + bsk;
           }
         }
         if (my_valid) {
@@ -1937,14 +1951,31 @@ __global__ __launch_bounds__(64 * kPW, 1) void wn_pipe_kernel(WnArgs a, int t0, 
       for (int u = 0; u < B && ok; ++u) {
         float acc = 0.f;                      // lane i < 16: the running skip sum of row r0 + i
         PIPE_STAMP(t, u, 0);
-        for (int l = 0; l < L - 2; ++l) {
-          float2 v;
-          Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, l};
-          if (!p_poll2(a.gsl + ((int64_t)l * B + u) * 256 * 2, (r0 + (lane & 15)) * 2, t + 1, v, sp)) {
-            ok = false;
-            break;
+        {
+          // layers 0 .. L-3's skip rows: every pending layer's granule re-polled at once, the
+          // ready prefix folded in (in layer order) each round — one round trip when they are
+          // all out (utterances queued behind another), one per arrival while the chain runs
+          constexpr int NL = kPLayers - 2;
+          const float* sl0 = a.gsl + (int64_t)u * 256 * 2;
+          const int off = (r0 + (lane & 15)) * 2;
+          int k = 0;
+          Spin sp{__builtin_amdgcn_s_memrealtime(), errw, ticks, 6, t, 0};
+          sp.chk = 31;
+          while (k < NL) {
+            asm volatile("" ::: "memory");
+            float2 v[NL];
+#pragma unroll
+            for (int l = 0; l < NL; ++l)
+              if (l >= k) v[l] = ld2_l2(sl0 + (int64_t)l * B * 256 * 2, off);
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+              if (l < k) continue;
+              if (__builtin_amdgcn_ballot_w64(__float_as_int(v[l].y) != t + 1) != 0) break;
+              acc = l == 0 ? v[l].x : (a.legacy ? (acc + v[l].x) * kSqrtHalf : acc + v[l].x);
+              k = l + 1;
+            }
+            if (k < NL && !sp.tick()) { ok = false; break; }
           }
-          acc = l == 0 ? v.x : (a.legacy ? (acc + v.x) * kSqrtHalf : acc + v.x);
         }
         if (!ok) break;
         // layer L-2's skip rows and layer L-1's gate outputs arrive from the same phase: both
@@ -2150,14 +2181,19 @@ int g_wn_timeout_ticks = 100000000;   // 1 s of s_memrealtime (100 MHz) per phas
 // 3: the layer-pipelined kernel (wn_pipe_kernel) for every eligible batch (B <= 8, 24 layers).
 // AVC_WN_GRID outside 0..3 is rejected by the first generate call (g_wn_grid_bad), as
 // autovc_wavenet_set_grid rejects it, rather than read as "every batch" with its fault unread
+// Default 3: the layer-pipelined kernel beats both others at every B <= 8 (B = 1 54.6 vs 86.2
+// (mode 2) vs 104.7 us per sample step for the launches, B = 8 54.2 vs 109.3 and 129.2 (mode 1);
+// profiles/r06/wn_pipe_v3_ab.txt).
+constexpr int kWnGridDefault = 3;
 int g_wn_grid_bad = 0;
 int g_wn_grid = [] {
   const char* e = getenv("AVC_WN_GRID");
-  if (!e) return 2;
+  if (!e) return kWnGridDefault;
   if (e[0] >= '0' && e[0] <= '3' && e[1] == 0) return e[0] - '0';
   g_wn_grid_bad = 1;
-  return 2;
+  return kWnGridDefault;
 }();
+int g_wn_grid_explicit = getenv("AVC_WN_GRID") != nullptr;   // the mode was chosen, not defaulted
 // which path the last autovc_wavenet_generate_f32 call took: 0 the per-layer launches, 1 the
 // all-CU persistent kernel, 2 the layer-pipelined persistent kernel (1, 2: the caller must read
 // the fault word)
@@ -2233,10 +2269,20 @@ int autovc_wavenet_set_grid(int on) {
   AVC_CHECK_ARG(on >= 0 && on <= 3, "autovc_wavenet_set_grid: 0 (off), 1 (B <= 8), 2 (B <= 2) or 3 (layer-pipelined, B <= 8)");
   g_wn_grid = on;
   g_wn_grid_bad = 0;
+  g_wn_grid_explicit = 1;
   return avc::kOk;
 }
 
 int autovc_wavenet_get_grid(void) { return g_wn_grid; }
+
+int autovc_wavenet_grid_explicit(void) { return g_wn_grid_explicit; }
+
+int autovc_wavenet_reset_grid(void) {
+  g_wn_grid = kWnGridDefault;
+  g_wn_grid_bad = 0;
+  g_wn_grid_explicit = 0;
+  return avc::kOk;
+}
 
 int autovc_wavenet_last_path(void) { return g_wn_last_path; }
 

@@ -344,11 +344,24 @@ class WaveNet(nn.Module):
                 _lib.call("autovc_wavenet_grid_diag", 1, ctypes.addressof(diag))
                 name = ("wn_grid_kernel (all-CU WaveNet generation)" if path == 1 else
                         "wn_pipe_kernel (layer-pipelined WaveNet generation)")
-                raise Fh.DeviceFault(
-                    f"{name}: a hand-off wait timed out "
-                    f"(kind, step, phase, workgroup, tag seen = {tuple(diag)}) — its 256 workgroups were not all "
-                    "resident (another process on this GPU?); outputs are NaN.  Run one generation process per "
-                    "GPU (INTEGRATION.md, Co-residency) or set AVC_WN_GRID=0 for the per-layer launches.")
+                msg = (f"{name}: a hand-off wait timed out "
+                       f"(kind, step, phase, workgroup, tag seen = {tuple(diag)}) — its 256 workgroups were not all "
+                       "resident (another process on this GPU?)")
+                if lib.autovc_wavenet_grid_explicit():
+                    # the persistent path was asked for (AVC_WN_GRID / autovc_wavenet_set_grid): fail loudly
+                    raise Fh.DeviceFault(
+                        msg + "; outputs are NaN.  Run one generation process per GPU (INTEGRATION.md, "
+                        "Co-residency) or set AVC_WN_GRID=0 for the per-layer launches.")
+                # the library's default choice: warn and regenerate this call on the per-layer launches
+                warnings.warn(msg + "; regenerating this call on the per-layer launches (INTEGRATION.md, "
+                              "Co-residency).", RuntimeWarning, stacklevel=2)
+                _lib.call("autovc_wavenet_set_grid", 0)
+                try:
+                    return self.generate(c, T=T, seed=seed, utt_base=utt_base, teacher=teacher,
+                                         return_mol=return_mol, log_scale_min=log_scale_min, chunk=chunk,
+                                         graph_steps=graph_steps)
+                finally:
+                    _lib.call("autovc_wavenet_reset_grid")
         return (y, mol) if return_mol else y
 
     def incremental_forward(self, initial_input=None, c=None, g=None, T=100, test_inputs=None,

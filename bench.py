@@ -243,7 +243,7 @@ def cpu_share():
     return allowed, len(phys) or (os.cpu_count() or 1)
 
 
-def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=True):
+def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=12.0, cpu=True):
     """BASELINE config 4 / SURVEY §8d C4: r9y9 WaveNet (24 layers, 512 residual channels),
     8 utterances x 128 conditioning frames (32,768 samples = 2.048 s each) synthesised in one
     batch.  Timed: the whole job (upsample, per-chunk conditioning GEMM, every sample step
@@ -264,6 +264,7 @@ def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=
     y = model.generate(c, seed=2, log_scale_min=hparams.log_scale_min)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    wn_path_b8 = _wn_path_name(_lib.load().autovc_wavenet_last_path())
     assert y.shape == (n_utt, T) and bool(torch.isfinite(y).all())
     packed = _lib.load().autovc_wavenet_packed_floats(model.layers, model.kernel_size, model.residual_channels,
                                                        model.gate_channels, model.skip_out_channels,
@@ -299,17 +300,25 @@ def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=10.0, cpu=
     out["b1"] = {"workload": f"1 utterance x {n1} samples (wavegen's batch of one)",
                  "us_per_sample_step": round(d1 / n1 * 1e6, 2), "samples_per_s": round(n1 / d1, 1),
                  "rtf": round(n1 / 16000.0 / d1, 3),
-                 "path": ("wn_grid_kernel (all-CU weight-resident dataflow, one launch per call)"
-                          if _lib.load().autovc_wavenet_get_grid() in (1, 2) else "per-layer launches")}
+                 "path": _wn_path_name(_lib.load().autovc_wavenet_last_path())}
+    out["path"] = wn_path_b8
     if cpu:
         out["cpu_baseline"] = wavenet_cpu_baseline(n_utt, seconds_cpu)
         out["vs_cpu_baseline"] = round(out["samples_per_s"] / out["cpu_baseline"]["value"], 1)
     return out
 
 
-def wavenet_cpu_baseline(n_utt, seconds):
-    """oracle/wavenet.py (fp32 torch CPU ops, the reference's own per-step structure) on a
-    bounded number of sample steps of the same batch."""
+def _wn_path_name(p):
+    return {0: "per-layer launches (hipGraph replay)",
+            1: "wn_grid_kernel (all-CU weight-resident dataflow, one launch per call)",
+            2: "wn_pipe_kernel (layer-pipelined weight-resident chain, one launch per call)"}.get(p, str(p))
+
+
+def wavenet_cpu_baseline(n_utt, seconds, steps=512, min_passes=3):
+    """oracle/wavenet.py (fp32 torch CPU ops, the reference's own per-step structure): after a
+    short warm-up pass, passes of `steps` incremental sample steps of the same batch are timed
+    until `seconds` have elapsed (at least `min_passes`); the value is the MEDIAN pass's rate
+    (a single pass swung 1.1k-1.5k samples/s between identical runs)."""
     from oracle import wavenet as ow
     threads, _ = cpu_share()
     torch.set_num_threads(threads)
@@ -317,19 +326,21 @@ def wavenet_cpu_baseline(n_utt, seconds):
     o = ow.OracleWaveNet(ow.make_weights(hp), hp, dtype=torch.float32)
     g = torch.Generator().manual_seed(4321)
     c = torch.clamp(torch.randn(n_utt, 80, 4, generator=g) * 0.18 + 0.43, 0, 1)
-    cu = o.upsample(c)          # 1024 samples: enough for the largest sample below
-    steps = 16
-    while True:
-        u = ow.philox_uniforms(3, list(range(n_utt)), 0, steps)
+    cu = o.upsample(c)          # 1024 samples: enough for the passes below
+    u = ow.philox_uniforms(3, list(range(n_utt)), 0, steps)
+    o.incremental(cu[:, :, :32], 32, uniforms=ow.philox_uniforms(3, list(range(n_utt)), 0, 32))   # warm-up
+    rates = []
+    t_start = time.perf_counter()
+    while len(rates) < min_passes or time.perf_counter() - t_start < seconds:
         t0 = time.perf_counter()
         o.incremental(cu[:, :, :steps], steps, uniforms=u)
-        dt = time.perf_counter() - t0
-        if dt > seconds / 4 or steps >= 1024:
-            break
-        steps *= 2
-    return {"value": round(n_utt * steps / dt, 1), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} incremental steps x {n_utt} utterances of oracle/wavenet.py (fp32, torch "
-                      f"{torch.__version__} CPU, {threads} threads), {dt:.2f} s"}
+        rates.append(n_utt * steps / (time.perf_counter() - t0))
+    rates.sort()
+    med = rates[len(rates) // 2]
+    return {"value": round(med, 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"median of {len(rates)} passes of {steps} incremental steps x {n_utt} utterances of "
+                      f"oracle/wavenet.py (fp32, torch {torch.__version__} CPU, {threads} threads), "
+                      f"{time.perf_counter() - t_start:.1f} s; pass rates {rates[0]:.0f}-{rates[-1]:.0f} samples/s"}
 
 
 def synthetic_wavs(n, base_index, seed=5000):

@@ -520,19 +520,27 @@ int autovc_colsum_f32(int64_t M, int N, const float* X, int64_t ld, float* out, 
  *   autovc_wavenet_ring_frames: frames of the per-layer input rings (power of two >=
  *            (taps-1) * max dilation + 1).
  */
-/* All-CU weight-resident generation (B <= 8, R = 512, G = 512, S = 256, 3 taps, 8..24 layers, a
- * 256-CU device): ONE persistent launch per autovc_wavenet_generate_f32 call whose 256
- * workgroups keep every gate weight of the sample chain on chip and hand each phase's outputs
- * to the next through tagged 16-byte granules (dataflow, no grid barrier).  Same
- * arguments and outputs; a hand-off wait that times out poisons the call's samples with NaN and
- * sets bit 2 of the autovc_wavenet_fault word.
- * Mode (AVC_WN_GRID or autovc_wavenet_set_grid): 0 never, 1 for every eligible batch, 2 (the
- * default) for B <= 2, where it beats the launches; any other AVC_WN_GRID
- * value makes autovc_wavenet_generate_f32 fail.  autovc_wavenet_last_path: 1 if the last
- * generate call ran the all-CU kernel (its caller must read autovc_wavenet_fault), 0 if the
+/* Persistent generation (B <= 8, R = 512, G = 512, S = 256, 3 taps, a 256-CU device): ONE
+ * launch per autovc_wavenet_generate_f32 call, same arguments and outputs, every hand-off a
+ * tagged 16-byte write-through granule (dataflow, no grid barrier); a wait that
+ * times out poisons the call's samples with NaN and sets bit 2 of the autovc_wavenet_fault word.
+ *   layer-pipelined (wn_pipe_kernel, 24 layers): ten CUs per layer hold its current-tap and
+ *   residual rows for the whole call; utterances travel through the layers one behind another.
+ *   all-CU (wn_grid_kernel, 8..24 layers): every CU holds one gate pair of every layer.
+ * Mode (AVC_WN_GRID or autovc_wavenet_set_grid): 0 never (per-layer launches), 1 all-CU for
+ * every eligible batch, 2 all-CU for B <= 2, 3 (the default) layer-pipelined for every eligible
+ * batch (other shapes run the launches); any other AVC_WN_GRID value makes
+ * autovc_wavenet_generate_f32 fail.  autovc_wavenet_grid_explicit: 1 if the mode was chosen
+ * (AVC_WN_GRID set or autovc_wavenet_set_grid called), 0 for the library default — the Python
+ * layer regenerates on the launches with a warning when a DEFAULT-mode persistent call times
+ * out, and raises when the mode was chosen; autovc_wavenet_reset_grid restores the default (3,
+ * not chosen).  autovc_wavenet_last_path: 2 if the last generate call ran the layer-pipelined
+ * kernel, 1 the all-CU kernel (for both the caller must read autovc_wavenet_fault), 0 the
  * per-layer launches. */
 int autovc_wavenet_set_grid(int on);
 int autovc_wavenet_get_grid(void);
+int autovc_wavenet_grid_explicit(void);
+int autovc_wavenet_reset_grid(void);
 int autovc_wavenet_last_path(void);
 /* The first wait of the all-CU generation that timed out since the last clear: out5 = {kind
  * (0 none, 1 layer inputs, 2 past-tap sums, 3 LDS handshake, 4 past-tap inputs, 5 past-tap

@@ -36,17 +36,26 @@ def _cond(B, Tc, seed=4321):
     return torch.from_numpy(np.clip(rs.normal(0.43, 0.18, (B, 80, Tc)), 0, 1).astype(np.float32))
 
 
-@pytest.fixture(params=[0, 1], ids=["launches", "grid"])
+def _restore_mode(prev, explicit):
+    from autovc_amd import _lib
+    if explicit:
+        _lib.call("autovc_wavenet_set_grid", prev)
+    else:
+        _lib.call("autovc_wavenet_reset_grid")
+
+
+@pytest.fixture(params=[0, 1, 3], ids=["launches", "grid", "pipe"])
 def wn_mode(request):
-    """Run a test with the per-layer launches and with the all-CU weight-resident generation
-    (wn_grid_kernel: B <= 8, 8..24 layers, 256 CUs); other shapes use the launches either way.
-    (The XCD-local form this fixture also ran until round 4 is retired: tools/retired/.)"""
+    """Run a test with the per-layer launches, the all-CU weight-resident generation
+    (wn_grid_kernel: B <= 8, 8..24 layers, 256 CUs) and the layer-pipelined one (wn_pipe_kernel:
+    B <= 8, 24 layers); other shapes use the launches either way.  (The XCD-local form this
+    fixture also ran until round 4 is retired: tools/retired/.)"""
     from autovc_amd import _lib
     lib = _lib.load()
-    prev = lib.autovc_wavenet_get_grid()
-    _lib.call("autovc_wavenet_set_grid", int(request.param == 1))
+    prev, explicit = lib.autovc_wavenet_get_grid(), lib.autovc_wavenet_grid_explicit()
+    _lib.call("autovc_wavenet_set_grid", request.param)
     yield request.param
-    _lib.call("autovc_wavenet_set_grid", prev)
+    _restore_mode(prev, explicit)
 
 
 def rel(a, b):
@@ -182,8 +191,9 @@ def _set_modes(grid):
     _lib.call("autovc_wavenet_set_grid", grid)
 
 
+@pytest.mark.parametrize("mode", [1, 3], ids=["grid", "pipe"])
 @pytest.mark.parametrize("B", [8, 1])
-def test_grid_generation_matches_launches(cuda, B):
+def test_grid_generation_matches_launches(cuda, B, mode):
     """The all-CU weight-resident generation (wn_grid_kernel: every gate weight of the chain
     on chip, each phase's outputs handed on in tagged granules, the past taps computed a step
     ahead by the same workgroups) against the per-layer launches: 24 layers, 2,048 free-running samples (16 ring wraps, 16 conditioning
@@ -200,17 +210,18 @@ def test_grid_generation_matches_launches(cuda, B):
     c = _cond(B, 8, seed=31).to(cuda)
     rs = np.random.RandomState(6)
     teacher = torch.from_numpy(rs.uniform(-0.9, 0.9, (B, 2048)).astype(np.float32)).to(cuda)
-    prev = lib.autovc_wavenet_get_grid()
+    prev, explicit = lib.autovc_wavenet_get_grid(), lib.autovc_wavenet_grid_explicit()
     out = {}
     try:
-        for mode in (0, 1):
-            _set_modes(mode)
+        for md in (0, mode):
+            _set_modes(md)
             y = m.generate(c, seed=17, log_scale_min=LSM)
+            assert lib.autovc_wavenet_last_path() == {0: 0, 1: 1, 3: 2}[md]
             _, mol = m.generate(c, seed=17, log_scale_min=LSM, teacher=teacher, return_mol=True)
-            out[mode] = (y, mol)
+            out[md] = (y, mol)
     finally:
-        _set_modes(prev)
-    (y0, m0), (y1, m1) = out[0], out[1]
+        _restore_mode(prev, explicit)
+    (y0, m0), (y1, m1) = out[0], out[mode]
     assert torch.isfinite(y1).all() and torch.isfinite(m1).all()
     assert rel(m1, m0) < 1e-5
     assert (y1 - y0).abs().max().item() < 1e-4
@@ -229,7 +240,7 @@ def test_grid_generation_timeout_surfaces(cuda):
     hp = ow.small_hparams(layers=8, stacks=2)
     m, _ = _model(hp, cuda)
     c = _cond(2, 1).to(cuda)
-    prev = lib.autovc_wavenet_get_grid()
+    prev, explicit = lib.autovc_wavenet_get_grid(), lib.autovc_wavenet_grid_explicit()
     try:
         _set_modes(1)
         _lib.call("autovc_wavenet_set_timeout_ticks", 1)
@@ -240,11 +251,11 @@ def test_grid_generation_timeout_surfaces(cuda):
         assert torch.isfinite(y).all()
     finally:
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        _set_modes(prev)
+        _restore_mode(prev, explicit)
 
 
 def test_grid_default_mode_small_batches(cuda):
-    """Mode 2 (the default) runs the all-CU form for up to two utterances: B = 1 and B = 2
+    """Mode 2 runs the all-CU form for up to two utterances: B = 1 and B = 2
     equal mode 1 bit for bit, B = 3 equals the launches bit for bit.  If its wait gives up
     (forced: a 1-tick timeout) the call raises DeviceFault naming AVC_WN_GRID=0 — it does not
     regenerate on the launches — and the mode is unchanged."""
@@ -255,7 +266,7 @@ def test_grid_default_mode_small_batches(cuda):
     hp = ow.small_hparams(layers=8, stacks=2)
     m, _ = _model(hp, cuda)
     c1, c2, c3 = _cond(1, 2, seed=3).to(cuda), _cond(2, 2, seed=4).to(cuda), _cond(3, 2, seed=5).to(cuda)
-    prev = lib.autovc_wavenet_get_grid()
+    prev, explicit = lib.autovc_wavenet_get_grid(), lib.autovc_wavenet_grid_explicit()
     try:
         out = {}
         for mode in (0, 1, 2):
@@ -273,4 +284,46 @@ def test_grid_default_mode_small_batches(cuda):
         assert torch.equal(m.generate(c1, seed=5, log_scale_min=LSM), out[2][0])   # the next call runs clean
     finally:
         _lib.call("autovc_wavenet_set_timeout_ticks", 0)
-        _set_modes(prev)
+        _restore_mode(prev, explicit)
+
+
+def test_pipe_default_mode_and_fallback(cuda):
+    """The library default (AVC_WN_GRID unset: mode 3) runs the layer-pipelined kernel for
+    B <= 8 at the r9y9 shape (24 layers) and the per-layer launches otherwise (B = 9, 8 layers).
+    A default-mode call whose wait gives up (forced: a 1-tick timeout) warns and regenerates on
+    the launches — the samples equal mode 0's — and the mode stays the unchosen default; the same
+    timeout with mode 3 chosen explicitly raises DeviceFault (ADVICE r5 on the default path)."""
+    from autovc_amd import _lib, functional as AF
+    lib = _lib.load()
+    if lib.autovc_lstm_xcd_supported(64, 512) == 0:
+        pytest.skip("needs 8 XCDs x 32 CUs")
+    prev, explicit = lib.autovc_wavenet_get_grid(), lib.autovc_wavenet_grid_explicit()
+    m, _ = _model(ow.HPARAMS, cuda)
+    small, _ = _model(ow.small_hparams(layers=8, stacks=2), cuda)
+    c1, c9 = _cond(1, 1, seed=3).to(cuda), _cond(9, 1, seed=4).to(cuda)
+    try:
+        _lib.call("autovc_wavenet_reset_grid")
+        assert lib.autovc_wavenet_get_grid() == 3 and lib.autovc_wavenet_grid_explicit() == 0
+        y = m.generate(c1, seed=5, log_scale_min=LSM)
+        assert lib.autovc_wavenet_last_path() == 2
+        m.generate(c9, seed=5, log_scale_min=LSM)
+        assert lib.autovc_wavenet_last_path() == 0
+        small.generate(c1, seed=5, log_scale_min=LSM)
+        assert lib.autovc_wavenet_last_path() == 0
+        _lib.call("autovc_wavenet_set_grid", 0)
+        y0 = m.generate(c1, seed=5, log_scale_min=LSM)
+        assert (y - y0).abs().max().item() < 1e-4
+        _lib.call("autovc_wavenet_reset_grid")
+        _lib.call("autovc_wavenet_set_timeout_ticks", 1)
+        with pytest.warns(RuntimeWarning, match="wn_pipe_kernel.*regenerating"):
+            yf = m.generate(c1, seed=5, log_scale_min=LSM)
+        assert torch.equal(yf, y0)
+        assert lib.autovc_wavenet_get_grid() == 3 and lib.autovc_wavenet_grid_explicit() == 0
+        _lib.call("autovc_wavenet_set_grid", 3)
+        with pytest.raises(AF.DeviceFault, match="wn_pipe_kernel.*AVC_WN_GRID=0"):
+            m.generate(c1, seed=5, log_scale_min=LSM)
+        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
+        assert torch.equal(m.generate(c1, seed=5, log_scale_min=LSM), y)   # the next call runs clean
+    finally:
+        _lib.call("autovc_wavenet_set_timeout_ticks", 0)
+        _restore_mode(prev, explicit)
