@@ -283,9 +283,12 @@ def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=12.0, cpu=
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "bytes_per_step": step_bytes,
-                        "note": "weight-streaming convention: packed per-step weights once per sample step; "
-                                "traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per sample step summed over its "
-                                "launches (profiles/wavenet_pmc.json)"}}
+                        "note": "weight-streaming convention: packed per-step weights once per sample step "
+                                "(SURVEY 8d); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per sample step of the "
+                                "generation kernel (profiles/wavenet_pmc.json, tools/gpu_r06_prof.sh wnpmc): the "
+                                "layer-pipelined kernel keeps the current-tap and residual rows on chip and moves "
+                                "the past-tap weights once per 4 utterances, so the step is bound by its 26 "
+                                "dependent hand-offs, not by HBM"}}
     # the reference's own call shape: wavegen synthesises ONE utterance at a time
     # (synthesis.py:58-69); 32 conditioning frames = 8,192 samples of one stream
     c1 = c[:1, :, :32].contiguous()
