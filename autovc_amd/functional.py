@@ -214,27 +214,11 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
         MARKS.mark(dev, side, [o for item in items for o in item[4]])
 
 
-# AVC_JOIN_MAIN=1: the batch still queued at the join runs on the main stream (idle there, waiting
-# for the side stream) instead of behind the side stream's last batches (A/B, round 6)
-_JOIN_MAIN = os.environ.get("AVC_JOIN_MAIN", "0") == "1"
-
-
 def join_grad_stream(dev=None):
     """Release queued gradient work and make the current stream wait for the gradient
-    stream (before anything reads the gradients)."""
-    if _JOIN_MAIN and _GRAD_QUEUE:
-        items = list(_GRAD_QUEUE)
-        _GRAD_QUEUE.clear()
-        prev = _PRECISION[0]
-        try:
-            for d, fn, inputs, prec, outs in items:
-                _PRECISION[0] = prec
-                _main_grad(d, outs, fn, *inputs)
-                if MARKS.active:
-                    for o in outs:
-                        MARKS.log(o.buf, GradMarks.FINAL)
-        finally:
-            _PRECISION[0] = prev
+    stream (before anything reads the gradients).  (Running the batch still queued here on the
+    idle main stream instead measured fp32 13.93-13.98 vs 13.94, bf16 7.87-7.92 vs 7.81-7.85
+    ms/step: profiles/r06/ab_join_{fp32,bf16}.txt.)"""
     _flush_grad_queue(beside_recurrence=False)
     _SIDE_WRITES.clear()
     if not _GRAD_PENDING:
