@@ -650,17 +650,35 @@ __global__ __launch_bounds__(64 * NW_) void lstm2_bwd_fused_kernel(BwdArgs a1, B
   auto arow_of = [&](int r) { return dG + ((int64_t)min(b0 + r, B - 1) * T + min(t, T - 1)) * K4 + kb; };
   auto brow_of = [&](int r) { return WT + (int64_t)(j0 + r) * K4 + kb; };
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // timing-only ablation builds (tools/lstm_bwd_ablate.sh; wrong results by design):
+  // AVC_ABL_EMPTY returns at once (launch boundary), AVC_ABL_NOMFMA skips the products,
+  // AVC_ABL_NOARRIVE returns after them, AVC_ABL_NOTAIL skips the last arriver's pointwise pass
+#ifdef AVC_ABL_EMPTY
+  return;
+#endif
+#ifndef AVC_ABL_NOMFMA
   if (!none) acc = tile_gemm<KCH_, NW_, D_, BF>(smem, arow_of, brow_of, ks);
+#endif
+#ifdef AVC_ABL_NOARRIVE
+  if (acc[0] == 12345.f) a1.P[0] = acc[1];
+  return;
+#endif
   const int64_t slab = (int64_t)B * H;
   const int ntile = gridDim.y * nt, tile = blockIdx.y * nt + ct;
   if (prod == 0) {
-    if (fused_arrive(smem, acc, false, a1.P + s * slab, B, H, b0, j0, f.cnt + tile, S))
+    if (fused_arrive(smem, acc, false, a1.P + s * slab, B, H, b0, j0, f.cnt + tile, S)) {
+#ifndef AVC_ABL_NOTAIL
       fused_pointwise<S, true>(a1, t1 - 1, t1 - 2, b0, j0);
+#endif
+    }
   } else {
     // layer 0's slabs: [S of its own recurrence (product 2) | S of dG1 W_ih1 (product 1)]
     float* P = a0.P + (prod == 2 ? s : S + s) * slab;
-    if (fused_arrive(smem, acc, none, P, B, H, b0, j0, f.cnt + ntile + tile, 2 * S))
+    if (fused_arrive(smem, acc, none, P, B, H, b0, j0, f.cnt + ntile + tile, 2 * S)) {
+#ifndef AVC_ABL_NOTAIL
       fused_pointwise<2 * S, false>(a0, t1, t1 - 1, b0, j0);
+#endif
+    }
   }
 }
 

@@ -18,7 +18,7 @@ def main():
     B, T = 64, 128
     g = torch.Generator(device=dev).manual_seed(0)
     bf = prec == "bf16"
-    for name, H, S in (("lstm2", 1024, 4), ("lstm1", 512, 8)):
+    for name, H, S in (("lstm2", 1024, int(os.environ.get("LBT_S2", "4"))), ("lstm1", 512, int(os.environ.get("LBT_S1", "8")))):
         gates = [torch.rand(B, T, 4 * H, device=dev, generator=g) for _ in range(2)]
         cs = [torch.randn(B, T, H, device=dev, generator=g) * 0.5 for _ in range(2)]
         WT = [torch.randn(H, 4 * H, device=dev, generator=g) * H ** -0.5 for _ in range(3)]
