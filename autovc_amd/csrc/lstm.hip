@@ -174,6 +174,18 @@ __device__ __forceinline__ f32x4 tile_gemm(float* lds, AR arow_of, BR brow_of, i
 // waves per workgroup, chunks of loads in flight
 constexpr int KCH = 64, NWV = 8, DPF = 2;
 using TileP = Tile<KCH, NWV, DPF>;
+// the fused backward steps' tile (tools/lstm_bwd_tile_sweep.sh builds variants: AVC_BKCH / AVC_BNW /
+// AVC_BD override it)
+#ifndef AVC_BKCH
+#define AVC_BKCH 64
+#endif
+#ifndef AVC_BNW
+#define AVC_BNW 8
+#endif
+#ifndef AVC_BD
+#define AVC_BD 2
+#endif
+constexpr int BKCH = AVC_BKCH, BNW = AVC_BNW, BD = AVC_BD;
 
 struct StepArgs {
   int B, T, H;
@@ -996,10 +1008,10 @@ void launch_lstm_fused_s(hipStream_t st, const BwdArgs& a, const float* dG, int 
                          FusedTile f) {
   const dim3 grid(a.H / TN, (a.B + TB - 1) / TB, S);
   if (a.dh_out)
-    hipLaunchKernelGGL((lstm_bwd_fused_kernel<KCH, NWV, DPF, BF, S, true>), grid, dim3(64 * NWV), 0, st, a, dG, t, tn,
+    hipLaunchKernelGGL((lstm_bwd_fused_kernel<BKCH, BNW, BD, BF, S, true>), grid, dim3(64 * BNW), 0, st, a, dG, t, tn,
                        tnp, WT, f);
   else
-    hipLaunchKernelGGL((lstm_bwd_fused_kernel<KCH, NWV, DPF, BF, S, false>), grid, dim3(64 * NWV), 0, st, a, dG, t, tn,
+    hipLaunchKernelGGL((lstm_bwd_fused_kernel<BKCH, BNW, BD, BF, S, false>), grid, dim3(64 * BNW), 0, st, a, dG, t, tn,
                        tnp, WT, f);
 }
 
@@ -1020,10 +1032,10 @@ void launch_lstm2_fused(hipStream_t st, int S, const BwdArgs& a1, const BwdArgs&
                         FusedTile f) {
   const dim3 grid(3 * a1.H / TN, (a1.B + TB - 1) / TB, S);
   if (S == 4)
-    hipLaunchKernelGGL((lstm2_bwd_fused_kernel<KCH, NWV, DPF, BF, 4>), grid, dim3(64 * NWV), 0, st, a1, a0, dG1, dG0,
+    hipLaunchKernelGGL((lstm2_bwd_fused_kernel<BKCH, BNW, BD, BF, 4>), grid, dim3(64 * BNW), 0, st, a1, a0, dG1, dG0,
                        t1, t0, w1, wi, w0, f);
   else
-    hipLaunchKernelGGL((lstm2_bwd_fused_kernel<KCH, NWV, DPF, BF, 2>), grid, dim3(64 * NWV), 0, st, a1, a0, dG1, dG0,
+    hipLaunchKernelGGL((lstm2_bwd_fused_kernel<BKCH, BNW, BD, BF, 2>), grid, dim3(64 * BNW), 0, st, a1, a0, dG1, dG0,
                        t1, t0, w1, wi, w0, f);
 }
 
