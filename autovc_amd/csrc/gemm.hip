@@ -805,25 +805,20 @@ GemmShape pick_config(int M, int N, int K, int splits) {
   constexpr int NCFG = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
   // round 3 (whole step, alternating): cfg 9 for the big grids too, 14.80-14.83 vs
   // 14.86-14.89 ms/step with identical losses (profiles/r03/ab_gemm_bigk.txt)
-  static const int big = [] { const char* e = getenv("AVC_GEMM_BIG"); return e ? atoi(e) : 9; }();
-  static const int small = [] { const char* e = getenv("AVC_GEMM_SMALL"); return e ? atoi(e) : 8; }();
+  static_assert(NCFG > 9, "tile configurations");
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
-  if (t128 >= 512) return kCfg[big >= 0 && big < NCFG ? big : 2];
+  if (t128 >= 512) return kCfg[9];
   // deep-K outputs that fill the chip once with 128-tiles (the LSTM weight gradients,
   // 4096 x 1024 over K = B*T = 8192, on the gradient side stream): 128x128/BK32 measured
   // 17.86 vs 17.98 ms/step against 64x64 (round 2, tools/ab_gemm_bigk.sh); its 8-wave form
   // (cfg 9: 64x32 per wave, pipelined fragment reads) 14.82-14.89 vs 14.95-14.98 ms/step in
   // round 3, where these GEMMs run at the end of the replayed step with the chip to themselves
-  // (profiles/r03/ab_gemm_bigk.txt; AVC_GEMM_BIGK=<cfg id> overrides, -1 = the 64x64 path)
-  static const int bigk = [] {
-    const char* e = getenv("AVC_GEMM_BIGK");
-    return e ? atoi(e) : 9;
-  }();
-  if (bigk >= 0 && bigk < NCFG && t128 >= 256 && K >= 4096) return kCfg[bigk];
+  // (profiles/r03/ab_gemm_bigk.txt)
+  if (t128 >= 256 && K >= 4096) return kCfg[9];
   // (cfg 13 — BK 32, two k-stages in flight — for these measured slower in the step, with the
   // BLSTM weight gradients split 32 / 16 / 8 ways: profiles/r05/ab_blstm_side2.txt)
   if (splits > 1) return kCfg[3];
-  return kCfg[small >= 0 && small < NCFG ? small : 8];
+  return kCfg[8];
 }
 
 template <int BM, int BN, int BK, int WM, int WN, bool PIPE = false, bool DEEP = false>
@@ -901,9 +896,9 @@ PlanBf16 plan_bf16(int M, int N, int K, int requested) {
     while (s > 1 && K / s < 512) --s;
     // shallow K (<= 1024) cannot split its way to a full chip: one 256-row tile per CU on
     // 32-128 CUs left the encoder BLSTM projections (8192 x 128 x 512) at 25 us; the caller's
-    // split on 128 / 64 tiles fills the chip (AVC_BF16_SHALLOW=0: the old plan)
-    static const bool shallow = [] { const char* e = getenv("AVC_BF16_SHALLOW"); return !e || e[0] != '0'; }();
-    if (!(shallow && K <= 1024 && t2 * s < 256)) return {2, s};
+    // split on 128 / 64 tiles fills the chip (step 8.415-8.419 vs 8.425-8.483 ms,
+    // profiles/r05/ab_bf16_shallow.txt)
+    if (!(K <= 1024 && t2 * s < 256)) return {2, s};
   }
   return {-1, requested};
 }
@@ -1029,10 +1024,8 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
       // the weight gradients (both operands K-strided) at most 2 splits: they run on the gradient
       // side stream beside the recurrences, where half the chip for twice as long costs the
       // step less than 4-way slabs and their reduce (training step 8.53-8.55 vs 8.99-9.05 ms;
-      // 3 splits 8.67-8.68, 1 split 8.75-8.79; profiles/r05/ab_bf16_dw_splits.txt).
-      // AVC_BF16_DW_SPLITS=<n> sets the cap (0 = the plan's choice)
-      static const int dw_cap = [] { const char* e = getenv("AVC_BF16_DW_SPLITS"); return e ? atoi(e) : 2; }();
-      if (dw_cap > 0 && a_trans && b_trans) splits = std::min(splits, dw_cap);
+      // 3 splits 8.67-8.68, 1 split 8.75-8.79; profiles/r05/ab_bf16_dw_splits.txt)
+      if (a_trans && b_trans) splits = std::min(splits, 2);
     }
   }
   GemmShape cfg = bf16 ? pick_config_bf16(M, N, batch > 1 ? batch : splits) : pick_config(M, N, K, splits);
@@ -1045,13 +1038,8 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
     // the 128-tile batched case (the Winograd GEMMs): 8 waves of 64x32 with pipelined fragment
     // reads (cfg 9) — isolated 78.6 vs 88.2 us on 8 x 2048x512x512 (tools/gemm_bench.hip wino,
     // profiles/r02/gemm_wino_sweep.txt), in the step 16.465-16.485 vs 16.491-16.542 ms
-    // alternating; AVC_GEMM_BATCHED_CFG=<id> overrides
-    static const int wino_cfg = [] {
-      const char* e = getenv("AVC_GEMM_BATCHED_CFG");
-      const int v = e ? atoi(e) : 9;
-      return (v >= 0 && v < (int)(sizeof(kCfg) / sizeof(kCfg[0]))) ? v : 9;   // out of range: the default
-    }();
-    cfg = g_force_cfg >= 0 ? kCfg[g_force_cfg] : t128 >= 512 ? kCfg[wino_cfg] : kCfg[8];
+    // alternating
+    cfg = g_force_cfg >= 0 ? kCfg[g_force_cfg] : t128 >= 512 ? kCfg[9] : kCfg[8];
   }
   const int BKc = cfg.bk;
   int64_t kps = ((int64_t)K + splits - 1) / splits;

@@ -336,11 +336,8 @@ struct BwdArgs {
 // The fused backward steps run at wave priority 3 (s_setprio): beside the gradient side
 // stream's GEMM waves — older, and so ahead in the SIMD's issue arbitration at equal priority —
 // the latency-bound step's waves issue first.  fp32 step 14.30-14.35 vs 14.37-14.41 ms, bf16
-// 9.01-9.03 alike (profiles/r05/ab_lstm_prio.txt); AVC_LSTM_PRIO=0 turns it off.
-int lstm_prio() {
-  static const int on = [] { const char* e = getenv("AVC_LSTM_PRIO"); return e && e[0] == '0' ? 0 : 1; }();
-  return on;
-}
+// 9.01-9.03 alike (profiles/r05/ab_lstm_prio.txt).
+int lstm_prio() { return 1; }
 __device__ __forceinline__ void step_priority(int prio) {
   if (__builtin_amdgcn_readfirstlane(prio)) __builtin_amdgcn_s_setprio(3);
 }

@@ -83,23 +83,21 @@ def _ws(device, nbytes, slot="main"):
 # make the main stream wait before the gradients are read.  AVC_GRAD_STREAM=0 disables.
 _GRAD_STREAM_ON = os.environ.get("AVC_GRAD_STREAM", "1") != "0"
 _GRAD_STREAM_ACTIVE = [False]
-# the side stream's priority (torch: lower = higher priority; 0 = default): AVC_GRAD_PRIORITY
-_GRAD_PRIORITY = int(os.environ.get("AVC_GRAD_PRIORITY", "0"))
+# (the side stream at high priority measured 32.9 vs 14.6 ms/step, DESIGN.md §9 2a: default priority)
 _GRAD_STREAMS: dict = {}
 # LDS left free per CU for the recurrence's step workgroup (37 KB) while side GEMMs run;
 # measured per precision (bench.py, same box, alternating): fp32 21.1 ms/step with room
 # kept vs 21.9 without (round 5 again: 14.06-14.08 vs 14.16-14.20); bf16 13.1 without vs 13.3
 # with in round 2, but with round 5's 256-row side GEMMs and the BLSTM weight gradients beside
 # the recurrences the room pays there too: 7.85-7.88 vs 7.91-7.93 (profiles/r05/ab_lds_reserve_r5.txt)
-GRAD_LDS_RESERVE = {"fp32": int(os.environ.get("AVC_GRAD_LDS_RESERVE", "38912")),
-                    "bf16": int(os.environ.get("AVC_GRAD_LDS_RESERVE_BF16", "38912"))}
+GRAD_LDS_RESERVE = {"fp32": 38912, "bf16": 38912}
 
 
 def _grad_stream(dev):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     st = _GRAD_STREAMS.get(idx)
     if st is None:
-        st = torch.cuda.Stream(torch.device("cuda", idx), priority=_GRAD_PRIORITY)
+        st = torch.cuda.Stream(torch.device("cuda", idx))
         _GRAD_STREAMS[idx] = st
     return st
 
@@ -377,18 +375,18 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
 
 
 # the LSTM weight / input gradients read the backward's bf16 dG copy, and the LSTM input
-# projections / input gradients the step's bf16 W_ih copy (AVC_BF16_SRC=0: the fp32 tensors)
+# projections / input gradients the step's bf16 W_ih copy (AVC_BF16_SRC=0: the fp32 tensors;
+# the W_ih copies alone measured within noise, profiles/r05/ab_bf16_wsrc.txt, and are kept)
 _BF16_SRC = os.environ.get("AVC_BF16_SRC", "1") != "0"
-_BF16_WSRC = os.environ.get("AVC_BF16_WSRC", "1") != "0"     # the W_ih copies alone
 
 
 def _wbf16(W):
     """The step's cached bf16 copy of a 2-D LSTM weight under bf16 (None otherwise)."""
-    if (_PRECISION[0] != "bf16" or not (_BF16_SRC and _BF16_WSRC) or not _cacheable(W) or W.dim() != 2
+    if (_PRECISION[0] != "bf16" or not _BF16_SRC or not _cacheable(W) or W.dim() != 2
             or W.shape[1] % 8):
         return None
     return conv_weight(W, 6)
-_DW_MIN_BLOCKS = int(os.environ.get("AVC_DW_MIN_BLOCKS", "1024"))
+_DW_MIN_BLOCKS = 1024   # (2048 / 4096: no faster, profiles/r02/ab_dw_min_blocks.txt)
 
 
 def _splits_for(M, N, K):
@@ -473,7 +471,7 @@ def _padded_weight(W, Cop, Cip):
 
 
 _WINOGRAD = os.environ.get("AVC_WINOGRAD", "1") != "0"
-_WINO_KEEP_XT = os.environ.get("AVC_WINO_KEEP_XT", "1") != "0"
+_WINO_KEEP_XT = True   # (False transforms x again: tests/test_generator_gpu.py; r02 ab_wino_keep_xt.txt)
 
 # ---------------------------------------------------------------- step-scoped weight transforms
 # Inside weight_scope() (the Solver's forward + backward: no parameter changes until the
@@ -483,7 +481,7 @@ _WINO_KEEP_XT = os.environ.get("AVC_WINO_KEEP_XT", "1") != "0"
 # (autovc_conv_weights_batched_f32) instead of one launch per layer and pass (the encoder
 # runs twice per step, solver_encoder.py:226-236).  Outside a scope nothing is cached.
 _WSCOPE = [None]
-_WBATCH = os.environ.get("AVC_WEIGHT_BATCH", "1") != "0"
+_WBATCH = True   # (False: per-layer transforms, bit-identical; tests/test_solver_gpu.py)
 _WSHAPE = {0: lambda Co, Ci: (8, Co, Ci), 1: lambda Co, Ci: (8, Ci, Co),
            2: lambda Co, Ci: (Co, KS * Ci), 3: lambda Co, Ci: (KS * Co, Ci),
            4: lambda Co, Ci: (Co, KS * Ci), 5: lambda Co, Ci: (KS * Co, Ci),   # 4 / 5: bf16 packs
@@ -586,7 +584,7 @@ def prepare_weights(convs, lstms, T, training, B=None):
                 for kind in kinds:
                     add(kind, W)
         W = m.weight_ih_l0   # the input projection's (and input gradient's) bf16 operand (_wbf16)
-        if _bf16_rec(H) and _BF16_SRC and _BF16_WSRC and _cacheable(W) and W.shape[1] % 8 == 0:
+        if _bf16_rec(H) and _BF16_SRC and _cacheable(W) and W.shape[1] % 8 == 0:
             add(6, W)
     for conv in convs:
         W = conv.weight
@@ -729,7 +727,7 @@ class ConvBNActFn(torch.autograd.Function):
         xp = _pad_last(x, Cip)
         Wp = _padded_weight(W, Cop, Cip)
         bp = b if (b is None or Cop == Co) else _pad_last(b, Cop)
-        # the weight gradient reuses the forward's Winograd input transform (AVC_WINO_KEEP_XT=0:
+        # the weight gradient reuses the forward's Winograd input transform (_WINO_KEEP_XT False:
         # recompute it in backward)
         keep = bool(training and _WINO_KEEP_XT and ctx.needs_input_grad[1])
         y, ctx.xt = _conv_fwd(xp, Wp, bp, T, keep_xt=True) if keep else (_conv_fwd(xp, Wp, bp, T), None)
@@ -1398,8 +1396,7 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     # workgroups; 8 ways: +0.1 ms/step), 8 ways at H=512 (fills the chip: -0.15 ms); bf16
     # 4 ways with the fused steps (decoder lstm1: 8.46-8.52 vs 8.55-8.57 ms/step for 8 ways,
     # profiles/r05/ab_lstm1_splits.txt; 8 ways measured best with the launch pair, round 2).
-    # AVC_LSTM_SPLITS overrides.
-    splits = int(os.environ.get("AVC_LSTM_SPLITS", "0")) or (4 if _bf16_rec(H) else (8 if H <= 512 else 4))
+    splits = 4 if _bf16_rec(H) else (8 if H <= 512 else 4)
     # the recurrent K (4H fp32 floats, 2H bf16 pairs) must cut into multiples of 64 per split
     kdim = 2 * H if _bf16_rec(H) else 4 * H
     while splits > 1 and kdim % (64 * splits):
@@ -1645,9 +1642,6 @@ class LSTM2StackFn(torch.autograd.Function):
 # than the launch boundary it saves.
 
 
-# AVC_BLSTM_CAT=0: the encoder BLSTM's per-direction projection GEMMs (two 128-column outputs
-# forward, and a dx pair whose second GEMM accumulates)
-_BLSTM_CAT = os.environ.get("AVC_BLSTM_CAT", "1") != "0"
 # the BLSTM weight/bias gradients on the side stream (bench, alternating, one box): bf16 all of
 # them (mode 1: 8.03-8.04 vs 8.29-8.30 ms/step on the main stream; 7.98-8.00 vs 8.01-8.03 for
 # mode 2); fp32 all but the last-differentiated pass's (mode 2: 14.00-14.02 vs 14.22-14.32 on
@@ -1701,16 +1695,12 @@ class BLSTMLayerFn(torch.autograd.Function):
         G = 4 * H
         dev = x.device
         gx = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32)
-        if _BLSTM_CAT:
-            # both directions' projections as one GEMM over [W_ih_f; W_ih_b] (same sums; one
-            # 8192 x 256 output instead of two 128-column ones), reused by the backward's dx
-            Wcat = _cat_scoped(Wih_f, Wih_b)
-            gemm(B * T, 2 * G, I, x, I, 0, Wcat, I, 0, gx, 2 * G, bias1=_cat_scoped(bih_f, bih_b),
-                 bias2=_cat_scoped(bhh_f, bhh_b))
-        else:
-            Wcat = None
-            gemm(B * T, G, I, x, I, 0, Wih_f, I, 0, gx, 2 * G, bias1=bih_f, bias2=bhh_f)
-            gemm(B * T, G, I, x, I, 0, Wih_b, I, 0, gx, 2 * G, bias1=bih_b, bias2=bhh_b, c_off=G)
+        # both directions' projections as one GEMM over [W_ih_f; W_ih_b] (same sums; one 8192 x 256
+        # output instead of two 128-column ones: bf16 -0.07, fp32 -0.01 ms/step,
+        # profiles/r05/ab_bf16src_blstm_cat.txt), reused by the backward's dx
+        Wcat = _cat_scoped(Wih_f, Wih_b)
+        gemm(B * T, 2 * G, I, x, I, 0, Wcat, I, 0, gx, 2 * G, bias1=_cat_scoped(bih_f, bih_b),
+             bias2=_cat_scoped(bhh_f, bhh_b))
         h = torch.empty((B, T, 2 * H), device=dev, dtype=torch.float32)
         c = torch.empty((B, T, 2 * H), device=dev, dtype=torch.float32)
         gates = torch.empty((B, T, 2 * G), device=dev, dtype=torch.float32) if save else None
@@ -1764,11 +1754,8 @@ class BLSTMLayerFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            if Wcat is not None:   # dx = [dG_f dG_b] [W_ih_f; W_ih_b]: one K = 2G GEMM, no accumulate pass
-                gemm(M, I, 2 * G, dG, 2 * G, 0, Wcat, I, 1, dx, I)
-            else:
-                gemm(M, I, G, dG, 2 * G, 0, Wih_f, I, 1, dx, I)
-                gemm(M, I, G, dG, 2 * G, 0, Wih_b, I, 1, dx, I, a_off=G, accumulate=True)
+            # dx = [dG_f dG_b] [W_ih_f; W_ih_b]: one K = 2G GEMM, no accumulate pass
+            gemm(M, I, 2 * G, dG, 2 * G, 0, Wcat, I, 1, dx, I)
         grads[0] = dx
         return tuple(grads)
 

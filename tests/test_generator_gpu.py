@@ -139,7 +139,7 @@ def test_conv_bn_act_train_fwd_bwd(cuda, act):
 
 def test_wino_weight_grad_reuses_forward_transform_bit_exact(cuda, monkeypatch):
     """The conv weight gradient fed with the forward's Winograd input transform (default)
-    equals the one that transforms x again (AVC_WINO_KEEP_XT=0) bit for bit."""
+    equals the one that transforms x again (_WINO_KEEP_XT False) bit for bit."""
     from autovc_amd import functional as AF
     torch.manual_seed(5)
     x = torch.randn(4, 64, 512).to(cuda)

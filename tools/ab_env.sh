@@ -1,6 +1,6 @@
 #!/bin/bash
 # Alternating fp32 bench runs under environment overrides given as arguments, e.g.
-#   bash tools/ab_env.sh "AVC_GRAD_LDS_RESERVE=38912" "AVC_GRAD_LDS_RESERVE=0"
+#   bash tools/ab_env.sh "AVC_BLSTM_SIDE=1" "AVC_BLSTM_SIDE=2"
 # (commas join several variables into one configuration: "AVC_A=1,AVC_B=0")
 # Each configuration runs twice, interleaved; results in gpurun_out/ab_env.txt.
 set -o pipefail
