@@ -132,6 +132,9 @@ sig("autovc_lstm_fwd_xcd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr,
     c_ptr, c_ptr)
 sig("autovc_lstm_fwd_xcd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr,
     c_ptr)
+sig("autovc_lstm_bwd_xcd_f32", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
+sig("autovc_lstm_bwd_xcd_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+    c_ptr)
 sig("autovc_lstm2_fwd_persist_bf16", c_int, c_int, c_int, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
     c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr)
 sig("autovc_lstm_persist_workspace_bytes", c_int, c_int, c_int)

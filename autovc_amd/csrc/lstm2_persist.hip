@@ -188,6 +188,7 @@ __device__ __forceinline__ bool grid_wait(const PArgs& a, int xcc, int* status, 
 __device__ int g_avc_fault = 0;
 constexpr int kFaultLstm2Persist = 1;    // lstm_persist_kernel, two layers (decoder lstm2 forward)
 constexpr int kFaultLstmXcdFwd = 2;      // lstm_xcd_fwd_kernel (decoder lstm1 forward)
+constexpr int kFaultLstmXcdBwd = 4;      // lstm_xcd_bwd_kernel (decoder lstm1 backward)
 constexpr int kFaultLstm1Persist = 8;    // lstm_persist_kernel, one layer (opt-in)
 int g_timeout_ticks = 0;             // 0 = the default 1 s; tests force a timeout with a tiny value
 
@@ -1403,7 +1404,228 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_fwd_kernel(XArgs a) {
   }
 }
 
+// Backward of the same layer (BPTT, reverse time), same XCD split, in one launch: slot s of
+// XCD x owns units 16s .. 16s+15 of batch rows 8x .. 8x+7 — the cells whose gate gradients
+// it writes and the 16 columns of dh_rec(t) = dG_{t+1} W_hh (K = 4H = 2048) it reduces.
+// W_hh's 16 columns stay in registers as MFMA A fragments (from the (H, 4H) transpose the
+// per-step path reads too); each wave takes a quarter of K and stages its slice of the
+// group's 8 dG_{t+1} rows (written by the XCD's 32 slots into its L2) through LDS with
+// coalesced sc1 loads, the 4 partial tiles are summed in LDS in fixed order, then the cell
+// math of lstm.hip pw_finish.  BF: the product on the bf16 copies (autovc_lstm_bwd_bf16's
+// numerics: RNE W_hh^T and dG, fp32 accumulation) — the exchange moves the bf16 dG rows
+// (half the bytes), 16 MFMAs per wave per step instead of 128.
+// (Round 3 measured the fp32 form alone at 4.2 vs 9.3 us per step but slower in the training
+// step of that schedule; profiles/r06/ab_lstm1_xcd_bwd.txt re-measures it in this one.)
+struct XBArgs {
+  int B, T;
+  const float* dh;           // dh_out (b*d_ldb + t*d_ldt), may be null
+  int64_t d_ldb, d_ldt;
+  const float* gates;        // (B,T,4H) i, f, g, o
+  const float* c;            // (B,T,H)
+  const float* WT;           // W_hh^T (H, 4H) fp32
+  const __bf16* WTb;         // its RNE bf16 copy (BF)
+  float* dG;                 // (B,T,4H)
+  __bf16* dGb;               // (B,T,4H) bf16 copy (BF: required, the exchanged operand)
+  int* bar;
+  int timeout_ticks;
+};
+
+template <int HH, bool BF>
+__global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
+  constexpr int U = HH / XSL;            // units per slot (16)
+  constexpr int K4 = 4 * HH;             // recurrent K
+  constexpr int KW = K4 / 4;             // k per wave
+  constexpr int KG = KW / 4;             // k per MFMA lane group (consecutive)
+  static_assert(U == 16, "tile shape");
+  constexpr int SS = BF ? KW + 8 : KW + 4;   // slab row stride in elements (bank spread)
+  using E = typename std::conditional<BF, __bf16, float>::type;
+  static_assert(4 * U * (XRB + 1) * 4 + 4 * (XRB + 1) * SS * (int)sizeof(E) <= XC_PAD_LDS, "LDS budget");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* part = lds;                      // [4 waves][U][XRB + 1]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  E* slab = reinterpret_cast<E*>(lds + 4 * U * (XRB + 1)) + wave * (XRB + 1) * SS;   // row XRB = 0
+  __shared__ int s_info[3];
+  const int T = a.T;
+  if (tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    const int xcc = (int)(x & 15);
+    const int slot = add_rlx(a.bar + (XC_CENSUS + xcc) * L, 1);
+    s_info[0] = xcc;
+    s_info[1] = slot;
+    s_info[2] = (xcc < XNX && slot < XSL) ? 0 : 1;
+    if (s_info[2]) st_rlx(a.bar + XC_ERR * L, 1);
+  }
+  for (int i = lane; i < SS; i += 64) slab[XRB * SS + i] = (E)0.f;
+  __syncthreads();
+  const int xcc = s_info[0] < XNX ? s_info[0] : 0, slot = s_info[1] < XSL ? s_info[1] : 0;
+  const int r0 = XRB * xcc, u0 = U * slot;
+  const int cb = tid >> 4, cu = tid & 15;
+  const bool cown = tid < XRB * U;
+  const int64_t cell0 = (int64_t)(r0 + cb) * T;     // (b, t) row base of this cell's batch row
+  auto fail = [&]() {
+    const float nan = __builtin_nanf("");
+    if (cown)
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a.dG[(cell0 + t) * K4 + q * HH + u0 + cu] = nan;
+          if (a.dGb) a.dGb[(cell0 + t) * K4 + q * HH + u0 + cu] = (__bf16)nan;
+        }
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdBwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (s_info[2]) {
+    if (s_info[0] < XNX && s_info[1] < XSL) fail();
+    if (tid == 0) __hip_atomic_fetch_or(&g_avc_fault, kFaultLstmXcdBwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // A fragments: lane -> unit u0 + lane % 16, k = KW wave + KG (lane / 16) + q (B alike)
+  const int kbase = KW * wave + KG * (lane >> 4);
+  float wf[BF ? 1 : KG];
+  bf16x8 wb[BF ? KG / 8 : 1];
+  if constexpr (BF) {
+    const __bf16* src = a.WTb + (int64_t)(u0 + (lane & 15)) * K4 + kbase;
+#pragma unroll
+    for (int q = 0; q < KG / 8; ++q) wb[q] = *reinterpret_cast<const bf16x8*>(src + 8 * q);
+  } else {
+    const float* src = a.WT + (int64_t)(u0 + (lane & 15)) * K4 + kbase;
+#pragma unroll
+    for (int q = 0; q < KG; q += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + q);
+      wf[q] = v[0]; wf[q + 1] = v[1]; wf[q + 2] = v[2]; wf[q + 3] = v[3];
+    }
+  }
+  const bool bvalid = (lane & 15) < XRB;
+  const E* brow = slab + (bvalid ? (lane & 15) : XRB) * SS + KG * (lane >> 4);
+  // pointwise operands of step t (prefetched one step ahead)
+  f32x4 gt = {0.f, 0.f, 0.f, 0.f};
+  float cc = 0.f, cpv = 0.f, dho = 0.f, dcs = 0.f;
+  auto load_pw = [&](int t) {
+    const float* g = a.gates + (cell0 + t) * K4 + u0 + cu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gt[q] = g[q * HH];
+    cc = a.c[(cell0 + t) * HH + u0 + cu];
+    cpv = t > 0 ? a.c[(cell0 + t - 1) * HH + u0 + cu] : 0.f;
+    dho = a.dh ? a.dh[(int64_t)(r0 + cb) * a.d_ldb + (int64_t)t * a.d_ldt + u0 + cu] : 0.f;
+  };
+  if (cown) load_pw(T - 1);
+  int* step_ctr = a.bar + (XC_STEP + xcc) * L;
+  for (int s = 0; s < T; ++s) {
+    const int t = T - 1 - s;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      // ---- XCD barrier: all 32 slots stored dG_{t+1}
+      if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        while (ld_rlx(step_ctr) < XSL * s) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout_ticks || ld_rlx(a.bar + XC_ERR * L)) {
+            st_rlx(a.bar + XC_ERR * L, 1);
+            ok = 0;
+            break;
+          }
+        }
+        s_info[2] = ok ? 0 : 1;
+      }
+      __syncthreads();
+      if (s_info[2]) {
+        fail();
+        return;
+      }
+      // ---- this wave's K quarter of the group's dG_{t+1} rows -> its LDS slab: coalesced sc1
+      // loads (whole lines per instruction: L1 is bypassed, so scattered fragment loads would
+      // re-fetch every line), then the products dh_rec = dG_{t+1} W_hh from LDS
+      {
+        constexpr int CPR = KW * (int)sizeof(E) / 16;    // 16-B chunks per row slice
+        constexpr int NL = XRB * CPR / 64;               // b128 loads per lane
+        const void* base = BF ? (const void*)(a.dGb + ((int64_t)r0 * T + t + 1) * K4 + KW * wave)
+                              : (const void*)(a.dG + ((int64_t)r0 * T + t + 1) * K4 + KW * wave);
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+        f32x4 v[NL];
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          const int ci = i * 64 + lane, row = ci / CPR, k16 = ci % CPR;
+          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               r, (uint32_t)((int64_t)row * T * K4 * (int)sizeof(E) + 16 * k16), 0,
+                                               16));
+        }
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          const int ci = i * 64 + lane, row = ci / CPR, k16 = ci % CPR;
+          *reinterpret_cast<f32x4*>(slab + row * SS + k16 * (16 / (int)sizeof(E))) = v[i];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if constexpr (BF) {
+#pragma unroll
+        for (int q = 0; q < KG / 8; ++q)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[q], *reinterpret_cast<const bf16x8*>(brow + 8 * q), acc, 0,
+                                                        0, 0);
+      } else {
+#pragma unroll
+        for (int q = 0; q < KG; q += 4) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + q);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q], bv[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 1], bv[1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 2], bv[2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 3], bv[3], acc, 0, 0, 0);
+        }
+      }
+    }
+    // C[unit 4 (lane / 16) + r][batch lane % 16]: the 4 waves' K quarters, summed in order
+    if (bvalid)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[(wave * U + 4 * (lane >> 4) + r) * (XRB + 1) + (lane & 15)] = acc[r];
+    __syncthreads();
+    float dgo[4];
+    if (cown) {
+#pragma clang fp contract(off)
+      const float dh = dho + (((part[(0 * U + cu) * (XRB + 1) + cb] + part[(1 * U + cu) * (XRB + 1) + cb]) +
+                               part[(2 * U + cu) * (XRB + 1) + cb]) + part[(3 * U + cu) * (XRB + 1) + cb]);
+      const float i_ = gt[0], f_ = gt[1], g_ = gt[2], o_ = gt[3];
+      const float tc = tanhf(cc);
+      const float dc = dcs + dh * o_ * (1.f - tc * tc);
+      dgo[0] = dc * g_ * i_ * (1.f - i_);
+      dgo[1] = dc * cpv * f_ * (1.f - f_);
+      dgo[2] = dc * i_ * (1.f - g_ * g_);
+      dgo[3] = dh * tc * o_ * (1.f - o_);
+      dcs = dc * f_;
+      // the exchanged copy first (fp32: dG, BF: dGb); the other after the arrive
+      if constexpr (BF) {
+        __bf16* db = a.dGb + (cell0 + t) * K4 + u0 + cu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) db[q * HH] = (__bf16)dgo[q];
+      } else {
+        float* d = a.dG + (cell0 + t) * K4 + u0 + cu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q * HH] = dgo[q];
+      }
+    }
+    if (s + 1 < T) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) add_l2(step_ctr, 1);
+    }
+    if (cown) {
+      if constexpr (BF) {
+        float* d = a.dG + (cell0 + t) * K4 + u0 + cu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q * HH] = dgo[q];
+      }
+      if (s + 1 < T) load_pw(t - 1);
+    }
+  }
+}
+
 int g_xcd_ok = -1;
+// dynamic LDS of the backward launch (A/B: AVC_XCD_BWD_LDS bytes; default the forward's pad)
+int xcd_bwd_lds() {
+  static const int v = [] { const char* e = getenv("AVC_XCD_BWD_LDS"); return e ? atoi(e) : XC_PAD_LDS; }();
+  return v;
+}
 
 bool xcd_fits() {
   if (g_xcd_ok < 0) {
@@ -1417,6 +1639,13 @@ bool xcd_fits() {
                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_fwd_kernel<512, false>, XNT, lb) == hipSuccess &&
                per >= 1 &&
                hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_fwd_kernel<512, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_bwd_kernel<512, false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess &&
+               hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lstm_xcd_bwd_kernel<512, false>, XNT, lb) ==
+                   hipSuccess &&
+               per >= 1 &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_xcd_bwd_kernel<512, true>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, lb) == hipSuccess;
   }
   return g_xcd_ok == 1;
@@ -1467,6 +1696,46 @@ extern "C" int autovc_lstm_fwd_xcd_bf16(int B, int T, int H, const float* gx, in
   a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
   AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
   hipLaunchKernelGGL((lstm_xcd_fwd_kernel<512, true>), dim3(XNX * XSL), dim3(XNT), XC_PAD_LDS, stream, a);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm_bwd_xcd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                                       const float* gates, const float* c_all, const float* WT, float* dG,
+                                       void* workspace, hipStream_t stream) {
+  static const char* fn = "autovc_lstm_bwd_xcd_f32";
+  AVC_CHECK_ARG(T > 0 && autovc_lstm_xcd_supported(B, H),
+                "%s: unsupported shape B=%d H=%d on this device (needs B=64, H=512, 8 XCDs x 32 CUs)", fn, B, H);
+  AVC_CHECK_ARG(gates && c_all && WT && dG && workspace, "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(WT) && AVC_ALIGNED16(dG) && AVC_ALIGNED16(workspace),
+                "%s: WT / dG / workspace must be 16-byte aligned", fn);
+  XBArgs a;
+  a.B = B; a.T = T; a.dh = dh_out; a.d_ldb = d_ldb; a.d_ldt = d_ldt; a.gates = gates; a.c = c_all;
+  a.WT = WT; a.WTb = nullptr; a.dG = dG; a.dGb = nullptr;
+  a.bar = static_cast<int*>(workspace);
+  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
+  AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
+  hipLaunchKernelGGL((lstm_xcd_bwd_kernel<512, false>), dim3(XNX * XSL), dim3(XNT), xcd_bwd_lds(), stream, a);
+  AVC_CHECK_LAUNCH(fn);
+  return avc::kOk;
+}
+
+extern "C" int autovc_lstm_bwd_xcd_bf16(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                                        const float* gates, const float* c_all, const uint16_t* WT_b, float* dG,
+                                        uint16_t* dGb, void* workspace, hipStream_t stream) {
+  static const char* fn = "autovc_lstm_bwd_xcd_bf16";
+  AVC_CHECK_ARG(T > 0 && autovc_lstm_xcd_supported(B, H),
+                "%s: unsupported shape B=%d H=%d on this device (needs B=64, H=512, 8 XCDs x 32 CUs)", fn, B, H);
+  AVC_CHECK_ARG(gates && c_all && WT_b && dG && dGb && workspace, "%s: null pointer", fn);
+  AVC_CHECK_ARG(AVC_ALIGNED16(WT_b) && AVC_ALIGNED16(dGb) && AVC_ALIGNED16(workspace),
+                "%s: WT_b / dGb / workspace must be 16-byte aligned", fn);
+  XBArgs a;
+  a.B = B; a.T = T; a.dh = dh_out; a.d_ldb = d_ldb; a.d_ldt = d_ldt; a.gates = gates; a.c = c_all;
+  a.WT = nullptr; a.WTb = reinterpret_cast<const __bf16*>(WT_b); a.dG = dG; a.dGb = reinterpret_cast<__bf16*>(dGb);
+  a.bar = static_cast<int*>(workspace);
+  a.timeout_ticks = g_timeout_ticks > 0 ? g_timeout_ticks : 100000000;
+  AVC_HIP(avc::zero_async(workspace, XC_BYTES, stream), fn);
+  hipLaunchKernelGGL((lstm_xcd_bwd_kernel<512, true>), dim3(XNX * XSL), dim3(XNT), xcd_bwd_lds(), stream, a);
   AVC_CHECK_LAUNCH(fn);
   return avc::kOk;
 }

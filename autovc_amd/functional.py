@@ -93,17 +93,24 @@ _GRAD_STREAMS: dict = {}
 GRAD_LDS_RESERVE = {"fp32": 38912, "bf16": 38912}
 
 
-def _grad_stream(dev):
+def _grad_stream(dev, k=0):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    st = _GRAD_STREAMS.get(idx)
+    st = _GRAD_STREAMS.get((idx, k))
     if st is None:
         st = torch.cuda.Stream(torch.device("cuda", idx))
-        _GRAD_STREAMS[idx] = st
+        _GRAD_STREAMS[(idx, k)] = st
     return st
 
 
+# A/B (round 6): consecutive flushes alternate over this many side streams; AVC_JOIN_MAIN=1
+# runs the batch still queued at the join on the main stream
+_SIDE_STREAMS = int(os.environ.get("AVC_SIDE_STREAMS", "1"))
+_JOIN_MAIN = os.environ.get("AVC_JOIN_MAIN", "0") == "1"
+_FLUSHES = [0]
+
+
 _GRAD_QUEUE: list = []
-_GRAD_PENDING: set = set()   # device indices whose side stream has work not yet joined
+_GRAD_PENDING: set = set()   # (device index, k) of side streams with work not yet joined
 
 
 def _grad_launch(dev, outs, fn, *inputs):
@@ -182,13 +189,15 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
     _GRAD_QUEUE.clear()
     dev = items[0][0]
     main = torch.cuda.current_stream(dev)
-    side = _grad_stream(dev)
+    k = _FLUSHES[0] % _SIDE_STREAMS
+    _FLUSHES[0] += 1
+    side = _grad_stream(dev, k)
     if after is not None:
         side.wait_event(after)
     else:
         side.wait_stream(main)
     _GRAD_STREAM_ACTIVE[0] = True
-    _GRAD_PENDING.add(side.device.index)
+    _GRAD_PENDING.add((side.device.index, k))
     prev_prec = _PRECISION[0]
     _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0)
     try:
@@ -217,18 +226,31 @@ def join_grad_stream(dev=None):
     stream (before anything reads the gradients).  (Running the batch still queued here on the
     idle main stream instead measured fp32 13.93-13.98 vs 13.94, bf16 7.87-7.92 vs 7.81-7.85
     ms/step: profiles/r06/ab_join_{fp32,bf16}.txt.)"""
+    if _JOIN_MAIN and _GRAD_QUEUE:
+        items = list(_GRAD_QUEUE)
+        _GRAD_QUEUE.clear()
+        prev = _PRECISION[0]
+        try:
+            for d, fn, inputs, prec, outs in items:
+                _PRECISION[0] = prec
+                _main_grad(d, outs, fn, *inputs)
+                if MARKS.active:
+                    for o in outs:
+                        MARKS.log(o.buf, GradMarks.FINAL)
+        finally:
+            _PRECISION[0] = prev
     _flush_grad_queue(beside_recurrence=False)
     _SIDE_WRITES.clear()
+    _FLUSHES[0] = 0
     if not _GRAD_PENDING:
         return
     dev = dev or torch.device("cuda", torch.cuda.current_device())
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    st = _GRAD_STREAMS.get(idx)
-    if st is not None and idx in _GRAD_PENDING:
+    for key in sorted(k for k in _GRAD_PENDING if k[0] == idx):
         # only a side stream with work since the last join is waited on: inside a graph
         # capture (autovc_amd.graph) the wait must be on work of the same capture
-        torch.cuda.current_stream(dev).wait_stream(st)
-        _GRAD_PENDING.discard(idx)
+        torch.cuda.current_stream(dev).wait_stream(_GRAD_STREAMS[key])
+        _GRAD_PENDING.discard(key)
 
 
 class GradMarks:
@@ -1397,12 +1419,35 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     # 4 ways with the fused steps (decoder lstm1: 8.46-8.52 vs 8.55-8.57 ms/step for 8 ways,
     # profiles/r05/ab_lstm1_splits.txt; 8 ways measured best with the launch pair, round 2).
     splits = 4 if _bf16_rec(H) else (8 if H <= 512 else 4)
+    if os.environ.get("AVC_LSTM1_SPLITS"):
+        splits = int(os.environ["AVC_LSTM1_SPLITS"])
     # the recurrent K (4H fp32 floats, 2H bf16 pairs) must cut into multiples of 64 per split
     kdim = 2 * H if _bf16_rec(H) else 4 * H
     while splits > 1 and kdim % (64 * splits):
         splits //= 2
-    ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
+    if lstm_xcd(B, H) and _XCD_BWD_ON:
+        # one XCD-local persistent launch (csrc/lstm2_persist.hip lstm_xcd_bwd_kernel)
+        ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmxb")
+        mark = _grad_mark(dev)
+        if _bf16_rec(H):
+            dGb = torch.empty((B, T, 4 * H), device=dev, dtype=torch.bfloat16)
+            _lib.call("autovc_lstm_bwd_xcd_bf16", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
+                      WT.data_ptr(), dG.data_ptr(), dGb.data_ptr(), ws, _s())
+        else:
+            _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
+                      WT.data_ptr(), dG.data_ptr(), ws, _s())
+        if _XCD_BWD_RESERVE is not None:
+            saved = dict(GRAD_LDS_RESERVE)
+            GRAD_LDS_RESERVE.update({k: _XCD_BWD_RESERVE for k in GRAD_LDS_RESERVE})
+            try:
+                _flush_grad_queue(after=mark)
+            finally:
+                GRAD_LDS_RESERVE.update(saved)
+        else:
+            _flush_grad_queue(after=mark)
+        return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=dGb if _bf16_rec(H) else None)
+    ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     # (keeping the batch past this recurrence, to run beside the encoder BLSTMs instead,
     # measured slower: bf16 9.06-9.07 vs 9.03, fp32 15.62-15.64 vs 14.41-14.46 ms,
     # profiles/r05/ab_grad_defer.txt)
@@ -1478,6 +1523,7 @@ class DeviceFault(RuntimeError):
 _FAULT_BITS = (
     (1, "lstm_persist_kernel / lstm2_rs_kernel, two layers (decoder lstm2 forward)", "h/c", "AVC_LSTM2_PERSIST=0"),
     (2, "lstm_xcd_fwd_kernel (decoder lstm1 forward)", "h/c", "AVC_LSTM_XCD=0"),
+    (4, "lstm_xcd_bwd_kernel (decoder lstm1 backward)", "gate gradients", "AVC_LSTM_XCD_BWD=0"),
     (8, "lstm_persist_kernel, one layer (decoder lstm1 forward)", "h/c", "AVC_LSTM_PERSIST=0"),
 )
 
@@ -1517,9 +1563,11 @@ _XCD_ON = os.environ.get("AVC_LSTM_XCD", "1") != "0"
 
 
 # The backward the same way (lstm_xcd_bwd_kernel: 4.2 vs 9.3 us per step alone) lost inside
-# the training step, where the split-K launches' idle CUs host queued weight-gradient GEMMs
-# (15.91-16.93 vs 15.65 ms/step, profiles/r03/ab_lstm_xcd.txt): retired to
-# tools/retired/ (round 5), the fused split-K backward step is the product path.
+# the round-3 training step, where the split-K launches' idle CUs host queued weight-gradient
+# GEMMs (15.91-16.93 vs 15.65 ms/step, profiles/r03/ab_lstm_xcd.txt); round 6 re-measures it
+# (fp32 and bf16) in the current schedule: AVC_LSTM_XCD_BWD=1 selects it.
+_XCD_BWD_ON = os.environ.get("AVC_LSTM_XCD_BWD", "0") != "0"
+_XCD_BWD_RESERVE = int(os.environ["AVC_XCD_BWD_RESERVE"]) if "AVC_XCD_BWD_RESERVE" in os.environ else None
 
 
 def lstm_xcd(B, H):

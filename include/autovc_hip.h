@@ -392,6 +392,19 @@ int autovc_lstm_fwd_xcd_f32(int B, int T, int H, const float* gx, int64_t gx_ldb
 int autovc_lstm_fwd_xcd_bf16(int B, int T, int H, const float* gx, int64_t gx_ldb, int64_t gx_ldt,
                              const uint16_t* W_hh_b, float* h, int64_t h_ldb, int64_t h_ldt, float* c_all,
                              float* gates, void* workspace, hipStream_t stream);
+/* The same layer's backward (BPTT, model_vc_mel.py:90,111 under autograd) as one XCD-local
+ * launch: arguments and outputs of autovc_lstm_bwd_f32 (WT = W_hh^T (H, 4H), dG (B,T,4H))
+ * without its split count / workspace, plus the autovc_lstm_xcd_workspace_bytes() workspace.
+ * Per step only the group's 8 rows of dG_{t+1} move, through the XCD's L2.  The bf16 form
+ * is autovc_lstm_bwd_bf16's numerics (RNE bf16 W_hh^T and dG in the product, fp32 cell
+ * math) and writes dGb, the bf16 copy of dG, which it also exchanges.  Same shapes and
+ * fault path as the forward. */
+int autovc_lstm_bwd_xcd_f32(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                            const float* gates, const float* c_all, const float* WT, float* dG,
+                            void* workspace, hipStream_t stream);
+int autovc_lstm_bwd_xcd_bf16(int B, int T, int H, const float* dh_out, int64_t d_ldb, int64_t d_ldt,
+                             const float* gates, const float* c_all, const uint16_t* WT_b, float* dG,
+                             uint16_t* dGb, void* workspace, hipStream_t stream);
 /* Co-residency failures reach the caller without a per-call sync: a persistent launch
  * whose grid barrier timed out writes NaN over the h / c it owns (so the loss turns NaN)
  * and sets bit 0 of a sticky per-device fault word.  autovc_fault_status (synchronises

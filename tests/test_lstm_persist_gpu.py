@@ -333,3 +333,101 @@ def test_xcd_local_lstm_bf16_matches_bf16_per_step_launches(cuda, T):
         d = (a.double() - r.double()).abs()
         assert d.max().item() < 2e-2 * max(r.abs().max().item(), 1e-30), (name, d.max().item())
         assert d.mean().item() < 1e-4 * max(r.abs().max().item(), 1e-30), (name, d.mean().item())
+
+
+def _bwd_inputs(B, T, H, dev, seed):
+    gx, W, _, _ = _inputs(B, T, H, dev, seed=seed)
+    _, c, g = _run1("autovc_lstm_fwd_f32", B, T, H, gx, W[0], dev)
+    dh = (torch.randn(B, T, H, generator=torch.Generator().manual_seed(seed + 1)) * 0.1).to(dev)
+    return W[0], c, g, dh
+
+
+@pytest.mark.parametrize("T", [1, 2, 128])
+def test_xcd_local_lstm_backward_matches_split_k_launches(cuda, T):
+    """Decoder lstm1 backward as one XCD-local persistent launch (autovc_lstm_bwd_xcd_f32)
+    against the per-step split-K launches (autovc_lstm_bwd_f32) on the same W_hh^T: dG within
+    fp32 summation-order noise (relative to its max), a second call bit-identical, no fault."""
+    from autovc_amd import _lib, functional as AF
+    if not _xcd_supported():
+        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
+    B, H = 64, 512
+    AF.check_device_faults(cuda)
+    W, c, g, dh = _bwd_inputs(B, T, H, cuda, 11)
+    WT = W.t().contiguous()
+    st = _lib.stream_ptr(cuda)
+    ref = torch.full((B, T, 4 * H), float("nan"), device=cuda)
+    ws = torch.empty(4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, 8), dtype=torch.uint8, device=cuda)
+    _lib.call("autovc_lstm_bwd_f32", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(), WT.data_ptr(),
+              ref.data_ptr(), 0, 8, ws.data_ptr(), st)
+    wx = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
+    outs = []
+    for _ in range(2):
+        got = torch.full((B, T, 4 * H), float("nan"), device=cuda)
+        _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(),
+                  WT.data_ptr(), got.data_ptr(), wx.data_ptr(), st)
+        torch.cuda.synchronize()
+        outs.append(got)
+    AF.check_device_faults(cuda)
+    assert bool(torch.isfinite(outs[0]).all())
+    err = (outs[0].double() - ref.double()).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-5, err
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("T", [3, 128])
+def test_xcd_local_lstm_backward_bf16_matches_bf16_launches(cuda, T):
+    """autovc_lstm_bwd_xcd_bf16 against the per-step bf16 backward (autovc_lstm_bwd_bf16):
+    the same RNE bf16 W_hh^T and dG copies in the product, fp32 accumulation in another
+    order; dG and its bf16 copy dGb both compared, dGb = RNE(dG) exactly."""
+    from autovc_amd import _lib
+    if not _xcd_supported():
+        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
+    B, H = 64, 512
+    W, c, g, dh = _bwd_inputs(B, T, H, cuda, 17)
+    WTb = W.t().contiguous().bfloat16()
+    st = _lib.stream_ptr(cuda)
+    outs = []
+    for xcd in (False, True):
+        dG = torch.full((B, T, 4 * H), float("nan"), device=cuda)
+        dGb = torch.full((B, T, 4 * H), float("nan"), device=cuda, dtype=torch.bfloat16)
+        if xcd:
+            ws = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
+            _lib.call("autovc_lstm_bwd_xcd_bf16", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(),
+                      WTb.data_ptr(), dG.data_ptr(), dGb.data_ptr(), ws.data_ptr(), st)
+        else:
+            ws = torch.empty(4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, 4), dtype=torch.uint8,
+                             device=cuda)
+            _lib.call("autovc_lstm_bwd_bf16", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(),
+                      WTb.data_ptr(), dG.data_ptr(), dGb.data_ptr(), 0, 4, ws.data_ptr(), st)
+        torch.cuda.synchronize()
+        outs.append((dG, dGb))
+    (r, rb), (a, ab) = outs
+    assert bool(torch.isfinite(a).all())
+    assert torch.equal(ab, a.bfloat16())
+    d = (a.double() - r.double()).abs()
+    scale = r.abs().max().item()
+    assert d.max().item() < 2e-2 * scale, d.max().item()
+    assert d.mean().item() < 1e-4 * scale, d.mean().item()
+
+
+def test_xcd_local_lstm_backward_timeout_surfaces(cuda):
+    """A backward group that times out writes NaN over its dG and names its own kernel."""
+    from autovc_amd import _lib, functional as AF
+    if not _xcd_supported():
+        pytest.skip("XCD-local LSTM needs 8 XCDs x 32 CUs")
+    B, H, T = 64, 512, 16
+    AF.check_device_faults(cuda)
+    W, c, g, dh = _bwd_inputs(B, T, H, cuda, 11)
+    WT = W.t().contiguous()
+    dG = torch.zeros(B, T, 4 * H, device=cuda)
+    wx = torch.empty(_lib.load().autovc_lstm_xcd_workspace_bytes(), dtype=torch.uint8, device=cuda)
+    _lib.call("autovc_lstm_persist_set_timeout_ticks", 1)
+    try:
+        _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, g.data_ptr(), c.data_ptr(),
+                  WT.data_ptr(), dG.data_ptr(), wx.data_ptr(), _lib.stream_ptr(cuda))
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("autovc_lstm_persist_set_timeout_ticks", 0)
+    assert bool(torch.isnan(dG).any())
+    with pytest.raises(AF.DeviceFault, match="lstm_xcd_bwd_kernel.*AVC_LSTM_XCD_BWD=0"):
+        AF.check_device_faults(cuda)

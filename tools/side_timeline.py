@@ -76,15 +76,17 @@ def install():
         AF._GRAD_QUEUE.clear()
         dev = items[0][0]
         main = torch.cuda.current_stream(dev)
-        side = AF._grad_stream(dev)
+        k = AF._FLUSHES[0] % AF._SIDE_STREAMS
+        AF._FLUSHES[0] += 1
+        side = AF._grad_stream(dev, k)
         if after is not None:
             side.wait_event(after)
         else:
             side.wait_stream(main)
-        tag = f"side{nrec[0]}.{nfl[0]}" if beside_recurrence else "side_final"
+        tag = (f"side{nrec[0]}.{nfl[0]}" if beside_recurrence else "side_final") + (f"@{k}" if k else "")
         stamp(f"{tag}_begin(n={len(items)})", side)
         AF._GRAD_STREAM_ACTIVE[0] = True
-        AF._GRAD_PENDING.add(side.device.index)
+        AF._GRAD_PENDING.add((side.device.index, k))
         prev = AF._PRECISION[0]
         _lib.call("autovc_gemm_set_lds_reserve", AF.GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0)
         try:
