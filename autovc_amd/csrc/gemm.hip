@@ -298,6 +298,32 @@ struct OpTile {
     else if (act == 2) store_bf16_kr_act<SET, 2>(lds, cl);
     else store_bf16_kr_act<SET, 0>(lds, cl);
   }
+  // fp32 as three bf16 planes (X6 mode of gemm_bf16_kernel): hi = RNE(x), mid = RNE(x - hi),
+  // lo = RNE(x - hi - mid).  Both differences are exact in fp32, and x - hi - mid has at most
+  // 8 significant bits, so hi + mid + lo == x exactly (normal numbers).  Images `pe` elements
+  // apart; RK: [row][LDB], CK: [k][LDK].
+  template <int LDB, int SET = 0>
+  __device__ __forceinline__ void store_x3(__bf16* lds, int pe) const {
+    static_assert(EB == 4, "the split needs fp32 operands");
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int r, k;
+      coords(i, r, k);
+      const f32x4 x = SET ? v2[i] : v[i];
+      bf16x4 hi, mid, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = (__bf16)x[e];
+        const float r1 = x[e] - (float)hi[e];
+        mid[e] = (__bf16)r1;
+        lo[e] = (__bf16)(r1 - (float)mid[e]);
+      }
+      __bf16* d = lds + (RK ? r * LDB + k : k * (ROWS + 32) + r);
+      *reinterpret_cast<bf16x4*>(d) = hi;
+      *reinterpret_cast<bf16x4*>(d + pe) = mid;
+      *reinterpret_cast<bf16x4*>(d + 2 * pe) = lo;
+    }
+  }
   // fragment values of MFMAs p = 4g .. 4g+3 (k = h*BK/2 + p) for tile row `row`
   __device__ __forceinline__ f32x4 frag4(const float* lds, int row, int h, int g) const {
     if (RK) return *reinterpret_cast<const f32x4*>(lds + row * LD + h * (BK / 2) + 4 * g);
@@ -489,7 +515,16 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_kernel(
 // applied on load (Opnd::coef / act).
 // SRC: bit 0 = A, bit 1 = B is held in memory as bf16 (ld in bf16 elements; conv channel
 // counts multiples of 8).
-template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool DEEP = false, int BNOP = 0, int SRC = 0>
+// X6 (precision "fp32", the fp32 GEMMs on bf16 MFMA): each fp32 operand is staged as its three
+// bf16 planes (OpTile::store_x3) and the product a*b = (ah + am + al)(bh + bm + bl) is taken
+// as ah*bh into one accumulator and ah*bm + am*bh + ah*bl + al*bh + am*bm into a second; the
+// three dropped terms (am*bl, al*bm, al*bl) are below 2^-24 |a b|, and bf16 x bf16 products
+// are exact in fp32.  The small terms sum at their own magnitude, so adding the two
+// accumulators once at the end leaves the rounding of a plain fp32 accumulation
+// (tests/test_gemm_x6_gpu.py: error against fp64 within that of gemm_kernel).  Six
+// 32x32x16 bf16 MFMAs do the work of 8 fp32 32x32x2 MFMAs at 16x their rate.
+template <int BM, int BN, int BK, int WM, int WN, bool A_RK, bool B_RK, bool DEEP = false, int BNOP = 0, int SRC = 0,
+          bool X6 = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     int M, int N, int K, Opnd A, Opnd B, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias1, const float* __restrict__ bias2, int accumulate,
@@ -512,8 +547,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   using TBt = OpTile<B_RK, BN, BK, NT, (SRC & 2) ? 2 : 4>;
   // RK operands: [row][BK + 8] images read with ds_read_b128; CK operands: [k][rows + 32]
   // images read with ds_read_b64_tr_b16
-  constexpr int A_EL = A_RK ? BM * LDB : BK * TA::LDK;
-  constexpr int B_EL = B_RK ? BN * LDB : BK * TBt::LDK;
+  constexpr int A_EL1 = A_RK ? BM * LDB : BK * TA::LDK;
+  constexpr int B_EL1 = B_RK ? BN * LDB : BK * TBt::LDK;
+  constexpr int NPL = X6 ? 3 : 1;                  // planes per operand image
+  constexpr int A_EL = NPL * A_EL1, B_EL = NPL * B_EL1;
+  static_assert(!X6 || (BNOP == 0 && SRC == 0), "X6: fp32 operands");
   __shared__ __attribute__((aligned(16))) __bf16 smem[2][A_EL + B_EL];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -533,24 +571,42 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   const int nk = (int)((kend - kbeg + BK - 1) / BK);
 
   f32x16 acc[TI][TJ];
+  f32x16 acs[X6 ? TI : 1][X6 ? TJ : 1];            // X6: the small terms
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if constexpr (X6)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acs[i][j][r] = 0.f;
 
   TA sa;
   TBt sb;
   sa.init(A, m0, kbeg, M);
   sb.init(B, n0, kbeg, N);
   auto stage = [&](__bf16* img) {
+    if constexpr (X6) {
+      sa.template store_x3<LDB>(img, A_EL1);
+      sb.template store_x3<LDB>(img + A_EL, B_EL1);
+      return;
+    }
     if constexpr (A_RK) sa.template store_bf16<LDB, 0, ABN>(img, A.act, cl);
     else sa.template store_bf16_kr<0, ABN>(img, A.act, cl);
     if constexpr (B_RK) sb.template store_bf16<LDB, 0, BBN>(img + A_EL, B.act, cl);
     else sb.template store_bf16_kr<0, BBN>(img + A_EL, B.act, cl);
   };
   auto stage2 = [&](__bf16* img) {   // from the second staging set
+    if constexpr (X6) {
+      sa.template store_x3<LDB, 1>(img, A_EL1);
+      sb.template store_x3<LDB, 1>(img + A_EL, B_EL1);
+      return;
+    }
     if constexpr (A_RK) sa.template store_bf16<LDB, 1, ABN>(img, A.act, cl);
     else sa.template store_bf16_kr<1, ABN>(img, A.act, cl);
     if constexpr (B_RK) sb.template store_bf16<LDB, 1, BBN>(img + A_EL, B.act, cl);
@@ -585,6 +641,37 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
   };
   auto compute = [&](const __bf16* As) {
     const __bf16* Bs = As + A_EL;
+    if constexpr (X6) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 fa[3][TI], fb[3][TJ];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+            fa[q][i] = A_RK ? *reinterpret_cast<const bf16x8*>(As + q * A_EL1 + (wr * WM + i * 32 + li) * LDB +
+                                                                ks * 16 + 8 * h)
+                            : frag_tr(As + q * A_EL1, TA::LDK, wr * WM + i * 32, ks);
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            fb[q][j] = B_RK ? *reinterpret_cast<const bf16x8*>(Bs + q * B_EL1 + (wc * WN + j * 32 + li) * LDB +
+                                                                ks * 16 + 8 * h)
+                            : frag_tr(Bs + q * B_EL1, TBt::LDK, wc * WN + j * 32, ks);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+            acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[1][j], acs[i][j], 0, 0, 0);
+            acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[0][j], acs[i][j], 0, 0, 0);
+            acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[2][j], acs[i][j], 0, 0, 0);
+            acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][i], fb[0][j], acs[i][j], 0, 0, 0);
+            acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[1][j], acs[i][j], 0, 0, 0);
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 fa[TI], fb[TJ];
@@ -633,6 +720,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
     }
   }
 
+  if constexpr (X6)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += acs[i][j];
   float* out = slab ? slab + (int64_t)blockIdx.z * M * N : C;
   const int64_t ld = slab ? N : ldc;
 #pragma unroll
@@ -976,7 +1068,69 @@ void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t s
   }
 }
 
+// precision "fp32" GEMMs on bf16 MFMA (gemm_bf16_kernel X6): 256x128/BK16 (8 waves of 64x64)
+// for grids of >= 128 such tiles, 128x128/BK32 (4 waves of 64x64), 64x64/BK32 for small
+// outputs.  Three bf16 planes per operand image: 86-110 KB of LDS for the 256-row tile.
+int g_fp32_x6 = [] { const char* e = getenv("AVC_FP32_X6"); return e ? atoi(e) : 0; }();
+constexpr GemmShape kCfgX6[] = {
+    {0, 256, 128, 16},
+    {1, 128, 128, 32},
+    {2, 64, 64, 32},
+};
+// (cfg, splits) that put >= 192 workgroups on the chip with >= 1024 k per split, largest tile
+// first; otherwise the 64x64 tile with the caller's split.  z: batch (no split) or 0.
+PlanBf16 plan_x6(int M, int N, int K, int requested, int z) {
+  const int64_t t0 = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
+  const int64_t t1 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  if (z > 0) return {t0 * z >= 192 ? 0 : t1 * z >= 192 ? 1 : 2, 1};
+  for (int s = 1; s <= 4; ++s)
+    if (t0 * s >= 192 && (s == 1 || K / s >= 1024)) return {0, s};
+  for (int s = 1; s <= 4; ++s)
+    if (t1 * s >= 192 && (s == 1 || K / s >= 1024)) return {1, s};
+  return {2, requested};
+}
+template <int BM, int BN, int BK, bool AR, bool BR>
+constexpr unsigned x6_lds_bytes() {
+  return 3u * bf16_lds_bytes<BM, BN, BK, AR, BR>();
+}
+template <int BM, int BN, int BK, int WM, int WN>
+void launch_layouts_x6(int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
+                       float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+#define AVC_L(AR, BR) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, AR, BR, BM == 256, 0, 0, true>), grid, \
+                                         dim3(NT), dyn_lds_for(x6_lds_bytes<BM, BN, BK, AR, BR>()), st, M, N, K, oa, \
+                                         ob, C, ldc, b1, b2, acc, kps, slab, g_batch)
+  if (!a_trans && !b_trans) AVC_L(true, true);
+  else if (!a_trans && b_trans) AVC_L(true, false);
+  else if (a_trans && !b_trans) AVC_L(false, true);
+  else AVC_L(false, false);
+#undef AVC_L
+}
+void launch_gemm_x6(int id, int a_trans, int b_trans, dim3 grid, hipStream_t st, int M, int N, int K, Opnd oa, Opnd ob,
+                    float* C, int64_t ldc, const float* b1, const float* b2, int acc, int kps, float* slab) {
+  switch (id) {
+    case 0: launch_layouts_x6<256, 128, 16, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    case 1: launch_layouts_x6<128, 128, 32, 64, 64>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+    default: launch_layouts_x6<64, 64, 32, 32, 32>(a_trans, b_trans, grid, st, M, N, K, oa, ob, C, ldc, b1, b2, acc, kps, slab); break;
+  }
+}
+
 }  // namespace
+
+// precision "fp32" GEMMs through the bf16-plane kernel (1) or the fp32 MFMA kernel (0);
+// returns the previous mode
+extern "C" int autovc_gemm_set_fp32_x6(int on) {
+  const int prev = g_fp32_x6;
+  g_fp32_x6 = on ? 1 : 0;
+  return prev;
+}
+
+// the split-K factor autovc_gemm_f32 will use for a request (size its workspace with it)
+extern "C" int autovc_gemm_f32_splits(int M, int N, int K, int requested) {
+  if (requested < 1) requested = 1;
+  if (!g_fp32_x6 || M <= 0 || N <= 0 || K <= 0) return requested;
+  return plan_x6(M, N, K, requested, 0).splits;
+}
 
 // split-K workspace: the partial slabs (tiles rounded up to 256 x 256), summed in split order
 // by splitk_reduce_kernel
@@ -1033,7 +1187,15 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
     const PlanBf16 pl = plan_bf16(M, N, K, splits);
     if (pl.cfg >= 0) cfg = kCfgBf16[pl.cfg];
   }
-  if (batch > 1 && !bf16) {   // batched: tile count x batch decides between 128x128 and 64x64
+  const bool x6 = !bf16 && g_fp32_x6 && g_force_cfg < 0;
+  if (x6) {
+    // the planned split, never above the caller's (its workspace): callers size it with
+    // autovc_gemm_f32_splits
+    const PlanBf16 pl = plan_x6(M, N, K, splits, batch > 1 ? batch : 0);
+    cfg = kCfgX6[pl.cfg];
+    if (batch == 1) splits = std::min(splits, pl.splits);
+  }
+  if (batch > 1 && !bf16 && !x6) {   // batched: tile count x batch decides between 128x128 and 64x64
     const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * batch;
     // the 128-tile batched case (the Winograd GEMMs): 8 waves of 64x32 with pipelined fragment
     // reads (cfg 9) — isolated 78.6 vs 88.2 us on 8 x 2048x512x512 (tools/gemm_bench.hip wino,
@@ -1055,6 +1217,9 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
   if (bf16)
     launch_gemm_bf16(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate,
                      (int)kps, slab, src);
+  else if (x6)
+    launch_gemm_x6(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
+                   slab);
   else
     launch_gemm(cfg.id, a_trans, b_trans, grid, stream, M, N, K, oa, ob, C, ldc, bias1, bias2, accumulate, (int)kps,
                 slab);

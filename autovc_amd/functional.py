@@ -376,8 +376,10 @@ def gemm(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, *, a_conv=None, b_co
     ac = a_conv or (0, 0, 0)
     bc = b_conv or (0, 0, 0)
     ws = 0
-    if _PRECISION[0] == "bf16":   # the library plans large bf16 GEMMs' split-K itself
+    if _PRECISION[0] == "bf16":   # the library plans large GEMMs' split-K itself
         splits = _lib.load().autovc_gemm_bf16_splits(M, N, K, splits)
+    else:
+        splits = _lib.load().autovc_gemm_f32_splits(M, N, K, splits)
     if splits > 1:
         ws = _ws(C.device, 4 * _lib.load().autovc_gemm_workspace_floats(M, N, splits), "gemm")
     src = 0
@@ -1681,6 +1683,8 @@ class LSTM2StackFn(torch.autograd.Function):
         grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]),
                                      dGb=dG1b if bf else None)
         grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0, dGb=dG0b if bf else None)
+        if _EARLY_FLUSH:
+            _flush_grad_queue(beside_recurrence=_EARLY_FLUSH == 1)
         return (grads0[0], *grads0[1:], *grads1[1:], None)
 
 
@@ -1696,6 +1700,9 @@ class LSTM2StackFn(torch.autograd.Function):
 # the main stream; mode 1 14.46, where the side stream's tail then runs past the backward).
 # profiles/r05/ab_blstm_side.txt, ab_blstm_side2.txt.  AVC_BLSTM_SIDE=0 / 1 / 2 forces a mode
 _BLSTM_SIDE_ENV = os.environ.get("AVC_BLSTM_SIDE")
+# A/B (round 6): release lstm2's weight gradients as soon as they are queued (1: with the LDS
+# reserve, 2: without) instead of beside lstm1's backward recurrence
+_EARLY_FLUSH = int(os.environ.get("AVC_EARLY_FLUSH", "0"))
 
 
 _BLSTM_LAST_PASS = [False]   # set around the encoder pass whose backward ends the step

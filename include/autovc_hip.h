@@ -91,6 +91,14 @@ int autovc_gemm_f32(int M, int N, int K,
                     const float* B, int64_t ldb, int b_trans, int b_conv_T, int b_conv_C, int b_tap0,
                     float* C, int64_t ldc, const float* bias1, const float* bias2,
                     int accumulate, int splits, float* workspace, hipStream_t stream);
+/* How autovc_gemm_f32 and the fp32 batched GEMMs compute (returns the previous mode):
+ * 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); 1 = bf16 MFMA on each operand's three-plane split
+ * (fp32 = hi + mid + lo bf16, exact), the six products above 2^-24 |a b| accumulated as a
+ * large and a small partial: an fp32 GEMM to fp32 rounding, on the 16x faster bf16 units. */
+int autovc_gemm_set_fp32_x6(int on);
+/* The split-K factor autovc_gemm_f32 uses for `requested` (the bf16-plane mode plans its own
+ * split for large outputs, never above the request): size the workspace with it. */
+int autovc_gemm_f32_splits(int M, int N, int K, int requested);
 /* LDS bytes per CU that GEMM launches (fp32 and bf16) leave free from now on (0 = none):
  * their workgroups are padded so that no more of them share a CU than fit beside that
  * reserve — a latency-bound kernel on another stream keeps a slot on every CU. */
