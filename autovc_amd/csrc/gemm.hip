@@ -690,7 +690,42 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_bf16_kernel(
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
   };
-  if (DEEP) {
+#ifndef AVC_X6_SCHED
+#define AVC_X6_SCHED 6
+#endif
+  if constexpr (X6 && DEEP) {
+    // as the DEEP loop below, with the refills unconditional (past-K loads read zeros; a
+    // stage written past the last k is never computed), so that each half is one straight
+    // block: the next stage's split conversions and LDS writes are interleaved between the
+    // MFMAs (AVC_X6_SCHED vector instructions per MFMA) instead of following them.  Isolated
+    // (profiles/r06/gemm_x6_sched.txt): 6 per MFMA 374 vs 390 us for 0 on the LSTM dW
+    // 4096x1024x8192, others within 2 %; the unconditional refills alone took the step from
+    // 13.05 to 12.85-12.89 ms (ab_fp32_x6_v3.txt)
+    constexpr int NMF = TI * TJ * 6 * (BK / 16);
+    auto interleave = [&]() {
+      if constexpr (AVC_X6_SCHED > 0) {
+#pragma unroll
+        for (int q = 0; q < NMF; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, AVC_X6_SCHED, 0);
+        }
+      }
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      compute(smem[0]);
+      stage(smem[1]);
+      load1();
+      interleave();
+      __syncthreads();
+      if (kt + 1 < nk) {
+        compute(smem[1]);
+        stage2(smem[0]);
+        load2();
+        interleave();
+        __syncthreads();
+      }
+    }
+  } else if (DEEP) {
     // two register stages in flight: at the top of an iteration LDS buffer 0 holds stage kt,
     // set 1 (v) stage kt + 1 and set 2 (v2) stage kt + 2; each half computes one buffer and
     // refills the other from the set whose loads are oldest, then reloads that set
@@ -1068,10 +1103,13 @@ void launch_gemm_bf16(int id, int a_trans, int b_trans, dim3 grid, hipStream_t s
   }
 }
 
-// precision "fp32" GEMMs on bf16 MFMA (gemm_bf16_kernel X6): 256x128/BK16 (8 waves of 64x64)
-// for grids of >= 128 such tiles, 128x128/BK32 (4 waves of 64x64), 64x64/BK32 for small
-// outputs.  Three bf16 planes per operand image: 86-110 KB of LDS for the 256-row tile.
-int g_fp32_x6 = [] { const char* e = getenv("AVC_FP32_X6"); return e ? atoi(e) : 0; }();
+// precision "fp32" GEMMs on bf16 MFMA (gemm_bf16_kernel X6), the default: 256x128/BK16 (8 waves
+// of 64x64, two stages in flight), 128x128/BK32 (4 waves of 64x64), 64x64/BK32 for small
+// outputs.  Three bf16 planes per operand image: 86-110 KB of LDS for the 256-row tile.  Step
+// A/B (alternating, one box): 13.05-13.06 vs 14.00-14.08 ms/step with the fp32 MFMA kernel
+// (profiles/r06/ab_fp32_x6_v2.txt; isolated 1.3-1.6x on the step's shapes,
+// gemm_x6_time_v2.txt).  AVC_FP32_X6=0 (or autovc_gemm_set_fp32_x6(0)) selects gemm_kernel.
+int g_fp32_x6 = [] { const char* e = getenv("AVC_FP32_X6"); return e ? atoi(e) : 1; }();
 constexpr GemmShape kCfgX6[] = {
     {0, 256, 128, 16},
     {1, 128, 128, 32},
