@@ -1621,11 +1621,11 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
 }
 
 int g_xcd_ok = -1;
-// dynamic LDS of the backward launch (A/B: AVC_XCD_BWD_LDS bytes; default the forward's pad)
-int xcd_bwd_lds() {
-  static const int v = [] { const char* e = getenv("AVC_XCD_BWD_LDS"); return e ? atoi(e) : XC_PAD_LDS; }();
-  return v;
-}
+// dynamic LDS of the backward launch: just over half a CU's 160 KB (one workgroup per CU) while
+// leaving room for one X6 / fp32 GEMM workgroup beside it (12.43 vs 12.69-12.71 ms/step with the
+// forward's 96 KB pad: profiles/r06/ab_lstm1_xcd_bwd_x6.txt)
+constexpr int kXcdBwdLds = 82432;
+int xcd_bwd_lds() { return kXcdBwdLds; }
 
 bool xcd_fits() {
   if (g_xcd_ok < 0) {

@@ -93,24 +93,21 @@ _GRAD_STREAMS: dict = {}
 GRAD_LDS_RESERVE = {"fp32": 38912, "bf16": 38912}
 
 
-def _grad_stream(dev, k=0):
+def _grad_stream(dev):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    st = _GRAD_STREAMS.get((idx, k))
+    st = _GRAD_STREAMS.get(idx)
     if st is None:
         st = torch.cuda.Stream(torch.device("cuda", idx))
-        _GRAD_STREAMS[(idx, k)] = st
+        _GRAD_STREAMS[idx] = st
     return st
 
 
-# A/B (round 6): consecutive flushes alternate over this many side streams; AVC_JOIN_MAIN=1
-# runs the batch still queued at the join on the main stream
-_SIDE_STREAMS = int(os.environ.get("AVC_SIDE_STREAMS", "1"))
+# A/B (round 6): AVC_JOIN_MAIN=1 runs the batch still queued at the join on the main stream
 _JOIN_MAIN = os.environ.get("AVC_JOIN_MAIN", "0") == "1"
-_FLUSHES = [0]
 
 
 _GRAD_QUEUE: list = []
-_GRAD_PENDING: set = set()   # (device index, k) of side streams with work not yet joined
+_GRAD_PENDING: set = set()   # device indices whose side stream has work not yet joined
 
 
 def _grad_launch(dev, outs, fn, *inputs):
@@ -176,7 +173,7 @@ def _grad_mark(dev):
     return ev
 
 
-def _flush_grad_queue(beside_recurrence=True, after=None):
+def _flush_grad_queue(beside_recurrence=True, after=None, lds_reserve=None):
     """Issue every queued gradient launch on the side stream, ordered after `after` (an
     event from _grad_mark) or else after all main-stream work issued so far (their
     inputs), inputs marked as in use by the side stream.  The LDS reserve only pays beside
@@ -189,17 +186,17 @@ def _flush_grad_queue(beside_recurrence=True, after=None):
     _GRAD_QUEUE.clear()
     dev = items[0][0]
     main = torch.cuda.current_stream(dev)
-    k = _FLUSHES[0] % _SIDE_STREAMS
-    _FLUSHES[0] += 1
-    side = _grad_stream(dev, k)
+    side = _grad_stream(dev)
     if after is not None:
         side.wait_event(after)
     else:
         side.wait_stream(main)
     _GRAD_STREAM_ACTIVE[0] = True
-    _GRAD_PENDING.add((side.device.index, k))
+    _GRAD_PENDING.add(side.device.index)
     prev_prec = _PRECISION[0]
-    _lib.call("autovc_gemm_set_lds_reserve", GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0)
+    if lds_reserve is None:
+        lds_reserve = GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0
+    _lib.call("autovc_gemm_set_lds_reserve", lds_reserve)
     try:
         with torch.cuda.stream(side):
             for _, fn, inputs, prec, _outs in items:
@@ -241,16 +238,16 @@ def join_grad_stream(dev=None):
             _PRECISION[0] = prev
     _flush_grad_queue(beside_recurrence=False)
     _SIDE_WRITES.clear()
-    _FLUSHES[0] = 0
     if not _GRAD_PENDING:
         return
     dev = dev or torch.device("cuda", torch.cuda.current_device())
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    for key in sorted(k for k in _GRAD_PENDING if k[0] == idx):
+    st = _GRAD_STREAMS.get(idx)
+    if st is not None and idx in _GRAD_PENDING:
         # only a side stream with work since the last join is waited on: inside a graph
         # capture (autovc_amd.graph) the wait must be on work of the same capture
-        torch.cuda.current_stream(dev).wait_stream(_GRAD_STREAMS[key])
-        _GRAD_PENDING.discard(key)
+        torch.cuda.current_stream(dev).wait_stream(st)
+        _GRAD_PENDING.discard(idx)
 
 
 class GradMarks:
@@ -1421,14 +1418,12 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     # 4 ways with the fused steps (decoder lstm1: 8.46-8.52 vs 8.55-8.57 ms/step for 8 ways,
     # profiles/r05/ab_lstm1_splits.txt; 8 ways measured best with the launch pair, round 2).
     splits = 4 if _bf16_rec(H) else (8 if H <= 512 else 4)
-    if os.environ.get("AVC_LSTM1_SPLITS"):
-        splits = int(os.environ["AVC_LSTM1_SPLITS"])
     # the recurrent K (4H fp32 floats, 2H bf16 pairs) must cut into multiples of 64 per split
     kdim = 2 * H if _bf16_rec(H) else 4 * H
     while splits > 1 and kdim % (64 * splits):
         splits //= 2
     dG = torch.empty((B, T, 4 * H), device=dev, dtype=torch.float32)
-    if lstm_xcd(B, H) and _XCD_BWD_ON:
+    if lstm_xcd(B, H) and _xcd_bwd():
         # one XCD-local persistent launch (csrc/lstm2_persist.hip lstm_xcd_bwd_kernel)
         ws = _ws(dev, _lib.load().autovc_lstm_xcd_workspace_bytes(), "lstmxb")
         mark = _grad_mark(dev)
@@ -1439,15 +1434,9 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
         else:
             _lib.call("autovc_lstm_bwd_xcd_f32", B, T, H, dh.data_ptr(), T * H, H, gates.data_ptr(), c.data_ptr(),
                       WT.data_ptr(), dG.data_ptr(), ws, _s())
-        if _XCD_BWD_RESERVE is not None:
-            saved = dict(GRAD_LDS_RESERVE)
-            GRAD_LDS_RESERVE.update({k: _XCD_BWD_RESERVE for k in GRAD_LDS_RESERVE})
-            try:
-                _flush_grad_queue(after=mark)
-            finally:
-                GRAD_LDS_RESERVE.update(saved)
-        else:
-            _flush_grad_queue(after=mark)
+        # the queued GEMMs unpadded beside it: the launch holds 80.5 KB of LDS on every CU for
+        # its whole length, which no per-step recurrence workgroup needs to share
+        _flush_grad_queue(after=mark, lds_reserve=0)
         return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=dGb if _bf16_rec(H) else None)
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     # (keeping the batch past this recurrence, to run beside the encoder BLSTMs instead,
@@ -1564,12 +1553,18 @@ def lstm_persistent(B, H):
 _XCD_ON = os.environ.get("AVC_LSTM_XCD", "1") != "0"
 
 
-# The backward the same way (lstm_xcd_bwd_kernel: 4.2 vs 9.3 us per step alone) lost inside
-# the round-3 training step, where the split-K launches' idle CUs host queued weight-gradient
-# GEMMs (15.91-16.93 vs 15.65 ms/step, profiles/r03/ab_lstm_xcd.txt); round 6 re-measures it
-# (fp32 and bf16) in the current schedule: AVC_LSTM_XCD_BWD=1 selects it.
-_XCD_BWD_ON = os.environ.get("AVC_LSTM_XCD_BWD", "0") != "0"
-_XCD_BWD_RESERVE = int(os.environ["AVC_XCD_BWD_RESERVE"]) if "AVC_XCD_BWD_RESERVE" in os.environ else None
+# The backward the same way (lstm_xcd_bwd_kernel, 1.0 vs 1.55 ms per call in the step graph):
+# under precision fp32, once the X6 GEMMs had shortened the side stream (the main stream's
+# lstm1 backward then ran 2.3 ms beside them), 12.43 vs 12.95-12.99 ms/step; under bf16 neutral
+# (7.88-7.92 both) and slower before X6 (profiles/r06/ab_lstm1_xcd_bwd.txt, ab_lstm1_xcd_bwd_x6.txt).
+# AVC_LSTM_XCD_BWD=0 / 1 forces it; by default fp32 only.
+_XCD_BWD_ENV = os.environ.get("AVC_LSTM_XCD_BWD")
+
+
+def _xcd_bwd():
+    if _XCD_BWD_ENV is not None:
+        return _XCD_BWD_ENV == "1"
+    return _PRECISION[0] != "bf16"
 
 
 def lstm_xcd(B, H):
@@ -1683,8 +1678,6 @@ class LSTM2StackFn(torch.autograd.Function):
         grads1 = _lstm_grads_from_dG(dG1, h0, W_ih1, h1, ctx.params[1], (False,) + tuple(need1[1:]),
                                      dGb=dG1b if bf else None)
         grads0 = _lstm_grads_from_dG(dG0, x, W_ih0, h0, ctx.params[0], need0, dGb=dG0b if bf else None)
-        if _EARLY_FLUSH:
-            _flush_grad_queue(beside_recurrence=_EARLY_FLUSH == 1)
         return (grads0[0], *grads0[1:], *grads1[1:], None)
 
 
@@ -1700,9 +1693,6 @@ class LSTM2StackFn(torch.autograd.Function):
 # the main stream; mode 1 14.46, where the side stream's tail then runs past the backward).
 # profiles/r05/ab_blstm_side.txt, ab_blstm_side2.txt.  AVC_BLSTM_SIDE=0 / 1 / 2 forces a mode
 _BLSTM_SIDE_ENV = os.environ.get("AVC_BLSTM_SIDE")
-# A/B (round 6): release lstm2's weight gradients as soon as they are queued (1: with the LDS
-# reserve, 2: without) instead of beside lstm1's backward recurrence
-_EARLY_FLUSH = int(os.environ.get("AVC_EARLY_FLUSH", "0"))
 
 
 _BLSTM_LAST_PASS = [False]   # set around the encoder pass whose backward ends the step

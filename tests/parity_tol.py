@@ -47,7 +47,7 @@ def check_trajectory(traj, ref=None):
     smaller per-GEMM error than fp32 MFMA, tools/x6_bias_probe.py) end L_recon 0.02 % and L_cd
     8.9 % from float64 — nearer than the golden (0.27 %, 7.7 %) on L_recon — but L_cd 15.4 %
     from the golden, past its 14.3 %; fp32 MFMA with the im2col convs lands 13.5 % away."""
-    default = ref is None or ref is G["solver_traj"]
+    default = ref is None or np.array_equal(np.asarray(ref), G["solver_traj"])
     ref = G["solver_traj"] if ref is None else ref
     traj = np.asarray(traj, np.float64)
     tol = trajectory_tolerance()

@@ -64,7 +64,7 @@ def install():
         stamp(f"rec{nrec[0]}_begin(q={len(AF._GRAD_QUEUE)})", torch.cuda.current_stream(dev))
         return orig_mark(dev)
 
-    def flush(beside_recurrence=True, after=None):
+    def flush(beside_recurrence=True, after=None, lds_reserve=None):
         # functional._flush_grad_queue with stamps: main when the recurrence is done, side
         # when its batch starts and ends
         nfl[0] += 1
@@ -76,19 +76,19 @@ def install():
         AF._GRAD_QUEUE.clear()
         dev = items[0][0]
         main = torch.cuda.current_stream(dev)
-        k = AF._FLUSHES[0] % AF._SIDE_STREAMS
-        AF._FLUSHES[0] += 1
-        side = AF._grad_stream(dev, k)
+        side = AF._grad_stream(dev)
         if after is not None:
             side.wait_event(after)
         else:
             side.wait_stream(main)
-        tag = (f"side{nrec[0]}.{nfl[0]}" if beside_recurrence else "side_final") + (f"@{k}" if k else "")
+        tag = f"side{nrec[0]}.{nfl[0]}" if beside_recurrence else "side_final"
         stamp(f"{tag}_begin(n={len(items)})", side)
         AF._GRAD_STREAM_ACTIVE[0] = True
-        AF._GRAD_PENDING.add((side.device.index, k))
+        AF._GRAD_PENDING.add(side.device.index)
         prev = AF._PRECISION[0]
-        _lib.call("autovc_gemm_set_lds_reserve", AF.GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0)
+        if lds_reserve is None:
+            lds_reserve = AF.GRAD_LDS_RESERVE[items[0][3]] if beside_recurrence else 0
+        _lib.call("autovc_gemm_set_lds_reserve", lds_reserve)
         try:
             with torch.cuda.stream(side):
                 for _, fn, inputs, prec, _outs in items:
