@@ -46,6 +46,7 @@ sig("autovc_preprocess_f64", c_ptr, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_
 sig("autovc_gemm_workspace_floats", c_int, c_int, c_int)
 sig("autovc_gemm_set_lds_reserve", c_int)
 sig("autovc_gemm_set_fp32_x6", c_int)
+sig("autovc_gemm_fp32_x6")
 sig("autovc_gemm_f32_splits", c_int, c_int, c_int, c_int)
 sig("autovc_stream_create_cu_mask", c_int, c_ptr, c_ptr)
 sig("autovc_stream_destroy", c_ptr)

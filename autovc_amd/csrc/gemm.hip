@@ -1170,6 +1170,8 @@ extern "C" int autovc_gemm_f32_splits(int M, int N, int K, int requested) {
   return plan_x6(M, N, K, requested, 0).splits;
 }
 
+extern "C" int autovc_gemm_fp32_x6(void) { return g_fp32_x6; }
+
 // split-K workspace: the partial slabs (tiles rounded up to 256 x 256), summed in split order
 // by splitk_reduce_kernel
 extern "C" int64_t autovc_gemm_workspace_floats(int M, int N, int splits) {

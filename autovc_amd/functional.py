@@ -102,10 +102,6 @@ def _grad_stream(dev):
     return st
 
 
-# A/B (round 6): AVC_JOIN_MAIN=1 runs the batch still queued at the join on the main stream
-_JOIN_MAIN = os.environ.get("AVC_JOIN_MAIN", "0") == "1"
-
-
 _GRAD_QUEUE: list = []
 _GRAD_PENDING: set = set()   # device indices whose side stream has work not yet joined
 
@@ -223,19 +219,6 @@ def join_grad_stream(dev=None):
     stream (before anything reads the gradients).  (Running the batch still queued here on the
     idle main stream instead measured fp32 13.93-13.98 vs 13.94, bf16 7.87-7.92 vs 7.81-7.85
     ms/step: profiles/r06/ab_join_{fp32,bf16}.txt.)"""
-    if _JOIN_MAIN and _GRAD_QUEUE:
-        items = list(_GRAD_QUEUE)
-        _GRAD_QUEUE.clear()
-        prev = _PRECISION[0]
-        try:
-            for d, fn, inputs, prec, outs in items:
-                _PRECISION[0] = prec
-                _main_grad(d, outs, fn, *inputs)
-                if MARKS.active:
-                    for o in outs:
-                        MARKS.log(o.buf, GradMarks.FINAL)
-        finally:
-            _PRECISION[0] = prev
     _flush_grad_queue(beside_recurrence=False)
     _SIDE_WRITES.clear()
     if not _GRAD_PENDING:
@@ -1393,6 +1376,18 @@ class LSTMLayerFn(torch.autograd.Function):
     def backward(ctx, dh):
         x, W_ih, W_hh, h, c, gates = ctx.saved_tensors
         return _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, ctx.params, ctx.needs_input_grad[:5]) + (None,)
+
+
+def set_fp32_gemm(mode):
+    """precision fp32's GEMMs: "x6" (bf16 MFMA on exact three-plane operand splits, the default,
+    fp32-accurate: csrc/gemm.hip) or "mfma" (v_mfma_f32_32x32x2_f32).  Returns the previous mode."""
+    if mode not in ("x6", "mfma"):
+        raise ValueError("set_fp32_gemm: 'x6' or 'mfma'")
+    return "x6" if _lib.load().autovc_gemm_set_fp32_x6(1 if mode == "x6" else 0) else "mfma"
+
+
+def fp32_gemm_mode():
+    return "x6" if _lib.load().autovc_gemm_fp32_x6() else "mfma"
 
 
 def _bf16_rec(H):

@@ -189,7 +189,9 @@ class Solver(object):
             if self._graphs is None:
                 from .graph import StepGraphs
                 self._graphs = StepGraphs(self._forward_backward, self.G)
-            g_loss, l_id, l_psnt, l_cd, x_psnt = self._graphs.run(self.precision, x_real, emb_org)
+            # the fp32 GEMM mode (X6 / fp32 MFMA) selects other kernels: a graph of its own
+            key = (self.precision, AF.fp32_gemm_mode())
+            g_loss, l_id, l_psnt, l_cd, x_psnt = self._graphs.run(key, x_real, emb_org)
         else:
             g_loss, l_id, l_psnt, l_cd, x_psnt = self._forward_backward(x_real, emb_org)
         self._after_backward()

@@ -672,6 +672,21 @@ def main():
               "grad_exchange": None if world == 1 else "bf16 all-to-all + fp32 shard sums + bf16 all-gather",
               "note": "BASELINE config 3 precision; the headline value above is config 2 (fp32)"}
 
+    f32m = None
+    if not args.no_bf16 and args.precision == "fp32":
+        # the same fp32 step with the GEMMs on fp32 MFMA instead of the default three-plane bf16
+        # split (both fp32-accurate: tests/test_gemm_x6_gpu.py), for comparison
+        prev = AF.set_fp32_gemm("mfma")
+        try:
+            timed_steps(max(2, args.warmup // 2))
+            dtm, lm = timed_steps(args.steps)
+            AF.check_device_faults(dev)
+        finally:
+            AF.set_fp32_gemm(prev)
+        f32m = {"value": round(world * B * T * args.steps / dtm, 1), "unit": "mel-frames/s",
+                "ms_per_step": round(dtm / args.steps * 1000, 3), "final_loss": round(float(lm[0].item()), 6),
+                "note": "precision fp32 with every GEMM on v_mfma_f32_32x32x2_f32 (AVC_FP32_X6=0)"}
+
     roof = blstm = None
     if not args.no_roofline and rank == 0:
         roof = lstm_roofline(solver, B, T, dev)
@@ -697,6 +712,10 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1000, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16", "data": "synthetic (clamped N(0.43,0.18) mels, unit-norm*0.8 emb)",
+            "fp32_gemm": (AF.fp32_gemm_mode() + (": fp32 operands split exactly into three bf16 planes, six bf16 MFMA "
+                          "products per pair in two fp32 accumulators (error vs fp64 <= the fp32-MFMA kernel's)"
+                          if AF.fp32_gemm_mode() == "x6" else ": v_mfma_f32_32x32x2_f32"))
+            if args.precision == "fp32" else None,
             "dist_backend": torch.distributed.get_backend() if world > 1 else None,
             "world_size": torch.distributed.get_world_size() if world > 1 else 1,
             "rank_ms_per_step": rank_ms,
@@ -707,7 +726,7 @@ def main():
             "final_loss": round(last_loss, 6),
             "roofline": roof, "blstm_roofline": blstm,
             "step_roofline": step_roofline(B, dt / args.steps * 1000, args.precision),
-            "cpu_baseline": cpu, "bf16": bf,
+            "cpu_baseline": cpu, "bf16": bf, "fp32_mfma": f32m,
             "wavenet": wn,
             "e2e": e2e, "frontend": fe,
         }

@@ -96,6 +96,7 @@ int autovc_gemm_f32(int M, int N, int K,
  * (fp32 = hi + mid + lo bf16, exact), the six products above 2^-24 |a b| accumulated as a
  * large and a small partial: an fp32 GEMM to fp32 rounding, on the 16x faster bf16 units. */
 int autovc_gemm_set_fp32_x6(int on);
+int autovc_gemm_fp32_x6(void);   /* the current mode */
 /* The split-K factor autovc_gemm_f32 uses for `requested` (the bf16-plane mode plans its own
  * split for large outputs, never above the request): size the workspace with it. */
 int autovc_gemm_f32_splits(int M, int N, int K, int requested);
