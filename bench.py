@@ -243,7 +243,7 @@ def cpu_share():
     return allowed, len(phys) or (os.cpu_count() or 1)
 
 
-def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=12.0, cpu=True):
+def wavenet_bench(dev, n_utt=8, Tc=128, warmup_steps=256, seconds_cpu=20.0, cpu=True):
     """BASELINE config 4 / SURVEY §8d C4: r9y9 WaveNet (24 layers, 512 residual channels),
     8 utterances x 128 conditioning frames (32,768 samples = 2.048 s each) synthesised in one
     batch.  Timed: the whole job (upsample, per-chunk conditioning GEMM, every sample step
@@ -317,11 +317,13 @@ def _wn_path_name(p):
             2: "wn_pipe_kernel (layer-pipelined weight-resident chain, one launch per call)"}.get(p, str(p))
 
 
-def wavenet_cpu_baseline(n_utt, seconds, steps=512, min_passes=3):
+def wavenet_cpu_baseline(n_utt, seconds, steps=512, min_passes=7):
     """oracle/wavenet.py (fp32 torch CPU ops, the reference's own per-step structure): after a
     short warm-up pass, passes of `steps` incremental sample steps of the same batch are timed
     until `seconds` have elapsed (at least `min_passes`); the value is the MEDIAN pass's rate
-    (a single pass swung 1.1k-1.5k samples/s between identical runs)."""
+    (a single pass swung 1.1k-1.5k samples/s between identical runs; with 3-5
+    passes over 12 s three round-6 runs on different boxes read 1,367-1,539, hence >= 7 passes
+    over >= 20 s)."""
     from oracle import wavenet as ow
     threads, _ = cpu_share()
     torch.set_num_threads(threads)

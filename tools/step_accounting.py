@@ -17,6 +17,7 @@ CATS = [
     ("lstm1 bwd", r"lstm_bwd_(rec|pointwise|fused)|lstm_xcd_bwd"),
     ("encoder BLSTM", r"blstm_"),
     ("GEMM fp32", r"gemm_kernel<"),
+    ("GEMM fp32 on bf16 planes (X6)", r"gemm_bf16_kernel<.*, true>\("),
     ("GEMM bf16", r"gemm_bf16_kernel<"),
     ("split-K reduce", r"splitk_reduce|splitk_stats"),
     ("Winograd transforms", r"wino_"),
