@@ -1437,7 +1437,10 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
   constexpr int KW = K4 / 4;             // k per wave
   constexpr int KG = KW / 4;             // k per MFMA lane group (consecutive)
   static_assert(U == 16, "tile shape");
-  constexpr int SS = BF ? KW + 8 : KW + 4;   // slab row stride in elements (bank spread)
+  // slab row stride in elements (bank spread).  fp32: the wave's K quarter arrives in two
+  // rounds of half the k (each lane group's 128 k as two 64-k chunks), so the slab holds 256 k
+  // per row: 41 KB of LDS per workgroup instead of 77, room for a GEMM workgroup beside it
+  constexpr int SS = BF ? KW + 8 : KW / 2 + 4;
   using E = typename std::conditional<BF, __bf16, float>::type;
   static_assert(4 * U * (XRB + 1) * 4 + 4 * (XRB + 1) * SS * (int)sizeof(E) <= XC_PAD_LDS, "LDS budget");
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1496,7 +1499,7 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
     }
   }
   const bool bvalid = (lane & 15) < XRB;
-  const E* brow = slab + (bvalid ? (lane & 15) : XRB) * SS + KG * (lane >> 4);
+  const E* brow = slab + (bvalid ? (lane & 15) : XRB) * SS + (BF ? KG : KG / 2) * (lane >> 4);
   // pointwise operands of step t (prefetched one step ahead)
   f32x4 gt = {0.f, 0.f, 0.f, 0.f};
   float cc = 0.f, cpv = 0.f, dho = 0.f, dcs = 0.f;
@@ -1536,13 +1539,44 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
       // ---- this wave's K quarter of the group's dG_{t+1} rows -> its LDS slab: coalesced sc1
       // loads (whole lines per instruction: L1 is bypassed, so scattered fragment loads would
       // re-fetch every line), then the products dh_rec = dG_{t+1} W_hh from LDS
-      {
+      if constexpr (!BF) {
+        // load i = 8 h + r: row r, round h; lane group g = lane / 16 takes the 16 float4 of its
+        // chunk k = KG g + 64 h + 4 (lane % 16) .. +3 (256 contiguous bytes per lane group)
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.dG + ((int64_t)r0 * T + t + 1) * K4 + KW * wave), (short)0, 0x7fffffff, 0x00020000);
+        f32x4 v[2 * XRB];
+        const int kl = KG * (lane >> 4) + 4 * (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 2 * XRB; ++i) {
+          const int row = i % XRB, h = i / XRB;
+          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               r, (uint32_t)(((int64_t)row * T * K4 + kl + 64 * h) * 4), 0, 16));
+        }
+        float* sl = reinterpret_cast<float*>(slab) + (KG / 2) * (lane >> 4) + 4 * (lane & 15);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int row = 0; row < XRB; ++row) *reinterpret_cast<f32x4*>(sl + row * SS) = v[h * XRB + row];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int q = 0; q < KG / 2; q += 4) {
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + q);
+            const int w0 = (KG / 2) * h + q;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[w0], bv[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[w0 + 1], bv[1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[w0 + 2], bv[2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[w0 + 3], bv[3], acc, 0, 0, 0);
+          }
+          // (the next round's writes follow this wave's own slab reads in program order)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+        }
+      } else {
         constexpr int CPR = KW * (int)sizeof(E) / 16;    // 16-B chunks per row slice
         constexpr int NL = XRB * CPR / 64;               // b128 loads per lane
-        const void* base = BF ? (const void*)(a.dGb + ((int64_t)r0 * T + t + 1) * K4 + KW * wave)
-                              : (const void*)(a.dG + ((int64_t)r0 * T + t + 1) * K4 + KW * wave);
-        const __amdgpu_buffer_rsrc_t r =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<__bf16*>(a.dGb + ((int64_t)r0 * T + t + 1) * K4 + KW * wave), (short)0, 0x7fffffff, 0x00020000);
         f32x4 v[NL];
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
@@ -1564,15 +1598,6 @@ __global__ __launch_bounds__(XNT, 1) void lstm_xcd_bwd_kernel(XBArgs a) {
         for (int q = 0; q < KG / 8; ++q)
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[q], *reinterpret_cast<const bf16x8*>(brow + 8 * q), acc, 0,
                                                         0, 0);
-      } else {
-#pragma unroll
-        for (int q = 0; q < KG; q += 4) {
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + q);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q], bv[0], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 1], bv[1], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 2], bv[2], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q + 3], bv[3], acc, 0, 0, 0);
-        }
       }
     }
     // C[unit 4 (lane / 16) + r][batch lane % 16]: the 4 waves' K quarters, summed in order
@@ -1624,6 +1649,9 @@ int g_xcd_ok = -1;
 // dynamic LDS of the backward launch: just over half a CU's 160 KB (one workgroup per CU) while
 // leaving room for one X6 / fp32 GEMM workgroup beside it (12.43 vs 12.69-12.71 ms/step with the
 // forward's 96 KB pad: profiles/r06/ab_lstm1_xcd_bwd_x6.txt)
+// (With the fp32 slab halved the kernel needs 39.7 KB; requesting only that — so that the side
+// GEMM workgroups co-reside — measured the same step, 12.51-12.53 vs 12.52-12.55 ms:
+// profiles/r06/ab_xcd_bwd_lds.txt.)
 constexpr int kXcdBwdLds = 82432;
 int xcd_bwd_lds() { return kXcdBwdLds; }
 
