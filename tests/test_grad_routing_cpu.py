@@ -16,12 +16,22 @@ def test_blstm_last_pass_flag_nests_and_restores():
 
 def test_blstm_side_defaults_by_precision(monkeypatch):
     monkeypatch.setattr(AF, "_BLSTM_SIDE_ENV", None)
-    with AF.precision("fp32"):      # mode 2: every pass but the last-differentiated one
-        assert AF._blstm_side(last_pass=False) is True
-        assert AF._blstm_side(last_pass=True) is False
-    with AF.precision("bf16"):      # mode 1: all of them
-        assert AF._blstm_side(last_pass=False) is True
-        assert AF._blstm_side(last_pass=True) is True
+    for prec in ("fp32", "bf16"):   # mode 2: every pass but the last-differentiated one
+        with AF.precision(prec):
+            assert AF._blstm_side(last_pass=False) is True
+            assert AF._blstm_side(last_pass=True) is False
+
+
+def test_lstm1_backward_routing_defaults(monkeypatch):
+    """The XCD-local lstm1 backward in both precisions (AVC_LSTM_XCD_BWD forces it); its weight
+    gradients on the main stream under bf16 only."""
+    monkeypatch.setattr(AF, "_XCD_BWD_ENV", None)
+    for prec, dw_main in (("fp32", False), ("bf16", True)):
+        with AF.precision(prec):
+            assert AF._xcd_bwd() is True
+            assert AF._lstm1_dw_main() is dw_main
+    monkeypatch.setattr(AF, "_XCD_BWD_ENV", "0")
+    assert AF._xcd_bwd() is False
 
 
 def test_blstm_side_overrides(monkeypatch):
