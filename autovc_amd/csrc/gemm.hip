@@ -1215,11 +1215,14 @@ static int gemm_impl(bool bf16, int batch, int64_t a_bs, int64_t b_bs, int64_t c
       AVC_CHECK_ARG(pl.splits <= splits || workspace,
                     "autovc_gemm_bf16_f32: split-K plan needs the workspace of autovc_gemm_bf16_splits");
       splits = pl.splits;
-      // the weight gradients (both operands K-strided) at most 2 splits: they run on the gradient
+      // the weight gradients (both operands K-strided) at most 3 splits: they run on the gradient
       // side stream beside the recurrences, where half the chip for twice as long costs the
       // step less than 4-way slabs and their reduce (training step 8.53-8.55 vs 8.99-9.05 ms;
       // 3 splits 8.67-8.68, 1 split 8.75-8.79; profiles/r05/ab_bf16_dw_splits.txt)
-      if (a_trans && b_trans) splits = std::min(splits, 2);
+      // (round 6, with the XCD-local lstm1 backward and the bf16 routing: 3 splits 7.56-7.65 vs
+      // 7.61-7.66 ms/step for 2 over six alternating pairs, uncapped 7.69;
+      // profiles/r06/ab_bf16_dw_splits_r06.txt)
+      if (a_trans && b_trans) splits = std::min(splits, 3);
     }
   }
   GemmShape cfg = bf16 ? pick_config_bf16(M, N, batch > 1 ? batch : splits) : pick_config(M, N, K, splits);
