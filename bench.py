@@ -206,6 +206,52 @@ def blstm_roofline(dev, B, T, H=32):
     return out
 
 
+def gemm_x6_roofline(dev, M=4096, N=1024, K=8192, reps=20):
+    """The step's largest GEMM shape (decoder lstm2's dW_hh: 4H x H over K = B*T, both operands
+    K-strided, the library's split plan) under precision fp32 on its default X6 kernel and on
+    the fp32 MFMA kernel, HIP events over `reps` launches on the launch stream.  X6 issues six
+    v_mfma_f32_32x32x16_bf16 per fp32 product: its MFMA roofline is the bf16 dense peak / 6."""
+    from autovc_amd import _lib
+    st = _lib.stream_ptr(dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    A = torch.randn(K, M, device=dev, generator=g)
+    Bm = torch.randn(K, N, device=dev, generator=g)
+    C = torch.zeros(M, N, device=dev)
+    out = {}
+    prev = _lib.load().autovc_gemm_fp32_x6()
+    try:
+        for mode in (1, 0):
+            _lib.load().autovc_gemm_set_fp32_x6(mode)
+            splits = _lib.load().autovc_gemm_f32_splits(M, N, K, 1)
+            ws = torch.empty(4 * max(1, _lib.load().autovc_gemm_workspace_floats(M, N, splits)), dtype=torch.uint8,
+                             device=dev)
+
+            def launch():
+                _lib.call("autovc_gemm_f32", M, N, K, A.data_ptr(), M, 1, 0, 0, 0, Bm.data_ptr(), N, 1, 0, 0, 0,
+                          C.data_ptr(), N, 0, 0, 0, splits, ws.data_ptr(), st)
+            for _ in range(3):
+                launch()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                launch()
+            e1.record()
+            torch.cuda.synchronize()
+            out[mode] = e0.elapsed_time(e1) / reps * 1e3
+    finally:
+        _lib.load().autovc_gemm_set_fp32_x6(prev)
+    flop = 2.0 * M * N * K
+    tf = flop / (out[1] * 1e-6) / 1e12
+    return {"kernel": f"gemm_bf16_kernel<256, 128, 16, 64, 64, false, false, true, 0, 0, true> (X6: fp32 GEMM on "
+                      f"bf16 planes), LSTM dW {M}x{N}x{K}, both operands K-strided",
+            "bound": "mfma", "achieved": round(tf, 1), "unit": "TFLOP/s (fp32-equivalent)",
+            "peak": round(2500.0 / 6, 1), "frac": round(tf / (2500.0 / 6), 4), "traffic": None,
+            "avg_launch_us": round(out[1], 1), "fp32_mfma_kernel_us": round(out[0], 1),
+            "fp32_mfma_kernel_tf": round(flop / (out[0] * 1e-6) / 1e12, 1),
+            "note": "peak = bf16 dense MFMA 2.5 PF / 6 products per fp32 product; MFMA busy 46 % by PMC "
+                    "(profiles/r06/x6_pmc_dw_v2.json); the fp32 MFMA kernel's peak is 157.3 TF"}
+
+
 def step_roofline(B, ms_per_step, precision="fp32"):
     """Whole-step MFMA fraction: algorithmic FLOPs (convs, LSTMs, linear
     fwd + bwd, the second encoder pass; 24.60 GFLOP per sample) / step time / peak."""
@@ -215,7 +261,9 @@ def step_roofline(B, ms_per_step, precision="fp32"):
     return {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(tf / peak, 4), "flop_per_step": flop,
             "note": f"{precision} dense MFMA peak (MI355X_MICROARCH.md); FLOPs = 2 x MACs of convs/LSTMs/linear, "
-                    "fwd+bwd, both encoder passes (SURVEY §8d C2)"}
+                    "fwd+bwd, both encoder passes (SURVEY §8d C2)" +
+                    ("; under fp32 the GEMMs run on the bf16 MFMA units (X6, 'gemm_roofline'), so this "
+                     "fp32-equivalent fraction is not bounded by 1" if precision == "fp32" else "")}
 
 
 def cpu_share():
@@ -689,10 +737,11 @@ def main():
                 "ms_per_step": round(dtm / args.steps * 1000, 3), "final_loss": round(float(lm[0].item()), 6),
                 "note": "precision fp32 with every GEMM on v_mfma_f32_32x32x2_f32 (AVC_FP32_X6=0)"}
 
-    roof = blstm = None
+    roof = blstm = groof = None
     if not args.no_roofline and rank == 0:
         roof = lstm_roofline(solver, B, T, dev)
         blstm = blstm_roofline(dev, B, T)
+        groof = gemm_x6_roofline(dev)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(B, T)
@@ -726,7 +775,7 @@ def main():
                        "hip_graph": not args.no_graph,
                        "dim_neck": 32, "dim_emb": 256, "dim_pre": 512, "freq": 32},
             "final_loss": round(last_loss, 6),
-            "roofline": roof, "blstm_roofline": blstm,
+            "roofline": roof, "blstm_roofline": blstm, "gemm_roofline": groof,
             "step_roofline": step_roofline(B, dt / args.steps * 1000, args.precision),
             "cpu_baseline": cpu, "bf16": bf, "fp32_mfma": f32m,
             "wavenet": wn,
