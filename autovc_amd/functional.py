@@ -1432,8 +1432,7 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
         # the queued GEMMs unpadded beside it: the launch holds 80.5 KB of LDS on every CU for
         # its whole length, which no per-step recurrence workgroup needs to share
         _flush_grad_queue(after=mark, lds_reserve=0)
-        return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=dGb if _bf16_rec(H) else None,
-                                   on_main=_lstm1_dw_main())
+        return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=dGb if _bf16_rec(H) else None)
     ws = _ws(dev, 4 * _lib.load().autovc_lstm_bwd_workspace_floats(B, H, splits), "lstm")
     # (keeping the batch past this recurrence, to run beside the encoder BLSTMs instead,
     # measured slower: bf16 9.06-9.07 vs 9.03, fp32 15.62-15.64 vs 14.41-14.46 ms,
@@ -1450,7 +1449,7 @@ def _lstm_layer_backward(dh, x, W_ih, W_hh, h, c, gates, params, needs):
     return _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=dGb if _bf16_rec(H) else None)
 
 
-def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=None, on_main=False):
+def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=None):
     """Parameter gradients (queued beside the next recurrence, into the flat gradient
     buffer) and dx of one large-H layer from its gate gradients dG (B, T, 4H).  dGb: the
     recurrence's bf16 copy of dG (bf16 recurrences), which the GEMMs read instead of dG."""
@@ -1462,22 +1461,21 @@ def _lstm_grads_from_dG(dG, x, W_ih, h, params, needs, dGb=None, on_main=False):
     dev = x.device
     M = B * T
     dx = dWih = dWhh = dbih = dbhh = None
-    launch = _main_grad if on_main else _grad_launch
     if needs[1]:
         go = _GradOut(p_ih, W_ih.shape, dev)
-        launch(dev, go, lambda go=go: gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I,
+        _grad_launch(dev, go, lambda go=go: gemm(4 * H, I, M, dG, 4 * H, 1, x, I, 1, go.buf, I,
                                                      splits=_splits_for(4 * H, I, M), accumulate=go.acc, **kb),
                      dG, x, *keep)
         dWih = go.result()
     if needs[2]:
         go = _GradOut(p_hh, (4 * H, H), dev)
-        launch(dev, go, lambda go=go: gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
+        _grad_launch(dev, go, lambda go=go: gemm(4 * H, H, M, dG, 4 * H, 1, h, H, 1, go.buf, H, b_conv=(T, H, -1),
                                                      splits=_splits_for(4 * H, H, M), accumulate=go.acc, **kb),
                      dG, h, *keep)
         dWhh = go.result()
     if needs[3] or needs[4]:
         gi, gh = _bias_outs(p_bih, p_bhh, (4 * H,), dev)
-        launch(dev, (gi, gh), lambda gi=gi, gh=gh: colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc),
+        _grad_launch(dev, (gi, gh), lambda gi=gi, gh=gh: colsum(dG.view(M, 4 * H), gi.buf, gh.buf, accumulate=gi.acc),
                      dG)
         dbih, dbhh = gi.result(), gh.result()
     if needs[0]:
@@ -1555,9 +1553,10 @@ _XCD_ON = os.environ.get("AVC_LSTM_XCD", "1") != "0"
 # lstm1 backward then ran 2.3 ms beside them), 12.43 vs 12.95-12.99 ms/step (profiles/r06/
 # ab_lstm1_xcd_bwd.txt, ab_lstm1_xcd_bwd_x6.txt).  Under bf16 it alone is neutral (7.92-7.93 vs
 # 7.83-7.85): the recurrence shrinks to 0.33 ms but the side stream, with lstm1's weight
-# gradients queued behind lstm2's, becomes the tail (side_timeline_bf16_xcdbwd.txt); with those
-# three launches on the main stream right after it, 7.71-7.73 (ab_lstm1_dw_main.txt).  In fp32
-# the same move is slower (12.78-12.79 vs 12.60-12.64: X6 GEMMs fill the chip either way).
+# gradients queued behind lstm2's, becomes the tail (side_timeline_bf16_xcdbwd.txt); those three
+# launches on the main stream gave 7.71-7.73 (ab_lstm1_dw_main.txt; fp32 slower, 12.78 vs 12.62),
+# and once the BLSTM routing and the 3-split weight-gradient GEMMs had shortened the side
+# stream, back on the side stream 7.49-7.54 vs 7.62-7.64 (ab_bf16_rebalance.txt).
 # AVC_LSTM_XCD_BWD=0 / 1 forces the launch.
 _XCD_BWD_ENV = os.environ.get("AVC_LSTM_XCD_BWD")
 
@@ -1568,8 +1567,6 @@ def _xcd_bwd():
     return True
 
 
-def _lstm1_dw_main():
-    return _PRECISION[0] == "bf16"
 
 
 def lstm_xcd(B, H):

@@ -23,13 +23,11 @@ def test_blstm_side_defaults_by_precision(monkeypatch):
 
 
 def test_lstm1_backward_routing_defaults(monkeypatch):
-    """The XCD-local lstm1 backward in both precisions (AVC_LSTM_XCD_BWD forces it); its weight
-    gradients on the main stream under bf16 only."""
+    """The XCD-local lstm1 backward in both precisions (AVC_LSTM_XCD_BWD forces it)."""
     monkeypatch.setattr(AF, "_XCD_BWD_ENV", None)
-    for prec, dw_main in (("fp32", False), ("bf16", True)):
+    for prec in ("fp32", "bf16"):
         with AF.precision(prec):
             assert AF._xcd_bwd() is True
-            assert AF._lstm1_dw_main() is dw_main
     monkeypatch.setattr(AF, "_XCD_BWD_ENV", "0")
     assert AF._xcd_bwd() is False
 
