@@ -242,10 +242,18 @@ def gemm_x6_roofline(dev, M=4096, N=1024, K=8192, reps=20):
         _lib.load().autovc_gemm_set_fp32_x6(prev)
     flop = 2.0 * M * N * K
     tf = flop / (out[1] * 1e-6) / 1e12
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "r06", "x6_pmc_dw_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_dispatch")
     return {"kernel": f"gemm_bf16_kernel<256, 128, 16, 64, 64, false, false, true, 0, 0, true> (X6: fp32 GEMM on "
                       f"bf16 planes), LSTM dW {M}x{N}x{K}, both operands K-strided",
             "bound": "mfma", "achieved": round(tf, 1), "unit": "TFLOP/s (fp32-equivalent)",
-            "peak": round(2500.0 / 6, 1), "frac": round(tf / (2500.0 / 6), 4), "traffic": None,
+            "peak": round(2500.0 / 6, 1), "frac": round(tf / (2500.0 / 6), 4), "traffic": traffic,
+            "algorithmic_bytes": 4 * (M * K + N * K) + 4 * M * N,
+            "traffic_note": "PMC FETCH_SIZE x2 + WRITE_SIZE of the kernel dispatch (2 K splits: its writes are the "
+                            "two partial slabs; profiles/r06/x6_pmc_dw_traffic.json, L2 hit 74 %)",
             "avg_launch_us": round(out[1], 1), "fp32_mfma_kernel_us": round(out[0], 1),
             "fp32_mfma_kernel_tf": round(flop / (out[0] * 1e-6) / 1e12, 1),
             "note": "peak = bf16 dense MFMA 2.5 PF / 6 products per fp32 product; MFMA busy 46 % by PMC "
